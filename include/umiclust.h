@@ -1,0 +1,155 @@
+/*
+ * umiclust.h -- C ABI of the MI355X-native UMI clustering hot path.
+ *
+ * Drop-in for the `vsearch --cluster_fast ... --consout ... --clusters ...` subprocess that
+ * the reference runs per region bin:
+ *   - round 1: /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:8-56  (vsearch_cluster)
+ *   - round 2: /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:59-99 (vsearch_cluster_consensus)
+ * The reference's boundary is `subprocess.run(argv)` (vsearch_umi_cluster.py:21,71) with files
+ * as the only data exchange; `umiclust_run_argv` accepts that exact argv, `umiclust_run_fasta`
+ * the decoded parameters, and the session API (`umiclust_load` / `umiclust_cluster` /
+ * `umiclust_fetch`) the in-memory form used by the benchmark (inputs resident in HBM).
+ *
+ * Conventions: plain C types only; every function returns 0 (or a count) on success and a
+ * negative UMICLUST_E* code on failure, never throws across the ABI; one umiclust_ctx per
+ * (process, GPU); a context is not thread-safe, distinct contexts are.
+ */
+#ifndef UMICLUST_H
+#define UMICLUST_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UMICLUST_ABI_VERSION 1
+
+/* error codes (negative returns) */
+#define UMICLUST_OK 0
+#define UMICLUST_EINVAL (-22)   /* bad argument / parameters / argv */
+#define UMICLUST_EIO (-5)       /* file read/write failure */
+#define UMICLUST_ENOMEM (-12)   /* host or device allocation failed */
+#define UMICLUST_EDEVICE (-19)  /* no HIP device / HIP runtime error */
+#define UMICLUST_ESTATE (-77)   /* call out of order (e.g. cluster before load) */
+#define UMICLUST_ERANGE (-34)   /* a sequence exceeds the supported length (UMICLUST_MAX_LEN) */
+
+#define UMICLUST_MAX_LEN 72     /* longest sequence the kernels are compiled for */
+
+/* gap slots (vsearch --gapopen/--gapext letters): Q = gap in the query (CIGAR I, consumes the
+ * target), T = gap in the target (CIGAR D, consumes the query); L/I/R = left end, interior,
+ * right end. */
+enum { UMICLUST_QL = 0, UMICLUST_TL = 1, UMICLUST_QI = 2, UMICLUST_TI = 3, UMICLUST_QR = 4,
+       UMICLUST_TR = 5 };
+
+typedef struct umiclust_params {
+  double id;              /* --id */
+  double weak_id;         /* vsearch --weak_id (fraction); only classifies rejects */
+  int32_t minseqlength;   /* --minseqlength */
+  int32_t maxseqlength;   /* --maxseqlength */
+  int32_t wordlength;     /* --wordlength (8; the kernels require 8) */
+  int32_t minwordmatches; /* --minwordmatches (12 for wordlength 8) */
+  int32_t maxaccepts;     /* --maxaccepts (1) */
+  int32_t maxrejects;     /* --maxrejects (32) */
+  int32_t match;          /* --match */
+  int32_t mismatch;       /* --mismatch */
+  int32_t gap_open[6];    /* --gapopen, indexed by UMICLUST_QL..UMICLUST_TR */
+  int32_t gap_ext[6];     /* --gapext */
+  int32_t strand_both;    /* --strand both */
+  int32_t qmask_dust;     /* --qmask dust (vsearch default) */
+  int32_t clusterout_sort;/* --clusterout_sort */
+  int32_t clusterout_id;  /* --clusterout_id */
+  int32_t fasta_width;    /* --fasta_width (80) */
+  int32_t policy_boundary_open; /* E(i,0)/F(0,j) opened from the DP
+                                   boundary (1, default) or -inf (0) */
+} umiclust_params;
+
+/* presets */
+#define UMICLUST_PRESET_ROUND1 1          /* --gapopen 0E/40I --mismatch -40 --match 10 */
+#define UMICLUST_PRESET_VSEARCH_DEFAULT 2 /* --match 2 --mismatch -4 --gapopen 20I/2E */
+
+typedef struct umiclust_stats {
+  int64_t n_input;        /* records read */
+  int64_t n_kept;         /* records within [minseqlength, maxseqlength] */
+  int64_t n_clusters;
+  int64_t n_alignments;   /* alignments vsearch's procedure performs (GCUPS numerator set) */
+  int64_t cells;          /* sum of Lq*Lt over those alignments */
+  int64_t cells_computed; /* cells the GPU computed (incl. speculative work) */
+  int64_t kmer_postings;  /* prefilter postings touched */
+  int64_t n_blocks;       /* greedy blocks */
+  double t_total_s;       /* wall time of umiclust_cluster */
+  double t_prefilter_s;   /* kernel time, prefilter (HIP events) */
+  double t_align_s;       /* kernel time, alignment */
+  double t_consensus_s;   /* kernel time, traceback + consensus */
+  double t_host_s;        /* host greedy resolve */
+} umiclust_stats;
+
+typedef struct umiclust_ctx umiclust_ctx;
+
+/* ---- versioning / parameters ---- */
+int32_t umiclust_abi_version(void);
+/* fill p with a preset (UMICLUST_PRESET_*) and the given identity / length window */
+int32_t umiclust_params_init(umiclust_params *p, int32_t preset, double identity,
+                             int32_t minseqlength, int32_t maxseqlength);
+/* parse a vsearch argv (argv[0] may be "vsearch"); fills p and the path outputs (each
+ * buffer of pathcap bytes, may be NULL).  Unknown options -> UMICLUST_EINVAL. */
+int32_t umiclust_params_from_argv(umiclust_params *p, int32_t argc, const char *const *argv,
+                                  char *in_fasta, char *clusters_prefix, char *consout,
+                                  char *log_path, int32_t pathcap);
+
+/* ---- context ---- */
+/* device_id >= 0 selects a HIP device; there is no CPU backend (a missing device returns NULL
+ * and sets *err = UMICLUST_EDEVICE). */
+umiclust_ctx *umiclust_create(int32_t device_id, int32_t *err);
+void umiclust_destroy(umiclust_ctx *ctx);
+/* human-readable message for the last error on this context */
+const char *umiclust_last_error(const umiclust_ctx *ctx);
+
+/* ---- whole-file drop-in (vsearch CLI semantics) ---- */
+/* Reads in_fasta, clusters, writes <clusters_prefix><N> per cluster, the consout FASTA and a
+ * text log.  Any output path may be NULL. Returns number of clusters (>=0) or an error. */
+int64_t umiclust_run_fasta(umiclust_ctx *ctx, const umiclust_params *p, const char *in_fasta,
+                           const char *clusters_prefix, const char *consout, const char *log_path,
+                           umiclust_stats *stats);
+/* same, from the exact vsearch argv the reference builds (vsearch_umi_cluster.py:22-53). */
+int64_t umiclust_run_argv(umiclust_ctx *ctx, int32_t argc, const char *const *argv,
+                          umiclust_stats *stats);
+
+/* ---- session API (in-memory, inputs resident in HBM) ---- */
+/* Stage n sequences (concatenated ASCII `seqs`, record i at [offsets[i], offsets[i+1])) into
+ * device memory.  Length-filters, sorts and encodes on the device side of the boundary. */
+int32_t umiclust_load(umiclust_ctx *ctx, const umiclust_params *p, const char *seqs,
+                      const int64_t *offsets, int64_t n);
+/* Run the hot path on the loaded sequences (prefilter, alignment, greedy, consensus).
+ * Returns number of clusters. May be called repeatedly (benchmarking). */
+int64_t umiclust_cluster(umiclust_ctx *ctx, umiclust_stats *stats);
+/* Fetch results for the input records (input order):
+ *   cluster[i]  output cluster number (clusterout_sort numbering), -1 if length-filtered
+ *   strand[i]   0 '+', 1 '-' (orientation of record i relative to its centroid)
+ *   centroid[i] 1 if record i is its cluster's centroid
+ * and the consensus sequences: cluster c is cons[cons_off[c] .. cons_off[c+1]) (cons_off has
+ * n_clusters+1 entries; cons capacity cons_cap bytes). Any pointer may be NULL. */
+int64_t umiclust_fetch(umiclust_ctx *ctx, int32_t *cluster, uint8_t *strand, uint8_t *centroid,
+                       char *cons, int64_t cons_cap, int64_t *cons_off);
+
+/* ---- kernel-level entry points (parity tests) ---- */
+/* Align npairs (query, target) pairs with the production alignment kernel.  Sequences are
+ * ASCII; q/t record k at [q_off[k], q_off[k+1]).  Outputs per pair: score, matches,
+ * internal alignment length (columns minus the terminal gap runs, vsearch align_trim) and,
+ * if cigar_ops != NULL, the alignment ops ('M','D','I', alignment order) at
+ * cigar_ops[k*ops_stride ...] with their count in ops_len[k]. */
+int32_t umiclust_align_pairs(umiclust_ctx *ctx, const umiclust_params *p, const char *q,
+                             const int64_t *q_off, const char *t, const int64_t *t_off,
+                             int64_t npairs, int32_t *score, int32_t *matches,
+                             int32_t *internal_len, char *cigar_ops, int32_t ops_stride,
+                             int32_t *ops_len);
+/* DUST-mask and extract unique 8-mers of n sequences on the device (K1). masked receives the
+ * case-masked sequences (same layout as seqs); kmers[i*kstride ...] the sorted unique k-mer
+ * codes of strand s (0 '+', 1 '-') at kmers[(2*i+s)*kstride], counts in nk[2*i+s]. */
+int32_t umiclust_prep(umiclust_ctx *ctx, const umiclust_params *p, const char *seqs,
+                      const int64_t *offsets, int64_t n, char *masked, uint16_t *kmers,
+                      int32_t kstride, int32_t *nk);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1519 @@
+// driver.cpp -- host side of the MI355X UMI clustering hot path and the C ABI (include/umiclust.h).
+//
+// Replaces the `vsearch --cluster_fast` subprocess of
+// /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:21-54 (round 1) and :71-97 (round 2).
+// vsearch's greedy is sequential: query k (length-sorted) is compared with the centroids created
+// by queries 0..k-1.  This driver keeps that definition exactly while batching on the GPU:
+//
+//   for each block of B consecutive sorted queries (centroid set C_old frozen at block start):
+//     K2  prefilter every (query, strand) against C_old  -> exact top-41 list T_old
+//         and against the earlier queries of the same block -> peer list P (count >= threshold)
+//     K3W walk T_old on the device in batches of 8 (vsearch's pop loop), aligning with K3
+//     host pass 1: in sorted order, a query whose relevant peers (those that became centroids)
+//         cannot change its walk takes the device outcome; otherwise it is deferred
+//     round B: align everything a deferred query could need (T_old[0:32] and its live peers)
+//     host pass 2: exact merged walk (top-41 of T_old u P n N) for the deferred queries
+//     new centroids are appended to the index tile
+//
+// top-41 of (C_old u N) = top-41 of (top-41(C_old) u N), and a walk touches at most 32 entries,
+// so every alignment a deferred query can need exists after round B: the result is identical
+// to the sequential definition (vsearch --threads 1).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fcntl.h>
+#include <string>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <vector>
+
+#include "../../include/umiclust.h"
+#include "umiclust_internal.h"
+
+using namespace uc;
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    size_t c = count ? count : 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    if (e == hipSuccess) n = c;
+    return e;
+  }
+};
+
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    size_t c = count ? count : 1;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), c * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess) n = c;
+    return e;
+  }
+};
+
+struct Tile {
+  DevBuf<uint32_t> hist_off;  // [65536 hist][65537 off]
+  DevBuf<uint32_t> cursor;    // [65536]
+  DevBuf<uint16_t> post;
+  int32_t n = 0;              // centroids
+  int32_t base = 0;           // first centroid ordinal
+  int32_t built_n = -1;       // n at last build
+};
+
+struct Fail {
+  int code;
+};
+
+}  // namespace
+
+struct umiclust_ctx {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+
+  umiclust_params p{};
+  Scoring sc{};
+  int both = 2;
+  bool ambig = false;             // some kept sequence holds a non-ACGT (IUPAC) symbol
+  bool loaded = false;
+  bool clustered = false;
+
+  // input (host copies kept only for the file path outputs)
+  int64_t n_input = 0;
+  int32_t n = 0;                  // kept sequences
+  std::vector<int32_t> perm;      // sorted -> input index
+  std::vector<uint8_t> hlen;      // sorted lengths
+
+  // device: sequences
+  DevBuf<char> d_ascii;
+  DevBuf<int64_t> d_offs;
+  DevBuf<int32_t> d_perm;
+  DevBuf<uint32_t> d_codes;
+  DevBuf<uint8_t> d_lens;
+  DevBuf<uint16_t> d_kmers;
+  DevBuf<uint8_t> d_nk;
+  DevBuf<char> d_masked;
+  DevBuf<int32_t> d_iota;
+  // device: tables
+  DevBuf<uint8_t> d_acc;
+  DevBuf<uint16_t> d_rank;
+  std::vector<uint8_t> h_acc;
+  std::vector<uint16_t> h_rank;
+  // device: index
+  std::vector<Tile*> tiles;
+  Tile peer_tile;
+  DevBuf<TileView> d_tiles;
+  DevBuf<int32_t> d_cent;         // ordinal -> seqno
+  // device: per block
+  DevBuf<uint32_t> d_top_seqno;
+  DevBuf<uint8_t> d_top_count, d_ntop;
+  DevBuf<uint16_t> d_peer_id;
+  DevBuf<uint8_t> d_peer_count, d_npeer;
+  DevBuf<uint32_t> d_counters;    // [0] postings, [1..5] npairs per walk round
+  DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
+  DevBuf<WalkState> d_ws;
+  DevBuf<int32_t> d_sel;
+  DevBuf<uint32_t> d_g_seqno, d_g_res;
+  DevBuf<uint8_t> d_g_count;
+  DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
+  // host pinned mirrors
+  PinBuf<WalkState> h_ws;
+  PinBuf<uint8_t> h_ntop, h_npeer, h_peer_count;
+  PinBuf<uint16_t> h_peer_id;
+  PinBuf<uint32_t> h_g_seqno, h_g_res, h_bpq, h_bpt, h_bres, h_counters;
+  PinBuf<uint8_t> h_g_count;
+  PinBuf<int32_t> h_sel;
+
+  // results (sorted order)
+  std::vector<int32_t> cno;       // creation cluster number
+  std::vector<uint8_t> strand;
+  std::vector<int32_t> target;    // centroid seqno a member aligned to (-1 for centroids)
+  std::vector<int32_t> cent;      // ordinal -> seqno
+  int32_t nclusters = 0;
+  // outputs (output-cluster numbering)
+  std::vector<int32_t> rank_of;   // creation number -> output number
+  std::vector<int32_t> ostart, omemb;  // members per output cluster (centroid first)
+  std::vector<char> cons;
+  std::vector<int64_t> cons_off;
+  umiclust_stats stats{};
+  int32_t block_size = 16384;
+
+  void fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    err = buf;
+    throw Fail{code};
+  }
+  void hip(hipError_t e, const char* what) {
+    if (e != hipSuccess) fail(UMICLUST_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+  }
+};
+
+namespace {
+
+Scoring to_scoring(const umiclust_params& p) {
+  Scoring s{};
+  s.match = p.match;
+  s.mismatch = p.mismatch;
+  for (int k = 0; k < 6; k++) {
+    s.go[k] = p.gap_open[k];
+    s.ge[k] = p.gap_ext[k];
+  }
+  s.boundary_open = p.policy_boundary_open;
+  return s;
+}
+
+void validate(umiclust_ctx* c, const umiclust_params& p) {
+  if (p.wordlength != 8) c->fail(UMICLUST_EINVAL, "wordlength %d unsupported (8 required)", p.wordlength);
+  if (p.maxaccepts != 1 || p.maxrejects != 32)
+    c->fail(UMICLUST_EINVAL, "maxaccepts/maxrejects must be 1/32 (got %d/%d)", p.maxaccepts, p.maxrejects);
+  if (p.minseqlength < 1 || p.minseqlength > p.maxseqlength)
+    c->fail(UMICLUST_EINVAL, "bad length window [%d,%d]", p.minseqlength, p.maxseqlength);
+  if (!(p.id > 0.0 && p.id <= 1.0)) c->fail(UMICLUST_EINVAL, "--id must be in (0,1]");
+  if (p.minwordmatches < 0) c->fail(UMICLUST_EINVAL, "minwordmatches < 0");
+  int mx = std::abs(p.match) + std::abs(p.mismatch);
+  for (int k = 0; k < 6; k++) mx = std::max(mx, p.gap_open[k] + p.gap_ext[k]);
+  if (mx * 2 * kMaxLen > 15000) c->fail(UMICLUST_EINVAL, "scores too large for 16-bit DP");
+}
+
+// exact acceptance / id-order tables: id2 = 100.0*m/L (align_trim, iddef 2),
+// accept iff id2 >= 100.0*opt_id, both in IEEE double exactly as vsearch evaluates them.
+void build_tables(umiclust_ctx* c) {
+  const int NL = kTabL, NM = kTabM;
+  c->h_acc.assign((size_t)NL * NM, 0);
+  c->h_rank.assign((size_t)NL * NM, 0);
+  std::vector<std::pair<double, int>> v;
+  v.reserve((size_t)NL * NM);
+  const double thr = 100.0 * c->p.id;
+  for (int L = 0; L < NL; L++)
+    for (int m = 0; m < NM; m++) {
+      const double id = L > 0 ? 100.0 * m / L : 0.0;
+      c->h_acc[(size_t)L * NM + m] = (L > 0 && m <= L && id >= thr) ? 1 : 0;
+      v.push_back({id, L * NM + m});
+    }
+  std::sort(v.begin(), v.end());
+  uint16_t r = 0;
+  for (size_t i = 0; i < v.size(); i++) {
+    if (i > 0 && v[i].first != v[i - 1].first) r++;
+    c->h_rank[(size_t)v[i].second] = r;
+  }
+  c->hip(c->d_acc.ensure(c->h_acc.size()), "alloc acc");
+  c->hip(c->d_rank.ensure(c->h_rank.size()), "alloc rank");
+  c->hip(hipMemcpyAsync(c->d_acc.p, c->h_acc.data(), c->h_acc.size(), hipMemcpyHostToDevice, c->st), "acc");
+  c->hip(hipMemcpyAsync(c->d_rank.p, c->h_rank.data(), c->h_rank.size() * 2, hipMemcpyHostToDevice, c->st),
+         "rank");
+}
+
+DevSeqs dev_seqs(umiclust_ctx* c) {
+  DevSeqs s;
+  s.codes = c->d_codes.p;
+  s.lens = c->d_lens.p;
+  s.kmers = c->d_kmers.p;
+  s.nk = c->d_nk.p;
+  return s;
+}
+
+// (re)build one index tile over centroid ordinals [base, base+n) whose seqnos are cent[]
+void build_tile(umiclust_ctx* c, Tile& t, const int32_t* d_cent_seqno, int32_t first, int32_t n,
+                size_t post_cap) {
+  c->hip(t.hist_off.ensure(65536 + 65537), "tile alloc");
+  c->hip(t.cursor.ensure(65536), "tile alloc");
+  c->hip(t.post.ensure(post_cap), "tile alloc");
+  c->hip(hipMemsetAsync(t.hist_off.p, 0, 65536 * 4, c->st), "tile memset");
+  c->hip(hipMemsetAsync(t.cursor.p, 0, 65536 * 4, c->st), "tile memset");
+  c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, d_cent_seqno, first, n, t.hist_off.p, c->st),
+         "index count");
+  c->hip(launch_index_scan(t.hist_off.p, c->st), "index scan");
+  c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, d_cent_seqno, first, n, t.hist_off.p + 65536,
+                           t.cursor.p, t.post.p, c->st),
+         "index fill");
+  t.n = n;
+  t.built_n = n;
+}
+
+TileView view_of(const Tile& t) {
+  TileView v;
+  v.off = t.hist_off.p + 65536;
+  v.post = t.post.p;
+  v.n = t.n;
+  v.base = t.base;
+  return v;
+}
+
+inline unsigned long long cand_key(uint32_t count, uint32_t len, uint32_t seqno) {
+  return ((unsigned long long)(127u - count) << 56) | ((unsigned long long)len << 48) | seqno;
+}
+
+// One candidate of a merged walk.
+struct MCand {
+  unsigned long long key;
+  uint32_t seqno;
+  uint32_t res;  // alignment result (matches | internal << 8), valid if have
+  bool have;
+};
+
+// Outcome of one strand's walk.
+struct Outcome {
+  bool acc = false;
+  uint16_t rank = 0;
+  uint32_t t = 0xffffffffu;
+  int walked = 0;
+  int64_t cells = 0;
+};
+
+// vsearch search_onequery over a merged, sorted candidate list (maxaccepts 1, maxrejects 32).
+// Returns false if an alignment result is missing.
+bool merged_walk(const umiclust_ctx* c, std::vector<MCand>& L, int ql, Outcome& o) {
+  const int n = std::min<int>((int)L.size(), kTopHits);
+  int w = 0;
+  o = Outcome();
+  while (w < n && w < kWalk && !o.acc) {
+    const int b1 = std::min(std::min(n, w + kBatch), kWalk);
+    for (int x = w; x < b1; x++) {
+      if (!L[x].have) return false;
+      const uint32_t m = L[x].res & 0xffu, Li = (L[x].res >> 8) & 0xffu;
+      o.cells += (int64_t)ql * c->hlen[L[x].seqno];
+      if (c->h_acc[(size_t)Li * kTabM + m]) {
+        const uint16_t rk = c->h_rank[(size_t)Li * kTabM + m];
+        if (!o.acc || rk > o.rank || (rk == o.rank && L[x].seqno < o.t)) {
+          o.rank = rk;
+          o.t = L[x].seqno;
+        }
+        o.acc = true;
+      }
+    }
+    w = b1;
+  }
+  o.walked = w;
+  return true;
+}
+
+// search_findbest2_byid: max id, then lower target seqno, plus strand first.
+inline bool better(const Outcome& a, const Outcome& b) {
+  if (!a.acc) return false;
+  if (!b.acc) return true;
+  if (a.rank != b.rank) return a.rank > b.rank;
+  return a.t < b.t;
+}
+
+enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
+
+void ensure_block_buffers(umiclust_ctx* c, int32_t B) {
+  const size_t nqs = (size_t)B * c->both;
+  c->hip(c->d_top_seqno.ensure(nqs * kTopHits), "alloc");
+  c->hip(c->d_top_count.ensure(nqs * kTopHits), "alloc");
+  c->hip(c->d_ntop.ensure(nqs), "alloc");
+  c->hip(c->d_peer_id.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->d_peer_count.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->d_npeer.ensure(nqs), "alloc");
+  c->hip(c->d_counters.ensure(16), "alloc");
+  c->hip(c->d_pq.ensure(nqs * kBatch), "alloc");
+  c->hip(c->d_pt.ensure(nqs * kBatch), "alloc");
+  c->hip(c->d_outidx.ensure(nqs * kBatch), "alloc");
+  c->hip(c->d_res.ensure(nqs * kWalk), "alloc");
+  c->hip(c->d_ws.ensure(nqs), "alloc");
+  c->hip(c->h_ws.ensure(nqs), "pin");
+  c->hip(c->h_ntop.ensure(nqs), "pin");
+  c->hip(c->h_npeer.ensure(nqs), "pin");
+  c->hip(c->h_peer_count.ensure(nqs * kPeerCap), "pin");
+  c->hip(c->h_peer_id.ensure(nqs * kPeerCap), "pin");
+  c->hip(c->h_counters.ensure(16), "pin");
+}
+
+// Process one block [q0, q0+nq). Returns false if a peer list overflowed (caller shrinks B).
+bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& state,
+               double& t_pf, double& t_al, double& t_host) {
+  const int both = c->both;
+  const int32_t nqs = nq * both;
+  hipStream_t st = c->st;
+  // --- peer tile over the block's queries (block-local ids)
+  {
+    size_t cap = (size_t)nq * kMaxKmers + 16;
+    build_tile(c, c->peer_tile, c->d_iota.p, q0, nq, cap);
+    c->peer_tile.base = 0;
+  }
+  // --- tiles of C_old
+  std::vector<TileView> views;
+  for (Tile* t : c->tiles)
+    if (t->n > 0) views.push_back(view_of(*t));
+  c->hip(c->d_tiles.ensure(views.size() + 1), "alloc tiles");
+  if (!views.empty())
+    c->hip(hipMemcpyAsync(c->d_tiles.p, views.data(), views.size() * sizeof(TileView),
+                          hipMemcpyHostToDevice, st),
+           "tiles");
+  c->hip(hipMemsetAsync(c->d_counters.p, 0, 16 * 4, st), "memset");
+  PrefilterArgs a{};
+  a.seqs = dev_seqs(c);
+  a.tiles = c->d_tiles.p;
+  a.ntiles = (int32_t)views.size();
+  a.cent_seqno = c->d_cent.p;
+  a.q0 = q0;
+  a.nq = nq;
+  a.both = both;
+  a.minwordmatches = c->p.minwordmatches;
+  a.peer = view_of(c->peer_tile);
+  a.top_seqno = c->d_top_seqno.p;
+  a.top_count = c->d_top_count.p;
+  a.ntop = c->d_ntop.p;
+  a.peer_id = c->d_peer_id.p;
+  a.peer_count = c->d_peer_count.p;
+  a.npeer = c->d_npeer.p;
+  a.postings_touched = c->d_counters.p;
+  c->hip(hipEventRecord(c->ev0, st), "event");
+  c->hip(launch_prefilter(a, st), "prefilter");
+  c->hip(hipEventRecord(c->ev1, st), "event");
+  // --- device walk: init + up to 4 align rounds
+  hipEvent_t ea0, ea1;
+  c->hip(hipEventCreate(&ea0), "event");
+  c->hip(hipEventCreate(&ea1), "event");
+  DevSeqs ds = dev_seqs(c);
+  c->hip(launch_walk(-1, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
+                     c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
+                     c->d_outidx.p, c->d_counters.p + 1, st),
+         "walk");
+  c->hip(hipEventRecord(ea0, st), "event");
+  for (int r = 0; r < kWalk / kBatch; r++) {
+    c->hip(launch_align(ds, c->hlen[q0], c->ambig, c->d_pq.p, c->d_pt.p, nqs * kBatch,
+                        c->d_counters.p + 1 + r, c->d_outidx.p, c->sc, c->d_res.p, st),
+           "align");
+    c->hip(launch_walk(r, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
+                       c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
+                       c->d_outidx.p, c->d_counters.p + 2 + r, st),
+           "walk");
+  }
+  c->hip(hipEventRecord(ea1, st), "event");
+  // --- downloads
+  c->hip(hipMemcpyAsync(c->h_ws.p, c->d_ws.p, (size_t)nqs * sizeof(WalkState), hipMemcpyDeviceToHost, st), "d2h");
+  c->hip(hipMemcpyAsync(c->h_ntop.p, c->d_ntop.p, (size_t)nqs, hipMemcpyDeviceToHost, st), "d2h");
+  c->hip(hipMemcpyAsync(c->h_npeer.p, c->d_npeer.p, (size_t)nqs, hipMemcpyDeviceToHost, st), "d2h");
+  c->hip(hipMemcpyAsync(c->h_peer_id.p, c->d_peer_id.p, (size_t)nqs * kPeerCap * 2, hipMemcpyDeviceToHost, st),
+         "d2h");
+  c->hip(hipMemcpyAsync(c->h_peer_count.p, c->d_peer_count.p, (size_t)nqs * kPeerCap, hipMemcpyDeviceToHost, st),
+         "d2h");
+  c->hip(hipMemcpyAsync(c->h_counters.p, c->d_counters.p, 16 * 4, hipMemcpyDeviceToHost, st), "d2h");
+  c->hip(hipStreamSynchronize(st), "sync");
+  float ms = 0;
+  c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
+  t_pf += ms * 1e-3;
+  c->hip(hipEventElapsedTime(&ms, ea0, ea1), "elapsed");
+  t_al += ms * 1e-3;
+  c->stats.kmer_postings += c->h_counters.p[0];
+  // overflow?
+  for (int32_t qs = 0; qs < nqs; qs++)
+    if (c->h_npeer.p[qs] == 255) {
+      (void)hipEventDestroy(ea0);
+      (void)hipEventDestroy(ea1);
+      return false;
+    }
+  const double th0 = now_s();
+  // --- host pass 1
+  const WalkState* ws = c->h_ws.p;
+  std::vector<int32_t> deferred;
+  std::vector<int32_t> new_cents;
+  auto peer_relevant_blocked = [&](int32_t qs, int32_t qlocal, bool& blocked, bool& affects) {
+    const int np = c->h_npeer.p[qs];
+    const WalkState& w = ws[qs];
+    const bool exhausted = !w.acc && w.w < kWalk;  // walk ended because the list ran out
+    for (int x = 0; x < np; x++) {
+      const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
+      const uint8_t s = state[(size_t)q0 + pl];
+      if (s == ST_UNDET) {
+        blocked = true;
+        return;
+      }
+      if (s == ST_CENT) {
+        const uint32_t ps = (uint32_t)(q0 + pl);
+        const unsigned long long k =
+            cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps);
+        if (exhausted || w.w == 0 || k < w.lastkey) affects = true;
+      }
+    }
+    (void)qlocal;
+  };
+  for (int32_t ql = 0; ql < nq; ql++) {
+    const int32_t q = q0 + ql;
+    bool blocked = false, affects = false;
+    for (int s = 0; s < both && !blocked; s++) peer_relevant_blocked(ql * both + s, ql, blocked, affects);
+    if (blocked || affects) {
+      deferred.push_back(ql);
+      continue;
+    }
+    Outcome best;
+    int bs = 0;
+    for (int s = 0; s < both; s++) {
+      const WalkState& w = ws[ql * both + s];
+      Outcome o;
+      o.acc = w.acc;
+      o.rank = w.best_rank;
+      o.t = w.best_t;
+      o.walked = w.w;
+      o.cells = w.cells;
+      c->stats.n_alignments += w.w;
+      c->stats.cells += w.cells;
+      if (better(o, best)) {
+        best = o;
+        bs = s;
+      }
+    }
+    if (best.acc) {
+      state[q] = ST_MEMBER;
+      c->target[q] = (int32_t)best.t;
+      c->strand[q] = (uint8_t)bs;
+      c->cno[q] = c->cno[best.t];
+    } else {
+      state[q] = ST_CENT;
+      c->cno[q] = c->nclusters++;
+      new_cents.push_back(q);
+    }
+  }
+  t_host += now_s() - th0;
+  // --- round B for deferred queries (in order)
+  if (!deferred.empty()) {
+    const int32_t nd = (int32_t)deferred.size();
+    const int32_t nsel = nd * both;
+    c->hip(c->h_sel.ensure(nsel), "pin");
+    for (int32_t i = 0; i < nd; i++)
+      for (int s = 0; s < both; s++) c->h_sel.p[i * both + s] = deferred[i] * both + s;
+    c->hip(c->d_sel.ensure(nsel), "alloc");
+    c->hip(c->d_g_seqno.ensure((size_t)nsel * kWalk), "alloc");
+    c->hip(c->d_g_count.ensure((size_t)nsel * kWalk), "alloc");
+    c->hip(c->d_g_res.ensure((size_t)nsel * kWalk), "alloc");
+    c->hip(c->h_g_seqno.ensure((size_t)nsel * kWalk), "pin");
+    c->hip(c->h_g_count.ensure((size_t)nsel * kWalk), "pin");
+    c->hip(c->h_g_res.ensure((size_t)nsel * kWalk), "pin");
+    c->hip(hipMemcpyAsync(c->d_sel.p, c->h_sel.p, (size_t)nsel * 4, hipMemcpyHostToDevice, st), "h2d");
+    c->hip(launch_gather_blocked(c->d_sel.p, nsel, c->d_top_seqno.p, c->d_top_count.p, c->d_res.p,
+                                 c->d_g_seqno.p, c->d_g_count.p, c->d_g_res.p, st),
+           "gather");
+    c->hip(hipMemcpyAsync(c->h_g_seqno.p, c->d_g_seqno.p, (size_t)nsel * kWalk * 4, hipMemcpyDeviceToHost, st), "d2h");
+    c->hip(hipMemcpyAsync(c->h_g_count.p, c->d_g_count.p, (size_t)nsel * kWalk, hipMemcpyDeviceToHost, st), "d2h");
+    c->hip(hipMemcpyAsync(c->h_g_res.p, c->d_g_res.p, (size_t)nsel * kWalk * 4, hipMemcpyDeviceToHost, st), "d2h");
+    c->hip(hipStreamSynchronize(st), "sync");
+    const double th1 = now_s();
+    // pairs: T_old entries not walked + peers that are centroids or undetermined
+    std::vector<uint32_t> bpq, bpt;
+    std::vector<std::pair<int32_t, int32_t>> slot;  // (sel index, entry: <kWalk T_old, >=kWalk peer x)
+    for (int32_t i = 0; i < nsel; i++) {
+      const int32_t qs = c->h_sel.p[i];
+      const int32_t q = q0 + qs / both;
+      const uint32_t s = (uint32_t)(qs % both);
+      const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
+      for (int x = ws[qs].w; x < nt; x++) {
+        bpq.push_back(((uint32_t)q << 1) | s);
+        bpt.push_back(c->h_g_seqno.p[(size_t)i * kWalk + x]);
+        slot.push_back({i, x});
+      }
+      const int np = c->h_npeer.p[qs];
+      for (int x = 0; x < np; x++) {
+        const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
+        if (state[(size_t)q0 + pl] == ST_MEMBER) continue;
+        bpq.push_back(((uint32_t)q << 1) | s);
+        bpt.push_back((uint32_t)(q0 + pl));
+        slot.push_back({i, kWalk + x});
+      }
+    }
+    t_host += now_s() - th1;
+    const int32_t nb = (int32_t)bpq.size();
+    std::vector<uint32_t> bres(nb);
+    if (nb > 0) {
+      c->hip(c->d_bpq.ensure(nb), "alloc");
+      c->hip(c->d_bpt.ensure(nb), "alloc");
+      c->hip(c->d_bres.ensure(nb), "alloc");
+      c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
+      c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
+      c->hip(hipEventRecord(ea0, st), "event");
+      c->hip(launch_align(ds, c->hlen[q0], c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc,
+                          c->d_bres.p, st),
+             "align B");
+      for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[q0] * c->hlen[bpt[x]];
+      c->hip(hipEventRecord(ea1, st), "event");
+      c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st), "d2h");
+      c->hip(hipStreamSynchronize(st), "sync");
+      c->hip(hipEventElapsedTime(&ms, ea0, ea1), "elapsed");
+      t_al += ms * 1e-3;
+    }
+    const double th2 = now_s();
+    // peer results indexed [sel][x]
+    std::vector<uint32_t> peer_res((size_t)nsel * kPeerCap, 0);
+    std::vector<uint8_t> peer_have((size_t)nsel * kPeerCap, 0);
+    std::vector<uint32_t> tres((size_t)nsel * kWalk);
+    std::vector<uint8_t> thave((size_t)nsel * kWalk, 0);
+    for (int32_t i = 0; i < nsel; i++) {
+      const int32_t qs = c->h_sel.p[i];
+      for (int x = 0; x < ws[qs].w; x++) {
+        tres[(size_t)i * kWalk + x] = c->h_g_res.p[(size_t)i * kWalk + x];
+        thave[(size_t)i * kWalk + x] = 1;
+      }
+    }
+    for (int32_t k = 0; k < nb; k++) {
+      const int32_t i = slot[k].first, x = slot[k].second;
+      if (x < kWalk) {
+        tres[(size_t)i * kWalk + x] = bres[k];
+        thave[(size_t)i * kWalk + x] = 1;
+      } else {
+        peer_res[(size_t)i * kPeerCap + (x - kWalk)] = bres[k];
+        peer_have[(size_t)i * kPeerCap + (x - kWalk)] = 1;
+      }
+    }
+    // --- pass 2: exact merged walks in order
+    std::vector<MCand> L;
+    for (int32_t di = 0; di < nd; di++) {
+      const int32_t qlc = deferred[di];
+      const int32_t q = q0 + qlc;
+      Outcome best;
+      int bs = 0;
+      for (int s = 0; s < both; s++) {
+        const int32_t i = di * both + s;
+        const int32_t qs = qlc * both + s;
+        L.clear();
+        const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
+        for (int x = 0; x < nt; x++) {
+          const uint32_t sq = c->h_g_seqno.p[(size_t)i * kWalk + x];
+          L.push_back({cand_key(c->h_g_count.p[(size_t)i * kWalk + x], c->hlen[sq], sq), sq,
+                       tres[(size_t)i * kWalk + x], thave[(size_t)i * kWalk + x] != 0});
+        }
+        const int np = c->h_npeer.p[qs];
+        for (int x = 0; x < np; x++) {
+          const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
+          if (state[(size_t)q0 + pl] != ST_CENT) continue;
+          const uint32_t ps = (uint32_t)(q0 + pl);
+          L.push_back({cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps), ps,
+                       peer_res[(size_t)i * kPeerCap + x], peer_have[(size_t)i * kPeerCap + x] != 0});
+        }
+        std::sort(L.begin(), L.end(), [](const MCand& a, const MCand& b) { return a.key < b.key; });
+        Outcome o;
+        if (!merged_walk(c, L, c->hlen[q], o))
+          c->fail(UMICLUST_EDEVICE, "internal: missing alignment in merged walk (q=%d)", q);
+        c->stats.n_alignments += o.walked;
+        c->stats.cells += o.cells;
+        if (better(o, best)) {
+          best = o;
+          bs = s;
+        }
+      }
+      if (best.acc) {
+        state[q] = ST_MEMBER;
+        c->target[q] = (int32_t)best.t;
+        c->strand[q] = (uint8_t)bs;
+        c->cno[q] = c->cno[best.t];
+      } else {
+        state[q] = ST_CENT;
+        c->cno[q] = c->nclusters++;
+        new_cents.push_back(q);
+      }
+    }
+    t_host += now_s() - th2;
+    std::sort(new_cents.begin(), new_cents.end());
+  }
+  (void)hipEventDestroy(ea0);
+  (void)hipEventDestroy(ea1);
+  // --- append new centroids to the index
+  if (!new_cents.empty()) {
+    const int32_t ord0 = (int32_t)c->cent.size();
+    for (int32_t q : new_cents) c->cent.push_back(q);
+    c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4,
+                          hipMemcpyHostToDevice, st),
+           "h2d cent");
+    int32_t ord = ord0;
+    const int32_t ordend = (int32_t)c->cent.size();
+    while (ord < ordend) {
+      Tile* t = c->tiles.empty() ? nullptr : c->tiles.back();
+      if (!t || t->n >= kTile) {
+        t = new Tile();
+        t->base = ord;
+        t->n = 0;
+        c->tiles.push_back(t);
+      }
+      const int32_t take = std::min(ordend - ord, kTile - t->n);
+      const int32_t newn = t->n + take;
+      build_tile(c, *t, c->d_cent.p, t->base, newn, (size_t)kTile * kMaxKmers);
+      ord += take;
+    }
+  }
+  return true;
+}
+
+void cluster_all(umiclust_ctx* c) {
+  const double t0 = now_s();
+  const int32_t n = c->n;
+  c->cno.assign(n, -1);
+  c->strand.assign(n, 0);
+  c->target.assign(n, -1);
+  c->cent.clear();
+  c->nclusters = 0;
+  for (Tile* t : c->tiles) delete t;
+  c->tiles.clear();
+  c->stats = umiclust_stats{};
+  c->stats.n_input = c->n_input;
+  c->stats.n_kept = n;
+  c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
+  std::vector<uint8_t> state(n, ST_UNDET);
+  double t_pf = 0, t_al = 0, t_host = 0;
+  int32_t B = std::min<int32_t>(c->block_size, kTile);
+  ensure_block_buffers(c, B);
+  int32_t q0 = 0;
+  while (q0 < n) {
+    // a block holds one query length (the aligner is compiled per query length)
+    int32_t same = 1;
+    while (q0 + same < n && same < B && c->hlen[q0 + same] == c->hlen[q0]) same++;
+    const int32_t nq = same;
+    if (!run_block(c, q0, nq, state, t_pf, t_al, t_host)) {
+      if (nq == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
+      B = std::max(1, nq / 2);
+      continue;
+    }
+    c->stats.n_blocks++;
+    q0 += nq;
+    if (B < c->block_size) B = std::min<int32_t>(B * 2, c->block_size);
+  }
+  // --- output numbering: --clusterout_sort orders clusters by size desc, creation order
+  const int32_t K = c->nclusters;
+  std::vector<int32_t> size(K, 0);
+  for (int32_t s = 0; s < n; s++) size[c->cno[s]]++;
+  std::vector<int32_t> order(K);
+  for (int32_t k = 0; k < K; k++) order[k] = k;
+  if (c->p.clusterout_sort)
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return size[a] > size[b]; });
+  c->rank_of.assign(K, 0);
+  for (int32_t k = 0; k < K; k++) c->rank_of[order[k]] = k;
+  c->ostart.assign((size_t)K + 1, 0);
+  for (int32_t s = 0; s < n; s++) c->ostart[c->rank_of[c->cno[s]] + 1]++;
+  for (int32_t k = 0; k < K; k++) c->ostart[k + 1] += c->ostart[k];
+  c->omemb.assign(n, 0);
+  {
+    std::vector<int32_t> fill(c->ostart.begin(), c->ostart.end() - 1);
+    for (int32_t s = 0; s < n; s++) c->omemb[fill[c->rank_of[c->cno[s]]]++] = s;
+  }
+  // --- traceback for members, then consensus
+  double t_cons = 0;
+  {
+    std::vector<uint32_t> mpq, mpt;
+    std::vector<int32_t> opsidx(n, -1);
+    for (int32_t s = 0; s < n; s++)
+      if (c->target[s] >= 0) {
+        opsidx[s] = (int32_t)mpq.size();
+        mpq.push_back(((uint32_t)s << 1) | c->strand[s]);
+        mpt.push_back((uint32_t)c->target[s]);
+      }
+    const int32_t nm = (int32_t)mpq.size();
+    DevBuf<uint32_t> d_mpq, d_mpt, d_mout, d_dir;
+    DevBuf<uint8_t> d_ops, d_mstrand;
+    DevBuf<uint16_t> d_nops, d_conslen;
+    DevBuf<int32_t> d_cstart, d_mseq, d_mops, d_over;
+    DevBuf<char> d_cons;
+    c->hip(d_mpq.ensure(nm), "alloc");
+    c->hip(d_mpt.ensure(nm), "alloc");
+    c->hip(d_mout.ensure(nm), "alloc");
+    c->hip(d_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
+    c->hip(d_nops.ensure(nm), "alloc");
+    const int32_t chunk = 1 << 18;
+    c->hip(d_dir.ensure((size_t)chunk * kMaxLen * kCodeWords), "alloc");
+    if (nm > 0) {
+      c->hip(hipMemcpyAsync(d_mpq.p, mpq.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(d_mpt.p, mpt.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    }
+    hipEvent_t e0, e1;
+    c->hip(hipEventCreate(&e0), "event");
+    c->hip(hipEventCreate(&e1), "event");
+    c->hip(hipEventRecord(e0, c->st), "event");
+    DevSeqs ds = dev_seqs(c);
+    // members are in sorted (length-descending) order: one launch per query length and chunk
+    for (int32_t b = 0; b < nm;) {
+      const int32_t ql = c->hlen[mpq[b] >> 1];
+      int32_t e = b + 1;
+      while (e < nm && e - b < chunk && c->hlen[mpq[e] >> 1] == ql) e++;
+      c->hip(launch_traceback(ds, ql, d_mpq.p + b, d_mpt.p + b, e - b, c->sc, d_dir.p,
+                              d_ops.p + (size_t)b * kOpsStride, d_nops.p + b, d_mout.p + b, c->st),
+             "traceback");
+      b = e;
+    }
+    // consensus inputs in output-cluster order
+    std::vector<int32_t> mseq(n), mops(n);
+    std::vector<uint8_t> mstr(n);
+    for (int32_t x = 0; x < n; x++) {
+      const int32_t s = c->omemb[x];
+      mseq[x] = s;
+      mops[x] = opsidx[s];
+      mstr[x] = c->strand[s];
+    }
+    c->hip(d_cstart.ensure((size_t)K + 1), "alloc");
+    c->hip(d_mseq.ensure(n), "alloc");
+    c->hip(d_mops.ensure(n), "alloc");
+    c->hip(d_mstrand.ensure(n), "alloc");
+    c->hip(d_cons.ensure((size_t)std::max(K, 1) * kConsCap), "alloc");
+    c->hip(d_conslen.ensure((size_t)std::max(K, 1)), "alloc");
+    c->hip(d_over.ensure(1), "alloc");
+    c->hip(hipMemsetAsync(d_over.p, 0, 4, c->st), "memset");
+    c->hip(hipMemcpyAsync(d_cstart.p, c->ostart.data(), ((size_t)K + 1) * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    if (n > 0) {
+      c->hip(hipMemcpyAsync(d_mseq.p, mseq.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(d_mops.p, mops.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(d_mstrand.p, mstr.data(), (size_t)n, hipMemcpyHostToDevice, c->st), "h2d");
+    }
+    c->hip(launch_consensus(ds, d_cstart.p, K, d_mseq.p, d_mops.p, d_mstrand.p, d_ops.p, d_nops.p,
+                            d_cons.p, d_conslen.p, d_over.p, c->st),
+           "consensus");
+    c->hip(hipEventRecord(e1, c->st), "event");
+    std::vector<uint16_t> clen(K);
+    std::vector<char> craw((size_t)K * kConsCap);
+    int32_t over = 0;
+    if (K > 0) {
+      c->hip(hipMemcpyAsync(clen.data(), d_conslen.p, (size_t)K * 2, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(craw.data(), d_cons.p, (size_t)K * kConsCap, hipMemcpyDeviceToHost, c->st), "d2h");
+    }
+    c->hip(hipMemcpyAsync(&over, d_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    float ms = 0;
+    c->hip(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+    t_cons = ms * 1e-3;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (over) c->fail(UMICLUST_ERANGE, "consensus: %d clusters exceed the MSA column budget", over);
+    c->cons_off.assign((size_t)K + 1, 0);
+    for (int32_t k = 0; k < K; k++) c->cons_off[k + 1] = c->cons_off[k] + clen[k];
+    c->cons.resize((size_t)c->cons_off[K]);
+    for (int32_t k = 0; k < K; k++)
+      memcpy(c->cons.data() + c->cons_off[k], craw.data() + (size_t)k * kConsCap, clen[k]);
+  }
+  c->stats.n_clusters = K;
+  c->stats.t_prefilter_s = t_pf;
+  c->stats.t_align_s = t_al;
+  c->stats.t_consensus_s = t_cons;
+  c->stats.t_host_s = t_host;
+  c->stats.t_total_s = now_s() - t0;
+  c->clustered = true;
+}
+
+// ---------------------------------------------------------------- load
+void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs, int64_t n) {
+  if (!p || (!seqs && n > 0) || !offs || n < 0) c->fail(UMICLUST_EINVAL, "null argument");
+  validate(c, *p);
+  c->p = *p;
+  c->sc = to_scoring(*p);
+  c->both = p->strand_both ? 2 : 1;
+  build_tables(c);
+  c->n_input = n;
+  // length filter + stable sort by length desc (db_sortbylength; ties keep input order, O1)
+  const int64_t maxlen = std::min<int64_t>(p->maxseqlength, kMaxLen);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t L = offs[i + 1] - offs[i];
+    if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
+  }
+  std::vector<int64_t> cnt(kMaxLen + 2, 0);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t L = offs[i + 1] - offs[i];
+    if (L >= p->minseqlength && L <= maxlen) cnt[kMaxLen - L]++;
+  }
+  int64_t acc = 0;
+  for (int L = 0; L <= kMaxLen; L++) {
+    const int64_t t = cnt[L];
+    cnt[L] = acc;
+    acc += t;
+  }
+  if (acc > (int64_t)INT32_MAX / 2) c->fail(UMICLUST_ERANGE, "too many sequences in one bin");
+  c->n = (int32_t)acc;
+  c->perm.assign(c->n, 0);
+  c->hlen.assign(c->n, 0);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t L = offs[i + 1] - offs[i];
+    if (L >= p->minseqlength && L <= maxlen) {
+      const int64_t s = cnt[kMaxLen - L]++;
+      c->perm[s] = (int32_t)i;
+      c->hlen[s] = (uint8_t)L;
+    }
+  }
+  const int64_t bytes = n > 0 ? offs[n] - offs[0] : 0;
+  c->hip(c->d_ascii.ensure((size_t)bytes + 1), "alloc ascii");
+  c->hip(c->d_offs.ensure((size_t)n + 1), "alloc offs");
+  c->hip(c->d_perm.ensure((size_t)c->n + 1), "alloc perm");
+  std::vector<int64_t> rel((size_t)n + 1);
+  for (int64_t i = 0; i <= n; i++) rel[i] = offs[i] - offs[0];
+  if (bytes > 0)
+    c->hip(hipMemcpyAsync(c->d_ascii.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(c->d_offs.p, rel.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  if (c->n > 0)
+    c->hip(hipMemcpyAsync(c->d_perm.p, c->perm.data(), (size_t)c->n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+  const size_t ns = (size_t)c->n + 1;
+  c->hip(c->d_codes.ensure(ns * 2 * kCodeWords), "alloc");
+  c->hip(c->d_lens.ensure(ns), "alloc");
+  c->hip(c->d_kmers.ensure(ns * 2 * kKmerStride), "alloc");
+  c->hip(c->d_nk.ensure(ns * 2), "alloc");
+  c->hip(c->d_masked.ensure(ns * kMaxLen), "alloc");
+  c->hip(c->d_iota.ensure(ns), "alloc");
+  std::vector<int32_t> iota(ns);
+  for (size_t i = 0; i < ns; i++) iota[i] = (int32_t)i;
+  c->hip(hipMemcpyAsync(c->d_iota.p, iota.data(), ns * 4, hipMemcpyHostToDevice, c->st), "h2d");
+  DevBuf<uint32_t> d_amb;
+  c->hip(d_amb.ensure(1), "alloc");
+  c->hip(hipMemsetAsync(d_amb.p, 0, 4, c->st), "memset");
+  c->hip(launch_prep(c->d_ascii.p, c->d_offs.p, c->d_perm.p, c->n, p->qmask_dust, c->d_codes.p,
+                     c->d_lens.p, c->d_kmers.p, c->d_nk.p, c->d_masked.p, d_amb.p, c->st),
+         "prep");
+  uint32_t amb = 0;
+  c->hip(hipMemcpyAsync(&amb, d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+  c->hip(hipStreamSynchronize(c->st), "sync load");
+  c->ambig = amb != 0;
+  for (int32_t s = 0; s < c->n; s++)
+    if (c->hlen[s] < kMinTplLen) c->fail(UMICLUST_ERANGE, "sequence shorter than %d (minseqlength)", kMinTplLen);
+  c->loaded = true;
+  c->clustered = false;
+}
+
+// ---------------------------------------------------------------- FASTA I/O
+struct Fasta {
+  std::vector<char> raw;          // file contents
+  std::vector<int64_t> hdr_off;   // label start (after '>')
+  std::vector<int32_t> hdr_len;   // label length (truncated at whitespace)
+  std::vector<char> seq;          // concatenated sequences
+  std::vector<int64_t> seq_off;   // n+1
+};
+
+bool read_fasta(const char* path, Fasta& f) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return false;
+  }
+  f.raw.resize((size_t)sb.st_size + 1);
+  size_t got = 0;
+  while (got < (size_t)sb.st_size) {
+    ssize_t r = read(fd, f.raw.data() + got, (size_t)sb.st_size - got);
+    if (r <= 0) {
+      close(fd);
+      return false;
+    }
+    got += (size_t)r;
+  }
+  close(fd);
+  f.raw[got] = '\n';
+  const char* d = f.raw.data();
+  const size_t N = got;
+  f.seq.reserve(N / 8);
+  f.seq_off.push_back(0);
+  size_t i = 0;
+  bool in = false;
+  while (i < N) {
+    if (d[i] == '>') {
+      if (in) f.seq_off.push_back((int64_t)f.seq.size());
+      size_t j = i + 1;
+      size_t e = j;
+      while (e < N && d[e] != '\n' && d[e] != '\r' && d[e] != ' ' && d[e] != '\t') e++;
+      f.hdr_off.push_back((int64_t)j);
+      f.hdr_len.push_back((int32_t)(e - j));
+      while (e < N && d[e] != '\n') e++;
+      i = e + 1;
+      in = true;
+    } else {
+      size_t e = i;
+      while (e < N && d[e] != '\n') e++;
+      if (in)
+        for (size_t k = i; k < e; k++) {
+          const char ch = d[k];
+          if ((ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z')) f.seq.push_back(ch);
+        }
+      i = e + 1;
+    }
+  }
+  if (in) f.seq_off.push_back((int64_t)f.seq.size());
+  return true;
+}
+
+void put_wrapped(std::string& out, const char* s, int64_t len, int width) {
+  if (width <= 0) {
+    out.append(s, (size_t)len);
+    out.push_back('\n');
+    return;
+  }
+  if (len == 0) out.push_back('\n');
+  for (int64_t i = 0; i < len; i += width) {
+    out.append(s + i, (size_t)std::min<int64_t>(width, len - i));
+    out.push_back('\n');
+  }
+}
+
+bool write_file(const std::string& path, const std::string& data) {
+  FILE* fp = fopen(path.c_str(), "wb");
+  if (!fp) return false;
+  bool ok = fwrite(data.data(), 1, data.size(), fp) == data.size();
+  ok = (fclose(fp) == 0) && ok;
+  return ok;
+}
+
+int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
+                       const char* clusters_prefix, const char* consout, const char* log_path,
+                       umiclust_stats* stats) {
+  const double t0 = now_s();
+  Fasta f;
+  if (!in_fasta || !read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
+  const int64_t n = (int64_t)f.hdr_off.size();
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t L = f.seq_off[i + 1] - f.seq_off[i];
+    if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
+  }
+  const double t_read = now_s() - t0;
+  load_impl(c, p, f.seq.data(), f.seq_off.data(), n);
+  cluster_all(c);
+  const double t1 = now_s();
+  // masked sequences (vsearch prints the DUST-masked db sequence)
+  std::vector<char> masked((size_t)c->n * kMaxLen);
+  if (c->n > 0)
+    c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
+  const int32_t K = c->nclusters;
+  const int width = p->fasta_width;
+  if (consout) {
+    std::string out;
+    out.reserve((size_t)K * 256);
+    for (int32_t k = 0; k < K; k++) {
+      const int32_t cs = c->omemb[c->ostart[k]];
+      const int32_t ci = c->perm[cs];
+      out += ">centroid=";
+      out.append(f.raw.data() + f.hdr_off[ci], (size_t)f.hdr_len[ci]);
+      out += ";seqs=" + std::to_string(c->ostart[k + 1] - c->ostart[k]);
+      if (p->clusterout_id) out += ";clusterid=" + std::to_string(k);
+      out.push_back('\n');
+      put_wrapped(out, c->cons.data() + c->cons_off[k], c->cons_off[k + 1] - c->cons_off[k], width);
+    }
+    if (!write_file(consout, out)) c->fail(UMICLUST_EIO, "cannot write %s", consout);
+  }
+  if (clusters_prefix) {
+    std::string fn, out;
+    for (int32_t k = 0; k < K; k++) {
+      out.clear();
+      for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {
+        const int32_t s = c->omemb[x];
+        const int32_t i = c->perm[s];
+        out.push_back('>');
+        out.append(f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]);
+        out.push_back('\n');
+        put_wrapped(out, masked.data() + (size_t)s * kMaxLen, c->hlen[s], width);
+      }
+      fn = clusters_prefix;
+      fn += std::to_string(k);
+      if (!write_file(fn, out)) c->fail(UMICLUST_EIO, "cannot write %s", fn.c_str());
+    }
+  }
+  const double t_write = now_s() - t1;
+  if (log_path) {
+    const umiclust_stats& s = c->stats;
+    int64_t nt = 0, singles = 0;
+    int32_t smin = 0, smax = 0;
+    for (int32_t x = 0; x < c->n; x++) nt += c->hlen[x];
+    for (int32_t k = 0; k < K; k++) {
+      const int32_t sz = c->ostart[k + 1] - c->ostart[k];
+      singles += sz == 1;
+      smin = k ? std::min(smin, sz) : sz;
+      smax = std::max(smax, sz);
+    }
+    char buf[2048];
+    snprintf(buf, sizeof(buf),
+             "umiclust-mi355x (vsearch --cluster_fast drop-in, ABI %d)\n"
+             "Reading file %s\n"
+             "%lld nt in %lld seqs, min %d, max %d, avg %.0f\n"
+             "%lld sequences discarded by the length window [%d, %d]\n"
+             "Masking (dust), sorting by length, clustering (id %.4f, strand %s)\n"
+             "Clusters: %d Size min %d, max %d, avg %.1f\n"
+             "Singletons: %lld, %.1f%% of seqs, %.1f%% of clusters\n"
+             "Alignments: %lld, cells: %lld, k-mer postings: %lld, blocks: %lld\n"
+             "Time: read %.3f s, cluster %.3f s (prefilter %.3f, align %.3f, consensus %.3f, host %.3f), write %.3f s\n",
+             UMICLUST_ABI_VERSION, in_fasta, (long long)nt, (long long)c->n,
+             c->n ? (int)c->hlen[c->n - 1] : 0, c->n ? (int)c->hlen[0] : 0, c->n ? (double)nt / c->n : 0.0,
+             (long long)(n - c->n), p->minseqlength, p->maxseqlength, p->id, p->strand_both ? "both" : "plus",
+             K, smin, smax, K ? (double)c->n / K : 0.0, (long long)singles,
+             c->n ? 100.0 * singles / c->n : 0.0, K ? 100.0 * singles / K : 0.0,
+             (long long)s.n_alignments, (long long)s.cells, (long long)s.kmer_postings, (long long)s.n_blocks,
+             t_read, s.t_total_s, s.t_prefilter_s, s.t_align_s, s.t_consensus_s, s.t_host_s, t_write);
+    if (!write_file(log_path, buf)) c->fail(UMICLUST_EIO, "cannot write %s", log_path);
+  }
+  if (stats) *stats = c->stats;
+  return K;
+}
+
+// ---------------------------------------------------------------- argv
+// vsearch --gapopen/--gapext strings: "/"-separated tokens "<int>[QT][ILRE]*"
+// (no letter = all positions; E = both ends; Q/T restrict to query/target gaps).
+bool parse_gap(const char* s, int32_t* dst) {
+  const char* p = s;
+  while (*p) {
+    char* e = nullptr;
+    long v = strtol(p, &e, 10);
+    if (e == p) return false;
+    p = e;
+    bool q = false, t = false, I = false, L = false, R = false;
+    while (*p && *p != '/') {
+      switch (*p) {
+        case 'Q': q = true; break;
+        case 'T': t = true; break;
+        case 'I': I = true; break;
+        case 'E': L = R = true; break;
+        case 'L': L = true; break;
+        case 'R': R = true; break;
+        default: return false;
+      }
+      p++;
+    }
+    if (!q && !t) q = t = true;
+    if (!I && !L && !R) I = L = R = true;
+    if (q) {
+      if (L) dst[UMICLUST_QL] = (int32_t)v;
+      if (I) dst[UMICLUST_QI] = (int32_t)v;
+      if (R) dst[UMICLUST_QR] = (int32_t)v;
+    }
+    if (t) {
+      if (L) dst[UMICLUST_TL] = (int32_t)v;
+      if (I) dst[UMICLUST_TI] = (int32_t)v;
+      if (R) dst[UMICLUST_TR] = (int32_t)v;
+    }
+    if (*p == '/') p++;
+  }
+  return true;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int32_t umiclust_abi_version(void) { return UMICLUST_ABI_VERSION; }
+
+int32_t umiclust_params_init(umiclust_params* p, int32_t preset, double identity, int32_t minlen,
+                             int32_t maxlen) {
+  if (!p) return UMICLUST_EINVAL;
+  memset(p, 0, sizeof(*p));
+  p->id = identity;
+  p->weak_id = identity < 0.10 ? identity : 0.10;
+  p->minseqlength = minlen;
+  p->maxseqlength = maxlen;
+  p->wordlength = 8;
+  p->minwordmatches = 12;
+  p->maxaccepts = 1;
+  p->maxrejects = 32;
+  p->strand_both = 1;
+  p->qmask_dust = 1;
+  p->clusterout_sort = 1;
+  p->clusterout_id = 1;
+  p->fasta_width = 80;
+  p->policy_boundary_open = 1;
+  for (int k = 0; k < 6; k++) p->gap_ext[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 2 : 1;
+  if (preset == UMICLUST_PRESET_ROUND1) {
+    p->match = 10;
+    p->mismatch = -40;
+    for (int k = 0; k < 6; k++) p->gap_open[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 40 : 0;
+  } else if (preset == UMICLUST_PRESET_VSEARCH_DEFAULT) {
+    p->match = 2;
+    p->mismatch = -4;
+    for (int k = 0; k < 6; k++) p->gap_open[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 20 : 2;
+  } else {
+    return UMICLUST_EINVAL;
+  }
+  return UMICLUST_OK;
+}
+
+int32_t umiclust_params_from_argv(umiclust_params* p, int32_t argc, const char* const* argv,
+                                  char* in_fasta, char* clusters_prefix, char* consout,
+                                  char* log_path, int32_t pathcap) {
+  if (!p || argc < 0 || (argc > 0 && !argv)) return UMICLUST_EINVAL;
+  umiclust_params_init(p, UMICLUST_PRESET_VSEARCH_DEFAULT, 0.97, 32, 50000);
+  p->clusterout_sort = 0;
+  p->clusterout_id = 0;
+  p->strand_both = 0;
+  p->maxseqlength = 50000;
+  bool have_in = false;
+  auto put = [&](char* dst, const char* v) -> bool {
+    if (!dst) return true;
+    if ((int32_t)strlen(v) + 1 > pathcap) return false;
+    strcpy(dst, v);
+    return true;
+  };
+  if (in_fasta) in_fasta[0] = 0;
+  if (clusters_prefix) clusters_prefix[0] = 0;
+  if (consout) consout[0] = 0;
+  if (log_path) log_path[0] = 0;
+  int i = 0;
+  if (argc > 0 && argv[0] && argv[0][0] != '-') i = 1;  // program name
+  for (; i < argc; i++) {
+    const char* a = argv[i];
+    auto val = [&]() -> const char* { return (i + 1 < argc) ? argv[++i] : nullptr; };
+    if (!strcmp(a, "--clusterout_id")) p->clusterout_id = 1;
+    else if (!strcmp(a, "--clusterout_sort")) p->clusterout_sort = 1;
+    else if (!strcmp(a, "--quiet") || !strcmp(a, "--no_progress")) {}
+    else if (!strcmp(a, "--clusters")) { const char* v = val(); if (!v || !put(clusters_prefix, v)) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--consout")) { const char* v = val(); if (!v || !put(consout, v)) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--log")) { const char* v = val(); if (!v || !put(log_path, v)) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--cluster_fast")) { const char* v = val(); if (!v || !put(in_fasta, v)) return UMICLUST_EINVAL; have_in = true; }
+    else if (!strcmp(a, "--minseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->minseqlength = atoi(v); }
+    else if (!strcmp(a, "--maxseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxseqlength = atoi(v); }
+    else if (!strcmp(a, "--threads")) { if (!val()) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--strand")) {
+      const char* v = val();
+      if (!v) return UMICLUST_EINVAL;
+      if (!strcmp(v, "both")) p->strand_both = 1;
+      else if (!strcmp(v, "plus")) p->strand_both = 0;
+      else return UMICLUST_EINVAL;
+    }
+    else if (!strcmp(a, "--gapopen")) { const char* v = val(); if (!v || !parse_gap(v, p->gap_open)) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--gapext")) { const char* v = val(); if (!v || !parse_gap(v, p->gap_ext)) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--match")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->match = atoi(v); }
+    else if (!strcmp(a, "--mismatch")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->mismatch = atoi(v); }
+    else if (!strcmp(a, "--id")) {
+      const char* v = val();
+      if (!v) return UMICLUST_EINVAL;
+      p->id = atof(v);
+      p->weak_id = p->id < 0.10 ? p->id : 0.10;
+    }
+    else if (!strcmp(a, "--qmask")) {
+      const char* v = val();
+      if (!v) return UMICLUST_EINVAL;
+      if (!strcmp(v, "dust")) p->qmask_dust = 1;
+      else if (!strcmp(v, "none")) p->qmask_dust = 0;
+      else return UMICLUST_EINVAL;
+    }
+    else if (!strcmp(a, "--wordlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->wordlength = atoi(v); }
+    else if (!strcmp(a, "--minwordmatches")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->minwordmatches = atoi(v); }
+    else if (!strcmp(a, "--maxaccepts")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxaccepts = atoi(v); }
+    else if (!strcmp(a, "--maxrejects")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxrejects = atoi(v); }
+    else if (!strcmp(a, "--fasta_width")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->fasta_width = atoi(v); }
+    else return UMICLUST_EINVAL;
+  }
+  if (!have_in) return UMICLUST_EINVAL;
+  return UMICLUST_OK;
+}
+
+umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device_id < 0 || device_id >= ndev) {
+    if (err) *err = UMICLUST_EDEVICE;
+    return nullptr;
+  }
+  umiclust_ctx* c = new (std::nothrow) umiclust_ctx();
+  if (!c) {
+    if (err) *err = UMICLUST_ENOMEM;
+    return nullptr;
+  }
+  c->dev = device_id;
+  if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    if (err) *err = UMICLUST_EDEVICE;
+    return nullptr;
+  }
+  if (const char* b = getenv("UMICLUST_BLOCK")) c->block_size = std::max(1, std::min(kTile, atoi(b)));
+  if (err) *err = UMICLUST_OK;
+  return c;
+}
+
+void umiclust_destroy(umiclust_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  for (Tile* t : c->tiles) delete t;
+  c->tiles.clear();
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->st) (void)hipStreamDestroy(c->st);
+  delete c;
+}
+
+const char* umiclust_last_error(const umiclust_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+#define UC_GUARD(c, ...)                                \
+  do {                                                  \
+    if (!(c)) return UMICLUST_EINVAL;                   \
+    try {                                               \
+      (void)hipSetDevice((c)->dev);                     \
+      __VA_ARGS__                                       \
+    } catch (const Fail& f__) {                         \
+      return f__.code;                                  \
+    } catch (const std::bad_alloc&) {                   \
+      (c)->err = "host allocation failed";              \
+      return UMICLUST_ENOMEM;                           \
+    } catch (...) {                                     \
+      (c)->err = "unexpected exception";                \
+      return UMICLUST_EDEVICE;                          \
+    }                                                   \
+  } while (0)
+
+int64_t umiclust_run_fasta(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
+                           const char* clusters_prefix, const char* consout, const char* log_path,
+                           umiclust_stats* stats) {
+  UC_GUARD(c, {
+    if (!p) c->fail(UMICLUST_EINVAL, "null params");
+    return run_fasta_impl(c, p, in_fasta, clusters_prefix, consout, log_path, stats);
+  });
+}
+
+int64_t umiclust_run_argv(umiclust_ctx* c, int32_t argc, const char* const* argv, umiclust_stats* stats) {
+  UC_GUARD(c, {
+    umiclust_params p;
+    std::vector<char> in(4096), cl(4096), co(4096), lg(4096);
+    int32_t rc = umiclust_params_from_argv(&p, argc, argv, in.data(), cl.data(), co.data(), lg.data(), 4096);
+    if (rc != UMICLUST_OK) c->fail(rc, "cannot parse vsearch argv");
+    return run_fasta_impl(c, &p, in.data(), cl[0] ? cl.data() : nullptr, co[0] ? co.data() : nullptr,
+                          lg[0] ? lg.data() : nullptr, stats);
+  });
+}
+
+int32_t umiclust_load(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs,
+                      int64_t n) {
+  UC_GUARD(c, {
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t L = offs[i + 1] - offs[i];
+      if (p && L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
+    }
+    load_impl(c, p, seqs, offs, n);
+    return UMICLUST_OK;
+  });
+}
+
+int64_t umiclust_cluster(umiclust_ctx* c, umiclust_stats* stats) {
+  UC_GUARD(c, {
+    if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster before umiclust_load");
+    cluster_all(c);
+    if (stats) *stats = c->stats;
+    return c->nclusters;
+  });
+}
+
+int64_t umiclust_fetch(umiclust_ctx* c, int32_t* cluster, uint8_t* strand, uint8_t* centroid, char* cons,
+                       int64_t cons_cap, int64_t* cons_off) {
+  UC_GUARD(c, {
+    if (!c->clustered) c->fail(UMICLUST_ESTATE, "umiclust_fetch before umiclust_cluster");
+    const int64_t n = c->n_input;
+    if (cluster)
+      for (int64_t i = 0; i < n; i++) cluster[i] = -1;
+    if (strand) memset(strand, 0, (size_t)n);
+    if (centroid) memset(centroid, 0, (size_t)n);
+    for (int32_t s = 0; s < c->n; s++) {
+      const int32_t i = c->perm[s];
+      if (cluster) cluster[i] = c->rank_of[c->cno[s]];
+      if (strand) strand[i] = c->strand[s];
+      if (centroid) centroid[i] = c->target[s] < 0 ? 1 : 0;
+    }
+    const int32_t K = c->nclusters;
+    if (cons_off)
+      for (int32_t k = 0; k <= K; k++) cons_off[k] = c->cons_off[k];
+    if (cons) {
+      if ((int64_t)c->cons.size() > cons_cap) c->fail(UMICLUST_EINVAL, "consensus buffer too small");
+      memcpy(cons, c->cons.data(), c->cons.size());
+    }
+    return K;
+  });
+}
+
+int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const char* q, const int64_t* q_off,
+                             const char* t, const int64_t* t_off, int64_t npairs, int32_t* score,
+                             int32_t* matches, int32_t* internal_len, char* cigar_ops, int32_t ops_stride,
+                             int32_t* ops_len) {
+  UC_GUARD(c, {
+    if (!p || npairs < 0 || (npairs > 0 && (!q || !q_off || !t || !t_off))) c->fail(UMICLUST_EINVAL, "null argument");
+    umiclust_params pp = *p;
+    pp.minseqlength = 1;
+    pp.maxseqlength = kMaxLen;
+    validate(c, pp);
+    // load queries then targets as one sequence set without filtering/sorting
+    std::vector<char> all;
+    std::vector<int64_t> off;
+    off.push_back(0);
+    for (int64_t k = 0; k < npairs; k++) {
+      all.insert(all.end(), q + q_off[k], q + q_off[k + 1]);
+      off.push_back((int64_t)all.size());
+    }
+    for (int64_t k = 0; k < npairs; k++) {
+      all.insert(all.end(), t + t_off[k], t + t_off[k + 1]);
+      off.push_back((int64_t)all.size());
+    }
+    const int64_t ns = 2 * npairs;
+    for (int64_t i = 0; i < ns; i++)
+      if (off[i + 1] - off[i] < 1 || off[i + 1] - off[i] > kMaxLen) c->fail(UMICLUST_ERANGE, "pair sequence length");
+    Scoring sc = to_scoring(pp);
+    DevBuf<char> d_a;
+    DevBuf<int64_t> d_o;
+    DevBuf<uint32_t> d_codes, d_pq, d_pt, d_out, d_dir;
+    DevBuf<uint8_t> d_lens, d_nk, d_ops;
+    DevBuf<uint16_t> d_km, d_nops;
+    c->hip(d_a.ensure(all.size() + 1), "alloc");
+    c->hip(d_o.ensure(off.size()), "alloc");
+    c->hip(d_codes.ensure((size_t)ns * 2 * kCodeWords + 1), "alloc");
+    c->hip(d_lens.ensure((size_t)ns + 1), "alloc");
+    c->hip(d_km.ensure((size_t)ns * 2 * kKmerStride + 1), "alloc");
+    c->hip(d_nk.ensure((size_t)ns * 2 + 1), "alloc");
+    if (!all.empty()) c->hip(hipMemcpy(d_a.p, all.data(), all.size(), hipMemcpyHostToDevice), "h2d");
+    c->hip(hipMemcpy(d_o.p, off.data(), off.size() * 8, hipMemcpyHostToDevice), "h2d");
+    DevBuf<uint32_t> d_amb;
+    c->hip(d_amb.ensure(1), "alloc");
+    c->hip(hipMemsetAsync(d_amb.p, 0, 4, c->st), "memset");
+    c->hip(launch_prep(d_a.p, d_o.p, nullptr, (int32_t)ns, 0, d_codes.p, d_lens.p, d_km.p, d_nk.p, nullptr,
+                       d_amb.p, c->st),
+           "prep");
+    uint32_t amb = 0;
+    c->hip(hipMemcpyAsync(&amb, d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    // pairs grouped by query length (the aligner is compiled per query length)
+    std::vector<int64_t> ord(npairs);
+    for (int64_t k = 0; k < npairs; k++) {
+      ord[k] = k;
+      const int64_t ql = off[k + 1] - off[k];
+      if (ql < kMinTplLen) c->fail(UMICLUST_ERANGE, "query shorter than %d", kMinTplLen);
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+      return (off[a + 1] - off[a]) < (off[b + 1] - off[b]);
+    });
+    std::vector<uint32_t> pq(npairs), pt(npairs);
+    for (int64_t x = 0; x < npairs; x++) {
+      pq[x] = (uint32_t)ord[x] << 1;
+      pt[x] = (uint32_t)(npairs + ord[x]);
+    }
+    c->hip(d_pq.ensure(npairs + 1), "alloc");
+    c->hip(d_pt.ensure(npairs + 1), "alloc");
+    c->hip(d_out.ensure(npairs + 1), "alloc");
+    if (npairs > 0) {
+      c->hip(hipMemcpyAsync(d_pq.p, pq.data(), npairs * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(d_pt.p, pt.data(), npairs * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    }
+    DevSeqs ds{d_codes.p, d_lens.p, d_km.p, d_nk.p};
+    std::vector<uint32_t> sres(npairs);
+    std::vector<uint8_t> ops;
+    std::vector<uint16_t> nops;
+    if (cigar_ops) {
+      if (ops_stride < kOpsStride) c->fail(UMICLUST_EINVAL, "ops_stride < %d", kOpsStride);
+      c->hip(d_ops.ensure((size_t)npairs * kOpsStride + 1), "alloc");
+      c->hip(d_nops.ensure(npairs + 1), "alloc");
+      c->hip(d_dir.ensure((size_t)npairs * kMaxLen * kCodeWords + 1), "alloc");
+    }
+    for (int64_t b0 = 0; b0 < npairs;) {
+      const int32_t ql = (int32_t)(off[ord[b0] + 1] - off[ord[b0]]);
+      int64_t e = b0 + 1;
+      while (e < npairs && off[ord[e] + 1] - off[ord[e]] == ql) e++;
+      if (cigar_ops)
+        c->hip(launch_traceback(ds, ql, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), sc, d_dir.p,
+                                d_ops.p + (size_t)b0 * kOpsStride, d_nops.p + b0, d_out.p + b0, c->st),
+               "traceback");
+      else
+        c->hip(launch_align(ds, ql, amb != 0, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), nullptr, nullptr, sc,
+                            d_out.p + b0, c->st),
+               "align");
+      b0 = e;
+    }
+    if (npairs > 0)
+      c->hip(hipMemcpyAsync(sres.data(), d_out.p, (size_t)npairs * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    if (cigar_ops) {
+      ops.resize((size_t)npairs * kOpsStride);
+      nops.resize(npairs);
+      c->hip(hipMemcpyAsync(ops.data(), d_ops.p, ops.size(), hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(nops.data(), d_nops.p, (size_t)npairs * 2, hipMemcpyDeviceToHost, c->st), "d2h");
+    }
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    std::vector<uint32_t> res(npairs);
+    for (int64_t x = 0; x < npairs; x++) {
+      const int64_t k = ord[x];
+      res[k] = sres[x];
+      if (cigar_ops) {
+        const int n = nops[x];
+        memcpy(cigar_ops + (size_t)k * ops_stride, ops.data() + (size_t)x * kOpsStride + kOpsStride - n, (size_t)n);
+        if (ops_len) ops_len[k] = n;
+      }
+    }
+    for (int64_t k = 0; k < npairs; k++) {
+      if (matches) matches[k] = (int32_t)(res[k] & 0xffu);
+      if (internal_len) internal_len[k] = (int32_t)((res[k] >> 8) & 0xffu);
+      if (score) score[k] = (int32_t)(int16_t)(res[k] >> 16);
+    }
+    return UMICLUST_OK;
+  });
+}
+
+int32_t umiclust_prep(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offsets,
+                      int64_t n, char* masked, uint16_t* kmers, int32_t kstride, int32_t* nk) {
+  UC_GUARD(c, {
+    if (!p || n < 0 || (n > 0 && (!seqs || !offsets))) c->fail(UMICLUST_EINVAL, "null argument");
+    for (int64_t i = 0; i < n; i++)
+      if (offsets[i + 1] - offsets[i] > kMaxLen) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
+    DevBuf<char> d_a, d_m;
+    DevBuf<int64_t> d_o;
+    DevBuf<uint32_t> d_codes;
+    DevBuf<uint8_t> d_lens, d_nk;
+    DevBuf<uint16_t> d_km;
+    const int64_t bytes = n > 0 ? offsets[n] - offsets[0] : 0;
+    std::vector<int64_t> rel((size_t)n + 1);
+    for (int64_t i = 0; i <= n; i++) rel[i] = offsets[i] - offsets[0];
+    c->hip(d_a.ensure((size_t)bytes + 1), "alloc");
+    c->hip(d_o.ensure((size_t)n + 1), "alloc");
+    c->hip(d_codes.ensure((size_t)n * 2 * kCodeWords + 1), "alloc");
+    c->hip(d_lens.ensure((size_t)n + 1), "alloc");
+    c->hip(d_nk.ensure((size_t)n * 2 + 1), "alloc");
+    c->hip(d_km.ensure((size_t)n * 2 * kKmerStride + 1), "alloc");
+    c->hip(d_m.ensure((size_t)n * kMaxLen + 1), "alloc");
+    if (bytes > 0) c->hip(hipMemcpy(d_a.p, seqs + offsets[0], (size_t)bytes, hipMemcpyHostToDevice), "h2d");
+    c->hip(hipMemcpy(d_o.p, rel.data(), rel.size() * 8, hipMemcpyHostToDevice), "h2d");
+    c->hip(launch_prep(d_a.p, d_o.p, nullptr, (int32_t)n, p->qmask_dust, d_codes.p, d_lens.p, d_km.p, d_nk.p, d_m.p,
+                       nullptr, c->st),
+           "prep");
+    std::vector<char> m((size_t)n * kMaxLen);
+    std::vector<uint16_t> km((size_t)n * 2 * kKmerStride);
+    std::vector<uint8_t> nkv((size_t)n * 2);
+    if (n > 0) {
+      c->hip(hipMemcpyAsync(m.data(), d_m.p, m.size(), hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(km.data(), d_km.p, km.size() * 2, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(nkv.data(), d_nk.p, nkv.size(), hipMemcpyDeviceToHost, c->st), "d2h");
+    }
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t L = offsets[i + 1] - offsets[i];
+      if (masked) memcpy(masked + (offsets[i] - offsets[0]), m.data() + (size_t)i * kMaxLen, (size_t)L);
+      for (int s = 0; s < 2; s++) {
+        if (nk) nk[2 * i + s] = nkv[(size_t)2 * i + s];
+        if (kmers)
+          for (int x = 0; x < nkv[(size_t)2 * i + s] && x < kstride; x++)
+            kmers[(size_t)(2 * i + s) * kstride + x] = km[(size_t)(2 * i + s) * kKmerStride + x];
+      }
+    }
+    return UMICLUST_OK;
+  });
+}
+
+}  // extern "C"

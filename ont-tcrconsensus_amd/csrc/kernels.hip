@@ -1,0 +1,1076 @@
+// kernels.hip -- MI355X (gfx950) kernels of the UMI clustering hot path.
+//
+// The reference delegates this arithmetic to vsearch (`--cluster_fast`, invoked at
+// /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:21-54 and :71-97).  Kernels:
+//   K1 k_prep        DUST soft-mask (vsearch mask.cc) + unique 8-mers both strands (unique.cc)
+//   KI k_index_*     CSR inverted index tile over centroid k-mers (dbindex.cc analogue)
+//   K2 k_prefilter   shared-unique-k-mer counting against every centroid + top-41 selection
+//                    (searchcore.cc search_topscores / minheap.cc order), LDS u8 counters
+//   K3 k_align       Gotoh global alignment, one alignment per lane, with the vsearch
+//                    traceback's path statistics carried FORWARD through the DP so that no
+//                    direction matrix is stored (align_simd.cc search16/backtrack16 + align_trim)
+//   K3T k_traceback  same DP with a 4-bit direction matrix in HBM + explicit traceback, for
+//                    the one chosen hit per member (the CIGAR feeding the consensus)
+//   K4 k_consensus   star MSA + column majority vote per cluster (msa.cc)
+// All integer/byte work: VALU + LDS, no MFMA (not a dense contraction).
+#include <hip/hip_runtime.h>
+
+#include "umiclust_internal.h"
+
+namespace uc {
+
+// ------------------------------------------------------------------ character maps
+// 4-bit IUPAC code (vsearch chrmap_4bit): A1 C2 G4 T/U8, ambiguity codes OR-ed, N15.
+__constant__ uint8_t c_map4[256];
+
+static uint8_t h_map4[256];
+static bool h_maps_init = false;
+
+static void host_maps() {
+  if (h_maps_init) return;
+  const char* iupac = "ACGTURYSWKMBDHVN";
+  const uint8_t v4[] = {1, 2, 4, 8, 8, 5, 10, 6, 9, 12, 3, 14, 13, 11, 7, 15};
+  for (int i = 0; i < 256; i++) h_map4[i] = 0;
+  for (int i = 0; iupac[i]; i++) {
+    h_map4[(uint8_t)iupac[i]] = v4[i];
+    h_map4[(uint8_t)(iupac[i] | 0x20)] = v4[i];
+  }
+  h_maps_init = true;
+}
+
+static hipError_t ensure_maps(hipStream_t st) {
+  host_maps();
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_map4), h_map4, 256, 0, hipMemcpyHostToDevice, st);
+}
+
+__device__ __forceinline__ uint32_t code2_of4(uint32_t c4) {
+  // chrmap_2bit: A0 C1 G2 T3, anything else 0
+  return c4 == 2 ? 1u : (c4 == 4 ? 2u : (c4 == 8 ? 3u : 0u));
+}
+__device__ __forceinline__ uint32_t comp4(uint32_t c4) {
+  // complement of an IUPAC bitmask = nibble bit reversal (A<->T, C<->G, R<->Y, ...)
+  return ((c4 & 1u) << 3) | ((c4 & 2u) << 1) | ((c4 & 4u) >> 1) | ((c4 & 8u) >> 3);
+}
+
+// ------------------------------------------------------------------ K1: prep
+// One thread per (sorted) sequence.  LDS scratch per thread: residues, DUST words/counts and
+// the k-mer sort buffer (runtime-indexed arrays must not live in VGPRs).
+constexpr int kPrepThreads = 64;
+struct PrepScratch {
+  uint8_t ch[kMaxLen];     // original characters
+  uint8_t words[64];
+  uint8_t counts[64];
+  uint16_t km[kMaxKmers + 3];
+};
+
+__device__ int dust_wo(const uint8_t* s2, int len, int* beg, int* end, uint8_t* words,
+                       uint8_t* counts) {
+  // vsearch mask.cc wo(): smallest region is 8 => l1 = len - 3 + 1 - 5
+  int l1 = len - 3 + 1 - 5;
+  if (l1 < 0) {
+    *beg = 0;
+    *end = len - 1;
+    return 0;
+  }
+  int w = 0;
+  for (int j = 0; j < len; j++) {
+    w = ((w << 2) | s2[j]) & 63;
+    words[j] = (uint8_t)w;
+  }
+  int bestv = 0, besti = 0, bestj = 0;
+  for (int i = 0; i < l1; i++) {
+    for (int x = 0; x < 64; x++) counts[x] = 0;
+    int sum = 0;
+    for (int j = 2; j < len - i; j++) {
+      int x = words[i + j];
+      int c = counts[x];
+      if (c) {
+        sum += c;
+        // v = 10*sum/j (integer); v > bestv  <=>  10*sum >= (bestv+1)*j
+        if (10 * sum >= (bestv + 1) * j) {
+          bestv = (10 * sum) / j;
+          besti = i;
+          bestj = j;
+        }
+      }
+      counts[x] = (uint8_t)(c + 1);
+    }
+  }
+  *beg = besti;
+  *end = besti + bestj;
+  return bestv;
+}
+
+__global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ ascii,
+                                                       const int64_t* __restrict__ offs,
+                                                       const int32_t* __restrict__ perm, int32_t n,
+                                                       int dust, uint32_t* __restrict__ codes,
+                                                       uint8_t* __restrict__ lens,
+                                                       uint16_t* __restrict__ kmers,
+                                                       uint8_t* __restrict__ nk,
+                                                       char* __restrict__ masked,
+                                                       uint32_t* __restrict__ ambig) {
+  __shared__ PrepScratch scr[kPrepThreads];
+  int s = blockIdx.x * kPrepThreads + threadIdx.x;
+  if (s >= n) return;
+  PrepScratch& P = scr[threadIdx.x];
+  int r = perm ? perm[s] : s;
+  int64_t b = offs[r];
+  int len = (int)(offs[r + 1] - b);
+  for (int x = 0; x < len; x++) P.ch[x] = (uint8_t)ascii[b + x];
+  // lower-case mask bits (bit x set = masked), 3 words
+  uint32_t mk0 = 0, mk1 = 0, mk2 = 0;
+  if (dust) {
+    // dust(): the whole sequence upper-cased, masked intervals lower-cased
+    uint8_t* codes2 = reinterpret_cast<uint8_t*>(P.km);  // >= 72 bytes available (136)
+    for (int x = 0; x < len; x++) codes2[x] = (uint8_t)code2_of4(c_map4[P.ch[x]]);
+    for (int i = 0; i < len; i += 32) {
+      int l = (len > i + 64) ? 64 : len - i;
+      int a = 0, e = 0;
+      int v = dust_wo(codes2 + i, l, &a, &e, P.words, P.counts);
+      if (v > 20) {
+        for (int j = a + i; j <= e + i; j++) {
+          if (j < 32) mk0 |= 1u << j;
+          else if (j < 64) mk1 |= 1u << (j - 32);
+          else mk2 |= 1u << (j - 64);
+        }
+      }
+    }
+  }
+  auto masked_at = [&](int x) -> uint32_t {
+    return x < 32 ? (mk0 >> x) & 1u : (x < 64 ? (mk1 >> (x - 32)) & 1u : (mk2 >> (x - 64)) & 1u);
+  };
+  lens[s] = (uint8_t)len;
+  // masked ASCII (what vsearch prints) and 4-bit codes for both strands
+  uint32_t w0[kCodeWords], w1[kCodeWords];
+#pragma unroll
+  for (int w = 0; w < kCodeWords; w++) { w0[w] = 0; w1[w] = 0; }
+  for (int x = 0; x < len; x++) {
+    uint8_t c = P.ch[x];
+    uint8_t up = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+    if (dust) c = masked_at(x) ? (uint8_t)(up | 0x20) : up;
+    if (masked) masked[(int64_t)s * kMaxLen + x] = (char)c;
+    P.ch[x] = c;
+  }
+  uint32_t any_amb = 0;
+  for (int x = 0; x < len; x++) {
+    uint32_t c4 = c_map4[P.ch[x]];
+    any_amb |= (c4 != 1u && c4 != 2u && c4 != 4u && c4 != 8u) ? 1u : 0u;
+    int xr = len - 1 - x;
+#pragma unroll
+    for (int w = 0; w < kCodeWords; w++) {
+      if ((x >> 3) == w) w0[w] |= c4 << ((x & 7) * 4);
+      if ((xr >> 3) == w) w1[w] |= comp4(c4) << ((xr & 7) * 4);
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < kCodeWords; w++) {
+    codes[((int64_t)s * 2 + 0) * kCodeWords + w] = w0[w];
+    codes[((int64_t)s * 2 + 1) * kCodeWords + w] = w1[w];
+  }
+  if (any_amb && ambig) atomicOr(ambig, 1u);
+  // unique 8-mers per strand, masked windows skipped (unique.cc), sorted ascending
+  for (int st = 0; st < 2; st++) {
+    uint32_t km = 0, bad = 0;
+    int cnt = 0;
+    for (int y = 0; y < len; y++) {
+      int x = st ? len - 1 - y : y;
+      uint32_t c4 = c_map4[P.ch[x]];
+      if (st) c4 = comp4(c4);
+      bad = ((bad << 1) | masked_at(x)) & 0xffu;
+      km = ((km << 2) | code2_of4(c4)) & 0xffffu;
+      if (y >= 7 && !bad) {
+        // insertion into sorted unique list
+        int pos = cnt;
+        bool dup = false;
+        while (pos > 0 && P.km[pos - 1] >= km) {
+          if (P.km[pos - 1] == km) { dup = true; break; }
+          pos--;
+        }
+        if (!dup) {
+          for (int z = cnt; z > pos; z--) P.km[z] = P.km[z - 1];
+          P.km[pos] = (uint16_t)km;
+          cnt++;
+        }
+      }
+    }
+    uint16_t* dst = kmers + ((int64_t)s * 2 + st) * kKmerStride;
+    for (int z = 0; z < cnt; z++) dst[z] = P.km[z];
+    nk[(int64_t)s * 2 + st] = (uint8_t)cnt;
+  }
+}
+
+hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
+                       int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
+                       char* masked, uint32_t* ambig, hipStream_t st) {
+  hipError_t e = ensure_maps(st);
+  if (e != hipSuccess) return e;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prep, dim3((n + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0, st,
+                     ascii, offs, perm, n, dust, codes, lens, kmers, nk, masked, ambig);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ KI: index tile build
+__global__ void k_index_count(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
+                              const int32_t* __restrict__ cent_seqno, int32_t first, int32_t count,
+                              uint32_t* __restrict__ hist) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= count) return;
+  int32_t s = cent_seqno[first + c];
+  int n = nk[(int64_t)s * 2];
+  const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
+  for (int x = 0; x < n; x++) atomicAdd(&hist[k[x]], 1u);
+}
+
+__global__ __launch_bounds__(1024) void k_index_scan(const uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ off) {
+  // exclusive scan of 65536 counters, one workgroup: 64 per thread
+  __shared__ uint32_t part[1024];
+  int t = threadIdx.x;
+  uint32_t loc[64];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int x = 0; x < 64; x++) {
+    loc[x] = sum;
+    sum += hist[t * 64 + x];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    uint32_t v = (t >= d) ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t base = part[t] - sum;
+#pragma unroll
+  for (int x = 0; x < 64; x++) off[t * 64 + x] = base + loc[x];
+  if (t == 1023) off[65536] = part[1023];
+}
+
+__global__ void k_index_fill(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
+                             const int32_t* __restrict__ cent_seqno, int32_t first, int32_t count,
+                             const uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                             uint16_t* __restrict__ post) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= count) return;
+  int32_t s = cent_seqno[first + c];
+  int n = nk[(int64_t)s * 2];
+  const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
+  for (int x = 0; x < n; x++) {
+    uint32_t pos = off[k[x]] + atomicAdd(&cursor[k[x]], 1u);
+    post[pos] = (uint16_t)c;
+  }
+}
+
+hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
+                              int32_t first, int32_t count, uint32_t* hist, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_index_count, dim3((count + 255) / 256), dim3(256), 0, st, kmers, nk,
+                     cent_seqno, first, count, hist);
+  return hipGetLastError();
+}
+hipError_t launch_index_scan(uint32_t* hist_to_off, hipStream_t st) {
+  // hist_to_off: [65536] histogram followed by [65537] offsets
+  hipLaunchKernelGGL(k_index_scan, dim3(1), dim3(1024), 0, st, hist_to_off, hist_to_off + 65536);
+  return hipGetLastError();
+}
+hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
+                             int32_t first, int32_t count, const uint32_t* off, uint32_t* cursor,
+                             uint16_t* post, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_index_fill, dim3((count + 255) / 256), dim3(256), 0, st, kmers, nk,
+                     cent_seqno, first, count, off, cursor, post);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K2: prefilter
+// One workgroup per (query, strand).  Per index tile: u8 counters (4 per u32) for up to 65536
+// centroids in 64 KiB of LDS; every posting of every query k-mer is one ds_add_rtn_u32; the
+// posting that lifts a counter to the threshold min(12, #kmers) appends the centroid to an LDS
+// candidate list.  After the tile, candidates get 30-bit keys (count desc, length asc, id asc),
+// are bitonic-sorted and merged into the running top-41 (u64 keys over all tiles).  A threshold
+// of 0, or more crossers than the buffer holds, switches the tile to a chunked full scan, so the
+// result is exact in every case.
+constexpr int kPfThreads = 256;
+
+struct PfShared {
+  uint32_t cnt[kTile / 4];        // 64 KiB packed u8 counters
+  uint32_t cand[kCandCap];        // candidate local ids, then 30-bit keys
+  unsigned long long top[kTopHits];
+  unsigned long long merged[kTopHits];
+  uint16_t km[kMaxKmers + 3];
+  uint32_t ncand;
+  uint32_t overflow;
+  int32_t ntop;
+  uint32_t post_local;
+};
+
+__device__ __forceinline__ uint32_t cnt_get(const uint32_t* cnt, uint32_t c) {
+  return (cnt[c >> 2] >> ((c & 3) * 8)) & 0xffu;
+}
+
+// bitonic sort of n (power of two) u32 keys in LDS, ascending
+__device__ void bitonic_u32(uint32_t* a, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int l = i ^ j;
+        if (l > i) {
+          uint32_t x = a[i], y = a[l];
+          bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
+  PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
+  const int tid = threadIdx.x;
+  const int qs = blockIdx.x;
+  const int qlocal = qs / a.both;
+  const int strand = qs % a.both;
+  const int32_t q = a.q0 + qlocal;
+  const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
+  const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
+  const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
+  for (int x = tid; x < nk; x += kPfThreads) S.km[x] = qk[x];
+  if (tid == 0) {
+    S.ntop = 0;
+    S.post_local = 0;
+  }
+  __syncthreads();
+  int npeer = 0;
+  for (int t = 0; t <= a.ntiles; t++) {
+    const bool peer = (t == a.ntiles);
+    TileView tv;
+    if (peer) tv = a.peer;
+    else tv = a.tiles[t];
+    if (tv.n == 0) continue;
+    const int nwords = (tv.n + 3) >> 2;
+    for (int x = tid; x < nwords; x += kPfThreads) S.cnt[x] = 0;
+    if (tid == 0) {
+      S.ncand = 0;
+      S.overflow = 0;
+    }
+    __syncthreads();
+    if (thr > 0) {
+      uint32_t touched = 0;
+      for (int k = 0; k < nk; k++) {
+        const uint32_t beg = tv.off[S.km[k]], end = tv.off[S.km[k] + 1];
+        touched += end - beg;
+        for (uint32_t x = beg + tid; x < end; x += kPfThreads) {
+          const uint32_t c = tv.post[x];
+          const uint32_t sh = (c & 3) * 8;
+          const uint32_t old = atomicAdd(&S.cnt[c >> 2], 1u << sh);
+          if (((old >> sh) & 0xffu) + 1 == (uint32_t)thr) {
+            const uint32_t slot = atomicAdd(&S.ncand, 1u);
+            if (slot < (uint32_t)kCandCap) S.cand[slot] = c;
+            else S.overflow = 1;
+          }
+        }
+      }
+      if (tid == 0) S.post_local += touched;
+    }
+    __syncthreads();
+    const bool scan_mode = (thr == 0) || S.overflow;
+    // chunks: either the crosser list (one chunk) or the whole tile in kCandCap slices
+    const int nchunks = scan_mode ? (tv.n + kCandCap - 1) / kCandCap : 1;
+    for (int ch = 0; ch < nchunks; ch++) {
+      int nc;
+      if (scan_mode) {
+        __syncthreads();
+        if (tid == 0) S.ncand = 0;
+        __syncthreads();
+        const int c0 = ch * kCandCap;
+        const int c1 = min(tv.n, c0 + kCandCap);
+        for (int c = c0 + tid; c < c1; c += kPfThreads)
+          if ((int)cnt_get(S.cnt, (uint32_t)c) >= thr) S.cand[atomicAdd(&S.ncand, 1u)] = (uint32_t)c;
+        __syncthreads();
+      }
+      nc = (int)min(S.ncand, (uint32_t)kCandCap);
+      // keys: (127-count) << 23 | len << 16 | local id   (30 bits)
+      for (int x = tid; x < nc; x += kPfThreads) {
+        const uint32_t c = S.cand[x];
+        const uint32_t cntv = cnt_get(S.cnt, c);
+        const int32_t sq = peer ? (a.q0 + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
+        uint32_t key = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
+        if (peer && (int)c >= qlocal) key = 0xffffffffu;  // only earlier queries of the block
+        S.cand[x] = key;
+      }
+      int np2 = 1;
+      while (np2 < nc) np2 <<= 1;
+      for (int x = nc + tid; x < np2; x += kPfThreads) S.cand[x] = 0xffffffffu;
+      __syncthreads();
+      if (np2 > 1) bitonic_u32(S.cand, np2);
+      if (peer) {
+        if (tid == 0) {
+          for (int x = 0; x < nc; x++) {
+            const uint32_t key = S.cand[x];
+            if (key == 0xffffffffu) break;
+            if (npeer < kPeerCap) {
+              a.peer_id[(int64_t)qs * kPeerCap + npeer] = (uint16_t)(key & 0xffffu);
+              a.peer_count[(int64_t)qs * kPeerCap + npeer] = (uint8_t)(127u - (key >> 23));
+            }
+            npeer++;
+          }
+        }
+      } else if (tid == 0) {
+        // merge sorted S.cand[0..nc) into running top (u64: (127-count)<<56 | len<<48 | seqno)
+        int i = 0, j = 0, o = 0;
+        const int ntop = S.ntop;
+        while (o < kTopHits && (i < ntop || j < nc)) {
+          unsigned long long kj = ~0ull;
+          if (j < nc) {
+            const uint32_t key = S.cand[j];
+            const uint32_t c = key & 0xffffu;
+            kj = ((unsigned long long)(key >> 23) << 56) |
+                 ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
+                 (unsigned long long)(uint32_t)a.cent_seqno[tv.base + (int32_t)c];
+          }
+          const unsigned long long ki = (i < ntop) ? S.top[i] : ~0ull;
+          if (ki <= kj) { S.merged[o++] = ki; i++; }
+          else { S.merged[o++] = kj; j++; }
+        }
+        for (int x = 0; x < o; x++) S.top[x] = S.merged[x];
+        S.ntop = o;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    const int ntop = S.ntop;
+    for (int x = 0; x < ntop; x++) {
+      a.top_seqno[(int64_t)qs * kTopHits + x] = (uint32_t)(S.top[x] & 0xffffffffull);
+      a.top_count[(int64_t)qs * kTopHits + x] = (uint8_t)(127u - (uint32_t)(S.top[x] >> 56));
+    }
+    a.ntop[qs] = (uint8_t)ntop;
+    a.npeer[qs] = (uint8_t)(npeer > kPeerCap ? 255 : npeer);
+    if (a.postings_touched) atomicAdd(a.postings_touched, S.post_local);
+  }
+}
+
+hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
+  const int nqs = a.nq * a.both;
+  if (nqs <= 0) return hipSuccess;
+  const size_t smem = sizeof(PfShared);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_prefilter,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_prefilter, dim3(nqs), dim3(kPfThreads), smem, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K3: alignment (stats)
+__device__ __forceinline__ int sx16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
+__device__ __forceinline__ uint32_t pack_hf(int h, int f) {
+  return ((uint32_t)f << 16) | ((uint32_t)h & 0xffffu);
+}
+
+constexpr int kNegInf = -16000;  // below any reachable score (|score| <= 72*40 + gaps)
+
+// Query rows are unrolled: QL is a compile-time constant (the driver cuts greedy blocks at length
+// changes, so every pair of a launch has the same query length) and the per-row state lives in
+// VGPRs with compile-time indices.  Target columns run as a runtime loop (lanes may have different
+// target lengths); the target's last column takes the target-right gap penalties (one select per
+// column, shared by all rows).
+//
+// Forward-carried traceback (no direction matrix).  vsearch's acceptance needs, along the path
+// backtrack16 picks, the matches m and internal_len = columns - leading gap run - trailing gap run
+// (align_trim).  For every real DP cell the leading CIGAR run is exactly the boundary run (row -1
+// or column -1) the path starts with, so columns - leading run = the number of moves INTO real
+// cells, a.  Each DP state carries the summary a | m << 8 of the path the traceback would follow
+// from it (boundary states carry 0), selected with backtrack16's strict priorities
+// (diagonal > up/D > left/I; a gap extends only if strictly better than reopening).
+// The trailing gap run is backtrack16's first run from the end cell (last row, last column):
+//  * an I run walks left along the last row; with Lext(j) = run length when arriving at column j in
+//    an I run: Lh(j) = left(j) ? 1 + Lext(j-1) : 0, Lext(j) = extleft(j) ? 1 + Lext(j-1) : Lh(j);
+//  * a D run walks up the last column: the F state's summary carries the length of its trailing D
+//    run in bits 16-23 (opening from H inherits H's run, so consecutive D runs merge exactly as
+//    CIGAR runs do); H inherits it only when it takes F.
+// Per row: HE[i] = H(i, j-1) | E(i, j) << 16 and SS[i] = S_H(i, j-1) | S_E(i, j) << 16, 16 bits each.
+template <int QL, bool AMB>
+__device__ __forceinline__ void align_column(uint32_t (&HE)[QL], uint32_t (&SS)[QL],
+                                             const uint32_t (&qw)[(QL + 7) / 8], uint32_t tcode,
+                                             int j, const Scoring& sc, int QRt, int Rt, int& Lext,
+                                             int& trail) {
+  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
+  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  const bool tamb = AMB && ((tcode & (tcode - 1u)) != 0u || tcode == 0u);
+  // row -1 of this column: H(-1, j-1) (diagonal of row 0) and F(0, j); boundary summaries are 0
+  int Hd = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
+  uint32_t SHd = 0;
+  int F = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - QRt : kNegInf;
+  uint32_t SF = 0x10001u;  // one real D move, trailing D run 1
+#pragma unroll
+  for (int i = 0; i < QL; i++) {
+    const uint32_t qcode = (qw[i >> 3] >> ((i & 7) * 4)) & 15u;
+    int sub;
+    uint32_t e;
+    if (AMB) {
+      // IUPAC: any ambiguous symbol scores 0; a match is a non-empty code intersection
+      const bool amb = tamb || (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+      sub = amb ? 0 : (qcode == tcode ? sc.match : sc.mismatch);
+      e = (qcode & tcode) ? (1u << 8) : 0u;
+    } else {
+      const bool eq = qcode == tcode;
+      sub = eq ? sc.match : sc.mismatch;
+      e = eq ? (1u << 8) : 0u;
+    }
+    const uint32_t he = HE[i];
+    const uint32_t ss = SS[i];
+    const int Hl = sx16(he);
+    const int E = (int)he >> 16;
+    const uint32_t SE = ss >> 16;
+    int h = Hd + sub;
+    uint32_t sh = SHd + 1u + e;
+    const bool fb = F > h;  // up: D chosen
+    h = fb ? F : h;
+    sh = fb ? SF : sh;
+    const bool eb = E > h;  // left: I chosen
+    h = eb ? E : h;
+    sh = eb ? SE : sh;
+    const int fo = h - QRt, fe = F - Rt;
+    const bool fx = fe > fo;  // extup
+    SF = (fx ? SF : sh) + 0x10001u;
+    const int qrq = (i == QL - 1) ? QRqr : QRqi;
+    const int rq = (i == QL - 1) ? Rqr : Rqi;
+    const int eo = h - qrq, ee = E - rq;
+    const bool ex = ee > eo;  // extleft
+    const uint32_t sen = (ex ? SE : sh) + 1u;
+    if (i == QL - 1) {
+      // last row: I-run counters; the value left by the last column is the end cell's
+      const int lh = eb ? 1 + Lext : 0;
+      Lext = ex ? 1 + Lext : lh;
+      trail = eb ? lh : (int)(sh >> 16);
+    }
+    F = fx ? fe : fo;
+    Hd = Hl;
+    SHd = ss & 0xffffu;
+    // materialise the next row's diagonal now: otherwise SDWA folding reads the old packed words
+    // in row i+1, both generations stay live and every column ends in a 2*QL-register copy
+    asm volatile("" : "+v"(Hd), "+v"(SHd));
+    HE[i] = pack_hf(h, ex ? ee : eo);
+    SS[i] = (sh & 0xffffu) | (sen << 16);
+  }
+}
+
+template <int QL, bool AMB>
+__global__ __launch_bounds__(64) void k_align(DevSeqs s, const uint32_t* __restrict__ pq,
+                                              const uint32_t* __restrict__ pt, int32_t npairs,
+                                              const uint32_t* __restrict__ dev_npairs,
+                                              const uint32_t* __restrict__ outidx, Scoring sc,
+                                              uint32_t* __restrict__ out) {
+  constexpr int CW = (QL + 7) / 8;
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= npairs) return;
+  if (dev_npairs && k >= (int)*dev_npairs) return;
+  const uint32_t qv = pq[k];
+  const int32_t q = (int32_t)(qv >> 1);
+  const int qstr = (int)(qv & 1u);
+  const int32_t t = (int32_t)pt[k];
+  const int tl = s.lens[t];
+  uint32_t qw[CW];
+#pragma unroll
+  for (int w = 0; w < CW; w++) qw[w] = s.codes[((int64_t)q * 2 + qstr) * kCodeWords + w];
+  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
+  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
+  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  uint32_t HE[QL], SS[QL];
+  {
+    // boundary column -1: H(i,-1) = -(GO_TL + (i+1) GE_TL), E(i,0) opened from it; built
+    // incrementally in VGPRs (an opaque zero keeps the compiler from materialising 2*QL scalars)
+    int vz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+    int hleft = vz - sc.go[1];
+    const int QRqi = sc.go[2] + sc.ge[2], QRqr = sc.go[4] + sc.ge[4];
+#pragma unroll
+    for (int i = 0; i < QL; i++) {
+      hleft -= sc.ge[1];
+      const int qrq = (i == QL - 1) ? QRqr : QRqi;
+      HE[i] = pack_hf(hleft, sc.boundary_open ? hleft - qrq : kNegInf);
+      SS[i] = 1u << 16;  // S_H(i,-1) = 0 (boundary), S_E(i,0) = one real move
+    }
+  }
+  int Lext = 0, trail = 0;
+  uint32_t tword = 0;
+  for (int j = 0; j < tl; j++) {
+    if ((j & 7) == 0) tword = tcp[j >> 3];
+    const uint32_t tcode = tword & 15u;
+    tword >>= 4;
+    // keep the per-row query codes from being hoisted out of the column loop (that would pin
+    // QL extra VGPRs); re-extracting them is one v_bfe per cell
+#pragma unroll
+    for (int w = 0; w < CW; w++) asm volatile("" : "+v"(qw[w]));
+    const bool lc = (j == tl - 1);
+    align_column<QL, AMB>(HE, SS, qw, tcode, j, sc, lc ? QRtr : QRti, lc ? Rtr : Rti, Lext, trail);
+  }
+  const int H = sx16(HE[QL - 1]);
+  const uint32_t S = SS[QL - 1] & 0xffffu;
+  const uint32_t m = S >> 8, acols = S & 0xffu;
+  const uint32_t internal = acols - (uint32_t)trail;
+  out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
+}
+
+typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
+                        const uint32_t*, Scoring, uint32_t*);
+
+template <int L>
+struct AlignTable {
+  static void fill(AlignFn* t) {
+    t[2 * L] = k_align<L, false>;
+    t[2 * L + 1] = k_align<L, true>;
+    AlignTable<L - 1>::fill(t);
+  }
+};
+template <>
+struct AlignTable<kMinTplLen - 1> {
+  static void fill(AlignFn*) {}
+};
+
+hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq,
+                        const uint32_t* pt, int32_t npairs, const uint32_t* dev_npairs,
+                        const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st) {
+  static AlignFn table[2 * (kMaxLen + 1)] = {};
+  static bool init = false;
+  if (!init) {
+    AlignTable<kMaxLen>::fill(table);
+    init = true;
+  }
+  if (npairs <= 0) return hipSuccess;
+  if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(table[2 * qlen + (ambig ? 1 : 0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
+                     pq, pt, npairs, dev_npairs, outidx, sc, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K3W: device-side walk
+// vsearch search_onequery pops candidates best-first in batches of MAXDELAYED = 8 and stops
+// after the batch in which it has an accept, after maxaccepts+maxrejects-1 = 32 candidates, or
+// when the list is exhausted.  The walk runs on the device over the top lists (in-block peers
+// are resolved later by the host): round r evaluates batch r of every unfinished query-strand and
+// emits the pairs of batch r+1.  Acceptance and the id order come from host-built tables, so the
+// IEEE-double test `100.0*matches/internal >= 100.0*id` is exactly vsearch's.
+__global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
+                       const uint32_t* __restrict__ top_seqno, const uint8_t* __restrict__ top_count,
+                       const uint8_t* __restrict__ ntop, const uint8_t* __restrict__ lens,
+                       const uint32_t* __restrict__ res, const uint8_t* __restrict__ acc_tab,
+                       const uint16_t* __restrict__ rank_tab, WalkState* __restrict__ ws,
+                       uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
+                       uint32_t* __restrict__ outidx, uint32_t* __restrict__ npairs) {
+  const int qs = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qs >= nqs) return;
+  const int32_t q = q0 + qs / both;
+  const uint32_t strand = (uint32_t)(qs % both);
+  const int nt = ntop[qs];
+  WalkState w;
+  if (round < 0) {
+    w.w = 0;
+    w.done = (nt == 0) ? 1 : 0;
+    w.acc = 0;
+    w.best_rank = 0;
+    w.best_t = 0xffffffffu;
+    w.cells = 0;
+    w.lastkey = 0;
+  } else {
+    w = ws[qs];
+    if (w.done) return;
+    const int b0 = round * kBatch, b1 = min(nt, b0 + kBatch);
+    const int ql = lens[q];
+    for (int x = b0; x < b1; x++) {
+      const uint32_t r = res[(int64_t)qs * kWalk + x];
+      const uint32_t m = r & 0xffu, L = (r >> 8) & 0xffu;
+      const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
+      w.cells += (uint32_t)(ql * lens[t]);
+      if (acc_tab[L * kTabM + m]) {
+        const uint16_t rk = rank_tab[L * kTabM + m];
+        if (!w.acc || rk > w.best_rank || (rk == w.best_rank && t < w.best_t)) {
+          w.best_rank = rk;
+          w.best_t = t;
+        }
+        w.acc = 1;
+      }
+    }
+    w.w = (uint8_t)b1;
+    const uint32_t tl = lens[top_seqno[(int64_t)qs * kTopHits + b1 - 1]];
+    w.lastkey = ((unsigned long long)(127u - top_count[(int64_t)qs * kTopHits + b1 - 1]) << 56) |
+                ((unsigned long long)tl << 48) | top_seqno[(int64_t)qs * kTopHits + b1 - 1];
+    if (w.acc || b1 >= nt || b1 >= kWalk) w.done = 1;
+  }
+  ws[qs] = w;
+  if (!w.done) {
+    const int b0 = w.w, b1 = min(nt, b0 + kBatch);
+    const uint32_t base = atomicAdd(npairs, (uint32_t)(b1 - b0));
+    for (int x = b0; x < b1; x++) {
+      const uint32_t k = base + (uint32_t)(x - b0);
+      pq[k] = ((uint32_t)q << 1) | strand;
+      pt[k] = top_seqno[(int64_t)qs * kTopHits + x];
+      outidx[k] = (uint32_t)qs * kWalk + (uint32_t)x;
+    }
+  }
+}
+
+hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
+                       const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
+                       const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
+                       const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
+                       uint32_t* outidx, uint32_t* npairs, hipStream_t st) {
+  if (nqs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_walk, dim3((nqs + 255) / 256), dim3(256), 0, st, round, q0, nqs, both,
+                     top_seqno, top_count, ntop, lens, res, acc_tab, rank_tab, ws, pq, pt, outidx,
+                     npairs);
+  return hipGetLastError();
+}
+
+// gather the candidate lists and walked results of selected query-strands (host round B)
+__global__ void k_gather_blocked(const int32_t* __restrict__ sel, int32_t nsel,
+                                 const uint32_t* __restrict__ top_seqno,
+                                 const uint8_t* __restrict__ top_count,
+                                 const uint32_t* __restrict__ res, uint32_t* __restrict__ g_seqno,
+                                 uint8_t* __restrict__ g_count, uint32_t* __restrict__ g_res) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nsel * kWalk) return;
+  const int i = k / kWalk, x = k % kWalk;
+  const int qs = sel[i];
+  g_seqno[k] = top_seqno[(int64_t)qs * kTopHits + x];
+  g_count[k] = top_count[(int64_t)qs * kTopHits + x];
+  g_res[k] = res[(int64_t)qs * kWalk + x];
+}
+
+hipError_t launch_gather_blocked(const int32_t* sel, int32_t nsel, const uint32_t* top_seqno,
+                                 const uint8_t* top_count, const uint32_t* res, uint32_t* g_seqno,
+                                 uint8_t* g_count, uint32_t* g_res, hipStream_t st) {
+  if (nsel <= 0) return hipSuccess;
+  const int n = nsel * kWalk;
+  hipLaunchKernelGGL(k_gather_blocked, dim3((n + 255) / 256), dim3(256), 0, st, sel, nsel, top_seqno,
+                     top_count, res, g_seqno, g_count, g_res);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K3T: traceback
+// Same DP (rows unrolled) without summaries; the direction nibble of every cell (bit0 up = D
+// chosen, bit1 left = I chosen, bit2 D-extension, bit3 I-extension) goes to HBM as one column of
+// CW words per step, laid out [column][word][pair] so a wave's stores are coalesced; then each lane
+// runs backtrack16 over its own matrix.
+template <int QL>
+__global__ __launch_bounds__(64) void k_traceback(DevSeqs s, const uint32_t* __restrict__ pq,
+                                                  const uint32_t* __restrict__ pt, int32_t npairs,
+                                                  Scoring sc, uint32_t* __restrict__ dirbuf,
+                                                  uint8_t* __restrict__ ops,
+                                                  uint16_t* __restrict__ nops,
+                                                  uint32_t* __restrict__ out) {
+  constexpr int CW = (QL + 7) / 8;
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= npairs) return;
+  const uint32_t qv = pq[k];
+  const int32_t q = (int32_t)(qv >> 1);
+  const int qstr = (int)(qv & 1u);
+  const int32_t t = (int32_t)pt[k];
+  const int tl = s.lens[t];
+  uint32_t qw[CW];
+#pragma unroll
+  for (int w = 0; w < CW; w++) qw[w] = s.codes[((int64_t)q * 2 + qstr) * kCodeWords + w];
+  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
+  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
+  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
+  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  uint32_t HE[QL];
+#pragma unroll
+  for (int i = 0; i < QL; i++) {
+    const int hleft = -(sc.go[1] + (i + 1) * sc.ge[1]);
+    const int qrq = (i == QL - 1) ? QRqr : QRqi;
+    HE[i] = pack_hf(hleft, sc.boundary_open ? hleft - qrq : kNegInf);
+  }
+  uint32_t tword = 0;
+  for (int j = 0; j < tl; j++) {
+    if ((j & 7) == 0) tword = tcp[j >> 3];
+    const uint32_t tcode = tword & 15u;
+    tword >>= 4;
+    const bool tamb = (tcode & (tcode - 1u)) != 0u || tcode == 0u;
+    // keep the per-row query codes from being hoisted out of the column loop (that would pin
+    // QL extra VGPRs); re-extracting them is one v_bfe per cell
+#pragma unroll
+    for (int w = 0; w < CW; w++) asm volatile("" : "+v"(qw[w]));
+    const bool lc = (j == tl - 1);
+    const int QRt = lc ? QRtr : QRti;
+    const int Rt = lc ? Rtr : Rti;
+    int Hd = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
+    int F = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - QRt : kNegInf;
+    uint32_t dw[CW];
+#pragma unroll
+    for (int w = 0; w < CW; w++) dw[w] = 0;
+#pragma unroll
+    for (int i = 0; i < QL; i++) {
+      const uint32_t qcode = (qw[i >> 3] >> ((i & 7) * 4)) & 15u;
+      const bool amb = tamb || (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+      const int sub = amb ? 0 : (qcode == tcode ? sc.match : sc.mismatch);
+      const uint32_t he = HE[i];
+      const int Hl = sx16(he);
+      const int E = (int)he >> 16;
+      int h = Hd + sub;
+      uint32_t d = 0;
+      if (F > h) { h = F; d |= 1u; }
+      if (E > h) { h = E; d |= 2u; }
+      const int fo = h - QRt, fe = F - Rt;
+      if (fe > fo) { F = fe; d |= 4u; } else F = fo;
+      const int qrq = (i == QL - 1) ? QRqr : QRqi;
+      const int rq = (i == QL - 1) ? Rqr : Rqi;
+      const int eo = h - qrq, ee = E - rq;
+      int En = eo;
+      if (ee > eo) { En = ee; d |= 8u; }
+      dw[i >> 3] |= d << ((i & 7) * 4);
+      Hd = Hl;
+      HE[i] = pack_hf(h, En);
+    }
+#pragma unroll
+    for (int w = 0; w < CW; w++) dirbuf[((int64_t)j * CW + w) * npairs + k] = dw[w];
+  }
+  const int H = sx16(HE[QL - 1]);
+  // backtrack16
+  uint8_t* o = ops + (int64_t)k * kOpsStride;
+  int n = 0;
+  int i = QL - 1, j = tl - 1;
+  int aligned = 0, matches = 0;
+  uint32_t op = 0;  // 0 none, 'M','D','I'
+  while (i >= 0 && j >= 0) {
+    aligned++;
+    const uint32_t d = (dirbuf[((int64_t)j * CW + (i >> 3)) * npairs + k] >> ((i & 7) * 4)) & 15u;
+    if (op == 'I' && (d & 8u)) {
+      j--;
+    } else if (op == 'D' && (d & 4u)) {
+      i--;
+    } else if (d & 2u) {
+      j--;
+      op = 'I';
+    } else if (d & 1u) {
+      i--;
+      op = 'D';
+    } else {
+      const uint32_t qcode = (s.codes[((int64_t)q * 2 + qstr) * kCodeWords + (i >> 3)] >> ((i & 7) * 4)) & 15u;
+      const uint32_t tcode = (tcp[j >> 3] >> ((j & 7) * 4)) & 15u;
+      if (qcode & tcode) matches++;
+      i--;
+      j--;
+      op = 'M';
+    }
+    o[kOpsStride - 1 - n] = (uint8_t)op;
+    n++;
+  }
+  while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
+  while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
+  nops[k] = (uint16_t)n;
+  // align_trim on the op string (alignment order = o[kOpsStride-n .. kOpsStride-1])
+  const uint8_t* a0 = o + kOpsStride - n;
+  int tlft = 0, trgt = 0;
+  if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
+  if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
+  if (tlft >= aligned) trgt = 0;
+  const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
+  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
+}
+
+typedef void (*TraceFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, Scoring, uint32_t*,
+                        uint8_t*, uint16_t*, uint32_t*);
+template <int L>
+struct TraceTable {
+  static void fill(TraceFn* t) {
+    t[L] = k_traceback<L>;
+    TraceTable<L - 1>::fill(t);
+  }
+};
+template <>
+struct TraceTable<kMinTplLen - 1> {
+  static void fill(TraceFn*) {}
+};
+
+hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
+                            int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,
+                            uint16_t* nops, uint32_t* out, hipStream_t st) {
+  static TraceFn table[kMaxLen + 1] = {};
+  static bool init = false;
+  if (!init) {
+    TraceTable<kMaxLen>::fill(table);
+    init = true;
+  }
+  if (npairs <= 0) return hipSuccess;
+  if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(table[qlen], dim3((npairs + 63) / 64), dim3(64), 0, st, s, pq, pt, npairs, sc,
+                     dirbuf, ops, nops, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ K4: consensus
+// One workgroup per cluster.  maxi[p] = longest member insertion before centroid position p
+// (LDS atomicMax), the profile of residues per MSA column by LDS atomics; the gap count of a
+// column is (members - residues) because every member contributes exactly one symbol to every
+// column (msa.cc pads each insertion slot to maxi).  Columns inside the left/right centroid
+// overhang are censored; a column emits the first strict maximum of A,C,G,T (N if none) iff its
+// count >= the gap count.
+constexpr int kConsThreads = 256;
+struct ConsShared {
+  int32_t maxi[kMaxLen + 1];
+  int32_t slot[kMaxLen + 2];
+  uint32_t prof[kMsaCols][5];
+  int32_t emit[kMsaCols];
+  int32_t alnlen;
+};
+
+__device__ __forceinline__ int sym_of4(uint32_t c4) {
+  return c4 == 1 ? 0 : (c4 == 2 ? 1 : (c4 == 4 ? 2 : (c4 == 8 ? 3 : 4)));
+}
+
+__global__ __launch_bounds__(kConsThreads) void k_consensus(
+    DevSeqs s, const int32_t* __restrict__ cstart, int32_t nclusters,
+    const int32_t* __restrict__ member_seqno, const int32_t* __restrict__ member_opsidx,
+    const uint8_t* __restrict__ member_strand, const uint8_t* __restrict__ ops,
+    const uint16_t* __restrict__ nops, char* __restrict__ cons, uint16_t* __restrict__ conslen,
+    int32_t* __restrict__ overflow) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char cs_smem[];
+  ConsShared& S = *reinterpret_cast<ConsShared*>(cs_smem);
+  const int c = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int m0 = cstart[c], m1 = cstart[c + 1];
+  const int m = m1 - m0;
+  const int32_t cent = member_seqno[m0];
+  const int clen = s.lens[cent];
+  for (int x = tid; x <= clen; x += kConsThreads) S.maxi[x] = 0;
+  __syncthreads();
+  for (int mi = m0 + 1 + tid; mi < m1; mi += kConsThreads) {
+    const int oi = member_opsidx[mi];
+    const int n = nops[oi];
+    const uint8_t* a0 = ops + (int64_t)oi * kOpsStride + kOpsStride - n;
+    int pos = 0, run = 0;
+    for (int x = 0; x < n; x++) {
+      const uint8_t o = a0[x];
+      if (o == 'D') {
+        run++;
+      } else {
+        if (run) { atomicMax(&S.maxi[pos], run); run = 0; }
+        pos++;
+      }
+    }
+    if (run) atomicMax(&S.maxi[pos], run);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int p = 0; p <= clen; p++) {
+      S.slot[p] = acc;  // first column of insertion slot p; centroid residue p at acc + maxi[p]
+      acc += S.maxi[p] + 1;
+    }
+    S.alnlen = acc - 1;
+  }
+  __syncthreads();
+  const int alnlen = S.alnlen;
+  if (alnlen > kMsaCols) {
+    if (tid == 0) {
+      atomicAdd(overflow, 1);
+      conslen[c] = 0;
+    }
+    return;
+  }
+  for (int x = tid; x < alnlen; x += kConsThreads) {
+    S.prof[x][0] = S.prof[x][1] = S.prof[x][2] = S.prof[x][3] = S.prof[x][4] = 0;
+  }
+  __syncthreads();
+  // centroid residues
+  for (int p = tid; p < clen; p += kConsThreads) {
+    const uint32_t c4 = (s.codes[(int64_t)cent * 2 * kCodeWords + (p >> 3)] >> ((p & 7) * 4)) & 15u;
+    atomicAdd(&S.prof[S.slot[p] + S.maxi[p]][sym_of4(c4)], 1u);
+  }
+  for (int mi = m0 + 1 + tid; mi < m1; mi += kConsThreads) {
+    const int32_t sq = member_seqno[mi];
+    const int st = member_strand[mi];
+    const uint32_t* code = s.codes + ((int64_t)sq * 2 + st) * kCodeWords;
+    const int oi = member_opsidx[mi];
+    const int n = nops[oi];
+    const uint8_t* a0 = ops + (int64_t)oi * kOpsStride + kOpsStride - n;
+    int pos = 0, tpos = 0, run = 0;
+    for (int x = 0; x < n; x++) {
+      const uint8_t o = a0[x];
+      if (o == 'D') {
+        const uint32_t c4 = (code[tpos >> 3] >> ((tpos & 7) * 4)) & 15u;
+        atomicAdd(&S.prof[S.slot[pos] + run][sym_of4(c4)], 1u);
+        run++;
+        tpos++;
+      } else {
+        run = 0;
+        if (o == 'M') {
+          const uint32_t c4 = (code[tpos >> 3] >> ((tpos & 7) * 4)) & 15u;
+          atomicAdd(&S.prof[S.slot[pos] + S.maxi[pos]][sym_of4(c4)], 1u);
+          tpos++;
+        }
+        pos++;
+      }
+    }
+  }
+  __syncthreads();
+  const int left = S.maxi[0], right = S.maxi[clen];
+  for (int x = tid; x < alnlen; x += kConsThreads) {
+    int e = -1;
+    if (x >= left && x < alnlen - right) {
+      const uint32_t* pr = S.prof[x];
+      int best = 0;
+      uint32_t bc = 0;
+      for (int y = 0; y < 4; y++)
+        if (pr[y] > bc) { bc = pr[y]; best = y; }
+      if (bc == 0 && pr[4] > 0) { bc = pr[4]; best = 4; }
+      const uint32_t res = pr[0] + pr[1] + pr[2] + pr[3] + pr[4];
+      const uint32_t gaps = (uint32_t)m - res;
+      if (bc >= gaps) e = best;
+    }
+    S.emit[x] = e;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const char sym[5] = {'A', 'C', 'G', 'T', 'N'};
+    int n = 0;
+    char* dst = cons + (int64_t)c * kConsCap;
+    for (int x = 0; x < alnlen; x++) {
+      if (S.emit[x] >= 0) {
+        if (n < kConsCap) dst[n] = sym[S.emit[x]];
+        n++;
+      }
+    }
+    if (n > kConsCap) {
+      atomicAdd(overflow, 1);
+      n = kConsCap;
+    }
+    conslen[c] = (uint16_t)n;
+  }
+}
+
+hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t nclusters,
+                            const int32_t* member_seqno, const int32_t* member_opsidx,
+                            const uint8_t* member_strand, const uint8_t* ops,
+                            const uint16_t* nops, char* cons, uint16_t* conslen,
+                            int32_t* overflow, hipStream_t st) {
+  if (nclusters <= 0) return hipSuccess;
+  const size_t smem = sizeof(ConsShared);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_consensus,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_consensus, dim3(nclusters), dim3(kConsThreads), smem, st, s, cstart,
+                     nclusters, member_seqno, member_opsidx, member_strand, ops, nops, cons,
+                     conslen, overflow);
+  return hipGetLastError();
+}
+
+}  // namespace uc

@@ -1,0 +1,273 @@
+"""ctypes binding of the C ABI declared in include/umiclust.h (libumiclust.so, built in-tree).
+
+There is no CPU fallback: if the library or a HIP device is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libumiclust.so")
+
+QL, TL, QI, TI, QR, TR = range(6)
+PRESET_ROUND1 = 1
+PRESET_VSEARCH_DEFAULT = 2
+MAX_LEN = 72
+
+ERRORS = {-22: "EINVAL", -5: "EIO", -12: "ENOMEM", -19: "EDEVICE", -77: "ESTATE", -34: "ERANGE"}
+
+
+class UmiclustError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"umiclust error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("id", C.c_double),
+        ("weak_id", C.c_double),
+        ("minseqlength", C.c_int32),
+        ("maxseqlength", C.c_int32),
+        ("wordlength", C.c_int32),
+        ("minwordmatches", C.c_int32),
+        ("maxaccepts", C.c_int32),
+        ("maxrejects", C.c_int32),
+        ("match", C.c_int32),
+        ("mismatch", C.c_int32),
+        ("gap_open", C.c_int32 * 6),
+        ("gap_ext", C.c_int32 * 6),
+        ("strand_both", C.c_int32),
+        ("qmask_dust", C.c_int32),
+        ("clusterout_sort", C.c_int32),
+        ("clusterout_id", C.c_int32),
+        ("fasta_width", C.c_int32),
+        ("policy_boundary_open", C.c_int32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("n_input", C.c_int64),
+        ("n_kept", C.c_int64),
+        ("n_clusters", C.c_int64),
+        ("n_alignments", C.c_int64),
+        ("cells", C.c_int64),
+        ("cells_computed", C.c_int64),
+        ("kmer_postings", C.c_int64),
+        ("n_blocks", C.c_int64),
+        ("t_total_s", C.c_double),
+        ("t_prefilter_s", C.c_double),
+        ("t_align_s", C.c_double),
+        ("t_consensus_s", C.c_double),
+        ("t_host_s", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol include/umiclust.h declares
+EXPORTS = [
+    "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
+    "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv",
+    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_align_pairs", "umiclust_prep",
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise UmiclustError(-19, f"{LIB_PATH} not built (run `make -C ont-tcrconsensus_amd` or "
+                                 "__graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    L.umiclust_abi_version.restype = C.c_int32
+    L.umiclust_params_init.restype = C.c_int32
+    L.umiclust_params_init.argtypes = [P(Params), C.c_int32, C.c_double, C.c_int32, C.c_int32]
+    L.umiclust_params_from_argv.restype = C.c_int32
+    L.umiclust_params_from_argv.argtypes = [P(Params), C.c_int32, P(C.c_char_p), C.c_char_p, C.c_char_p,
+                                            C.c_char_p, C.c_char_p, C.c_int32]
+    L.umiclust_create.restype = C.c_void_p
+    L.umiclust_create.argtypes = [C.c_int32, P(C.c_int32)]
+    L.umiclust_destroy.restype = None
+    L.umiclust_destroy.argtypes = [C.c_void_p]
+    L.umiclust_last_error.restype = C.c_char_p
+    L.umiclust_last_error.argtypes = [C.c_void_p]
+    L.umiclust_run_fasta.restype = C.c_int64
+    L.umiclust_run_fasta.argtypes = [C.c_void_p, P(Params), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                     P(Stats)]
+    L.umiclust_run_argv.restype = C.c_int64
+    L.umiclust_run_argv.argtypes = [C.c_void_p, C.c_int32, P(C.c_char_p), P(Stats)]
+    L.umiclust_load.restype = C.c_int32
+    L.umiclust_load.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_int64]
+    L.umiclust_cluster.restype = C.c_int64
+    L.umiclust_cluster.argtypes = [C.c_void_p, P(Stats)]
+    L.umiclust_fetch.restype = C.c_int64
+    L.umiclust_fetch.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_uint8), P(C.c_uint8), C.c_void_p, C.c_int64,
+                                 P(C.c_int64)]
+    L.umiclust_align_pairs.restype = C.c_int32
+    L.umiclust_align_pairs.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_void_p, P(C.c_int64),
+                                       C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_int32,
+                                       P(C.c_int32)]
+    L.umiclust_prep.restype = C.c_int32
+    L.umiclust_prep.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_int64, C.c_void_p,
+                                P(C.c_uint16), C.c_int32, P(C.c_int32)]
+    _lib = L
+    return L
+
+
+def params(preset: int = PRESET_ROUND1, identity: float = 0.93, minlen: int = 58, maxlen: int = 68) -> Params:
+    p = Params()
+    rc = lib().umiclust_params_init(C.byref(p), preset, identity, minlen, maxlen)
+    if rc != 0:
+        raise UmiclustError(rc, "params_init")
+    return p
+
+
+def params_from_argv(argv: list[str]) -> tuple[Params, dict]:
+    p = Params()
+    bufs = [C.create_string_buffer(4096) for _ in range(4)]
+    arr = (C.c_char_p * len(argv))(*[str(a).encode() for a in argv])
+    rc = lib().umiclust_params_from_argv(C.byref(p), len(argv), arr, *bufs, 4096)
+    if rc != 0:
+        raise UmiclustError(rc, f"cannot parse argv {argv!r}")
+    keys = ["in_fasta", "clusters_prefix", "consout", "log"]
+    return p, {k: (b.value.decode() or None) for k, b in zip(keys, bufs)}
+
+
+def _i64(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def _pack(seqs) -> tuple[np.ndarray, np.ndarray]:
+    """list of str/bytes -> (uint8 buffer, int64 offsets)."""
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+    off = np.zeros(len(bs) + 1, np.int64)
+    if bs:
+        np.cumsum([len(b) for b in bs], out=off[1:])
+    buf = np.frombuffer(b"".join(bs) + b"\0", np.uint8).copy()
+    return buf, off
+
+
+class Context:
+    """One device context (one per process and GPU)."""
+
+    def __init__(self, device: int = 0):
+        err = C.c_int32(0)
+        self._h = lib().umiclust_create(device, C.byref(err))
+        if not self._h:
+            raise UmiclustError(err.value, f"no HIP device {device} (there is no CPU backend)")
+
+    def close(self):
+        if self._h:
+            lib().umiclust_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str) -> int:
+        if rc < 0:
+            msg = lib().umiclust_last_error(self._h)
+            raise UmiclustError(int(rc), f"{what}: {msg.decode() if msg else ''}")
+        return rc
+
+    def run_fasta(self, p: Params, in_fasta: str, clusters_prefix: str | None, consout: str | None,
+                  log: str | None) -> dict:
+        st = Stats()
+        enc = lambda x: x.encode() if x else None  # noqa: E731
+        k = lib().umiclust_run_fasta(self._h, C.byref(p), enc(in_fasta), enc(clusters_prefix), enc(consout),
+                                     enc(log), C.byref(st))
+        self._check(k, "run_fasta")
+        return st.as_dict()
+
+    def run_argv(self, argv: list[str]) -> dict:
+        st = Stats()
+        arr = (C.c_char_p * len(argv))(*[str(a).encode() for a in argv])
+        k = lib().umiclust_run_argv(self._h, len(argv), arr, C.byref(st))
+        self._check(k, "run_argv")
+        return st.as_dict()
+
+    def load(self, p: Params, seqs=None, buf: np.ndarray | None = None, off: np.ndarray | None = None) -> None:
+        if seqs is not None:
+            buf, off = _pack(seqs)
+        n = len(off) - 1
+        self._check(lib().umiclust_load(self._h, C.byref(p), buf.ctypes.data, _i64(off), n), "load")
+        self._n = n
+
+    def cluster(self) -> dict:
+        st = Stats()
+        self._check(lib().umiclust_cluster(self._h, C.byref(st)), "cluster")
+        return st.as_dict()
+
+    def fetch(self) -> dict:
+        n = self._n
+        cl = np.empty(max(n, 1), np.int32)
+        sd = np.empty(max(n, 1), np.uint8)
+        ce = np.empty(max(n, 1), np.uint8)
+        k = self._check(lib().umiclust_fetch(self._h, None, None, None, None, 0, None), "fetch")
+        off = np.zeros(k + 1, np.int64)
+        self._check(lib().umiclust_fetch(self._h, None, None, None, None, 0, _i64(off)), "fetch")
+        cons = np.zeros(int(off[-1]) + 1, np.uint8)
+        P = C.POINTER
+        self._check(lib().umiclust_fetch(self._h, cl.ctypes.data_as(P(C.c_int32)), sd.ctypes.data_as(P(C.c_uint8)),
+                                         ce.ctypes.data_as(P(C.c_uint8)), cons.ctypes.data, len(cons), _i64(off)),
+                    "fetch")
+        raw = cons.tobytes()
+        return dict(n_clusters=int(k), cluster=cl[:n], strand=sd[:n], centroid=ce[:n],
+                    consensus=[raw[off[c]:off[c + 1]].decode() for c in range(k)])
+
+    def align_pairs(self, p: Params, queries, targets, with_ops: bool = False) -> dict:
+        qb, qo = _pack(queries)
+        tb, to = _pack(targets)
+        n = len(qo) - 1
+        P = C.POINTER
+        sc = np.zeros(max(n, 1), np.int32)
+        m = np.zeros(max(n, 1), np.int32)
+        il = np.zeros(max(n, 1), np.int32)
+        stride = 2 * MAX_LEN
+        ops = np.zeros(max(n, 1) * stride, np.uint8) if with_ops else None
+        nops = np.zeros(max(n, 1), np.int32) if with_ops else None
+        rc = lib().umiclust_align_pairs(self._h, C.byref(p), qb.ctypes.data, _i64(qo), tb.ctypes.data, _i64(to), n,
+                                        sc.ctypes.data_as(P(C.c_int32)), m.ctypes.data_as(P(C.c_int32)),
+                                        il.ctypes.data_as(P(C.c_int32)), ops.ctypes.data if with_ops else None,
+                                        stride, nops.ctypes.data_as(P(C.c_int32)) if with_ops else None)
+        self._check(rc, "align_pairs")
+        out = dict(score=sc[:n], matches=m[:n], internal_len=il[:n])
+        if with_ops:
+            raw = ops.tobytes()
+            out["ops"] = [raw[k * stride:k * stride + nops[k]].decode() for k in range(n)]
+        return out
+
+    def prep(self, p: Params, seqs) -> dict:
+        b, o = _pack(seqs)
+        n = len(o) - 1
+        masked = np.zeros(len(b), np.uint8)
+        kst = 68
+        km = np.zeros(max(n, 1) * 2 * kst, np.uint16)
+        nk = np.zeros(max(n, 1) * 2, np.int32)
+        P = C.POINTER
+        rc = lib().umiclust_prep(self._h, C.byref(p), b.ctypes.data, _i64(o), n, masked.ctypes.data,
+                                 km.ctypes.data_as(P(C.c_uint16)), kst, nk.ctypes.data_as(P(C.c_int32)))
+        self._check(rc, "prep")
+        mb = masked.tobytes()
+        return dict(masked=[mb[o[i]:o[i + 1]].decode() for i in range(n)],
+                    kmers=[[list(km[(2 * i + s) * kst:(2 * i + s) * kst + nk[2 * i + s]]) for s in range(2)]
+                           for i in range(n)])

@@ -1,0 +1,144 @@
+"""ctypes wrapper for the CPU ORACLE (oracle/liborc_umiclust.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker.  The product path (ont-tcrconsensus_amd/) never loads it.
+Parity of the oracle itself against vsearch is UNPINNED (see umiclust_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liborc_umiclust.so")
+
+QL, TL, QI, TI, QR, TR = range(6)
+
+
+class OrcParams(C.Structure):
+    _fields_ = [
+        ("id", C.c_double),
+        ("weak_id", C.c_double),
+        ("minseqlength", C.c_int32),
+        ("maxseqlength", C.c_int32),
+        ("wordlength", C.c_int32),
+        ("minwordmatches", C.c_int32),
+        ("maxaccepts", C.c_int32),
+        ("maxrejects", C.c_int32),
+        ("match", C.c_int32),
+        ("mismatch", C.c_int32),
+        ("gap_open", C.c_int32 * 6),
+        ("gap_ext", C.c_int32 * 6),
+        ("strand_both", C.c_int32),
+        ("qmask_dust", C.c_int32),
+        ("clusterout_sort", C.c_int32),
+        ("clusterout_id", C.c_int32),
+        ("fasta_width", C.c_int32),
+        ("policy_boundary_open", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = C.CDLL(_LIB)
+        L.orc_params_preset.argtypes = [C.POINTER(OrcParams), C.c_int, C.c_double, C.c_int, C.c_int]
+        L.orc_align.restype = C.c_int
+        L.orc_align.argtypes = [C.POINTER(OrcParams), C.c_char_p, C.c_int, C.c_char_p, C.c_int] + \
+            [C.POINTER(C.c_int)] * 7 + [C.POINTER(C.c_double), C.c_char_p]
+        L.orc_dust.argtypes = [C.c_char_p, C.c_int]
+        L.orc_unique_kmers.restype = C.c_int
+        L.orc_unique_kmers.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32)]
+        L.orc_cluster.restype = C.c_int64
+        L.orc_cluster.argtypes = [C.POINTER(OrcParams), C.c_int32, C.POINTER(C.c_char_p),
+                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_uint8),
+                                  C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.c_char_p, C.c_int64,
+                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.orc_run_fasta.restype = C.c_int64
+        L.orc_run_fasta.argtypes = [C.POINTER(OrcParams), C.c_char_p, C.c_char_p, C.c_char_p,
+                                    C.POINTER(C.c_int64)]
+        _lib = L
+    return _lib
+
+
+def params(preset: int = 1, identity: float = 0.93, minlen: int = 58, maxlen: int = 68) -> OrcParams:
+    p = OrcParams()
+    lib().orc_params_preset(C.byref(p), preset, identity, minlen, maxlen)
+    return p
+
+
+def align(p: OrcParams, q: str, t: str) -> dict:
+    ints = [C.c_int() for _ in range(7)]
+    idv = C.c_double()
+    cig = C.create_string_buffer(2 * (len(q) + len(t)) + 8)
+    score = lib().orc_align(C.byref(p), q.encode(), len(q), t.encode(), len(t),
+                            *[C.byref(x) for x in ints], C.byref(idv), cig)
+    keys = ["columns", "matches", "mismatches", "gaps", "trim_left", "trim_right", "internal_len"]
+    out = {k: v.value for k, v in zip(keys, ints)}
+    out.update(score=score, id=idv.value, cigar=cig.value.decode())
+    return out
+
+
+def dust(seq: str) -> str:
+    b = C.create_string_buffer(seq.encode(), len(seq) + 1)
+    lib().orc_dust(b, len(seq))
+    return b.value.decode()
+
+
+def unique_kmers(seq: str, k: int = 8, mask: bool = True) -> list[int]:
+    out = (C.c_uint32 * max(1, len(seq)))()
+    n = lib().orc_unique_kmers(seq.encode(), len(seq), k, int(mask), out)
+    return list(out[:n])
+
+
+def cluster(p: OrcParams, seqs: list) -> dict:
+    """Cluster in-memory sequences (list of str/bytes, input order)."""
+    n = len(seqs)
+    bs = [s.encode() if isinstance(s, str) else bytes(s) for s in seqs]
+    arr = (C.c_char_p * max(1, n))(*bs)
+    lens = np.array([len(s) for s in bs], dtype=np.int32)
+    ocl = np.empty(max(1, n), np.int32)
+    ost = np.empty(max(1, n), np.uint8)
+    oce = np.empty(max(1, n), np.uint8)
+    osr = np.empty(max(1, n), np.int32)
+    cap = int(2 * lens.sum() + 16)
+    cbuf = C.create_string_buffer(cap)
+    coff = np.empty(n + 2, np.int64)
+    st = np.zeros(8, np.int64)
+    P = C.POINTER
+    k = lib().orc_cluster(C.byref(p), n, arr, lens.ctypes.data_as(P(C.c_int32)),
+                          ocl.ctypes.data_as(P(C.c_int32)), ost.ctypes.data_as(P(C.c_uint8)),
+                          oce.ctypes.data_as(P(C.c_uint8)), osr.ctypes.data_as(P(C.c_int32)),
+                          cbuf, cap, coff.ctypes.data_as(P(C.c_int64)), st.ctypes.data_as(P(C.c_int64)))
+    if k < 0:
+        raise RuntimeError(f"orc_cluster failed: {k}")
+    raw = cbuf.raw
+    cons = [raw[coff[c]:coff[c + 1]].decode() for c in range(k)]
+    kept = int(st[0])
+    return dict(n_clusters=int(k), cluster=ocl[:n].copy(), strand=ost[:n].copy(),
+                centroid=oce[:n].copy(), sorted=osr[:kept].copy(), consensus=cons,
+                stats=dict(kept=kept, clusters=int(st[1]), alignments=int(st[2]), cells=int(st[3]),
+                           postings=int(st[4]), candidates=int(st[5]), dust_masked=int(st[6])))
+
+
+def run_fasta(p: OrcParams, in_fasta: str, clusters_prefix: str | None, consout: str | None) -> dict:
+    st = np.zeros(8, np.int64)
+    k = lib().orc_run_fasta(C.byref(p), in_fasta.encode(),
+                            clusters_prefix.encode() if clusters_prefix else None,
+                            consout.encode() if consout else None,
+                            st.ctypes.data_as(C.POINTER(C.c_int64)))
+    if k < 0:
+        raise RuntimeError(f"orc_run_fasta failed: {k}")
+    return dict(n_clusters=int(k), kept=int(st[0]), alignments=int(st[2]), cells=int(st[3]))

@@ -1,0 +1,233 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on the same seeded inputs.
+Bit-exact for every integer/byte result: alignment score/matches/internal length/ops, DUST masks,
+k-mer sets, cluster membership, strands, centroids, consensus bytes and the written files."""
+import os
+import random
+
+import numpy as np
+import orc
+import pytest
+from umiclust import _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _mutate(rng, a, nedits, alphabet="ACGT"):
+    b = list(a)
+    for _ in range(nedits):
+        x = rng.randrange(len(b))
+        u = rng.random()
+        if u < 0.4:
+            b[x] = rng.choice(alphabet)
+        elif u < 0.7:
+            b.insert(x, rng.choice(alphabet))
+        elif len(b) > 1:
+            del b[x]
+    return "".join(b)
+
+
+def _expand(cigar):
+    import re
+    return "".join(o * (int(n) if n else 1) for n, o in re.findall(r"(\d*)([MDI])", cigar))
+
+
+def _pairs(seed, n, qlens, tl_lo=16, tl_hi=72, ambig=False):
+    rng = random.Random(seed)
+    qs, ts = [], []
+    alpha = "ACGTN" if ambig else "ACGT"
+    for _ in range(n):
+        ql = rng.choice(qlens)
+        q = "".join(rng.choice("ACGT") for _ in range(ql))
+        kind = rng.random()
+        if kind < 0.6:
+            t = _mutate(rng, q, rng.randint(0, 10), alpha)
+        elif kind < 0.8:
+            t = "".join(rng.choice(alpha) for _ in range(rng.randint(tl_lo, tl_hi)))
+        else:
+            t = q[rng.randint(0, 6):] + "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 6)))
+        t = t[:tl_hi] if len(t) >= 1 else "A"
+        if ambig and rng.random() < 0.3:
+            x = rng.randrange(len(q))
+            q = q[:x] + rng.choice("NRYKM") + q[x + 1:]
+        qs.append(q)
+        ts.append(t)
+    return qs, ts
+
+
+@pytest.mark.parametrize("preset,ambig", [(1, False), (2, False), (1, True), (2, True)])
+def test_align_pairs_vs_oracle(gpu_ctx, preset, ambig):
+    p = _lib.params(preset, 0.93, 32, 72)
+    op = orc.params(preset, 0.93, 32, 72)
+    qs, ts = _pairs(100 + preset + 10 * ambig, 3000, list(range(32, 73)), ambig=ambig)
+    r = gpu_ctx.align_pairs(p, qs, ts)
+    tb = gpu_ctx.align_pairs(p, qs, ts, with_ops=True)
+    for k, (q, t) in enumerate(zip(qs, ts)):
+        o = orc.align(op, q, t)
+        got = (int(r["score"][k]), int(r["matches"][k]), int(r["internal_len"][k]))
+        assert got == (o["score"], o["matches"], o["internal_len"]), (k, q, t, got, o)
+        # explicit traceback kernel agrees with both
+        assert tb["ops"][k] == _expand(o["cigar"]), (k, q, t)
+        assert (int(tb["score"][k]), int(tb["matches"][k]), int(tb["internal_len"][k])) == got
+
+
+def test_align_known_answers(gpu_ctx):
+    p = _lib.params(1, 0.93, 32, 72)
+    base = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
+    qs = [base, base, "TT" + base[:62], base[:40] + base[41:], base, "G" + "A" * 33 + "C"]
+    ts = [base, base[:20] + "A" + base[21:], base[:62], base, base + "TT", "G" + "A" * 32 + "C"]
+    r = gpu_ctx.align_pairs(p, qs, ts, with_ops=True)
+    assert int(r["score"][0]) == 640 and int(r["internal_len"][0]) == 64
+    assert int(r["matches"][1]) == 63
+    assert r["ops"][2] == "DD" + "M" * 62  # leading overhang: terminal gap, trimmed
+    assert int(r["internal_len"][2]) == 62
+    assert r["ops"][4] == "M" * 64 + "II"
+    assert r["ops"][5] == "M" + "D" + "M" * 33  # tie: gap placed leftmost (backtrack16 order)
+
+
+def test_prep_vs_oracle(gpu_ctx):
+    rng = random.Random(5)
+    seqs = ["ACACACACACACACACACACACACACACACGTAGCTAGCTAGCATCGATCGATCGTAGCTAGCA",
+            "TTTAAATTTAAATTTAAATTTAAATTTAAATTTAAATTTGGCCGGCCGGCCGGCCGGCAAAAAAAAAAA"[:72]]
+    seqs += synth.make_umis(50, seed=9, max_reads=400).as_list()
+    seqs += ["".join(rng.choice("AC") for _ in range(rng.randint(16, 72))) for _ in range(100)]
+    seqs += ["".join(rng.choice("ACGTN") for _ in range(rng.randint(16, 72))) for _ in range(100)]
+    p = _lib.params(1, 0.93, 1, 72)
+    out = gpu_ctx.prep(p, seqs)
+    from pyref import revcomp
+    for s, m, km in zip(seqs, out["masked"], out["kmers"]):
+        om = orc.dust(s)
+        assert m == om
+        assert sorted(km[0]) == sorted(set(orc.unique_kmers(om, 8, True)))
+        assert sorted(km[1]) == sorted(set(orc.unique_kmers(revcomp(om), 8, True)))
+
+
+def _cmp_cluster(gpu, ora):
+    assert gpu["n_clusters"] == ora["n_clusters"]
+    assert np.array_equal(gpu["cluster"], ora["cluster"])
+    assert np.array_equal(gpu["strand"], ora["strand"])
+    assert np.array_equal(gpu["centroid"], ora["centroid"])
+    assert gpu["consensus"] == ora["consensus"]
+
+
+CASES = [
+    # (n_molecules, seed, max_reads, preset, identity, orient_mix, error_rate)
+    (60, 1, 800, 1, 0.93, 0.0, 0.015),
+    (60, 2, 800, 1, 0.93, 0.4, 0.015),
+    (300, 3, 4000, 1, 0.90, 0.1, 0.015),
+    (300, 4, 4000, 2, 0.97, 0.1, 0.003),
+    (100, 5, 3000, 1, 0.93, 0.2, 0.06),
+    (1500, 6, 30000, 1, 0.93, 0.0, 0.015),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"m{c[0]}_s{c[1]}_p{c[3]}_id{c[4]}" for c in CASES])
+def test_cluster_vs_oracle(gpu_ctx, case):
+    nm, seed, mr, preset, idn, mix, err = case
+    u = synth.make_umis(nm, seed=seed, max_reads=mr, orient_mix=mix, error_rate=err)
+    seqs = u.as_list()
+    gpu_ctx.load(_lib.params(preset, idn, 58, 68), seqs)
+    st = gpu_ctx.cluster()
+    g = gpu_ctx.fetch()
+    o = orc.cluster(orc.params(preset, idn, 58, 68), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"]
+    assert st["cells"] == o["stats"]["cells"]
+
+
+@pytest.mark.parametrize("block", [1, 7, 64, 1000])
+def test_block_size_invariance(block, monkeypatch):
+    """Small greedy blocks stress the in-block dependency resolution (deferred queries, peers)."""
+    u = synth.make_umis(200, seed=21, max_reads=2500, orient_mix=0.2)
+    seqs = u.as_list()
+    monkeypatch.setenv("UMICLUST_BLOCK", str(block))
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.93, 58, 68), seqs)
+        ctx.cluster()
+        g = ctx.fetch()
+    _cmp_cluster(g, orc.cluster(orc.params(1, 0.93, 58, 68), seqs))
+
+
+def test_edge_inputs(gpu_ctx):
+    p = _lib.params(1, 0.93, 58, 68)
+    op = orc.params(1, 0.93, 58, 68)
+    base = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
+    for seqs in ([], ["ACGT"], [base], [base] * 5, [base, base[:57], base + "ACGTA", base[:58], base + "A" * 4],
+                 [base.replace("G", "N", 3)] * 3 + [base]):
+        gpu_ctx.load(p, seqs)
+        gpu_ctx.cluster()
+        g = gpu_ctx.fetch()
+        o = orc.cluster(op, seqs) if seqs else dict(n_clusters=0, cluster=np.zeros(0, np.int32),
+                                                     strand=np.zeros(0, np.uint8),
+                                                     centroid=np.zeros(0, np.uint8), consensus=[])
+        _cmp_cluster(g, o)
+
+
+def _read_dir(d):
+    return {fn: open(os.path.join(d, fn), "rb").read() for fn in sorted(os.listdir(d)) if not fn.endswith(".log")}
+
+
+@pytest.mark.parametrize("round_", [1, 2])
+def test_dropin_files_vs_oracle(tmp_path, round_):
+    from umiclust.vsearch_umi_cluster import vsearch_cluster, vsearch_cluster_consensus
+    u = synth.make_umis(150, seed=31 + round_, max_reads=2500, orient_mix=0.1,
+                       error_rate=0.015 if round_ == 1 else 0.002)
+    fa = tmp_path / "region_cluster7_detected_umis.fasta"
+    synth.write_umi_fasta(str(fa), u)
+    out = tmp_path / "gpu"
+    out.mkdir()
+    if round_ == 1:
+        ret = vsearch_cluster.options(num_cpus=25).remote(umi_fasta=str(fa), clustering_out_dir=str(out),
+                                                          threads=25, min_umi_length=58, max_umi_length=68,
+                                                          identity=0.93)
+        log = "vsearch_cluster.log"
+    else:
+        ret = vsearch_cluster_consensus.options(num_cpus=25).remote(
+            umi_fasta=str(fa), clustering_consensus_out_dir=str(out), threads=25, min_umi_length=58,
+            max_umi_length=68, identity=0.97)
+        log = "vsearch_cluster_consensus.log"
+    assert ret == os.path.join(str(out), "umi_clusters_consensus.fasta")
+    assert (out / log).exists()
+    ref = tmp_path / "oracle"
+    ref.mkdir()
+    op = orc.params(1 if round_ == 1 else 2, 0.93 if round_ == 1 else 0.97, 58, 68)
+    orc.run_fasta(op, str(fa), str(ref) + "/cluster", str(ref / "umi_clusters_consensus.fasta"))
+    assert _read_dir(out) == _read_dir(ref)
+    # the consumer runs unchanged on the GPU outputs
+    from umiclust.parse_umi_clusters import parse_umi_clusters
+    sm = parse_umi_clusters.remote(ret, str(tmp_path / "wo.txt"), min_reads_per_cluster=4, max_reads_per_cluster=60)
+    assert sm and os.path.exists(sm)
+
+
+def test_run_argv_matches_reference_argv(tmp_path):
+    """umiclust_run_argv consumes the exact argv the reference passes to vsearch."""
+    from umiclust.vsearch_umi_cluster import context, round1_argv
+    u = synth.make_umis(40, seed=77, max_reads=600)
+    fa = tmp_path / "in.fasta"
+    synth.write_umi_fasta(str(fa), u)
+    (tmp_path / "o").mkdir()
+    st = context().run_argv(round1_argv(str(fa), str(tmp_path / "o"), 25, 58, 68, 0.93))
+    assert st["n_clusters"] == orc.run_fasta(orc.params(1, 0.93, 58, 68), str(fa), None, None)["n_clusters"]
+
+
+def test_full_scale_properties():
+    """BASELINE config 2 size (2M reads): deterministic across runs and structurally valid."""
+    u = synth.config_umis(2)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.90, 58, 68), buf=u.seq, off=u.off)
+        s1 = ctx.cluster()
+        a = ctx.fetch()
+        s2 = ctx.cluster()
+        b = ctx.fetch()
+    _cmp_cluster(a, b)
+    assert s1["n_alignments"] == s2["n_alignments"] and s1["cells"] == s2["cells"]
+    cl = a["cluster"]
+    k = a["n_clusters"]
+    sizes = np.bincount(cl[cl >= 0], minlength=k)
+    assert np.all(np.diff(sizes) <= 0)  # --clusterout_sort
+    assert int(a["centroid"].sum()) == k
+    lens = np.diff(u.off)
+    cen_len = np.zeros(k, np.int64)
+    cen_len[cl[a["centroid"] == 1]] = lens[a["centroid"] == 1]
+    kept = cl >= 0
+    assert np.all(lens[kept] <= cen_len[cl[kept]])  # centroids are the longest of their cluster
+    assert all(56 <= len(c) <= 72 for c in a["consensus"][:1000])

@@ -1,0 +1,147 @@
+"""The CPU oracle (oracle/umiclust_oracle.c) against hand-derived known answers and against the
+independently written Python restatement (oracle/pyref.py).  Parity with vsearch itself is
+unpinned offline; these tests pin the restatement's internal consistency."""
+import random
+
+import orc
+import pyref
+import pytest
+from umiclust import synth
+
+
+@pytest.fixture(scope="module")
+def r1():
+    return orc.params(1, 0.93)
+
+
+@pytest.fixture(scope="module")
+def r2():
+    return orc.params(2, 0.97)
+
+
+def test_identical(r1):
+    a = orc.align(r1, "ACGTACGTAC", "ACGTACGTAC")
+    assert (a["cigar"], a["score"], a["matches"], a["internal_len"], a["id"]) == ("10M", 100, 10, 10, 100.0)
+
+
+def test_one_mismatch(r1):
+    a = orc.align(r1, "ACGTACGTAC", "ACGTTCGTAC")
+    assert (a["cigar"], a["score"], a["matches"], a["mismatches"], a["id"]) == ("10M", 50, 9, 1, 90.0)
+
+
+def test_internal_deletion_round1(r1):
+    # one extra query residue: interior gap open 40 + ext 2
+    a = orc.align(r1, "ACGTACGTACGGA", "ACGTACTACGGA")
+    assert (a["cigar"], a["score"], a["internal_len"]) == ("6MD6M", 12 * 10 - 42, 13)
+
+
+def test_terminal_gaps_are_trimmed(r1):
+    # leading query overhang: terminal gap open 0, ext 1 (0E); align_trim drops it from the id
+    a = orc.align(r1, "TT" + "ACGTACGTACGGA", "ACGTACGTACGGA")
+    assert (a["cigar"], a["score"], a["trim_left"], a["internal_len"], a["id"]) == ("2D13M", 128, 2, 13, 100.0)
+    b = orc.align(r1, "ACGTACGTACGGA", "ACGTACGTACGGA" + "TT")
+    assert (b["cigar"], b["trim_right"], b["id"]) == ("13M2I", 2, 100.0)
+
+
+def test_terminal_gap_cost_round2(r2):
+    # vsearch defaults: terminal open 2 ext 1
+    a = orc.align(r2, "TT" + "ACGTACGTACGGA", "ACGTACGTACGGA")
+    assert (a["cigar"], a["score"]) == ("2D13M", 13 * 2 - (2 + 2 * 1))
+
+
+def test_tie_places_gap_leftmost(r1):
+    # GAAAC vs GAAC: the D may sit on any A; backtrack16 prefers the diagonal walking back, so the
+    # gap lands on the leftmost A (hand-derived in DESIGN.md)
+    a = orc.align(r1, "GAAAC", "GAAC")
+    assert a["cigar"] == "MD3M"
+    assert a["score"] == 40 - 42
+
+
+def test_only_first_run_trimmed(r1):
+    # a leading D run followed by an I run: only the first run is a terminal gap
+    a = orc.align(r1, "GGGGGACGTACGTAC", "CCACGTACGTAC")
+    assert a["cigar"].startswith(("5D", "2I")) or a["trim_left"] > 0
+    assert a["internal_len"] == a["columns"] - a["trim_left"] - a["trim_right"]
+
+
+def test_n_matches_anything(r1):
+    a = orc.align(r1, "ACGTNCGTAC", "ACGTACGTAC")
+    assert a["matches"] == 10 and a["score"] == 90  # N scores 0 but counts as a match
+
+
+def test_identity_threshold_is_ieee_double():
+    # 100.0*0.93 == 93.0 exactly; 93/100 passes, 92/99 (92.929..) does not
+    assert 100.0 * 93 / 100 >= 100.0 * 0.93
+    assert not (100.0 * 92 / 99 >= 100.0 * 0.93)
+
+
+@pytest.mark.parametrize("preset", [1, 2])
+def test_align_matches_python_restatement(preset):
+    p, pp = orc.params(preset, 0.93), pyref.P(preset, 0.93)
+    rng = random.Random(7 + preset)
+    for _ in range(400):
+        a = "".join(rng.choice("ACGT") for _ in range(rng.randint(16, 40)))
+        b = list(a)
+        for _ in range(rng.randint(0, 8)):
+            x = rng.randrange(len(b))
+            u = rng.random()
+            if u < 0.4:
+                b[x] = rng.choice("ACGT")
+            elif u < 0.7:
+                b.insert(x, rng.choice("ACGT"))
+            elif len(b) > 5:
+                del b[x]
+        b = "".join(b)
+        if rng.random() < 0.1:
+            b = "".join(rng.choice("ACGTN") for _ in range(rng.randint(10, 40)))
+        r = orc.align(p, a, b)
+        sc, cg, mt = pyref.nw(pp, a, b)
+        idv, il = pyref.trim_id(cg, mt)
+        assert (r["score"], r["cigar"], r["matches"], r["internal_len"]) == (sc, cg, mt, il)
+        assert r["id"] == idv
+
+
+def test_dust_masks_low_complexity():
+    s = "ACACACACACACACACACACACACACACACGTAGCTAGCTAGCATCGATCGATCGTAGCTAGCA"
+    m = orc.dust(s)
+    assert m == pyref.dust(s)
+    assert m[:30] == s[:30].lower() and m[30:].isupper()
+    rnd = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
+    assert orc.dust(rnd) == rnd  # a typical UMI is not masked
+
+
+def test_kmers_skip_masked():
+    s = "acgtacgtACGTTGCAAGCTTACG"
+    ks = orc.unique_kmers(s, 8, True)
+    assert set(ks) == pyref.kmers(s, 8, True)
+    assert len(set(orc.unique_kmers(s, 8, False))) == len(pyref.kmers(s, 8, False))
+
+
+@pytest.mark.parametrize("preset,identity", [(1, 0.93), (1, 0.90), (2, 0.97)])
+def test_cluster_matches_python_restatement(preset, identity):
+    u = synth.make_umis(30, seed=11 + preset, max_reads=300, orient_mix=0.3)
+    seqs = u.as_list()
+    r = orc.cluster(orc.params(preset, identity), seqs)
+    c, s, cons = pyref.cluster(pyref.P(preset, identity), seqs)
+    assert list(r["cluster"]) == c
+    assert list(r["strand"]) == s
+    assert r["consensus"] == cons
+
+
+def test_cluster_invariants():
+    u = synth.make_umis(200, seed=5, max_reads=3000)
+    seqs = u.as_list()
+    r = orc.cluster(orc.params(1, 0.93), seqs)
+    k = r["n_clusters"]
+    cl = r["cluster"]
+    sizes = [int((cl == c).sum()) for c in range(k)]
+    assert sizes == sorted(sizes, reverse=True)  # --clusterout_sort
+    assert int(r["centroid"].sum()) == k
+    lens = [len(s) for s in seqs]
+    for c in range(k):
+        mem = [i for i in range(len(seqs)) if cl[i] == c]
+        cen = [i for i in mem if r["centroid"][i]]
+        assert len(cen) == 1
+        # greedy on length-sorted input: the centroid is the longest, earliest record
+        assert lens[cen[0]] == max(lens[i] for i in mem)
+    assert all(cl[i] == -1 for i in range(len(seqs)) if not 58 <= lens[i] <= 68)
