@@ -458,7 +458,10 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   auto peer_relevant_blocked = [&](int32_t qs, int32_t qlocal, bool& blocked, bool& affects) {
     const int np = c->h_npeer.p[qs];
     const WalkState& w = ws[qs];
-    const bool exhausted = !w.acc && w.w < kWalk;  // walk ended because the list ran out
+    // a centroid peer changes the walk if it ranks among the walked candidates, or if the last
+    // batch was not full (the list ended mid-batch: the peer would join that batch), or if the walk
+    // ended because the list ran out
+    const bool open_batch = (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
     for (int x = 0; x < np; x++) {
       const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
       const uint8_t s = state[(size_t)q0 + pl];
@@ -470,7 +473,7 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
         const uint32_t ps = (uint32_t)(q0 + pl);
         const unsigned long long k =
             cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps);
-        if (exhausted || w.w == 0 || k < w.lastkey) affects = true;
+        if (open_batch || k < w.lastkey) affects = true;
       }
     }
     (void)qlocal;
@@ -504,10 +507,8 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       state[q] = ST_MEMBER;
       c->target[q] = (int32_t)best.t;
       c->strand[q] = (uint8_t)bs;
-      c->cno[q] = c->cno[best.t];
     } else {
       state[q] = ST_CENT;
-      c->cno[q] = c->nclusters++;
       new_cents.push_back(q);
     }
   }
@@ -640,10 +641,8 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
         state[q] = ST_MEMBER;
         c->target[q] = (int32_t)best.t;
         c->strand[q] = (uint8_t)bs;
-        c->cno[q] = c->cno[best.t];
       } else {
         state[q] = ST_CENT;
-        c->cno[q] = c->nclusters++;
         new_cents.push_back(q);
       }
     }
@@ -711,6 +710,11 @@ void cluster_all(umiclust_ctx* c) {
     q0 += nq;
     if (B < c->block_size) B = std::min<int32_t>(B * 2, c->block_size);
   }
+  // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's
+  c->nclusters = (int32_t)c->cent.size();
+  for (int32_t k = 0; k < c->nclusters; k++) c->cno[c->cent[k]] = k;
+  for (int32_t s = 0; s < n; s++)
+    if (c->target[s] >= 0) c->cno[s] = c->cno[c->target[s]];
   // --- output numbering: --clusterout_sort orders clusters by size desc, creation order
   const int32_t K = c->nclusters;
   std::vector<int32_t> size(K, 0);
