@@ -81,6 +81,11 @@ typedef struct umiclust_stats {
   double t_align_s;       /* kernel time, alignment */
   double t_consensus_s;   /* kernel time, traceback + consensus */
   double t_host_s;        /* host greedy resolve */
+  int64_t n_deferred;     /* queries resolved by the host's exact merged walk (in-block peers) */
+  int64_t pairs_round_b;  /* alignments issued for deferred queries */
+  int64_t pairs_peer;     /* speculative in-block peer alignments */
+  double t_index_s;       /* kernel time, index tile rebuilds */
+  double t_sync_s;        /* host wall time blocked on device->host result copies */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

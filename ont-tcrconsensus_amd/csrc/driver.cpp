@@ -154,17 +154,14 @@ struct umiclust_ctx {
   DevBuf<uint32_t> d_counters;    // [0] postings, [1..5] npairs per walk round
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
   DevBuf<WalkState> d_ws;
-  DevBuf<int32_t> d_sel;
-  DevBuf<uint32_t> d_g_seqno, d_g_res;
-  DevBuf<uint8_t> d_g_count;
+  DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
   // host pinned mirrors
   PinBuf<WalkState> h_ws;
   PinBuf<uint8_t> h_ntop, h_npeer, h_peer_count;
   PinBuf<uint16_t> h_peer_id;
-  PinBuf<uint32_t> h_g_seqno, h_g_res, h_bpq, h_bpt, h_bres, h_counters;
-  PinBuf<uint8_t> h_g_count;
-  PinBuf<int32_t> h_sel;
+  PinBuf<uint32_t> h_counters, h_peer_res, h_top_seqno, h_res;
+  PinBuf<uint8_t> h_top_count;
 
   // results (sorted order)
   std::vector<int32_t> cno;       // creation cluster number
@@ -263,7 +260,7 @@ void build_tile(umiclust_ctx* c, Tile& t, const int32_t* d_cent_seqno, int32_t f
                 size_t post_cap) {
   c->hip(t.hist_off.ensure(65536 + 65537), "tile alloc");
   c->hip(t.cursor.ensure(65536), "tile alloc");
-  c->hip(t.post.ensure(post_cap), "tile alloc");
+  c->hip(t.post.ensure(post_cap + 16), "tile alloc");  // +16: 16-byte chunk reads past the end
   c->hip(hipMemsetAsync(t.hist_off.p, 0, 65536 * 4, c->st), "tile memset");
   c->hip(hipMemsetAsync(t.cursor.p, 0, 65536 * 4, c->st), "tile memset");
   c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, d_cent_seqno, first, n, t.hist_off.p, c->st),
@@ -363,21 +360,34 @@ void ensure_block_buffers(umiclust_ctx* c, int32_t B) {
   c->hip(c->h_peer_count.ensure(nqs * kPeerCap), "pin");
   c->hip(c->h_peer_id.ensure(nqs * kPeerCap), "pin");
   c->hip(c->h_counters.ensure(16), "pin");
+  c->hip(c->d_ppq.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->d_ppt.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->d_poutidx.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->d_peer_res.ensure(nqs * kPeerCap), "alloc");
+  c->hip(c->h_peer_res.ensure(nqs * kPeerCap), "pin");
+  c->hip(c->h_top_seqno.ensure(nqs * kTopHits), "pin");
+  c->hip(c->h_top_count.ensure(nqs * kTopHits), "pin");
+  c->hip(c->h_res.ensure(nqs * kWalk), "pin");
 }
 
 // Process one block [q0, q0+nq). Returns false if a peer list overflowed (caller shrinks B).
+//
+// One device pass (no host sync inside): peer tile, prefilter, the batch-of-8 walk over T_old
+// (up to 4 align rounds) and the alignment of every in-block peer pair; then one download of the
+// walk states, top lists, walked results and peer results.  The host resolves the block in order:
+// a (query, strand) without centroid peers takes the device walk; otherwise it runs the exact
+// merged walk over T_old u (peers that are centroids).  Only a merged walk that needs a T_old
+// entry the device did not align is deferred to round B (and queries whose peers are deferred).
 bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& state,
                double& t_pf, double& t_al, double& t_host) {
   const int both = c->both;
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
-  // --- peer tile over the block's queries (block-local ids)
   {
     size_t cap = (size_t)nq * kMaxKmers + 16;
     build_tile(c, c->peer_tile, c->d_iota.p, q0, nq, cap);
     c->peer_tile.base = 0;
   }
-  // --- tiles of C_old
   std::vector<TileView> views;
   for (Tile* t : c->tiles)
     if (t->n > 0) views.push_back(view_of(*t));
@@ -407,43 +417,56 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   c->hip(hipEventRecord(c->ev0, st), "event");
   c->hip(launch_prefilter(a, st), "prefilter");
   c->hip(hipEventRecord(c->ev1, st), "event");
-  // --- device walk: init + up to 4 align rounds
   hipEvent_t ea0, ea1;
   c->hip(hipEventCreate(&ea0), "event");
   c->hip(hipEventCreate(&ea1), "event");
   DevSeqs ds = dev_seqs(c);
+  const int32_t qlen = c->hlen[q0];
   c->hip(launch_walk(-1, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
                      c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
                      c->d_outidx.p, c->d_counters.p + 1, st),
          "walk");
   c->hip(hipEventRecord(ea0, st), "event");
   for (int r = 0; r < kWalk / kBatch; r++) {
-    c->hip(launch_align(ds, c->hlen[q0], c->ambig, c->d_pq.p, c->d_pt.p, nqs * kBatch,
-                        c->d_counters.p + 1 + r, c->d_outidx.p, c->sc, c->d_res.p, st),
+    c->hip(launch_align(ds, qlen, c->ambig, c->d_pq.p, c->d_pt.p, nqs * kBatch, c->d_counters.p + 1 + r,
+                        c->d_outidx.p, c->sc, c->d_res.p, st),
            "align");
     c->hip(launch_walk(r, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
                        c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
                        c->d_outidx.p, c->d_counters.p + 2 + r, st),
            "walk");
   }
+  c->hip(launch_peer_pairs(q0, nqs, both, c->d_peer_id.p, c->d_npeer.p, c->d_ppq.p, c->d_ppt.p, c->d_poutidx.p,
+                           c->d_counters.p + 8, st),
+         "peer pairs");
+  c->hip(launch_align(ds, qlen, c->ambig, c->d_ppq.p, c->d_ppt.p, nqs * kPeerCap, c->d_counters.p + 8,
+                      c->d_poutidx.p, c->sc, c->d_peer_res.p, st),
+         "align peers");
   c->hip(hipEventRecord(ea1, st), "event");
-  // --- downloads
-  c->hip(hipMemcpyAsync(c->h_ws.p, c->d_ws.p, (size_t)nqs * sizeof(WalkState), hipMemcpyDeviceToHost, st), "d2h");
-  c->hip(hipMemcpyAsync(c->h_ntop.p, c->d_ntop.p, (size_t)nqs, hipMemcpyDeviceToHost, st), "d2h");
-  c->hip(hipMemcpyAsync(c->h_npeer.p, c->d_npeer.p, (size_t)nqs, hipMemcpyDeviceToHost, st), "d2h");
-  c->hip(hipMemcpyAsync(c->h_peer_id.p, c->d_peer_id.p, (size_t)nqs * kPeerCap * 2, hipMemcpyDeviceToHost, st),
-         "d2h");
-  c->hip(hipMemcpyAsync(c->h_peer_count.p, c->d_peer_count.p, (size_t)nqs * kPeerCap, hipMemcpyDeviceToHost, st),
-         "d2h");
-  c->hip(hipMemcpyAsync(c->h_counters.p, c->d_counters.p, 16 * 4, hipMemcpyDeviceToHost, st), "d2h");
+  // --- one download
+  auto d2h = [&](void* dst, const void* src, size_t bytes) {
+    c->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st), "d2h");
+  };
+  d2h(c->h_ws.p, c->d_ws.p, (size_t)nqs * sizeof(WalkState));
+  d2h(c->h_ntop.p, c->d_ntop.p, (size_t)nqs);
+  d2h(c->h_npeer.p, c->d_npeer.p, (size_t)nqs);
+  d2h(c->h_peer_id.p, c->d_peer_id.p, (size_t)nqs * kPeerCap * 2);
+  d2h(c->h_peer_count.p, c->d_peer_count.p, (size_t)nqs * kPeerCap);
+  d2h(c->h_peer_res.p, c->d_peer_res.p, (size_t)nqs * kPeerCap * 4);
+  d2h(c->h_top_seqno.p, c->d_top_seqno.p, (size_t)nqs * kTopHits * 4);
+  d2h(c->h_top_count.p, c->d_top_count.p, (size_t)nqs * kTopHits);
+  d2h(c->h_res.p, c->d_res.p, (size_t)nqs * kWalk * 4);
+  d2h(c->h_counters.p, c->d_counters.p, 16 * 4);
+  const double tsync0 = now_s();
   c->hip(hipStreamSynchronize(st), "sync");
+  c->stats.t_sync_s += now_s() - tsync0;
   float ms = 0;
   c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
   t_pf += ms * 1e-3;
   c->hip(hipEventElapsedTime(&ms, ea0, ea1), "elapsed");
   t_al += ms * 1e-3;
   c->stats.kmer_postings += c->h_counters.p[0];
-  // overflow?
+  c->stats.pairs_peer += c->h_counters.p[8];
   for (int32_t qs = 0; qs < nqs; qs++)
     if (c->h_npeer.p[qs] == 255) {
       (void)hipEventDestroy(ea0);
@@ -451,55 +474,76 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       return false;
     }
   const double th0 = now_s();
-  // --- host pass 1
   const WalkState* ws = c->h_ws.p;
+  // T_old entries aligned so far: device walk [0, w); round B fills [w, 32)
+  std::vector<uint8_t> have_extra;  // per deferred (qs, x) filled in round B
   std::vector<int32_t> deferred;
   std::vector<int32_t> new_cents;
-  auto peer_relevant_blocked = [&](int32_t qs, int32_t qlocal, bool& blocked, bool& affects) {
+  std::vector<MCand> L;
+  std::vector<uint32_t> extra_res;   // [qs*kWalk + x] results of round B (valid if flag)
+  std::vector<uint8_t> extra_have;
+  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o) -> int {
+    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs T_old entries not aligned
     const int np = c->h_npeer.p[qs];
     const WalkState& w = ws[qs];
-    // a centroid peer changes the walk if it ranks among the walked candidates, or if the last
-    // batch was not full (the list ended mid-batch: the peer would join that batch), or if the walk
-    // ended because the list ran out
-    const bool open_batch = (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
+    bool cent_peer = false;
     for (int x = 0; x < np; x++) {
-      const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
-      const uint8_t s = state[(size_t)q0 + pl];
-      if (s == ST_UNDET) {
-        blocked = true;
-        return;
-      }
-      if (s == ST_CENT) {
-        const uint32_t ps = (uint32_t)(q0 + pl);
-        const unsigned long long k =
-            cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps);
-        if (open_batch || k < w.lastkey) affects = true;
-      }
+      const uint8_t s = state[(size_t)q0 + c->h_peer_id.p[(size_t)qs * kPeerCap + x]];
+      if (s == ST_UNDET) return 1;
+      cent_peer |= (s == ST_CENT);
     }
-    (void)qlocal;
-  };
-  for (int32_t ql = 0; ql < nq; ql++) {
-    const int32_t q = q0 + ql;
-    bool blocked = false, affects = false;
-    for (int s = 0; s < both && !blocked; s++) peer_relevant_blocked(ql * both + s, ql, blocked, affects);
-    if (blocked || affects) {
-      deferred.push_back(ql);
-      continue;
-    }
-    Outcome best;
-    int bs = 0;
-    for (int s = 0; s < both; s++) {
-      const WalkState& w = ws[ql * both + s];
-      Outcome o;
+    if (!cent_peer) {
       o.acc = w.acc;
       o.rank = w.best_rank;
       o.t = w.best_t;
       o.walked = w.w;
       o.cells = w.cells;
-      c->stats.n_alignments += w.w;
-      c->stats.cells += w.cells;
-      if (better(o, best)) {
-        best = o;
+      return 0;
+    }
+    L.clear();
+    const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
+    for (int x = 0; x < nt; x++) {
+      const uint32_t sq = c->h_top_seqno.p[(size_t)qs * kTopHits + x];
+      MCand m;
+      m.key = cand_key(c->h_top_count.p[(size_t)qs * kTopHits + x], c->hlen[sq], sq);
+      m.seqno = sq;
+      if (x < w.w) {
+        m.res = c->h_res.p[(size_t)qs * kWalk + x];
+        m.have = true;
+      } else if (allow_extra && extra_have[(size_t)qs * kWalk + x]) {
+        m.res = extra_res[(size_t)qs * kWalk + x];
+        m.have = true;
+      } else {
+        m.res = 0;
+        m.have = false;
+      }
+      L.push_back(m);
+    }
+    for (int x = 0; x < np; x++) {
+      const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
+      if (state[(size_t)q0 + pl] != ST_CENT) continue;
+      const uint32_t ps = (uint32_t)(q0 + pl);
+      MCand m;
+      m.key = cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps);
+      m.seqno = ps;
+      m.res = c->h_peer_res.p[(size_t)qs * kPeerCap + x];
+      m.have = true;
+      L.push_back(m);
+    }
+    std::sort(L.begin(), L.end(), [](const MCand& x, const MCand& y) { return x.key < y.key; });
+    return merged_walk(c, L, c->hlen[q], o) ? 0 : 2;
+  };
+  auto resolve = [&](int32_t ql, bool allow_extra) -> bool {
+    const int32_t q = q0 + ql;
+    Outcome best, os[2];
+    int bs = 0;
+    for (int s = 0; s < both; s++)
+      if (strand_outcome(ql * both + s, q, allow_extra, os[s]) != 0) return false;
+    for (int s = 0; s < both; s++) {
+      c->stats.n_alignments += os[s].walked;
+      c->stats.cells += os[s].cells;
+      if (better(os[s], best)) {
+        best = os[s];
         bs = s;
       }
     }
@@ -511,55 +555,29 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       state[q] = ST_CENT;
       new_cents.push_back(q);
     }
-  }
+    return true;
+  };
+  for (int32_t ql = 0; ql < nq; ql++)
+    if (!resolve(ql, false)) deferred.push_back(ql);
   t_host += now_s() - th0;
-  // --- round B for deferred queries (in order)
+  c->stats.n_deferred += (int64_t)deferred.size();
+  // --- round B: align every T_old entry a deferred query could still need, then resolve in order
   if (!deferred.empty()) {
-    const int32_t nd = (int32_t)deferred.size();
-    const int32_t nsel = nd * both;
-    c->hip(c->h_sel.ensure(nsel), "pin");
-    for (int32_t i = 0; i < nd; i++)
-      for (int s = 0; s < both; s++) c->h_sel.p[i * both + s] = deferred[i] * both + s;
-    c->hip(c->d_sel.ensure(nsel), "alloc");
-    c->hip(c->d_g_seqno.ensure((size_t)nsel * kWalk), "alloc");
-    c->hip(c->d_g_count.ensure((size_t)nsel * kWalk), "alloc");
-    c->hip(c->d_g_res.ensure((size_t)nsel * kWalk), "alloc");
-    c->hip(c->h_g_seqno.ensure((size_t)nsel * kWalk), "pin");
-    c->hip(c->h_g_count.ensure((size_t)nsel * kWalk), "pin");
-    c->hip(c->h_g_res.ensure((size_t)nsel * kWalk), "pin");
-    c->hip(hipMemcpyAsync(c->d_sel.p, c->h_sel.p, (size_t)nsel * 4, hipMemcpyHostToDevice, st), "h2d");
-    c->hip(launch_gather_blocked(c->d_sel.p, nsel, c->d_top_seqno.p, c->d_top_count.p, c->d_res.p,
-                                 c->d_g_seqno.p, c->d_g_count.p, c->d_g_res.p, st),
-           "gather");
-    c->hip(hipMemcpyAsync(c->h_g_seqno.p, c->d_g_seqno.p, (size_t)nsel * kWalk * 4, hipMemcpyDeviceToHost, st), "d2h");
-    c->hip(hipMemcpyAsync(c->h_g_count.p, c->d_g_count.p, (size_t)nsel * kWalk, hipMemcpyDeviceToHost, st), "d2h");
-    c->hip(hipMemcpyAsync(c->h_g_res.p, c->d_g_res.p, (size_t)nsel * kWalk * 4, hipMemcpyDeviceToHost, st), "d2h");
-    c->hip(hipStreamSynchronize(st), "sync");
     const double th1 = now_s();
-    // pairs: T_old entries not walked + peers that are centroids or undetermined
-    std::vector<uint32_t> bpq, bpt;
-    std::vector<std::pair<int32_t, int32_t>> slot;  // (sel index, entry: <kWalk T_old, >=kWalk peer x)
-    for (int32_t i = 0; i < nsel; i++) {
-      const int32_t qs = c->h_sel.p[i];
-      const int32_t q = q0 + qs / both;
-      const uint32_t s = (uint32_t)(qs % both);
-      const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
-      for (int x = ws[qs].w; x < nt; x++) {
-        bpq.push_back(((uint32_t)q << 1) | s);
-        bpt.push_back(c->h_g_seqno.p[(size_t)i * kWalk + x]);
-        slot.push_back({i, x});
+    std::vector<uint32_t> bpq, bpt, bidx;
+    for (int32_t ql : deferred)
+      for (int s = 0; s < both; s++) {
+        const int32_t qs = ql * both + s;
+        const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
+        for (int x = ws[qs].w; x < nt; x++) {
+          bpq.push_back(((uint32_t)(q0 + ql) << 1) | (uint32_t)s);
+          bpt.push_back(c->h_top_seqno.p[(size_t)qs * kTopHits + x]);
+          bidx.push_back((uint32_t)(qs * kWalk + x));
+        }
       }
-      const int np = c->h_npeer.p[qs];
-      for (int x = 0; x < np; x++) {
-        const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
-        if (state[(size_t)q0 + pl] == ST_MEMBER) continue;
-        bpq.push_back(((uint32_t)q << 1) | s);
-        bpt.push_back((uint32_t)(q0 + pl));
-        slot.push_back({i, kWalk + x});
-      }
-    }
     t_host += now_s() - th1;
     const int32_t nb = (int32_t)bpq.size();
+    c->stats.pairs_round_b += nb;
     std::vector<uint32_t> bres(nb);
     if (nb > 0) {
       c->hip(c->d_bpq.ensure(nb), "alloc");
@@ -568,10 +586,8 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
       c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
       c->hip(hipEventRecord(ea0, st), "event");
-      c->hip(launch_align(ds, c->hlen[q0], c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc,
-                          c->d_bres.p, st),
+      c->hip(launch_align(ds, qlen, c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc, c->d_bres.p, st),
              "align B");
-      for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[q0] * c->hlen[bpt[x]];
       c->hip(hipEventRecord(ea1, st), "event");
       c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st), "d2h");
       c->hip(hipStreamSynchronize(st), "sync");
@@ -579,73 +595,15 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       t_al += ms * 1e-3;
     }
     const double th2 = now_s();
-    // peer results indexed [sel][x]
-    std::vector<uint32_t> peer_res((size_t)nsel * kPeerCap, 0);
-    std::vector<uint8_t> peer_have((size_t)nsel * kPeerCap, 0);
-    std::vector<uint32_t> tres((size_t)nsel * kWalk);
-    std::vector<uint8_t> thave((size_t)nsel * kWalk, 0);
-    for (int32_t i = 0; i < nsel; i++) {
-      const int32_t qs = c->h_sel.p[i];
-      for (int x = 0; x < ws[qs].w; x++) {
-        tres[(size_t)i * kWalk + x] = c->h_g_res.p[(size_t)i * kWalk + x];
-        thave[(size_t)i * kWalk + x] = 1;
-      }
+    extra_res.assign((size_t)nqs * kWalk, 0);
+    extra_have.assign((size_t)nqs * kWalk, 0);
+    for (int32_t x = 0; x < nb; x++) {
+      extra_res[bidx[x]] = bres[x];
+      extra_have[bidx[x]] = 1;
     }
-    for (int32_t k = 0; k < nb; k++) {
-      const int32_t i = slot[k].first, x = slot[k].second;
-      if (x < kWalk) {
-        tres[(size_t)i * kWalk + x] = bres[k];
-        thave[(size_t)i * kWalk + x] = 1;
-      } else {
-        peer_res[(size_t)i * kPeerCap + (x - kWalk)] = bres[k];
-        peer_have[(size_t)i * kPeerCap + (x - kWalk)] = 1;
-      }
-    }
-    // --- pass 2: exact merged walks in order
-    std::vector<MCand> L;
-    for (int32_t di = 0; di < nd; di++) {
-      const int32_t qlc = deferred[di];
-      const int32_t q = q0 + qlc;
-      Outcome best;
-      int bs = 0;
-      for (int s = 0; s < both; s++) {
-        const int32_t i = di * both + s;
-        const int32_t qs = qlc * both + s;
-        L.clear();
-        const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
-        for (int x = 0; x < nt; x++) {
-          const uint32_t sq = c->h_g_seqno.p[(size_t)i * kWalk + x];
-          L.push_back({cand_key(c->h_g_count.p[(size_t)i * kWalk + x], c->hlen[sq], sq), sq,
-                       tres[(size_t)i * kWalk + x], thave[(size_t)i * kWalk + x] != 0});
-        }
-        const int np = c->h_npeer.p[qs];
-        for (int x = 0; x < np; x++) {
-          const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
-          if (state[(size_t)q0 + pl] != ST_CENT) continue;
-          const uint32_t ps = (uint32_t)(q0 + pl);
-          L.push_back({cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps), ps,
-                       peer_res[(size_t)i * kPeerCap + x], peer_have[(size_t)i * kPeerCap + x] != 0});
-        }
-        std::sort(L.begin(), L.end(), [](const MCand& a, const MCand& b) { return a.key < b.key; });
-        Outcome o;
-        if (!merged_walk(c, L, c->hlen[q], o))
-          c->fail(UMICLUST_EDEVICE, "internal: missing alignment in merged walk (q=%d)", q);
-        c->stats.n_alignments += o.walked;
-        c->stats.cells += o.cells;
-        if (better(o, best)) {
-          best = o;
-          bs = s;
-        }
-      }
-      if (best.acc) {
-        state[q] = ST_MEMBER;
-        c->target[q] = (int32_t)best.t;
-        c->strand[q] = (uint8_t)bs;
-      } else {
-        state[q] = ST_CENT;
-        new_cents.push_back(q);
-      }
-    }
+    for (int32_t ql : deferred)
+      if (!resolve(ql, true))
+        c->fail(UMICLUST_EDEVICE, "internal: deferred query %d still unresolved", q0 + ql);
     t_host += now_s() - th2;
     std::sort(new_cents.begin(), new_cents.end());
   }
@@ -660,6 +618,7 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
            "h2d cent");
     int32_t ord = ord0;
     const int32_t ordend = (int32_t)c->cent.size();
+    c->hip(hipEventRecord(c->ev0, st), "event");
     while (ord < ordend) {
       Tile* t = c->tiles.empty() ? nullptr : c->tiles.back();
       if (!t || t->n >= kTile) {
@@ -673,6 +632,10 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       build_tile(c, *t, c->d_cent.p, t->base, newn, (size_t)kTile * kMaxKmers);
       ord += take;
     }
+    c->hip(hipEventRecord(c->ev1, st), "event");
+    c->hip(hipEventSynchronize(c->ev1), "sync");
+    c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
+    c->stats.t_index_s += ms * 1e-3;
   }
   return true;
 }

@@ -286,20 +286,32 @@ hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int
 }
 
 // ------------------------------------------------------------------ K2: prefilter
-// One workgroup per (query, strand).  Per index tile: u8 counters (4 per u32) for up to 65536
-// centroids in 64 KiB of LDS; every posting of every query k-mer is one ds_add_rtn_u32; the
-// posting that lifts a counter to the threshold min(12, #kmers) appends the centroid to an LDS
-// candidate list.  After the tile, candidates get 30-bit keys (count desc, length asc, id asc),
-// are bitonic-sorted and merged into the running top-41 (u64 keys over all tiles).  A threshold
-// of 0, or more crossers than the buffer holds, switches the tile to a chunked full scan, so the
-// result is exact in every case.
-constexpr int kPfThreads = 256;
+// One 512-thread workgroup per (query, strand).  Per index tile: u8 counters (4 per u32) for up to
+// 65536 centroids in 64 KiB of LDS.
+//  count: the query's <= 65 posting lists are walked as one flat sequence of 16-byte chunks (8 u16
+//         postings); each thread keeps 4 chunk loads in flight, then issues fire-and-forget
+//         ds_add_u32 for the postings inside its list range (the memory system, not the atomics,
+//         must be kept busy: one dependent 2-byte load per atomic was latency-bound);
+//  scan:  the counters are read back 16 bytes per lane and a SWAR test finds every byte >= the
+//         threshold min(12, #kmers) (searchcore.cc search_topscores' `count >= minmatches`);
+//  top:   candidates get 30-bit keys (count desc, length asc, id asc), are bitonic-sorted and
+//         merged into the running top-41 (u64 keys over all tiles; minheap.cc order).
+// A threshold of 0, or more candidates than the LDS buffer holds, switches the tile to a chunked
+// exact path, so the result is exact in every case.
+constexpr int kPfThreads = 512;
+constexpr int kPfUnroll = 4;
+constexpr int kRankSel = 1024;  // candidate counts up to this are selected by rank
 
 struct PfShared {
   uint32_t cnt[kTile / 4];        // 64 KiB packed u8 counters
   uint32_t cand[kCandCap];        // candidate local ids, then 30-bit keys
   unsigned long long top[kTopHits];
   unsigned long long merged[kTopHits];
+  uint32_t best[kPeerCap + 1];    // the tile's best keys in order
+  unsigned long long bestk[kTopHits];
+  uint32_t kbeg[kMaxKmers + 3];   // posting range [kbeg, kend) of each query k-mer in this tile
+  uint32_t kend[kMaxKmers + 3];
+  uint32_t kchunk[kMaxKmers + 4]; // prefix sum of 16-byte chunks per list
   uint16_t km[kMaxKmers + 3];
   uint32_t ncand;
   uint32_t overflow;
@@ -331,6 +343,21 @@ __device__ void bitonic_u32(uint32_t* a, int n) {
   }
 }
 
+__device__ __forceinline__ void pf_add(uint32_t* cnt, uint32_t c) {
+  atomicAdd(&cnt[c >> 2], 1u << ((c & 3) * 8));  // result unused -> ds_add_u32 (no return)
+}
+
+__device__ __forceinline__ void pf_chunk(uint32_t* cnt, const uint4& v, uint32_t base, uint32_t lo,
+                                         uint32_t hi) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const uint32_t idx = base + (uint32_t)e;
+    const uint32_t c = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+    if (idx >= lo && idx < hi) pf_add(cnt, c);
+  }
+}
+
 __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
@@ -355,35 +382,99 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
     if (peer) tv = a.peer;
     else tv = a.tiles[t];
     if (tv.n == 0) continue;
-    const int nwords = (tv.n + 3) >> 2;
-    for (int x = tid; x < nwords; x += kPfThreads) S.cnt[x] = 0;
+    // zero the counters (whole uint4 groups: the scan reads 16 counters per lane)
+    const int nq4 = (tv.n + 15) >> 4;
+    uint4* cnt4 = reinterpret_cast<uint4*>(S.cnt);
+    for (int x = tid; x < nq4; x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < nk) {
+      const uint32_t b = tv.off[S.km[tid]], e = tv.off[S.km[tid] + 1];
+      S.kbeg[tid] = b;
+      S.kend[tid] = e;
+    }
     if (tid == 0) {
       S.ncand = 0;
       S.overflow = 0;
     }
     __syncthreads();
+    if (tid < 64) {
+      // exclusive prefix of 16-byte chunk counts over the <= 65 lists (wave 0, shuffles)
+      uint32_t carry = 0, touched = 0;
+      for (int k0 = 0; k0 < nk; k0 += 64) {
+        const int k = k0 + tid;
+        uint32_t nch = 0;
+        if (k < nk) {
+          const uint32_t b = S.kbeg[k], e = S.kend[k];
+          touched += e - b;
+          nch = (e > b) ? ((e - (b & ~7u) + 7u) >> 3) : 0u;
+        }
+        uint32_t inc = nch;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t v = __shfl_up(inc, d, 64);
+          if (tid >= d) inc += v;
+        }
+        if (k < nk) S.kchunk[k] = carry + inc - nch;
+        carry += __shfl(inc, 63, 64);
+      }
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) touched += __shfl_xor(touched, d, 64);
+      if (tid == 0) {
+        S.kchunk[nk] = carry;
+        S.post_local += touched;
+      }
+    }
+    __syncthreads();
     if (thr > 0) {
-      uint32_t touched = 0;
-      for (int k = 0; k < nk; k++) {
-        const uint32_t beg = tv.off[S.km[k]], end = tv.off[S.km[k] + 1];
-        touched += end - beg;
-        for (uint32_t x = beg + tid; x < end; x += kPfThreads) {
-          const uint32_t c = tv.post[x];
-          const uint32_t sh = (c & 3) * 8;
-          const uint32_t old = atomicAdd(&S.cnt[c >> 2], 1u << sh);
-          if (((old >> sh) & 0xffu) + 1 == (uint32_t)thr) {
-            const uint32_t slot = atomicAdd(&S.ncand, 1u);
-            if (slot < (uint32_t)kCandCap) S.cand[slot] = c;
-            else S.overflow = 1;
+      const uint32_t total = S.kchunk[nk];
+      int k = 0;
+      for (uint32_t g0 = (uint32_t)tid; g0 < total; g0 += kPfThreads * kPfUnroll) {
+        uint4 v[kPfUnroll];
+        uint32_t base[kPfUnroll], lo[kPfUnroll], hi[kPfUnroll];
+#pragma unroll
+        for (int u = 0; u < kPfUnroll; u++) {
+          const uint32_t g = g0 + (uint32_t)(u * kPfThreads);
+          lo[u] = hi[u] = base[u] = 0;
+          if (g < total) {
+            while (S.kchunk[k + 1] <= g) k++;
+            base[u] = (S.kbeg[k] & ~7u) + 8u * (g - S.kchunk[k]);
+            lo[u] = S.kbeg[k];
+            hi[u] = S.kend[k];
+            v[u] = *reinterpret_cast<const uint4*>(tv.post + base[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPfUnroll; u++)
+          if (hi[u] > lo[u]) pf_chunk(S.cnt, v[u], base[u], lo[u], hi[u]);
+      }
+    }
+    __syncthreads();
+    // scan: every counter >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
+    const int limit = peer ? min(tv.n, qlocal) : tv.n;  // peers: only earlier queries of the block
+    if (thr > 0) {
+      const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
+      const int lim4 = (limit + 15) >> 4;
+      for (int x = tid; x < lim4; x += kPfThreads) {
+        const uint4 v = cnt4[x];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          uint32_t m = (w[j] + add) & 0x80808080u;
+          while (m) {
+            const uint32_t byte = (uint32_t)__builtin_ctz(m) >> 3;
+            m &= m - 1u;
+            const uint32_t c = (uint32_t)x * 16u + (uint32_t)j * 4u + byte;
+            if ((int)c < limit) {
+              const uint32_t slot = atomicAdd(&S.ncand, 1u);
+              if (slot < (uint32_t)kCandCap) S.cand[slot] = c;
+              else S.overflow = 1;
+            }
           }
         }
       }
-      if (tid == 0) S.post_local += touched;
     }
     __syncthreads();
     const bool scan_mode = (thr == 0) || S.overflow;
-    // chunks: either the crosser list (one chunk) or the whole tile in kCandCap slices
-    const int nchunks = scan_mode ? (tv.n + kCandCap - 1) / kCandCap : 1;
+    const int nchunks = scan_mode ? (limit + kCandCap - 1) / kCandCap : 1;
     for (int ch = 0; ch < nchunks; ch++) {
       int nc;
       if (scan_mode) {
@@ -391,57 +482,84 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
         if (tid == 0) S.ncand = 0;
         __syncthreads();
         const int c0 = ch * kCandCap;
-        const int c1 = min(tv.n, c0 + kCandCap);
+        const int c1 = min(limit, c0 + kCandCap);
         for (int c = c0 + tid; c < c1; c += kPfThreads)
           if ((int)cnt_get(S.cnt, (uint32_t)c) >= thr) S.cand[atomicAdd(&S.ncand, 1u)] = (uint32_t)c;
         __syncthreads();
       }
       nc = (int)min(S.ncand, (uint32_t)kCandCap);
-      // keys: (127-count) << 23 | len << 16 | local id   (30 bits)
+      // keys: (127-count) << 23 | len << 16 | local id   (30 bits, unique within a tile; local-id
+      // order is seqno order, so key order is (count desc, length asc, seqno asc))
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(S.cnt, c);
         const int32_t sq = peer ? (a.q0 + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
-        uint32_t key = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
-        if (peer && (int)c >= qlocal) key = 0xffffffffu;  // only earlier queries of the block
-        S.cand[x] = key;
+        S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
       }
-      int np2 = 1;
-      while (np2 < nc) np2 <<= 1;
-      for (int x = nc + tid; x < np2; x += kPfThreads) S.cand[x] = 0xffffffffu;
       __syncthreads();
-      if (np2 > 1) bitonic_u32(S.cand, np2);
+      // best K of the tile in key order: by rank (all-pairs count, broadcast LDS reads) when the
+      // candidate set is small, by a bitonic sort otherwise
+      const int K = peer ? kPeerCap + 1 : kTopHits;
+      int nbest = nc < K ? nc : K;
+      if (nc <= kRankSel) {
+        for (int x = tid; x < nc; x += kPfThreads) {
+          const uint32_t kx = S.cand[x];
+          int r = 0;
+          for (int y = 0; y < nc; y++) r += S.cand[y] < kx;
+          if (r < K) S.best[r] = kx;
+        }
+      } else {
+        int np2 = 1;
+        while (np2 < nc) np2 <<= 1;
+        for (int x = nc + tid; x < np2; x += kPfThreads) S.cand[x] = 0xffffffffu;
+        __syncthreads();
+        bitonic_u32(S.cand, np2);
+        for (int x = tid; x < nbest; x += kPfThreads) S.best[x] = S.cand[x];
+      }
+      __syncthreads();
       if (peer) {
-        if (tid == 0) {
-          for (int x = 0; x < nc; x++) {
-            const uint32_t key = S.cand[x];
-            if (key == 0xffffffffu) break;
-            if (npeer < kPeerCap) {
-              a.peer_id[(int64_t)qs * kPeerCap + npeer] = (uint16_t)(key & 0xffffu);
-              a.peer_count[(int64_t)qs * kPeerCap + npeer] = (uint8_t)(127u - (key >> 23));
-            }
-            npeer++;
-          }
+        if (tid < nbest && npeer + tid < kPeerCap) {
+          const uint32_t key = S.best[tid];
+          a.peer_id[(int64_t)qs * kPeerCap + npeer + tid] = (uint16_t)(key & 0xffffu);
+          a.peer_count[(int64_t)qs * kPeerCap + npeer + tid] = (uint8_t)(127u - (key >> 23));
         }
-      } else if (tid == 0) {
-        // merge sorted S.cand[0..nc) into running top (u64: (127-count)<<56 | len<<48 | seqno)
-        int i = 0, j = 0, o = 0;
+        npeer += nc;
+      } else {
+        // merge the tile's best into the running top-41 (u64 keys, unique seqnos): every element
+        // of either sorted list finds its merged position by binary search in the other list
         const int ntop = S.ntop;
-        while (o < kTopHits && (i < ntop || j < nc)) {
-          unsigned long long kj = ~0ull;
-          if (j < nc) {
-            const uint32_t key = S.cand[j];
-            const uint32_t c = key & 0xffffu;
-            kj = ((unsigned long long)(key >> 23) << 56) |
-                 ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
-                 (unsigned long long)(uint32_t)a.cent_seqno[tv.base + (int32_t)c];
-          }
-          const unsigned long long ki = (i < ntop) ? S.top[i] : ~0ull;
-          if (ki <= kj) { S.merged[o++] = ki; i++; }
-          else { S.merged[o++] = kj; j++; }
+        if (tid < nbest) {
+          const uint32_t key = S.best[tid];
+          S.bestk[tid] = ((unsigned long long)(key >> 23) << 56) |
+                         ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
+                         (unsigned long long)(uint32_t)a.cent_seqno[tv.base + (int32_t)(key & 0xffffu)];
         }
-        for (int x = 0; x < o; x++) S.top[x] = S.merged[x];
-        S.ntop = o;
+        __syncthreads();
+        if (tid < nbest) {
+          const unsigned long long kj = S.bestk[tid];
+          int lo = 0, hi = ntop;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (S.top[mid] < kj) lo = mid + 1;
+            else hi = mid;
+          }
+          if (tid + lo < kTopHits) S.merged[tid + lo] = kj;
+        } else if (tid >= 64 && tid - 64 < ntop) {
+          const int i = tid - 64;
+          const unsigned long long ki = S.top[i];
+          int lo = 0, hi = nbest;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (S.bestk[mid] < ki) lo = mid + 1;
+            else hi = mid;
+          }
+          if (i + lo < kTopHits) S.merged[i + lo] = ki;
+        }
+        __syncthreads();
+        const int nm = min(kTopHits, ntop + nbest);
+        if (tid < nm) S.top[tid] = S.merged[tid];
+        __syncthreads();
+        if (tid == 0) S.ntop = nm;
       }
       __syncthreads();
     }
@@ -734,28 +852,31 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
   return hipGetLastError();
 }
 
-// gather the candidate lists and walked results of selected query-strands (host round B)
-__global__ void k_gather_blocked(const int32_t* __restrict__ sel, int32_t nsel,
-                                 const uint32_t* __restrict__ top_seqno,
-                                 const uint8_t* __restrict__ top_count,
-                                 const uint32_t* __restrict__ res, uint32_t* __restrict__ g_seqno,
-                                 uint8_t* __restrict__ g_count, uint32_t* __restrict__ g_res) {
+// every in-block peer pair (query vs an earlier query of the block that passed the k-mer
+// threshold) is aligned speculatively in the same pass, so the host can run the exact merged walk
+// without another round trip whichever peers turn out to be centroids
+__global__ void k_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* __restrict__ peer_id,
+                             const uint8_t* __restrict__ npeer, uint32_t* __restrict__ pq,
+                             uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
+                             uint32_t* __restrict__ npairs) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nsel * kWalk) return;
-  const int i = k / kWalk, x = k % kWalk;
-  const int qs = sel[i];
-  g_seqno[k] = top_seqno[(int64_t)qs * kTopHits + x];
-  g_count[k] = top_count[(int64_t)qs * kTopHits + x];
-  g_res[k] = res[(int64_t)qs * kWalk + x];
+  if (k >= nqs * kPeerCap) return;
+  const int qs = k / kPeerCap, x = k % kPeerCap;
+  const int np = npeer[qs];
+  if (np == 255 || x >= np) return;
+  const uint32_t slot = atomicAdd(npairs, 1u);
+  pq[slot] = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  pt[slot] = (uint32_t)(q0 + peer_id[(int64_t)qs * kPeerCap + x]);
+  outidx[slot] = (uint32_t)k;
 }
 
-hipError_t launch_gather_blocked(const int32_t* sel, int32_t nsel, const uint32_t* top_seqno,
-                                 const uint8_t* top_count, const uint32_t* res, uint32_t* g_seqno,
-                                 uint8_t* g_count, uint32_t* g_res, hipStream_t st) {
-  if (nsel <= 0) return hipSuccess;
-  const int n = nsel * kWalk;
-  hipLaunchKernelGGL(k_gather_blocked, dim3((n + 255) / 256), dim3(256), 0, st, sel, nsel, top_seqno,
-                     top_count, res, g_seqno, g_count, g_res);
+hipError_t launch_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* peer_id,
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
+                             uint32_t* npairs, hipStream_t st) {
+  const int n = nqs * kPeerCap;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_peer_pairs, dim3((n + 255) / 256), dim3(256), 0, st, q0, nqs, both, peer_id, npeer,
+                     pq, pt, outidx, npairs);
   return hipGetLastError();
 }
 

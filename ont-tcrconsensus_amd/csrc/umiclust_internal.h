@@ -100,9 +100,9 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
                        uint32_t* outidx, uint32_t* npairs, hipStream_t st);
-hipError_t launch_gather_blocked(const int32_t* sel, int32_t nsel, const uint32_t* top_seqno,
-                                 const uint8_t* top_count, const uint32_t* res, uint32_t* g_seqno,
-                                 uint8_t* g_count, uint32_t* g_res, hipStream_t st);
+hipError_t launch_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* peer_id,
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
+                             uint32_t* npairs, hipStream_t st);
 // traceback: ops[k*kOpsStride...] ('M','D','I' in alignment order), nops[k]
 hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
                             int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,

@@ -64,6 +64,11 @@ class Stats(C.Structure):
         ("t_align_s", C.c_double),
         ("t_consensus_s", C.c_double),
         ("t_host_s", C.c_double),
+        ("n_deferred", C.c_int64),
+        ("pairs_round_b", C.c_int64),
+        ("pairs_peer", C.c_int64),
+        ("t_index_s", C.c_double),
+        ("t_sync_s", C.c_double),
     ]
 
     def as_dict(self) -> dict:
