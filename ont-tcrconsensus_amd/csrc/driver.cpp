@@ -92,6 +92,8 @@ struct PinBuf {
   }
 };
 
+constexpr int32_t kDelta = 8192;  // centroids in the per-block delta tile before folding into base
+
 struct Tile {
   DevBuf<uint32_t> hist_off;  // [65536 hist][65537 off]
   DevBuf<uint32_t> cursor;    // [65536]
@@ -141,8 +143,12 @@ struct umiclust_ctx {
   DevBuf<uint16_t> d_rank;
   std::vector<uint8_t> h_acc;
   std::vector<uint16_t> h_rank;
-  // device: index
-  std::vector<Tile*> tiles;
+  // device: index = sealed tiles (kTile centroids each, built once) + an open base tile (rebuilt
+  // every kDelta new centroids) + a delta tile (rebuilt every block): an LSM layout, so a block
+  // only rebuilds postings of at most kDelta centroids
+  std::vector<Tile*> tiles;       // sealed
+  Tile base_tile, delta_tile;
+  int32_t sealed_end = 0, base_end = 0;
   Tile peer_tile;
   DevBuf<TileView> d_tiles;
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
@@ -391,6 +397,8 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   std::vector<TileView> views;
   for (Tile* t : c->tiles)
     if (t->n > 0) views.push_back(view_of(*t));
+  if (c->base_tile.n > 0) views.push_back(view_of(c->base_tile));
+  if (c->delta_tile.n > 0) views.push_back(view_of(c->delta_tile));
   c->hip(c->d_tiles.ensure(views.size() + 1), "alloc tiles");
   if (!views.empty())
     c->hip(hipMemcpyAsync(c->d_tiles.p, views.data(), views.size() * sizeof(TileView),
@@ -480,19 +488,32 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   std::vector<int32_t> deferred;
   std::vector<int32_t> new_cents;
   std::vector<MCand> L;
-  std::vector<uint32_t> extra_res;   // [qs*kWalk + x] results of round B (valid if flag)
+  std::vector<std::pair<unsigned long long, int>> cp;
+  std::vector<uint32_t> extra_res;   // [row*kWalk + x] results of round B (valid if flag)
   std::vector<uint8_t> extra_have;
+  std::vector<int32_t> extra_row;    // qs -> row of the round-B arrays (-1: none)
   auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o) -> int {
     // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs T_old entries not aligned
     const int np = c->h_npeer.p[qs];
     const WalkState& w = ws[qs];
-    bool cent_peer = false;
+    // a centroid peer changes the device walk only if it ranks among the walked candidates, or the
+    // last walked batch was not full (the list ended mid-batch: the peer would join that batch), or
+    // the walk ended because the list ran out
+    const bool open_batch = (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
+    int ncp = 0;
+    bool affects = false;
+    const uint16_t* pid = c->h_peer_id.p + (size_t)qs * kPeerCap;
+    const uint8_t* pcnt = c->h_peer_count.p + (size_t)qs * kPeerCap;
     for (int x = 0; x < np; x++) {
-      const uint8_t s = state[(size_t)q0 + c->h_peer_id.p[(size_t)qs * kPeerCap + x]];
+      const uint8_t s = state[(size_t)q0 + pid[x]];
       if (s == ST_UNDET) return 1;
-      cent_peer |= (s == ST_CENT);
+      if (s == ST_CENT) {
+        ncp++;
+        const uint32_t ps = (uint32_t)(q0 + pid[x]);
+        affects |= open_batch || cand_key(pcnt[x], c->hlen[ps], ps) < w.lastkey;
+      }
     }
-    if (!cent_peer) {
+    if (!affects) {
       o.acc = w.acc;
       o.rank = w.best_rank;
       o.t = w.best_t;
@@ -500,37 +521,50 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       o.cells = w.cells;
       return 0;
     }
+    // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
+    // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
+    cp.clear();
+    for (int y = 0; y < np; y++)
+      if (state[(size_t)q0 + pid[y]] == ST_CENT) {
+        const uint32_t ps = (uint32_t)(q0 + pid[y]);
+        cp.push_back({cand_key(pcnt[y], c->hlen[ps], ps), y});
+      }
+    std::sort(cp.begin(), cp.end());
     L.clear();
     const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
-    for (int x = 0; x < nt; x++) {
-      const uint32_t sq = c->h_top_seqno.p[(size_t)qs * kTopHits + x];
+    const uint32_t* ts = c->h_top_seqno.p + (size_t)qs * kTopHits;
+    const uint8_t* tc = c->h_top_count.p + (size_t)qs * kTopHits;
+    int i = 0;
+    size_t x = 0;
+    while ((int)L.size() < kWalk && (i < nt || x < cp.size())) {
+      const unsigned long long kt = (i < nt) ? cand_key(tc[i], c->hlen[ts[i]], ts[i]) : ~0ull;
+      const unsigned long long kp = (x < cp.size()) ? cp[x].first : ~0ull;
       MCand m;
-      m.key = cand_key(c->h_top_count.p[(size_t)qs * kTopHits + x], c->hlen[sq], sq);
-      m.seqno = sq;
-      if (x < w.w) {
-        m.res = c->h_res.p[(size_t)qs * kWalk + x];
-        m.have = true;
-      } else if (allow_extra && extra_have[(size_t)qs * kWalk + x]) {
-        m.res = extra_res[(size_t)qs * kWalk + x];
-        m.have = true;
+      if (kt < kp) {
+        m.key = kt;
+        m.seqno = ts[i];
+        if (i < w.w) {
+          m.res = c->h_res.p[(size_t)qs * kWalk + i];
+          m.have = true;
+        } else if (allow_extra && extra_row[qs] >= 0 && extra_have[(size_t)extra_row[qs] * kWalk + i]) {
+          m.res = extra_res[(size_t)extra_row[qs] * kWalk + i];
+          m.have = true;
+        } else {
+          m.res = 0;
+          m.have = false;
+        }
+        i++;
       } else {
-        m.res = 0;
-        m.have = false;
+        const int y = cp[x].second;
+        m.key = kp;
+        m.seqno = (uint32_t)(q0 + pid[y]);
+        m.res = c->h_peer_res.p[(size_t)qs * kPeerCap + y];
+        m.have = true;
+        x++;
       }
       L.push_back(m);
     }
-    for (int x = 0; x < np; x++) {
-      const int32_t pl = c->h_peer_id.p[(size_t)qs * kPeerCap + x];
-      if (state[(size_t)q0 + pl] != ST_CENT) continue;
-      const uint32_t ps = (uint32_t)(q0 + pl);
-      MCand m;
-      m.key = cand_key(c->h_peer_count.p[(size_t)qs * kPeerCap + x], c->hlen[ps], ps);
-      m.seqno = ps;
-      m.res = c->h_peer_res.p[(size_t)qs * kPeerCap + x];
-      m.have = true;
-      L.push_back(m);
-    }
-    std::sort(L.begin(), L.end(), [](const MCand& x, const MCand& y) { return x.key < y.key; });
+    (void)ncp;
     return merged_walk(c, L, c->hlen[q], o) ? 0 : 2;
   };
   auto resolve = [&](int32_t ql, bool allow_extra) -> bool {
@@ -595,11 +629,15 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       t_al += ms * 1e-3;
     }
     const double th2 = now_s();
-    extra_res.assign((size_t)nqs * kWalk, 0);
-    extra_have.assign((size_t)nqs * kWalk, 0);
+    extra_row.assign((size_t)nqs, -1);
+    for (size_t r = 0; r < deferred.size(); r++)
+      for (int s = 0; s < both; s++) extra_row[(size_t)deferred[r] * both + s] = (int32_t)(r * both + s);
+    extra_res.assign(deferred.size() * both * kWalk, 0);
+    extra_have.assign(deferred.size() * both * kWalk, 0);
     for (int32_t x = 0; x < nb; x++) {
-      extra_res[bidx[x]] = bres[x];
-      extra_have[bidx[x]] = 1;
+      const int32_t qs = (int32_t)(bidx[x] / kWalk), e = (int32_t)(bidx[x] % kWalk);
+      extra_res[(size_t)extra_row[qs] * kWalk + e] = bres[x];
+      extra_have[(size_t)extra_row[qs] * kWalk + e] = 1;
     }
     for (int32_t ql : deferred)
       if (!resolve(ql, true))
@@ -616,22 +654,27 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
     c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4,
                           hipMemcpyHostToDevice, st),
            "h2d cent");
-    int32_t ord = ord0;
     const int32_t ordend = (int32_t)c->cent.size();
     c->hip(hipEventRecord(c->ev0, st), "event");
-    while (ord < ordend) {
-      Tile* t = c->tiles.empty() ? nullptr : c->tiles.back();
-      if (!t || t->n >= kTile) {
-        t = new Tile();
-        t->base = ord;
-        t->n = 0;
-        c->tiles.push_back(t);
-      }
-      const int32_t take = std::min(ordend - ord, kTile - t->n);
-      const int32_t newn = t->n + take;
-      build_tile(c, *t, c->d_cent.p, t->base, newn, (size_t)kTile * kMaxKmers);
-      ord += take;
+    while (ordend - c->sealed_end >= kTile) {  // seal a full tile
+      Tile* t = new Tile();
+      t->base = c->sealed_end;
+      build_tile(c, *t, c->d_cent.p, t->base, kTile, (size_t)kTile * kMaxKmers);
+      c->tiles.push_back(t);
+      c->sealed_end += kTile;
+      c->base_end = std::max(c->base_end, c->sealed_end);
+      c->base_tile.n = 0;
     }
+    if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
+      c->base_tile.base = c->sealed_end;
+      build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, (size_t)kTile * kMaxKmers);
+      c->base_end = ordend;
+    }
+    c->delta_tile.base = c->base_end;
+    if (ordend > c->base_end)
+      build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, (size_t)kDelta * kMaxKmers);
+    else
+      c->delta_tile.n = 0;
     c->hip(hipEventRecord(c->ev1, st), "event");
     c->hip(hipEventSynchronize(c->ev1), "sync");
     c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
@@ -650,6 +693,8 @@ void cluster_all(umiclust_ctx* c) {
   c->nclusters = 0;
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();
+  c->base_tile.n = c->delta_tile.n = 0;
+  c->sealed_end = c->base_end = 0;
   c->stats = umiclust_stats{};
   c->stats.n_input = c->n_input;
   c->stats.n_kept = n;
