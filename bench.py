@@ -137,7 +137,9 @@ def main() -> None:
             "gcups": gcups,
             "breakdown_s_per_step": {"total": t_max / args.steps, "prefilter_kernels": t_pf, "align_kernels": t_al,
                                      "consensus_kernels": st["t_consensus_s"], "index_kernels": st["t_index_s"],
-                                     "host_resolve": st["t_host_s"], "host_wait_d2h": st["t_sync_s"]},
+                                     "host_resolve": st["t_host_s"], "host_pass1": st["t_host_pass1_s"],
+                                     "host_wait_d2h": st["t_sync_s"]},
+            "merged_walks": st["n_merged_walks"], "t_merged_walks": st["t_merged_s"],
             "deferred_queries": st["n_deferred"], "pairs_round_b": st["pairs_round_b"],
             "pairs_peer": st["pairs_peer"],
             "alignments_per_step": st["n_alignments"],

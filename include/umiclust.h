@@ -86,6 +86,9 @@ typedef struct umiclust_stats {
   int64_t pairs_peer;     /* speculative in-block peer alignments */
   double t_index_s;       /* kernel time, index tile rebuilds */
   double t_sync_s;        /* host wall time blocked on device->host result copies */
+  double t_host_pass1_s;  /* host first in-order pass of every block */
+  int64_t n_merged_walks; /* (query, strand) walks the host re-ran with in-block centroids */
+  double t_merged_s;      /* host time inside those merged walks */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

@@ -521,6 +521,9 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       o.cells = w.cells;
       return 0;
     }
+    c->stats.n_merged_walks++;
+    const double tm0 = now_s();
+    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{&c->stats.t_merged_s, tm0};
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
     cp.clear();
@@ -594,6 +597,7 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   for (int32_t ql = 0; ql < nq; ql++)
     if (!resolve(ql, false)) deferred.push_back(ql);
   t_host += now_s() - th0;
+  c->stats.t_host_pass1_s += now_s() - th0;
   c->stats.n_deferred += (int64_t)deferred.size();
   // --- round B: align every T_old entry a deferred query could still need, then resolve in order
   if (!deferred.empty()) {

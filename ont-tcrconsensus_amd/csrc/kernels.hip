@@ -859,23 +859,26 @@ __global__ void k_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16
                              const uint8_t* __restrict__ npeer, uint32_t* __restrict__ pq,
                              uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
                              uint32_t* __restrict__ npairs) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nqs * kPeerCap) return;
-  const int qs = k / kPeerCap, x = k % kPeerCap;
+  // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
+  // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
+  const int qs = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qs >= nqs) return;
   const int np = npeer[qs];
-  if (np == 255 || x >= np) return;
-  const uint32_t slot = atomicAdd(npairs, 1u);
-  pq[slot] = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
-  pt[slot] = (uint32_t)(q0 + peer_id[(int64_t)qs * kPeerCap + x]);
-  outidx[slot] = (uint32_t)k;
+  if (np == 255 || np == 0) return;
+  const uint32_t base = atomicAdd(npairs, (uint32_t)np);
+  const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  for (int x = 0; x < np; x++) {
+    pq[base + x] = qv;
+    pt[base + x] = (uint32_t)(q0 + peer_id[(int64_t)qs * kPeerCap + x]);
+    outidx[base + x] = (uint32_t)(qs * kPeerCap + x);
+  }
 }
 
 hipError_t launch_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* peer_id,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
                              uint32_t* npairs, hipStream_t st) {
-  const int n = nqs * kPeerCap;
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_peer_pairs, dim3((n + 255) / 256), dim3(256), 0, st, q0, nqs, both, peer_id, npeer,
+  if (nqs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, nqs, both, peer_id, npeer,
                      pq, pt, outidx, npairs);
   return hipGetLastError();
 }

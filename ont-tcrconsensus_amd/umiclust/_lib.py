@@ -69,6 +69,9 @@ class Stats(C.Structure):
         ("pairs_peer", C.c_int64),
         ("t_index_s", C.c_double),
         ("t_sync_s", C.c_double),
+        ("t_host_pass1_s", C.c_double),
+        ("n_merged_walks", C.c_int64),
+        ("t_merged_s", C.c_double),
     ]
 
     def as_dict(self) -> dict:
