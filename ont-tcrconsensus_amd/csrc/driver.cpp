@@ -5,19 +5,23 @@
 // vsearch's greedy is sequential: query k (length-sorted) is compared with the centroids created
 // by queries 0..k-1.  This driver keeps that definition exactly while batching on the GPU:
 //
-//   for each block of B consecutive sorted queries (centroid set C_old frozen at block start):
-//     K2  prefilter every (query, strand) against C_old  -> exact top-41 list T_old
-//         and against the earlier queries of the same block -> peer list P (count >= threshold)
-//     K3W walk T_old on the device in batches of 8 (vsearch's pop loop), aligning with K3
-//     host pass 1: in sorted order, a query whose relevant peers (those that became centroids)
-//         cannot change its walk takes the device outcome; otherwise it is deferred
-//     round B: align everything a deferred query could need (T_old[0:32] and its live peers)
-//     host pass 2: exact merged walk (top-41 of T_old u P n N) for the deferred queries
-//     new centroids are appended to the index tile
+//   for each block of B consecutive sorted queries of one length:
+//     K2  prefilter every (query, strand) against C_old (the index: centroids of the blocks before
+//         the peer window) -> exact top-41 list T_old, and against the earlier queries of the peer
+//         window (previous block + this block) -> peer list P (count >= threshold)
+//     K3W walk T_old on the device in batches of 8 (vsearch's pop loop), aligning with K3, and
+//         align every (query, peer) pair speculatively
+//     host pass 1: in sorted order, a query whose centroid peers cannot change its walk takes the
+//         device outcome; otherwise it runs the exact merged walk over T_old u centroid peers,
+//         deferred only if that walk needs a T_old entry the device did not align
+//     round B (side stream): align what deferred queries need; host pass 2 resolves them
+//     new centroids are appended to the LSM index (sealed / base / delta tiles)
 //
-// top-41 of (C_old u N) = top-41 of (top-41(C_old) u N), and a walk touches at most 32 entries,
-// so every alignment a deferred query can need exists after round B: the result is identical
-// to the sequential definition (vsearch --threads 1).
+// The passes form a software pipeline: pass k+1 is queued before the host resolves block k, so
+// the host work hides behind device work.  Pass k+1's index lacks block k, which is why its peer
+// window includes block k.  top-41 of (C_old u N) = top-41 of (top-41(C_old) u N), and a walk
+// touches at most 32 entries, so every alignment a query can need exists: the result is
+// identical to the sequential definition (vsearch --threads 1).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -107,6 +111,33 @@ struct Fail {
   int code;
 };
 
+// One greedy block in flight: its own peer tile, device outputs and pinned mirrors, so the device
+// runs block k+1 while the host resolves block k.
+struct Pass {
+  int32_t q0 = 0, nq = 0, w0 = 0;  // block [q0, q0+nq), peer window [w0, q0+nq)
+  bool live = false;
+  Tile peer_tile;
+  PinBuf<TileView> h_tiles;
+  DevBuf<TileView> d_tiles;
+  DevBuf<uint32_t> d_top_seqno;
+  DevBuf<uint8_t> d_top_count, d_ntop;
+  DevBuf<uint16_t> d_peer_id;
+  DevBuf<uint8_t> d_peer_count, d_npeer;
+  DevBuf<uint32_t> d_counters;  // [0] postings, [1..5] npairs per walk round, [8] peer pairs
+  DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
+  DevBuf<WalkState> d_ws;
+  DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
+  PinBuf<WalkState> h_ws;
+  PinBuf<uint8_t> h_ntop, h_npeer, h_peer_count, h_top_count;
+  PinBuf<uint16_t> h_peer_id;
+  PinBuf<uint32_t> h_counters, h_peer_res, h_top_seqno, h_res;
+  hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, download done
+  ~Pass() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 }  // namespace
 
 struct umiclust_ctx {
@@ -149,25 +180,15 @@ struct umiclust_ctx {
   std::vector<Tile*> tiles;       // sealed
   Tile base_tile, delta_tile;
   int32_t sealed_end = 0, base_end = 0;
-  Tile peer_tile;
-  DevBuf<TileView> d_tiles;
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
-  // device: per block
-  DevBuf<uint32_t> d_top_seqno;
-  DevBuf<uint8_t> d_top_count, d_ntop;
-  DevBuf<uint16_t> d_peer_id;
-  DevBuf<uint8_t> d_peer_count, d_npeer;
-  DevBuf<uint32_t> d_counters;    // [0] postings, [1..5] npairs per walk round
-  DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
-  DevBuf<WalkState> d_ws;
-  DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
+  // two passes in flight (software pipeline over blocks) + round B on a side stream
+  Pass pass[2];
+  int32_t pass_B = 0;
+  hipStream_t st_b = nullptr;
+  hipEvent_t evb[2] = {nullptr, nullptr};
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
-  // host pinned mirrors
-  PinBuf<WalkState> h_ws;
-  PinBuf<uint8_t> h_ntop, h_npeer, h_peer_count;
-  PinBuf<uint16_t> h_peer_id;
-  PinBuf<uint32_t> h_counters, h_peer_res, h_top_seqno, h_res;
-  PinBuf<uint8_t> h_top_count;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ix_events;  // index rebuild timing
+  size_t nix = 0;
 
   // results (sorted order)
   std::vector<int32_t> cno;       // creation cluster number
@@ -181,7 +202,7 @@ struct umiclust_ctx {
   std::vector<char> cons;
   std::vector<int64_t> cons_off;
   umiclust_stats stats{};
-  int32_t block_size = 16384;
+  int32_t block_size = 8192;
 
   void fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -346,147 +367,159 @@ inline bool better(const Outcome& a, const Outcome& b) {
 
 enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
 
-void ensure_block_buffers(umiclust_ctx* c, int32_t B) {
+void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   const size_t nqs = (size_t)B * c->both;
-  c->hip(c->d_top_seqno.ensure(nqs * kTopHits), "alloc");
-  c->hip(c->d_top_count.ensure(nqs * kTopHits), "alloc");
-  c->hip(c->d_ntop.ensure(nqs), "alloc");
-  c->hip(c->d_peer_id.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->d_peer_count.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->d_npeer.ensure(nqs), "alloc");
-  c->hip(c->d_counters.ensure(16), "alloc");
-  c->hip(c->d_pq.ensure(nqs * kBatch), "alloc");
-  c->hip(c->d_pt.ensure(nqs * kBatch), "alloc");
-  c->hip(c->d_outidx.ensure(nqs * kBatch), "alloc");
-  c->hip(c->d_res.ensure(nqs * kWalk), "alloc");
-  c->hip(c->d_ws.ensure(nqs), "alloc");
-  c->hip(c->h_ws.ensure(nqs), "pin");
-  c->hip(c->h_ntop.ensure(nqs), "pin");
-  c->hip(c->h_npeer.ensure(nqs), "pin");
-  c->hip(c->h_peer_count.ensure(nqs * kPeerCap), "pin");
-  c->hip(c->h_peer_id.ensure(nqs * kPeerCap), "pin");
-  c->hip(c->h_counters.ensure(16), "pin");
-  c->hip(c->d_ppq.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->d_ppt.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->d_poutidx.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->d_peer_res.ensure(nqs * kPeerCap), "alloc");
-  c->hip(c->h_peer_res.ensure(nqs * kPeerCap), "pin");
-  c->hip(c->h_top_seqno.ensure(nqs * kTopHits), "pin");
-  c->hip(c->h_top_count.ensure(nqs * kTopHits), "pin");
-  c->hip(c->h_res.ensure(nqs * kWalk), "pin");
+  c->hip(P.d_top_seqno.ensure(nqs * kTopHits), "alloc");
+  c->hip(P.d_top_count.ensure(nqs * kTopHits), "alloc");
+  c->hip(P.d_ntop.ensure(nqs), "alloc");
+  c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.d_npeer.ensure(nqs), "alloc");
+  c->hip(P.d_counters.ensure(16), "alloc");
+  c->hip(P.d_pq.ensure(nqs * kBatch), "alloc");
+  c->hip(P.d_pt.ensure(nqs * kBatch), "alloc");
+  c->hip(P.d_outidx.ensure(nqs * kBatch), "alloc");
+  c->hip(P.d_res.ensure(nqs * kWalk), "alloc");
+  c->hip(P.d_ws.ensure(nqs), "alloc");
+  c->hip(P.h_ws.ensure(nqs), "pin");
+  c->hip(P.h_ntop.ensure(nqs), "pin");
+  c->hip(P.h_npeer.ensure(nqs), "pin");
+  c->hip(P.h_peer_count.ensure(nqs * kPeerCap), "pin");
+  c->hip(P.h_peer_id.ensure(nqs * kPeerCap), "pin");
+  c->hip(P.h_counters.ensure(16), "pin");
+  c->hip(P.d_ppq.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.d_ppt.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.d_poutidx.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.d_peer_res.ensure(nqs * kPeerCap), "alloc");
+  c->hip(P.h_peer_res.ensure(nqs * kPeerCap), "pin");
+  c->hip(P.h_top_seqno.ensure(nqs * kTopHits), "pin");
+  c->hip(P.h_top_count.ensure(nqs * kTopHits), "pin");
+  c->hip(P.h_res.ensure(nqs * kWalk), "pin");
+  // fixed capacities, so a pass never frees memory a queued pass still reads
+  c->hip(P.peer_tile.post.ensure((size_t)2 * B * kMaxKmers + 16), "alloc");
+  c->hip(P.h_tiles.ensure(64), "pin");
+  c->hip(P.d_tiles.ensure(64), "alloc");
 }
 
-// Process one block [q0, q0+nq). Returns false if a peer list overflowed (caller shrinks B).
-//
-// One device pass (no host sync inside): peer tile, prefilter, the batch-of-8 walk over T_old
-// (up to 4 align rounds) and the alignment of every in-block peer pair; then one download of the
-// walk states, top lists, walked results and peer results.  The host resolves the block in order:
-// a (query, strand) without centroid peers takes the device walk; otherwise it runs the exact
-// merged walk over T_old u (peers that are centroids).  Only a merged walk that needs a T_old
-// entry the device did not align is deferred to round B (and queries whose peers are deferred).
-bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& state,
-               double& t_pf, double& t_al, double& t_host) {
+// Enqueue the device pass of block [q0, q0+nq) against the index as it stands (centroids of the
+// blocks before the peer window [w0, q0+nq)), with no host synchronisation: peer tile over the
+// window, prefilter, the batch-of-8 walk over T_old (up to 4 align rounds), the speculative
+// alignment of every (query, earlier window query) pair passing the k-mer threshold, and one
+// download of the walk states, top lists, walked results and peer results.
+void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) {
   const int both = c->both;
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
-  {
-    size_t cap = (size_t)nq * kMaxKmers + 16;
-    build_tile(c, c->peer_tile, c->d_iota.p, q0, nq, cap);
-    c->peer_tile.base = 0;
+  P.q0 = q0;
+  P.nq = nq;
+  P.w0 = w0;
+  P.live = true;
+  build_tile(c, P.peer_tile, c->d_iota.p, w0, q0 + nq - w0, (size_t)2 * c->pass_B * kMaxKmers);
+  P.peer_tile.base = 0;
+  int32_t nv = 0;
+  const size_t need = c->tiles.size() + 2;
+  if (need > P.h_tiles.n) {
+    c->hip(hipStreamSynchronize(st), "sync");  // rare: the views array grows
+    c->hip(P.h_tiles.ensure(need * 2), "pin");
+    c->hip(P.d_tiles.ensure(need * 2), "alloc");
   }
-  std::vector<TileView> views;
   for (Tile* t : c->tiles)
-    if (t->n > 0) views.push_back(view_of(*t));
-  if (c->base_tile.n > 0) views.push_back(view_of(c->base_tile));
-  if (c->delta_tile.n > 0) views.push_back(view_of(c->delta_tile));
-  c->hip(c->d_tiles.ensure(views.size() + 1), "alloc tiles");
-  if (!views.empty())
-    c->hip(hipMemcpyAsync(c->d_tiles.p, views.data(), views.size() * sizeof(TileView),
-                          hipMemcpyHostToDevice, st),
+    if (t->n > 0) P.h_tiles.p[nv++] = view_of(*t);
+  if (c->base_tile.n > 0) P.h_tiles.p[nv++] = view_of(c->base_tile);
+  if (c->delta_tile.n > 0) P.h_tiles.p[nv++] = view_of(c->delta_tile);
+  if (nv > 0)
+    c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
-  c->hip(hipMemsetAsync(c->d_counters.p, 0, 16 * 4, st), "memset");
+  c->hip(hipMemsetAsync(P.d_counters.p, 0, 16 * 4, st), "memset");
   PrefilterArgs a{};
   a.seqs = dev_seqs(c);
-  a.tiles = c->d_tiles.p;
-  a.ntiles = (int32_t)views.size();
+  a.tiles = P.d_tiles.p;
+  a.ntiles = nv;
   a.cent_seqno = c->d_cent.p;
   a.q0 = q0;
   a.nq = nq;
   a.both = both;
   a.minwordmatches = c->p.minwordmatches;
-  a.peer = view_of(c->peer_tile);
-  a.top_seqno = c->d_top_seqno.p;
-  a.top_count = c->d_top_count.p;
-  a.ntop = c->d_ntop.p;
-  a.peer_id = c->d_peer_id.p;
-  a.peer_count = c->d_peer_count.p;
-  a.npeer = c->d_npeer.p;
-  a.postings_touched = c->d_counters.p;
-  c->hip(hipEventRecord(c->ev0, st), "event");
+  a.peer = view_of(P.peer_tile);
+  a.peer_base = w0;
+  a.top_seqno = P.d_top_seqno.p;
+  a.top_count = P.d_top_count.p;
+  a.ntop = P.d_ntop.p;
+  a.peer_id = P.d_peer_id.p;
+  a.peer_count = P.d_peer_count.p;
+  a.npeer = P.d_npeer.p;
+  a.postings_touched = P.d_counters.p;
+  c->hip(hipEventRecord(P.ev[0], st), "event");
   c->hip(launch_prefilter(a, st), "prefilter");
-  c->hip(hipEventRecord(c->ev1, st), "event");
-  hipEvent_t ea0, ea1;
-  c->hip(hipEventCreate(&ea0), "event");
-  c->hip(hipEventCreate(&ea1), "event");
+  c->hip(hipEventRecord(P.ev[1], st), "event");
   DevSeqs ds = dev_seqs(c);
   const int32_t qlen = c->hlen[q0];
-  c->hip(launch_walk(-1, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
-                     c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
-                     c->d_outidx.p, c->d_counters.p + 1, st),
+  c->hip(launch_walk(-1, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
+                     c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 1, st),
          "walk");
-  c->hip(hipEventRecord(ea0, st), "event");
+  c->hip(hipEventRecord(P.ev[2], st), "event");
   for (int r = 0; r < kWalk / kBatch; r++) {
-    c->hip(launch_align(ds, qlen, c->ambig, c->d_pq.p, c->d_pt.p, nqs * kBatch, c->d_counters.p + 1 + r,
-                        c->d_outidx.p, c->sc, c->d_res.p, st),
+    c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * kBatch, P.d_counters.p + 1 + r,
+                        P.d_outidx.p, c->sc, P.d_res.p, st),
            "align");
-    c->hip(launch_walk(r, q0, nqs, both, c->d_top_seqno.p, c->d_top_count.p, c->d_ntop.p, c->d_lens.p,
-                       c->d_res.p, c->d_acc.p, c->d_rank.p, c->d_ws.p, c->d_pq.p, c->d_pt.p,
-                       c->d_outidx.p, c->d_counters.p + 2 + r, st),
+    c->hip(launch_walk(r, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
+                       c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2 + r,
+                       st),
            "walk");
   }
-  c->hip(launch_peer_pairs(q0, nqs, both, c->d_peer_id.p, c->d_npeer.p, c->d_ppq.p, c->d_ppt.p, c->d_poutidx.p,
-                           c->d_counters.p + 8, st),
+  c->hip(launch_peer_pairs(q0, w0, nqs, both, P.d_peer_id.p, P.d_npeer.p, P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p,
+                           P.d_counters.p + 8, st),
          "peer pairs");
-  c->hip(launch_align(ds, qlen, c->ambig, c->d_ppq.p, c->d_ppt.p, nqs * kPeerCap, c->d_counters.p + 8,
-                      c->d_poutidx.p, c->sc, c->d_peer_res.p, st),
+  c->hip(launch_align(ds, qlen, c->ambig, P.d_ppq.p, P.d_ppt.p, nqs * kPeerCap, P.d_counters.p + 8,
+                      P.d_poutidx.p, c->sc, P.d_peer_res.p, st),
          "align peers");
-  c->hip(hipEventRecord(ea1, st), "event");
-  // --- one download
+  c->hip(hipEventRecord(P.ev[3], st), "event");
   auto d2h = [&](void* dst, const void* src, size_t bytes) {
     c->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st), "d2h");
   };
-  d2h(c->h_ws.p, c->d_ws.p, (size_t)nqs * sizeof(WalkState));
-  d2h(c->h_ntop.p, c->d_ntop.p, (size_t)nqs);
-  d2h(c->h_npeer.p, c->d_npeer.p, (size_t)nqs);
-  d2h(c->h_peer_id.p, c->d_peer_id.p, (size_t)nqs * kPeerCap * 2);
-  d2h(c->h_peer_count.p, c->d_peer_count.p, (size_t)nqs * kPeerCap);
-  d2h(c->h_peer_res.p, c->d_peer_res.p, (size_t)nqs * kPeerCap * 4);
-  d2h(c->h_top_seqno.p, c->d_top_seqno.p, (size_t)nqs * kTopHits * 4);
-  d2h(c->h_top_count.p, c->d_top_count.p, (size_t)nqs * kTopHits);
-  d2h(c->h_res.p, c->d_res.p, (size_t)nqs * kWalk * 4);
-  d2h(c->h_counters.p, c->d_counters.p, 16 * 4);
+  d2h(P.h_ws.p, P.d_ws.p, (size_t)nqs * sizeof(WalkState));
+  d2h(P.h_ntop.p, P.d_ntop.p, (size_t)nqs);
+  d2h(P.h_npeer.p, P.d_npeer.p, (size_t)nqs);
+  d2h(P.h_peer_id.p, P.d_peer_id.p, (size_t)nqs * kPeerCap * 2);
+  d2h(P.h_peer_count.p, P.d_peer_count.p, (size_t)nqs * kPeerCap);
+  d2h(P.h_peer_res.p, P.d_peer_res.p, (size_t)nqs * kPeerCap * 4);
+  d2h(P.h_top_seqno.p, P.d_top_seqno.p, (size_t)nqs * kTopHits * 4);
+  d2h(P.h_top_count.p, P.d_top_count.p, (size_t)nqs * kTopHits);
+  d2h(P.h_res.p, P.d_res.p, (size_t)nqs * kWalk * 4);
+  d2h(P.h_counters.p, P.d_counters.p, 16 * 4);
+  c->hip(hipEventRecord(P.ev[4], st), "event");
+}
+
+// Wait for a pass and resolve its block on the host in sorted order.  Returns false if a peer
+// list overflowed (the caller re-runs the block in smaller pieces).  Every query of the peer
+// window before the block is already resolved, so peers are final or earlier in this block.
+//
+// A (query, strand) without centroid peers that could change its walk takes the device walk;
+// otherwise the host runs the exact merged walk over T_old u (peers that are centroids).  Only a
+// merged walk that needs a T_old entry the device did not align is deferred to round B (and
+// queries whose peers are deferred).
+bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::vector<int32_t>& new_cents,
+                  double& t_pf, double& t_al, double& t_host) {
+  const int both = c->both;
+  const int32_t q0 = P.q0, nq = P.nq, w0 = P.w0;
+  const int32_t nqs = nq * both;
   const double tsync0 = now_s();
-  c->hip(hipStreamSynchronize(st), "sync");
+  c->hip(hipEventSynchronize(P.ev[4]), "sync");
   c->stats.t_sync_s += now_s() - tsync0;
+  P.live = false;
   float ms = 0;
-  c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
+  c->hip(hipEventElapsedTime(&ms, P.ev[0], P.ev[1]), "elapsed");
   t_pf += ms * 1e-3;
-  c->hip(hipEventElapsedTime(&ms, ea0, ea1), "elapsed");
+  c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;
-  c->stats.kmer_postings += c->h_counters.p[0];
-  c->stats.pairs_peer += c->h_counters.p[8];
+  c->stats.kmer_postings += P.h_counters.p[0];
+  c->stats.pairs_peer += P.h_counters.p[8];
   for (int32_t qs = 0; qs < nqs; qs++)
-    if (c->h_npeer.p[qs] == 255) {
-      (void)hipEventDestroy(ea0);
-      (void)hipEventDestroy(ea1);
-      return false;
-    }
+    if (P.h_npeer.p[qs] == 255) return false;
+  new_cents.clear();
   const double th0 = now_s();
-  const WalkState* ws = c->h_ws.p;
-  // T_old entries aligned so far: device walk [0, w); round B fills [w, 32)
-  std::vector<uint8_t> have_extra;  // per deferred (qs, x) filled in round B
+  const WalkState* ws = P.h_ws.p;
   std::vector<int32_t> deferred;
-  std::vector<int32_t> new_cents;
   std::vector<MCand> L;
   std::vector<std::pair<unsigned long long, int>> cp;
   std::vector<uint32_t> extra_res;   // [row*kWalk + x] results of round B (valid if flag)
@@ -494,24 +527,20 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   std::vector<int32_t> extra_row;    // qs -> row of the round-B arrays (-1: none)
   auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o) -> int {
     // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs T_old entries not aligned
-    const int np = c->h_npeer.p[qs];
+    const int np = P.h_npeer.p[qs];
     const WalkState& w = ws[qs];
     // a centroid peer changes the device walk only if it ranks among the walked candidates, or the
     // last walked batch was not full (the list ended mid-batch: the peer would join that batch), or
     // the walk ended because the list ran out
     const bool open_batch = (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
-    int ncp = 0;
     bool affects = false;
-    const uint16_t* pid = c->h_peer_id.p + (size_t)qs * kPeerCap;
-    const uint8_t* pcnt = c->h_peer_count.p + (size_t)qs * kPeerCap;
+    const uint16_t* pid = P.h_peer_id.p + (size_t)qs * kPeerCap;
+    const uint8_t* pcnt = P.h_peer_count.p + (size_t)qs * kPeerCap;
     for (int x = 0; x < np; x++) {
-      const uint8_t s = state[(size_t)q0 + pid[x]];
+      const uint32_t ps = (uint32_t)(w0 + pid[x]);
+      const uint8_t s = state[ps];
       if (s == ST_UNDET) return 1;
-      if (s == ST_CENT) {
-        ncp++;
-        const uint32_t ps = (uint32_t)(q0 + pid[x]);
-        affects |= open_batch || cand_key(pcnt[x], c->hlen[ps], ps) < w.lastkey;
-      }
+      if (s == ST_CENT) affects |= open_batch || cand_key(pcnt[x], c->hlen[ps], ps) < w.lastkey;
     }
     if (!affects) {
       o.acc = w.acc;
@@ -527,16 +556,15 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
     cp.clear();
-    for (int y = 0; y < np; y++)
-      if (state[(size_t)q0 + pid[y]] == ST_CENT) {
-        const uint32_t ps = (uint32_t)(q0 + pid[y]);
-        cp.push_back({cand_key(pcnt[y], c->hlen[ps], ps), y});
-      }
+    for (int y = 0; y < np; y++) {
+      const uint32_t ps = (uint32_t)(w0 + pid[y]);
+      if (state[ps] == ST_CENT) cp.push_back({cand_key(pcnt[y], c->hlen[ps], ps), y});
+    }
     std::sort(cp.begin(), cp.end());
     L.clear();
-    const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
-    const uint32_t* ts = c->h_top_seqno.p + (size_t)qs * kTopHits;
-    const uint8_t* tc = c->h_top_count.p + (size_t)qs * kTopHits;
+    const int nt = std::min<int>(P.h_ntop.p[qs], kWalk);
+    const uint32_t* ts = P.h_top_seqno.p + (size_t)qs * kTopHits;
+    const uint8_t* tc = P.h_top_count.p + (size_t)qs * kTopHits;
     int i = 0;
     size_t x = 0;
     while ((int)L.size() < kWalk && (i < nt || x < cp.size())) {
@@ -547,7 +575,7 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
         m.key = kt;
         m.seqno = ts[i];
         if (i < w.w) {
-          m.res = c->h_res.p[(size_t)qs * kWalk + i];
+          m.res = P.h_res.p[(size_t)qs * kWalk + i];
           m.have = true;
         } else if (allow_extra && extra_row[qs] >= 0 && extra_have[(size_t)extra_row[qs] * kWalk + i]) {
           m.res = extra_res[(size_t)extra_row[qs] * kWalk + i];
@@ -560,14 +588,13 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
       } else {
         const int y = cp[x].second;
         m.key = kp;
-        m.seqno = (uint32_t)(q0 + pid[y]);
-        m.res = c->h_peer_res.p[(size_t)qs * kPeerCap + y];
+        m.seqno = (uint32_t)(w0 + pid[y]);
+        m.res = P.h_peer_res.p[(size_t)qs * kPeerCap + y];
         m.have = true;
         x++;
       }
       L.push_back(m);
     }
-    (void)ncp;
     return merged_walk(c, L, c->hlen[q], o) ? 0 : 2;
   };
   auto resolve = [&](int32_t ql, bool allow_extra) -> bool {
@@ -599,17 +626,18 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
   t_host += now_s() - th0;
   c->stats.t_host_pass1_s += now_s() - th0;
   c->stats.n_deferred += (int64_t)deferred.size();
-  // --- round B: align every T_old entry a deferred query could still need, then resolve in order
+  // --- round B (side stream, so the queued pass keeps the device busy): align every T_old entry a
+  // deferred query could still need, then resolve the deferred queries in order
   if (!deferred.empty()) {
     const double th1 = now_s();
     std::vector<uint32_t> bpq, bpt, bidx;
     for (int32_t ql : deferred)
       for (int s = 0; s < both; s++) {
         const int32_t qs = ql * both + s;
-        const int nt = std::min<int>(c->h_ntop.p[qs], kWalk);
+        const int nt = std::min<int>(P.h_ntop.p[qs], kWalk);
         for (int x = ws[qs].w; x < nt; x++) {
           bpq.push_back(((uint32_t)(q0 + ql) << 1) | (uint32_t)s);
-          bpt.push_back(c->h_top_seqno.p[(size_t)qs * kTopHits + x]);
+          bpt.push_back(P.h_top_seqno.p[(size_t)qs * kTopHits + x]);
           bidx.push_back((uint32_t)(qs * kWalk + x));
         }
       }
@@ -618,18 +646,20 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
     c->stats.pairs_round_b += nb;
     std::vector<uint32_t> bres(nb);
     if (nb > 0) {
+      hipStream_t sb = c->st_b;
       c->hip(c->d_bpq.ensure(nb), "alloc");
       c->hip(c->d_bpt.ensure(nb), "alloc");
       c->hip(c->d_bres.ensure(nb), "alloc");
-      c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
-      c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, st), "h2d");
-      c->hip(hipEventRecord(ea0, st), "event");
-      c->hip(launch_align(ds, qlen, c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc, c->d_bres.p, st),
+      c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+      c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+      c->hip(hipEventRecord(c->evb[0], sb), "event");
+      c->hip(launch_align(dev_seqs(c), c->hlen[q0], c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc,
+                          c->d_bres.p, sb),
              "align B");
-      c->hip(hipEventRecord(ea1, st), "event");
-      c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st), "d2h");
-      c->hip(hipStreamSynchronize(st), "sync");
-      c->hip(hipEventElapsedTime(&ms, ea0, ea1), "elapsed");
+      c->hip(hipEventRecord(c->evb[1], sb), "event");
+      c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
+      c->hip(hipStreamSynchronize(sb), "sync");
+      c->hip(hipEventElapsedTime(&ms, c->evb[0], c->evb[1]), "elapsed");
       t_al += ms * 1e-3;
     }
     const double th2 = now_s();
@@ -649,42 +679,48 @@ bool run_block(umiclust_ctx* c, int32_t q0, int32_t nq, std::vector<uint8_t>& st
     t_host += now_s() - th2;
     std::sort(new_cents.begin(), new_cents.end());
   }
-  (void)hipEventDestroy(ea0);
-  (void)hipEventDestroy(ea1);
-  // --- append new centroids to the index
-  if (!new_cents.empty()) {
-    const int32_t ord0 = (int32_t)c->cent.size();
-    for (int32_t q : new_cents) c->cent.push_back(q);
-    c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4,
-                          hipMemcpyHostToDevice, st),
-           "h2d cent");
-    const int32_t ordend = (int32_t)c->cent.size();
-    c->hip(hipEventRecord(c->ev0, st), "event");
-    while (ordend - c->sealed_end >= kTile) {  // seal a full tile
-      Tile* t = new Tile();
-      t->base = c->sealed_end;
-      build_tile(c, *t, c->d_cent.p, t->base, kTile, (size_t)kTile * kMaxKmers);
-      c->tiles.push_back(t);
-      c->sealed_end += kTile;
-      c->base_end = std::max(c->base_end, c->sealed_end);
-      c->base_tile.n = 0;
-    }
-    if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
-      c->base_tile.base = c->sealed_end;
-      build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, (size_t)kTile * kMaxKmers);
-      c->base_end = ordend;
-    }
-    c->delta_tile.base = c->base_end;
-    if (ordend > c->base_end)
-      build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, (size_t)kDelta * kMaxKmers);
-    else
-      c->delta_tile.n = 0;
-    c->hip(hipEventRecord(c->ev1, st), "event");
-    c->hip(hipEventSynchronize(c->ev1), "sync");
-    c->hip(hipEventElapsedTime(&ms, c->ev0, c->ev1), "elapsed");
-    c->stats.t_index_s += ms * 1e-3;
-  }
   return true;
+}
+
+// Append a block's new centroids (sorted seqnos) to the LSM index, enqueued on the main stream
+// behind any queued pass (which keeps reading the tiles as they were when it was enqueued).
+void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
+  if (new_cents.empty()) return;
+  hipStream_t st = c->st;
+  const int32_t ord0 = (int32_t)c->cent.size();
+  for (int32_t q : new_cents) c->cent.push_back(q);  // capacity reserved: no reallocation
+  c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4, hipMemcpyHostToDevice,
+                        st),
+         "h2d cent");
+  const int32_t ordend = (int32_t)c->cent.size();
+  if (c->nix >= c->ix_events.size()) {
+    hipEvent_t e0, e1;
+    c->hip(hipEventCreate(&e0), "event");
+    c->hip(hipEventCreate(&e1), "event");
+    c->ix_events.push_back({e0, e1});
+  }
+  const auto& ev = c->ix_events[c->nix++];
+  c->hip(hipEventRecord(ev.first, st), "event");
+  while (ordend - c->sealed_end >= kTile) {  // seal a full tile
+    Tile* t = new Tile();
+    t->base = c->sealed_end;
+    build_tile(c, *t, c->d_cent.p, t->base, kTile, (size_t)kTile * kMaxKmers);
+    c->tiles.push_back(t);
+    c->sealed_end += kTile;
+    c->base_end = std::max(c->base_end, c->sealed_end);
+    c->base_tile.n = 0;
+  }
+  if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
+    c->base_tile.base = c->sealed_end;
+    build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, (size_t)kTile * kMaxKmers);
+    c->base_end = ordend;
+  }
+  c->delta_tile.base = c->base_end;
+  if (ordend > c->base_end)
+    build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, (size_t)kDelta * kMaxKmers);
+  else
+    c->delta_tile.n = 0;
+  c->hip(hipEventRecord(ev.second, st), "event");
 }
 
 void cluster_all(umiclust_ctx* c) {
@@ -694,33 +730,82 @@ void cluster_all(umiclust_ctx* c) {
   c->strand.assign(n, 0);
   c->target.assign(n, -1);
   c->cent.clear();
+  c->cent.reserve((size_t)n + 1);
   c->nclusters = 0;
+  c->hip(hipStreamSynchronize(c->st), "sync");  // no queued work may still read the old tiles
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();
   c->base_tile.n = c->delta_tile.n = 0;
   c->sealed_end = c->base_end = 0;
+  c->nix = 0;
   c->stats = umiclust_stats{};
   c->stats.n_input = c->n_input;
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   std::vector<uint8_t> state(n, ST_UNDET);
   double t_pf = 0, t_al = 0, t_host = 0;
-  int32_t B = std::min<int32_t>(c->block_size, kTile);
-  ensure_block_buffers(c, B);
-  int32_t q0 = 0;
-  while (q0 < n) {
-    // a block holds one query length (the aligner is compiled per query length)
+  // blocks of at most B queries of one length (the aligner is compiled per query length); the peer
+  // window of a pass spans two blocks, so B <= 32767 keeps window-local ids within 16 bits
+  const int32_t B = std::max(1, std::min<int32_t>(c->block_size, kTile / 2 - 1));
+  c->pass_B = B;
+  for (Pass& P : c->pass) ensure_pass_buffers(c, P, B);
+  std::vector<std::pair<int32_t, int32_t>> blocks;
+  for (int32_t q0 = 0; q0 < n;) {
     int32_t same = 1;
     while (q0 + same < n && same < B && c->hlen[q0 + same] == c->hlen[q0]) same++;
-    const int32_t nq = same;
-    if (!run_block(c, q0, nq, state, t_pf, t_al, t_host)) {
-      if (nq == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
-      B = std::max(1, nq / 2);
+    blocks.push_back({q0, same});
+    q0 += same;
+  }
+  const int32_t nb = (int32_t)blocks.size();
+  std::vector<int32_t> new_cents;
+  // A block whose peer list overflowed: re-run it alone (window = itself, index complete up to it)
+  // in halving pieces, synchronously.
+  auto run_alone = [&](int32_t q0, int32_t nq) {
+    Pass& P = c->pass[0];
+    int32_t piece = nq;
+    for (int32_t q = q0; q < q0 + nq;) {
+      const int32_t m = std::min(piece, q0 + nq - q);
+      enqueue_pass(c, P, q, m, q);
+      if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+        if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
+        piece = std::max(1, m / 2);
+        continue;
+      }
+      append_centroids(c, new_cents);
+      c->stats.n_blocks++;
+      q += m;
+    }
+  };
+  // Software pipeline over blocks: pass k+1 is queued before the host resolves block k.  Pass j
+  // runs against the index of the blocks before its peer window, and the window covers every
+  // later query before block j's, so C_old u window = all queries before j: the merged walk is
+  // exact.  Invariant at the top of iteration k: pass k and (if any) pass k+1 are queued, the
+  // index holds blocks < k.
+  if (nb > 0) enqueue_pass(c, c->pass[0], blocks[0].first, blocks[0].second, blocks[0].first);
+  if (nb > 1) enqueue_pass(c, c->pass[1], blocks[1].first, blocks[1].second, blocks[0].first);
+  for (int32_t k = 0; k < nb; k++) {
+    Pass& P = c->pass[k & 1];
+    Pass& Q = c->pass[(k + 1) & 1];
+    if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+      // drain the queued pass k+1 (its window included block k) and restart the pipeline
+      if (Q.live) {
+        c->hip(hipEventSynchronize(Q.ev[4]), "sync");
+        Q.live = false;
+      }
+      run_alone(blocks[k].first, blocks[k].second);
+      if (k + 1 < nb) enqueue_pass(c, Q, blocks[k + 1].first, blocks[k + 1].second, blocks[k + 1].first);
+      if (k + 2 < nb) enqueue_pass(c, P, blocks[k + 2].first, blocks[k + 2].second, blocks[k + 1].first);
       continue;
     }
+    append_centroids(c, new_cents);
     c->stats.n_blocks++;
-    q0 += nq;
-    if (B < c->block_size) B = std::min<int32_t>(B * 2, c->block_size);
+    if (k + 2 < nb) enqueue_pass(c, P, blocks[k + 2].first, blocks[k + 2].second, blocks[k + 1].first);
+  }
+  c->hip(hipStreamSynchronize(c->st), "sync");
+  for (size_t i = 0; i < c->nix; i++) {
+    float ms = 0;
+    c->hip(hipEventElapsedTime(&ms, c->ix_events[i].first, c->ix_events[i].second), "elapsed");
+    c->stats.t_index_s += ms * 1e-3;
   }
   // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's
   c->nclusters = (int32_t)c->cent.size();
@@ -1254,7 +1339,14 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   }
   c->dev = device_id;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipStreamCreateWithFlags(&c->st_b, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
+      hipEventCreate(&c->pass[0].ev[0]) != hipSuccess || hipEventCreate(&c->pass[0].ev[1]) != hipSuccess ||
+      hipEventCreate(&c->pass[0].ev[2]) != hipSuccess || hipEventCreate(&c->pass[0].ev[3]) != hipSuccess ||
+      hipEventCreate(&c->pass[0].ev[4]) != hipSuccess || hipEventCreate(&c->pass[1].ev[0]) != hipSuccess ||
+      hipEventCreate(&c->pass[1].ev[1]) != hipSuccess || hipEventCreate(&c->pass[1].ev[2]) != hipSuccess ||
+      hipEventCreate(&c->pass[1].ev[3]) != hipSuccess || hipEventCreate(&c->pass[1].ev[4]) != hipSuccess) {
     delete c;
     if (err) *err = UMICLUST_EDEVICE;
     return nullptr;
@@ -1271,6 +1363,13 @@ void umiclust_destroy(umiclust_ctx* c) {
   c->tiles.clear();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (hipEvent_t e : c->evb)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ix_events) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }

@@ -449,7 +449,7 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
     }
     __syncthreads();
     // scan: every counter >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
-    const int limit = peer ? min(tv.n, qlocal) : tv.n;  // peers: only earlier queries of the block
+    const int limit = peer ? min(tv.n, q - a.peer_base) : tv.n;  // peers: only earlier queries of the window
     if (thr > 0) {
       const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
       const int lim4 = (limit + 15) >> 4;
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(S.cnt, c);
-        const int32_t sq = peer ? (a.q0 + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
+        const int32_t sq = peer ? (a.peer_base + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
         S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
       }
       __syncthreads();
@@ -852,10 +852,10 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
   return hipGetLastError();
 }
 
-// every in-block peer pair (query vs an earlier query of the block that passed the k-mer
+// every peer pair (query vs an earlier query of the peer window [w0, q) that passed the k-mer
 // threshold) is aligned speculatively in the same pass, so the host can run the exact merged walk
 // without another round trip whichever peers turn out to be centroids
-__global__ void k_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* __restrict__ peer_id,
+__global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* __restrict__ peer_id,
                              const uint8_t* __restrict__ npeer, uint32_t* __restrict__ pq,
                              uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
                              uint32_t* __restrict__ npairs) {
@@ -869,16 +869,16 @@ __global__ void k_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16
   const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
   for (int x = 0; x < np; x++) {
     pq[base + x] = qv;
-    pt[base + x] = (uint32_t)(q0 + peer_id[(int64_t)qs * kPeerCap + x]);
+    pt[base + x] = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
     outidx[base + x] = (uint32_t)(qs * kPeerCap + x);
   }
 }
 
-hipError_t launch_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* peer_id,
+hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* peer_id,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
                              uint32_t* npairs, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, nqs, both, peer_id, npeer,
+  hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, peer_id, npeer,
                      pq, pt, outidx, npairs);
   return hipGetLastError();
 }

@@ -62,13 +62,15 @@ struct PrefilterArgs {
   int32_t q0, nq;          // block of queries (sorted seqnos)
   int32_t both;            // strands per query (1 or 2)
   int32_t minwordmatches;
-  // peer tile (block-local mini index over the block's + strand k-mers), may be n=0
+  // peer tile: mini index over the + strand k-mers of the peer window [peer_base, q0+nq) (local
+  // id c = seqno - peer_base), may be n=0; a query sees the window entries before it
   TileView peer;
+  int32_t peer_base;
   // outputs
   uint32_t* top_seqno;     // [nqs*kTopHits]
   uint8_t* top_count;      // [nqs*kTopHits]
   uint8_t* ntop;           // [nqs]
-  uint16_t* peer_id;       // [nqs*kPeerCap] block-local
+  uint16_t* peer_id;       // [nqs*kPeerCap] window-local (seqno - peer_base)
   uint8_t* peer_count;     // [nqs*kPeerCap]
   uint8_t* npeer;          // [nqs] (255 = overflow)
   uint32_t* postings_touched;  // [1] atomic counter (stats)
@@ -100,7 +102,7 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
                        uint32_t* outidx, uint32_t* npairs, hipStream_t st);
-hipError_t launch_peer_pairs(int32_t q0, int32_t nqs, int32_t both, const uint16_t* peer_id,
+hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* peer_id,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
                              uint32_t* npairs, hipStream_t st);
 // traceback: ops[k*kOpsStride...] ('M','D','I' in alignment order), nops[k]
