@@ -116,7 +116,6 @@ struct Fail {
 struct Pass {
   int32_t q0 = 0, nq = 0, w0 = 0;  // block [q0, q0+nq), peer window [w0, q0+nq)
   bool live = false;
-  Tile peer_tile;
   PinBuf<TileView> h_tiles;
   DevBuf<TileView> d_tiles;
   DevBuf<uint32_t> d_top_seqno;
@@ -183,8 +182,9 @@ struct umiclust_ctx {
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
   // two passes in flight (software pipeline over blocks) + round B on a side stream
   Pass pass[2];
+  Tile blk_tile[3], solo_tile;    // per-block peer tiles (ring), overflow re-runs
   int32_t pass_B = 0;
-  hipStream_t st_b = nullptr;
+  hipStream_t st_b = nullptr, st_copy = nullptr;
   hipEvent_t evb[2] = {nullptr, nullptr};
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ix_events;  // index rebuild timing
@@ -396,17 +396,19 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.h_top_count.ensure(nqs * kTopHits), "pin");
   c->hip(P.h_res.ensure(nqs * kWalk), "pin");
   // fixed capacities, so a pass never frees memory a queued pass still reads
-  c->hip(P.peer_tile.post.ensure((size_t)2 * B * kMaxKmers + 16), "alloc");
   c->hip(P.h_tiles.ensure(64), "pin");
   c->hip(P.d_tiles.ensure(64), "alloc");
 }
 
 // Enqueue the device pass of block [q0, q0+nq) against the index as it stands (centroids of the
-// blocks before the peer window [w0, q0+nq)), with no host synchronisation: peer tile over the
-// window, prefilter, the batch-of-8 walk over T_old (up to 4 align rounds), the speculative
-// alignment of every (query, earlier window query) pair passing the k-mer threshold, and one
-// download of the walk states, top lists, walked results and peer results.
-void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) {
+// blocks before the peer window), with no host synchronisation: the block's own peer tile (kept
+// for the next block's window), prefilter, the batch-of-8 walk over T_old (up to 4 align rounds),
+// the speculative alignment of every (query, earlier window query) pair passing the k-mer
+// threshold, and one download of the walk states, top lists, walked results and peer results.
+// The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
+// alone (prev == nullptr).
+void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own) {
+  const int32_t w0 = prev ? prev->base : q0;
   const int both = c->both;
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
@@ -414,8 +416,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) 
   P.nq = nq;
   P.w0 = w0;
   P.live = true;
-  build_tile(c, P.peer_tile, c->d_iota.p, w0, q0 + nq - w0, (size_t)2 * c->pass_B * kMaxKmers);
-  P.peer_tile.base = 0;
+  build_tile(c, own, c->d_iota.p, q0, nq, (size_t)c->pass_B * kMaxKmers);
+  own.base = q0;
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -440,7 +442,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) 
   a.nq = nq;
   a.both = both;
   a.minwordmatches = c->p.minwordmatches;
-  a.peer = view_of(P.peer_tile);
+  a.peer[0] = prev ? view_of(*prev) : TileView{};
+  a.peer[1] = view_of(own);
   a.peer_base = w0;
   a.top_seqno = P.d_top_seqno.p;
   a.top_count = P.d_top_count.p;
@@ -474,8 +477,12 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) 
                       P.d_poutidx.p, c->sc, P.d_peer_res.p, st),
          "align peers");
   c->hip(hipEventRecord(P.ev[3], st), "event");
+  // the download runs on the copy stream, overlapping the next queued pass's kernels; the pass
+  // that next reuses these buffers is enqueued only after the host has waited for ev[4]
+  hipStream_t sc = c->st_copy;
+  c->hip(hipStreamWaitEvent(sc, P.ev[3], 0), "wait");
   auto d2h = [&](void* dst, const void* src, size_t bytes) {
-    c->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st), "d2h");
+    c->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, sc), "d2h");
   };
   d2h(P.h_ws.p, P.d_ws.p, (size_t)nqs * sizeof(WalkState));
   d2h(P.h_ntop.p, P.d_ntop.p, (size_t)nqs);
@@ -487,7 +494,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, int32_t w0) 
   d2h(P.h_top_count.p, P.d_top_count.p, (size_t)nqs * kTopHits);
   d2h(P.h_res.p, P.d_res.p, (size_t)nqs * kWalk * 4);
   d2h(P.h_counters.p, P.d_counters.p, 16 * 4);
-  c->hip(hipEventRecord(P.ev[4], st), "event");
+  c->hip(hipEventRecord(P.ev[4], sc), "event");
 }
 
 // Wait for a pass and resolve its block on the host in sorted order.  Returns false if a peer
@@ -765,7 +772,7 @@ void cluster_all(umiclust_ctx* c) {
     int32_t piece = nq;
     for (int32_t q = q0; q < q0 + nq;) {
       const int32_t m = std::min(piece, q0 + nq - q);
-      enqueue_pass(c, P, q, m, q);
+      enqueue_pass(c, P, q, m, nullptr, c->solo_tile);
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
         piece = std::max(1, m / 2);
@@ -780,9 +787,14 @@ void cluster_all(umiclust_ctx* c) {
   // runs against the index of the blocks before its peer window, and the window covers every
   // later query before block j's, so C_old u window = all queries before j: the merged walk is
   // exact.  Invariant at the top of iteration k: pass k and (if any) pass k+1 are queued, the
-  // index holds blocks < k.
-  if (nb > 0) enqueue_pass(c, c->pass[0], blocks[0].first, blocks[0].second, blocks[0].first);
-  if (nb > 1) enqueue_pass(c, c->pass[1], blocks[1].first, blocks[1].second, blocks[0].first);
+  // index holds blocks < k.  Block k's peer tile lives in blk_tile[k % 3] (used by passes k, k+1).
+  auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % 3]; };
+  auto enqueue = [&](int32_t k, bool with_prev) {
+    enqueue_pass(c, c->pass[k & 1], blocks[k].first, blocks[k].second, with_prev ? &tile_of(k - 1) : nullptr,
+                 tile_of(k));
+  };
+  if (nb > 0) enqueue(0, false);
+  if (nb > 1) enqueue(1, true);
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k & 1];
     Pass& Q = c->pass[(k + 1) & 1];
@@ -793,13 +805,13 @@ void cluster_all(umiclust_ctx* c) {
         Q.live = false;
       }
       run_alone(blocks[k].first, blocks[k].second);
-      if (k + 1 < nb) enqueue_pass(c, Q, blocks[k + 1].first, blocks[k + 1].second, blocks[k + 1].first);
-      if (k + 2 < nb) enqueue_pass(c, P, blocks[k + 2].first, blocks[k + 2].second, blocks[k + 1].first);
+      if (k + 1 < nb) enqueue(k + 1, false);
+      if (k + 2 < nb) enqueue(k + 2, true);
       continue;
     }
     append_centroids(c, new_cents);
     c->stats.n_blocks++;
-    if (k + 2 < nb) enqueue_pass(c, P, blocks[k + 2].first, blocks[k + 2].second, blocks[k + 1].first);
+    if (k + 2 < nb) enqueue(k + 2, true);
   }
   c->hip(hipStreamSynchronize(c->st), "sync");
   for (size_t i = 0; i < c->nix; i++) {
@@ -1340,6 +1352,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   c->dev = device_id;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_b, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
       hipEventCreate(&c->pass[0].ev[0]) != hipSuccess || hipEventCreate(&c->pass[0].ev[1]) != hipSuccess ||
@@ -1370,6 +1383,7 @@ void umiclust_destroy(umiclust_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
+  if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }

@@ -15,6 +15,8 @@
 // All integer/byte work: VALU + LDS, no MFMA (not a dense contraction).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "umiclust_internal.h"
 
 namespace uc {
@@ -212,15 +214,19 @@ hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* pe
 }
 
 // ------------------------------------------------------------------ KI: index tile build
-__global__ void k_index_count(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
-                              const int32_t* __restrict__ cent_seqno, int32_t first, int32_t count,
-                              uint32_t* __restrict__ hist) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per tile sequence, one lane per k-mer slot (<= kMaxKmers = 65: lane and lane + 64), so a
+// build issues its ~60 atomics per sequence from 60 lanes instead of one dependent chain.
+__global__ __launch_bounds__(256) void k_index_count(const uint16_t* __restrict__ kmers,
+                                                     const uint8_t* __restrict__ nk,
+                                                     const int32_t* __restrict__ cent_seqno, int32_t first,
+                                                     int32_t count, uint32_t* __restrict__ hist) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), x = threadIdx.x & 63;
   if (c >= count) return;
-  int32_t s = cent_seqno[first + c];
-  int n = nk[(int64_t)s * 2];
+  const int32_t s = cent_seqno[first + c];
+  const int n = nk[(int64_t)s * 2];
   const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
-  for (int x = 0; x < n; x++) atomicAdd(&hist[k[x]], 1u);
+  if (x < n) atomicAdd(&hist[k[x]], 1u);
+  if (x + 64 < n) atomicAdd(&hist[k[x + 64]], 1u);
 }
 
 __global__ __launch_bounds__(1024) void k_index_scan(const uint32_t* __restrict__ hist,
@@ -249,25 +255,25 @@ __global__ __launch_bounds__(1024) void k_index_scan(const uint32_t* __restrict_
   if (t == 1023) off[65536] = part[1023];
 }
 
-__global__ void k_index_fill(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
-                             const int32_t* __restrict__ cent_seqno, int32_t first, int32_t count,
-                             const uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
-                             uint16_t* __restrict__ post) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_index_fill(const uint16_t* __restrict__ kmers,
+                                                    const uint8_t* __restrict__ nk,
+                                                    const int32_t* __restrict__ cent_seqno, int32_t first,
+                                                    int32_t count, const uint32_t* __restrict__ off,
+                                                    uint32_t* __restrict__ cursor, uint16_t* __restrict__ post) {
+  // posting order within a list is arbitrary: the prefilter only counts
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), x = threadIdx.x & 63;
   if (c >= count) return;
-  int32_t s = cent_seqno[first + c];
-  int n = nk[(int64_t)s * 2];
+  const int32_t s = cent_seqno[first + c];
+  const int n = nk[(int64_t)s * 2];
   const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
-  for (int x = 0; x < n; x++) {
-    uint32_t pos = off[k[x]] + atomicAdd(&cursor[k[x]], 1u);
-    post[pos] = (uint16_t)c;
-  }
+  if (x < n) post[off[k[x]] + atomicAdd(&cursor[k[x]], 1u)] = (uint16_t)c;
+  if (x + 64 < n) post[off[k[x + 64]] + atomicAdd(&cursor[k[x + 64]], 1u)] = (uint16_t)c;
 }
 
 hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
                               int32_t first, int32_t count, uint32_t* hist, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_index_count, dim3((count + 255) / 256), dim3(256), 0, st, kmers, nk,
+  hipLaunchKernelGGL(k_index_count, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk,
                      cent_seqno, first, count, hist);
   return hipGetLastError();
 }
@@ -280,7 +286,7 @@ hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int
                              int32_t first, int32_t count, const uint32_t* off, uint32_t* cursor,
                              uint16_t* post, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_index_fill, dim3((count + 255) / 256), dim3(256), 0, st, kmers, nk,
+  hipLaunchKernelGGL(k_index_fill, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk,
                      cent_seqno, first, count, off, cursor, post);
   return hipGetLastError();
 }
@@ -376,12 +382,14 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
   }
   __syncthreads();
   int npeer = 0;
-  for (int t = 0; t <= a.ntiles; t++) {
-    const bool peer = (t == a.ntiles);
+  for (int t = 0; t < a.ntiles + 2; t++) {
+    const bool peer = (t >= a.ntiles);
     TileView tv;
-    if (peer) tv = a.peer;
+    if (peer) tv = a.peer[t - a.ntiles];
     else tv = a.tiles[t];
-    if (tv.n == 0) continue;
+    // peers: only the window queries before q (a peer tile's base is its first seqno)
+    const int limit = peer ? min(tv.n, q - tv.base) : tv.n;
+    if (limit <= 0) continue;
     // zero the counters (whole uint4 groups: the scan reads 16 counters per lane)
     const int nq4 = (tv.n + 15) >> 4;
     uint4* cnt4 = reinterpret_cast<uint4*>(S.cnt);
@@ -449,7 +457,6 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
     }
     __syncthreads();
     // scan: every counter >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
-    const int limit = peer ? min(tv.n, q - a.peer_base) : tv.n;  // peers: only earlier queries of the window
     if (thr > 0) {
       const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
       const int lim4 = (limit + 15) >> 4;
@@ -493,7 +500,7 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(S.cnt, c);
-        const int32_t sq = peer ? (a.peer_base + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
+        const int32_t sq = peer ? (tv.base + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
         S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
       }
       __syncthreads();
@@ -520,7 +527,8 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
       if (peer) {
         if (tid < nbest && npeer + tid < kPeerCap) {
           const uint32_t key = S.best[tid];
-          a.peer_id[(int64_t)qs * kPeerCap + npeer + tid] = (uint16_t)(key & 0xffffu);
+          a.peer_id[(int64_t)qs * kPeerCap + npeer + tid] =
+              (uint16_t)(tv.base + (int32_t)(key & 0xffffu) - a.peer_base);
           a.peer_count[(int64_t)qs * kPeerCap + npeer + tid] = (uint8_t)(127u - (key >> 23));
         }
         npeer += nc;
@@ -742,14 +750,200 @@ __global__ __launch_bounds__(64) void k_align(DevSeqs s, const uint32_t* __restr
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
 }
 
+// ------------------------------------------------------------------ K3P: packed 16-bit alignment
+// The same recurrences, summaries and strict priorities as k_align, two DP cells per 32-bit VALU
+// op (VOP3P v_pk_* on int16 halves).  A column is split into a top half (rows [0, TOP)) and a
+// bottom half (rows [TOP, QL)) that runs one column behind: register k holds row k of column j in
+// its low half and row TOP+k of column j-1 in its high half.  Within a step the rows are
+// processed in order, so the bottom half's upper neighbour (row TOP-1 of column j-1) is the top
+// half's carry-out of the previous step; one step costs one pass over TOP packed rows.
+// Branch-free selection: for |values| well inside int16, (a - b) >> 15 (arithmetic, per half) is
+// the mask of "b > a", which drives v_bfi for the summaries and v_pk_max for the scores.
+// Substitution: per 16-row group a match bit-mask of the column's target base, selected per step
+// from per-base masks built once per pair (non-ambiguous sequences only: one-hot codes).
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2s as_v2(uint32_t x) { return __builtin_bit_cast(v2s, x); }
+__device__ __forceinline__ uint32_t as_u(v2s x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)hi << 16) | ((uint32_t)lo & 0xffffu); }
+// mask of (b > a) per half
+// (opaque to the compiler, which otherwise rewrites it into per-half compares and selects)
+__device__ __forceinline__ uint32_t gt_mask(v2s b, v2s a) {
+  uint32_t d;
+  // op_sel_hi:[0,1]: the inline constant's low half serves both halves (its high half is 0)
+  asm("v_pk_sub_i16 %0, %1, %2\n\tv_pk_ashrrev_i16 %0, 15, %0 op_sel_hi:[0,1]" : "=&v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
+template <int QL>
+__global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __restrict__ pq,
+                                                 const uint32_t* __restrict__ pt, int32_t npairs,
+                                                 const uint32_t* __restrict__ dev_npairs,
+                                                 const uint32_t* __restrict__ outidx, Scoring sc,
+                                                 uint32_t* __restrict__ out) {
+  constexpr int TOP = (QL + 1) / 2, BOT = QL - TOP;  // BOT == TOP or TOP - 1
+  constexpr int NG = (TOP + 15) / 16;
+  constexpr int KL = BOT - 1;                        // register holding row QL-1 (high half)
+  const int k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= npairs) return;
+  if (dev_npairs && k >= (int)*dev_npairs) return;
+  const uint32_t qv = pq[k];
+  const int32_t q = (int32_t)(qv >> 1);
+  const int qstr = (int)(qv & 1u);
+  const int32_t t = (int32_t)pt[k];
+  const int tl = s.lens[t];
+  // per-base row masks: MT[g] / MB[g] hold, for base b at bits [16b, 16b+16), the rows of group g
+  // (top half / bottom half) whose query base is b
+  uint64_t MT[NG], MB[NG];
+#pragma unroll
+  for (int g = 0; g < NG; g++) MT[g] = MB[g] = 0;
+  {
+    const uint32_t* qc = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < QL; i++) {
+      if ((i & 7) == 0) w = qc[i >> 3];
+      const uint32_t b = (uint32_t)__builtin_ctz((w & 15u) | 16u) & 3u;
+      w >>= 4;
+      if (i < TOP) MT[i >> 4] |= 1ull << (16 * b + (i & 15));
+      else MB[(i - TOP) >> 4] |= 1ull << (16 * b + ((i - TOP) & 15));
+    }
+  }
+  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
+  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
+  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
+  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  const v2s MM = as_v2(pk2(sc.mismatch, sc.mismatch));
+  const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
+  v2s H[TOP], E[TOP];
+  uint32_t SH[TOP], SE[TOP];  // summaries; SH stored +1 (every consumer adds the move)
+  auto init_rows = [&](uint32_t keep_mask) {
+    // boundary column -1: H(i,-1) = -(GO_TL + (i+1) GE_TL), E(i,0) opened from it, S_H = 0,
+    // S_E = one real move; keep_mask selects the halves to (re)initialise
+    int vz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+#pragma unroll
+    for (int kk = 0; kk < TOP; kk++) {
+      const int i0 = kk, i1 = TOP + kk;
+      const int h0 = vz - sc.go[1] - (i0 + 1) * sc.ge[1];
+      const int h1 = vz - sc.go[1] - (i1 + 1) * sc.ge[1];
+      const int q1 = (i1 == QL - 1) ? QRqr : QRqi;
+      const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
+      const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
+      H[kk] = as_v2(bfi(keep_mask, pk2(h0, h1), as_u(H[kk])));
+      E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
+      SH[kk] = bfi(keep_mask, 0x00010001u, SH[kk]);
+      SE[kk] = bfi(keep_mask, 0x00010001u, SE[kk]);
+    }
+  };
+#pragma unroll
+  for (int kk = 0; kk < TOP; kk++) {
+    H[kk] = as_v2(0u);
+    E[kk] = as_v2(0u);
+    SH[kk] = SE[kk] = 0;
+  }
+  init_rows(0xffffffffu);
+  // carries of the top half's last row, consumed by the bottom half in the next step
+  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDF = 0;
+  int Lext = 0, trail = 0;
+  uint32_t tword = 0, tprev = 1;
+  for (int j = 0; j <= tl; j++) {
+    if ((j & 7) == 0) tword = tcp[j >> 3];
+    const uint32_t tcode = tword & 15u;
+    tword >>= 4;
+    const uint32_t bl = (uint32_t)__builtin_ctz(tcode | 16u) & 3u, bh = (uint32_t)__builtin_ctz(tprev | 16u) & 3u;
+    tprev = tcode;
+    uint32_t M[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++)
+      M[g] = ((uint32_t)(MT[g] >> (16 * bl)) & 0xffffu) | ((uint32_t)(MB[g] >> (16 * bh)) << 16);
+    const bool lc0 = (j == tl - 1), lc1 = (j == tl);
+    const uint32_t QRt = pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti);
+    const uint32_t Rt = pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti);
+    // row -1 (top half, column j) | carry (bottom half, column j-1)
+    const int hd0 = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
+    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
+    v2s Hd = as_v2(pk2(hd0, (int)cHd));
+    uint32_t SHd = pk2(1, (int)cSHd);
+    v2s F = as_v2(pk2(f0, (int)cF));
+    uint32_t SF = pk2(1, (int)cSF);
+    uint32_t DF = pk2(-1, (int)cDF);  // row the current D run opened from (-1: boundary)
+#pragma unroll
+    for (int kk = 0; kk < TOP; kk++) {
+      const uint32_t e = (M[kk >> 4] >> (kk & 15)) & 0x00010001u;
+      v2s h = Hd + MM + as_v2(e) * DELTA;
+      uint32_t sh = SHd + (e << 8);
+      const uint32_t mF = gt_mask(F, h);
+      h = __builtin_elementwise_max(h, F);
+      sh = bfi(mF, SF, sh);
+      const v2s Ec = E[kk];
+      const uint32_t mE = gt_mask(Ec, h);
+      h = __builtin_elementwise_max(h, Ec);
+      sh = bfi(mE, SE[kk], sh);
+      const uint32_t sh1 = sh + 0x00010001u;
+      int dr_last = 0;
+      bool eb_last = false;
+      if (kk == KL) {
+        // last row (high half): D run of the chosen F = rows since it opened (before DF moves on)
+        eb_last = (mE >> 31) != 0;
+        dr_last = (mF >> 31) != 0 ? (QL - 1) - (int)(short)(DF >> 16) : 0;
+      }
+      const v2s fo = h - as_v2(QRt), fe = F - as_v2(Rt);
+      const uint32_t mfx = gt_mask(fe, fo);
+      F = __builtin_elementwise_max(fo, fe);
+      // a new D run opened from H continues H's own D run when H took F
+      DF = bfi(mfx | (mF & ~mE), DF, pk2(kk, TOP + kk));
+      SF = bfi(mfx, SF + 0x00010001u, sh1);
+      const uint32_t qrq = pk2(QRqi, (TOP + kk == QL - 1) ? QRqr : QRqi);
+      const uint32_t rq = pk2(Rqi, (TOP + kk == QL - 1) ? Rqr : Rqi);
+      const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
+      const uint32_t mex = gt_mask(ee, eo);
+      if (kk == KL) {
+        // trailing I-run counters along the last row; the value left by the last column is the
+        // end cell's (vsearch align_trim's trailing run)
+        const bool ex = (mex >> 31) != 0;
+        const int lh = eb_last ? 1 + Lext : 0;
+        trail = eb_last ? lh : dr_last;
+        Lext = ex ? 1 + Lext : lh;
+      }
+      E[kk] = __builtin_elementwise_max(eo, ee);
+      SE[kk] = bfi(mex, SE[kk] + 0x00010001u, sh1);
+      Hd = H[kk];
+      SHd = SH[kk];
+      H[kk] = h;
+      SH[kk] = sh1;
+    }
+    // carry the top half's outputs into the bottom half of the next step
+    cHd = as_u(Hd) & 0xffffu;
+    cSHd = SHd & 0xffffu;
+    cF = as_u(F) & 0xffffu;
+    cSF = SF & 0xffffu;
+    cDF = DF & 0xffffu;
+    if (j == 0) {
+      // the bottom half processed column -1 in this step: restore the boundary column
+      init_rows(0xffff0000u);
+      Lext = 0;
+      trail = 0;
+    }
+  }
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16);
+  const uint32_t S = ((SH[KL] >> 16) - 1u) & 0xffffu;
+  const uint32_t m = S >> 8, acols = S & 0xffu;
+  const uint32_t internal = acols - (uint32_t)trail;
+  out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
+}
+
 typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
                         const uint32_t*, Scoring, uint32_t*);
 
 template <int L>
 struct AlignTable {
   static void fill(AlignFn* t) {
-    t[2 * L] = k_align<L, false>;
-    t[2 * L + 1] = k_align<L, true>;
+    t[3 * L] = k_align_pk<L>;
+    t[3 * L + 1] = k_align<L, false>;
+    t[3 * L + 2] = k_align<L, true>;
     AlignTable<L - 1>::fill(t);
   }
 };
@@ -761,15 +955,19 @@ struct AlignTable<kMinTplLen - 1> {
 hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq,
                         const uint32_t* pt, int32_t npairs, const uint32_t* dev_npairs,
                         const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st) {
-  static AlignFn table[2 * (kMaxLen + 1)] = {};
+  static AlignFn table[3 * (kMaxLen + 1)] = {};
   static bool init = false;
+  static int variant0 = 0;
   if (!init) {
     AlignTable<kMaxLen>::fill(table);
+    // UMICLUST_ALIGN=scalar selects the one-cell-per-op kernel (cross-checks / benchmarks)
+    const char* v = getenv("UMICLUST_ALIGN");
+    variant0 = (v && v[0] == 's') ? 1 : 0;
     init = true;
   }
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(table[2 * qlen + (ambig ? 1 : 0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
+  hipLaunchKernelGGL(table[3 * qlen + (ambig ? 2 : variant0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
                      pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
 }

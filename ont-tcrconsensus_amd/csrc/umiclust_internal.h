@@ -62,9 +62,10 @@ struct PrefilterArgs {
   int32_t q0, nq;          // block of queries (sorted seqnos)
   int32_t both;            // strands per query (1 or 2)
   int32_t minwordmatches;
-  // peer tile: mini index over the + strand k-mers of the peer window [peer_base, q0+nq) (local
-  // id c = seqno - peer_base), may be n=0; a query sees the window entries before it
-  TileView peer;
+  // peer tiles: mini indexes over the + strand k-mers of the previous block and of this block
+  // (base = first seqno, local id c = seqno - base; n = 0 if absent); together they cover the peer
+  // window [peer_base, q0+nq), and a query sees the window entries before it
+  TileView peer[2];
   int32_t peer_base;
   // outputs
   uint32_t* top_seqno;     // [nqs*kTopHits]
