@@ -99,13 +99,24 @@ struct PinBuf {
 constexpr int32_t kDelta = 8192;  // centroids in the per-block delta tile before folding into base
 
 struct Tile {
-  DevBuf<uint32_t> hist_off;  // [65536 hist][65537 off]
-  DevBuf<uint32_t> cursor;    // [65536]
-  DevBuf<uint16_t> post;
-  int32_t n = 0;              // centroids
-  int32_t base = 0;           // first centroid ordinal
+  DevBuf<uint32_t> hist;      // [kBins], all zero between builds (the scan re-zeroes it)
+  DevBuf<uint32_t> off;       // [kBins + 1] padded list offsets, tile-relative
+  DevBuf<uint32_t> cursor;    // [kBins]
+  DevBuf<uint32_t> partial;   // [kScanBlocks]
+  uint64_t post_base = 0;     // the tile's slot in the postings arena
+  size_t post_cap = 0;        // slot capacity (postings)
+  int32_t n = 0;              // sequences
+  int32_t base = 0;           // first centroid ordinal / first seqno (peer tiles)
+  int32_t seg = 0;            // counter segment / peer region
   int32_t built_n = -1;       // n at last build
 };
+
+// postings a tile slot of nseq sequences can need: every k-mer plus up to 7 padding postings per
+// non-empty list
+inline size_t tile_cap(int64_t nseq) {
+  const int64_t raw = nseq * kMaxKmers;
+  return (size_t)((raw + 7 * std::min<int64_t>(kBins, raw) + 64) & ~int64_t(7));
+}
 
 struct Fail {
   int code;
@@ -120,6 +131,9 @@ struct Pass {
   DevBuf<TileView> d_tiles;
   DevBuf<uint32_t> d_top_seqno;
   DevBuf<uint8_t> d_top_count, d_ntop;
+  DevBuf<unsigned long long> d_ptop;  // per-(query-strand, part) prefilter lists
+  DevBuf<uint8_t> d_pntop, d_ppeer_count, d_pnpeer;
+  DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
   DevBuf<uint32_t> d_counters;  // [0] postings, [1..5] npairs per walk round, [8] peer pairs
@@ -183,6 +197,9 @@ struct umiclust_ctx {
   // two passes in flight (software pipeline over blocks) + round B on a side stream
   Pass pass[2];
   Tile blk_tile[3], solo_tile;    // per-block peer tiles (ring), overflow re-runs
+  DevBuf<uint16_t> arena;         // postings of every tile (one buffer, one descriptor per pass)
+  uint64_t sealed_slot0 = 0;      // arena index of sealed tile 0's slot
+  int32_t index_end = 0;          // centroid ordinals [0, index_end) are indexed
   int32_t pass_B = 0;
   hipStream_t st_b = nullptr, st_copy = nullptr;
   hipEvent_t evb[2] = {nullptr, nullptr};
@@ -282,19 +299,22 @@ DevSeqs dev_seqs(umiclust_ctx* c) {
   return s;
 }
 
-// (re)build one index tile over centroid ordinals [base, base+n) whose seqnos are cent[]
-void build_tile(umiclust_ctx* c, Tile& t, const int32_t* d_cent_seqno, int32_t first, int32_t n,
-                size_t post_cap) {
-  c->hip(t.hist_off.ensure(65536 + 65537), "tile alloc");
-  c->hip(t.cursor.ensure(65536), "tile alloc");
-  c->hip(t.post.ensure(post_cap + 16), "tile alloc");  // +16: 16-byte chunk reads past the end
-  c->hip(hipMemsetAsync(t.hist_off.p, 0, 65536 * 4, c->st), "tile memset");
-  c->hip(hipMemsetAsync(t.cursor.p, 0, 65536 * 4, c->st), "tile memset");
-  c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, d_cent_seqno, first, n, t.hist_off.p, c->st),
-         "index count");
-  c->hip(launch_index_scan(t.hist_off.p, c->st), "index scan");
-  c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, d_cent_seqno, first, n, t.hist_off.p + 65536,
-                           t.cursor.p, t.post.p, c->st),
+// (re)build one index tile over sequences map[first .. first+n) with ordinals xoff + c; postings
+// vbase + ((xoff + c) % seg_mod) / kParts (umiclust_internal.h), in the tile's arena slot
+void build_tile(umiclust_ctx* c, Tile& t, const int32_t* map, int32_t first, int32_t n, int32_t xoff, int32_t vbase,
+                int32_t seg_mod) {
+  if (!t.hist.p) {
+    c->hip(t.hist.ensure(kBins), "tile alloc");
+    c->hip(hipMemsetAsync(t.hist.p, 0, (size_t)kBins * 4, c->st), "tile memset");
+  }
+  c->hip(t.off.ensure(kBins + 1), "tile alloc");
+  c->hip(t.cursor.ensure(kBins), "tile alloc");
+  c->hip(t.partial.ensure(kScanBlocks), "tile alloc");
+  if (tile_cap(n) > t.post_cap) c->fail(UMICLUST_EDEVICE, "internal: index tile slot too small");
+  uint16_t* post = c->arena.p + t.post_base;
+  c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, t.hist.p, c->st), "index count");
+  c->hip(launch_index_scan(t.hist.p, t.partial.p, t.off.p, t.cursor.p, post, c->st), "index scan");
+  c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, vbase, seg_mod, t.cursor.p, post, c->st),
          "index fill");
   t.n = n;
   t.built_n = n;
@@ -302,10 +322,11 @@ void build_tile(umiclust_ctx* c, Tile& t, const int32_t* d_cent_seqno, int32_t f
 
 TileView view_of(const Tile& t) {
   TileView v;
-  v.off = t.hist_off.p + 65536;
-  v.post = t.post.p;
+  v.off = t.off.p;
+  v.post_base = t.post_base;
   v.n = t.n;
   v.base = t.base;
+  v.seg = t.seg;
   return v;
 }
 
@@ -372,6 +393,11 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_top_seqno.ensure(nqs * kTopHits), "alloc");
   c->hip(P.d_top_count.ensure(nqs * kTopHits), "alloc");
   c->hip(P.d_ntop.ensure(nqs), "alloc");
+  c->hip(P.d_ptop.ensure(nqs * kParts * kTopHits), "alloc");
+  c->hip(P.d_pntop.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_ppeer_id.ensure(nqs * kParts * kPeerCap), "alloc");
+  c->hip(P.d_ppeer_count.ensure(nqs * kParts * kPeerCap), "alloc");
+  c->hip(P.d_pnpeer.ensure(nqs * kParts), "alloc");
   c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
@@ -407,7 +433,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // threshold, and one download of the walk states, top lists, walked results and peer results.
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
-void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own) {
+void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own, int32_t region) {
   const int32_t w0 = prev ? prev->base : q0;
   const int both = c->both;
   const int32_t nqs = nq * both;
@@ -416,8 +442,9 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   P.nq = nq;
   P.w0 = w0;
   P.live = true;
-  build_tile(c, own, c->d_iota.p, q0, nq, (size_t)c->pass_B * kMaxKmers);
+  build_tile(c, own, c->d_iota.p, q0, nq, 0, region * kPeerRegion, 1 << 30);
   own.base = q0;
+  own.seg = region;
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -435,8 +462,28 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipMemsetAsync(P.d_counters.p, 0, 16 * 4, st), "memset");
   PrefilterArgs a{};
   a.seqs = dev_seqs(c);
+  a.arena = c->arena.p;
   a.tiles = P.d_tiles.p;
   a.ntiles = nv;
+  // centroid tiles are in segment order (sealed tiles, then base and delta); each pass addresses its
+  // postings from the lowest arena slot it reads
+  a.ncent = c->index_end;
+  a.nseg = (c->index_end + kSegCentroids - 1) / kSegCentroids;
+  if (a.nseg > kMaxSegs) c->fail(UMICLUST_ERANGE, "more than %d centroids in one bin", kMaxSegs * kSegCentroids);
+  for (int s = 0, vi = 0; s <= a.nseg; s++) {
+    while (vi < nv && P.h_tiles.p[vi].seg < s) vi++;
+    a.seg_tile[s] = s == a.nseg ? nv : vi;
+  }
+  {
+    uint64_t peer_lo = own.post_base;
+    if (prev) peer_lo = std::min(peer_lo, prev->post_base);
+    for (int s = 0; s < std::max(a.nseg, 1); s++) {
+      uint64_t lo = (s == std::max(a.nseg, 1) - 1) ? peer_lo : UINT64_MAX;
+      if (a.nseg > 0)
+        for (int v = a.seg_tile[s]; v < a.seg_tile[s + 1]; v++) lo = std::min(lo, P.h_tiles.p[v].post_base);
+      a.seg_base[s] = lo;
+    }
+  }
   a.cent_seqno = c->d_cent.p;
   a.q0 = q0;
   a.nq = nq;
@@ -445,6 +492,11 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.peer[0] = prev ? view_of(*prev) : TileView{};
   a.peer[1] = view_of(own);
   a.peer_base = w0;
+  a.ptop = P.d_ptop.p;
+  a.pntop = P.d_pntop.p;
+  a.ppeer_id = P.d_ppeer_id.p;
+  a.ppeer_count = P.d_ppeer_count.p;
+  a.pnpeer = P.d_pnpeer.p;
   a.top_seqno = P.d_top_seqno.p;
   a.top_count = P.d_top_count.p;
   a.ntop = P.d_ntop.p;
@@ -711,7 +763,10 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   while (ordend - c->sealed_end >= kTile) {  // seal a full tile
     Tile* t = new Tile();
     t->base = c->sealed_end;
-    build_tile(c, *t, c->d_cent.p, t->base, kTile, (size_t)kTile * kMaxKmers);
+    t->seg = t->base / kSegCentroids;
+    t->post_cap = tile_cap(kTile);
+    t->post_base = c->sealed_slot0 + (uint64_t)c->tiles.size() * t->post_cap;
+    build_tile(c, *t, c->d_cent.p, t->base, kTile, t->base, kCentBase, kSegCentroids);
     c->tiles.push_back(t);
     c->sealed_end += kTile;
     c->base_end = std::max(c->base_end, c->sealed_end);
@@ -719,14 +774,19 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   }
   if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
     c->base_tile.base = c->sealed_end;
-    build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, (size_t)kTile * kMaxKmers);
+    c->base_tile.seg = c->sealed_end / kSegCentroids;
+    build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, c->sealed_end, kCentBase,
+               kSegCentroids);
     c->base_end = ordend;
   }
   c->delta_tile.base = c->base_end;
+  c->delta_tile.seg = c->base_end / kSegCentroids;
   if (ordend > c->base_end)
-    build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, (size_t)kDelta * kMaxKmers);
+    build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, c->base_end, kCentBase,
+               kSegCentroids);
   else
     c->delta_tile.n = 0;
+  c->index_end = ordend;
   c->hip(hipEventRecord(ev.second, st), "event");
 }
 
@@ -744,6 +804,7 @@ void cluster_all(umiclust_ctx* c) {
   c->tiles.clear();
   c->base_tile.n = c->delta_tile.n = 0;
   c->sealed_end = c->base_end = 0;
+  c->index_end = 0;
   c->nix = 0;
   c->stats = umiclust_stats{};
   c->stats.n_input = c->n_input;
@@ -751,11 +812,29 @@ void cluster_all(umiclust_ctx* c) {
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   std::vector<uint8_t> state(n, ST_UNDET);
   double t_pf = 0, t_al = 0, t_host = 0;
-  // blocks of at most B queries of one length (the aligner is compiled per query length); the peer
-  // window of a pass spans two blocks, so B <= 32767 keeps window-local ids within 16 bits
-  const int32_t B = std::max(1, std::min<int32_t>(c->block_size, kTile / 2 - 1));
+  // blocks of at most B queries of one length (the aligner is compiled per query length); a block's
+  // peer tile fills one kPeerRegion of the prefilter counters, so B <= kMaxBlock
+  const int32_t B = std::max(1, std::min<int32_t>(c->block_size, kMaxBlock));
   c->pass_B = B;
   for (Pass& P : c->pass) ensure_pass_buffers(c, P, B);
+  // postings arena: the base, delta, peer-ring and solo slots, then the sealed tile slots in creation
+  // order (n / kTile of them at most); a prefilter pass reads the slots of one counter segment (plus
+  // the first four in its last pass), which keeps its 32-bit buffer offsets in range
+  {
+    uint64_t off = 0;
+    auto slot = [&](Tile& t, int64_t nseq) {
+      t.post_base = off;
+      t.post_cap = tile_cap(nseq);
+      off += t.post_cap;
+    };
+    slot(c->base_tile, kTile);
+    slot(c->delta_tile, kDelta);
+    for (Tile& t : c->blk_tile) slot(t, kMaxBlock);
+    slot(c->solo_tile, kMaxBlock);
+    c->sealed_slot0 = off;
+    off += (uint64_t)(n / kTile) * tile_cap(kTile);
+    c->hip(c->arena.ensure((size_t)off + 64), "alloc arena");
+  }
   std::vector<std::pair<int32_t, int32_t>> blocks;
   for (int32_t q0 = 0; q0 < n;) {
     int32_t same = 1;
@@ -772,7 +851,7 @@ void cluster_all(umiclust_ctx* c) {
     int32_t piece = nq;
     for (int32_t q = q0; q < q0 + nq;) {
       const int32_t m = std::min(piece, q0 + nq - q);
-      enqueue_pass(c, P, q, m, nullptr, c->solo_tile);
+      enqueue_pass(c, P, q, m, nullptr, c->solo_tile, 0);
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
         piece = std::max(1, m / 2);
@@ -791,7 +870,7 @@ void cluster_all(umiclust_ctx* c) {
   auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % 3]; };
   auto enqueue = [&](int32_t k, bool with_prev) {
     enqueue_pass(c, c->pass[k & 1], blocks[k].first, blocks[k].second, with_prev ? &tile_of(k - 1) : nullptr,
-                 tile_of(k));
+                 tile_of(k), k & 1);
   };
   if (nb > 0) enqueue(0, false);
   if (nb > 1) enqueue(1, true);

@@ -214,116 +214,177 @@ hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* pe
 }
 
 // ------------------------------------------------------------------ KI: index tile build
-// One wave per tile sequence, one lane per k-mer slot (<= kMaxKmers = 65: lane and lane + 64), so a
-// build issues its ~60 atomics per sequence from 60 lanes instead of one dependent chain.
+// CSR over bins (part << 16 | k-mer) of the tile's + strand unique 8-mers (vsearch dbindex.cc
+// analogue).  The sequence with ordinal x (centroid ordinal; peer tiles: position in the block) goes
+// to part x % kParts and its posting is directly its prefilter counter index (layout in
+// umiclust_internal.h).  Lists are padded to multiples of 8 postings; padding postings point at 64
+// spare counters.  One wave per tile sequence, one lane per k-mer slot (<= kMaxKmers = 65: lane and
+// lane + 64), so a build issues its ~60 atomics per sequence from 60 lanes.
 __global__ __launch_bounds__(256) void k_index_count(const uint16_t* __restrict__ kmers,
                                                      const uint8_t* __restrict__ nk,
-                                                     const int32_t* __restrict__ cent_seqno, int32_t first,
-                                                     int32_t count, uint32_t* __restrict__ hist) {
+                                                     const int32_t* __restrict__ map, int32_t first,
+                                                     int32_t count, int32_t xoff, uint32_t* __restrict__ hist) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6), x = threadIdx.x & 63;
   if (c >= count) return;
-  const int32_t s = cent_seqno[first + c];
+  const int32_t s = map[first + c];
   const int n = nk[(int64_t)s * 2];
   const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
-  if (x < n) atomicAdd(&hist[k[x]], 1u);
-  if (x + 64 < n) atomicAdd(&hist[k[x + 64]], 1u);
+  const uint32_t pb = (uint32_t)((xoff + c) & (kParts - 1)) << 16;
+  if (x < n) atomicAdd(&hist[pb | k[x]], 1u);
+  if (x + 64 < n) atomicAdd(&hist[pb | k[x + 64]], 1u);
 }
 
-__global__ __launch_bounds__(1024) void k_index_scan(const uint32_t* __restrict__ hist,
-                                                     uint32_t* __restrict__ off) {
-  // exclusive scan of 65536 counters, one workgroup: 64 per thread
-  __shared__ uint32_t part[1024];
-  int t = threadIdx.x;
-  uint32_t loc[64];
-  uint32_t sum = 0;
+__device__ __forceinline__ uint32_t pad8(uint32_t v) { return (v + 7u) & ~7u; }
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
-  for (int x = 0; x < 64; x++) {
-    loc[x] = sum;
-    sum += hist[t * 64 + x];
-  }
-  part[t] = sum;
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// exclusive scan of the padded list sizes of kBins bins in two launches: per-block sums, then each
+// block adds the sum of the blocks before it (a strided read of <= kScanBlocks partials) to its own
+// scan.  The apply pass also writes the fill cursors (= list starts) and the padding postings, and
+// re-zeroes the histogram for the tile's next build.
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ partial) {
+  __shared__ uint32_t ws[4];
+  const uint4 v = reinterpret_cast<const uint4*>(hist + (size_t)blockIdx.x * kScanPer)[threadIdx.x];
+  const uint32_t s = wave_sum(pad8(v.x) + pad8(v.y) + pad8(v.z) + pad8(v.w));
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    uint32_t v = (t >= d) ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t base = part[t] - sum;
+  if (threadIdx.x == 0) partial[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(uint32_t* __restrict__ hist,
+                                                    const uint32_t* __restrict__ partial,
+                                                    uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                    uint16_t* __restrict__ post) {
+  __shared__ uint32_t ws[4], wsum[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, b = blockIdx.x;
+  uint32_t p = 0;
+  for (int i = t; i < b; i += 256) p += partial[i];
+  p = wave_sum(p);
+  if (lane == 0) ws[wave] = p;
+  uint4* h4 = reinterpret_cast<uint4*>(hist + (size_t)b * kScanPer);
+  const uint4 v = h4[t];
+  const uint32_t nn[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t pp[4] = {pad8(v.x), pad8(v.y), pad8(v.z), pad8(v.w)};
+  const uint32_t s = pp[0] + pp[1] + pp[2] + pp[3];
+  uint32_t inc = s;
 #pragma unroll
-  for (int x = 0; x < 64; x++) off[t * 64 + x] = base + loc[x];
-  if (t == 1023) off[65536] = part[1023];
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t base = ws[0] + ws[1] + ws[2] + ws[3];
+  for (int w = 0; w < wave; w++) base += wsum[w];
+  const uint32_t e = base + inc - s;
+  const uint32_t oo[4] = {e, e + pp[0], e + pp[0] + pp[1], e + pp[0] + pp[1] + pp[2]};
+  const uint4 o = make_uint4(oo[0], oo[1], oo[2], oo[3]);
+  reinterpret_cast<uint4*>(off + (size_t)b * kScanPer)[t] = o;
+  reinterpret_cast<uint4*>(cursor + (size_t)b * kScanPer)[t] = o;
+  // padding postings, spread over the 64 spare counters
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    for (uint32_t u = oo[j] + nn[j]; u < oo[j] + pp[j]; u++)
+      post[u] = (uint16_t)(kDummy + ((u ^ (u >> 6)) & 63u));
+  h4[t] = make_uint4(0u, 0u, 0u, 0u);
+  if (b == kScanBlocks - 1 && t == 255) off[kBins] = e + s;
 }
 
 __global__ __launch_bounds__(256) void k_index_fill(const uint16_t* __restrict__ kmers,
                                                     const uint8_t* __restrict__ nk,
-                                                    const int32_t* __restrict__ cent_seqno, int32_t first,
-                                                    int32_t count, const uint32_t* __restrict__ off,
+                                                    const int32_t* __restrict__ map, int32_t first,
+                                                    int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod,
                                                     uint32_t* __restrict__ cursor, uint16_t* __restrict__ post) {
   // posting order within a list is arbitrary: the prefilter only counts
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6), x = threadIdx.x & 63;
   if (c >= count) return;
-  const int32_t s = cent_seqno[first + c];
+  const int32_t s = map[first + c];
   const int n = nk[(int64_t)s * 2];
   const uint16_t* k = kmers + (int64_t)s * 2 * kKmerStride;
-  if (x < n) post[off[k[x]] + atomicAdd(&cursor[k[x]], 1u)] = (uint16_t)c;
-  if (x + 64 < n) post[off[k[x + 64]] + atomicAdd(&cursor[k[x + 64]], 1u)] = (uint16_t)c;
+  const uint32_t xx = (uint32_t)(xoff + c);
+  const uint32_t pb = (xx & (kParts - 1)) << 16;
+  const uint16_t val = (uint16_t)(vbase + ((xx % (uint32_t)seg_mod) >> kPartShift));
+  if (x < n) post[atomicAdd(&cursor[pb | k[x]], 1u)] = val;
+  if (x + 64 < n) post[atomicAdd(&cursor[pb | k[x + 64]], 1u)] = val;
 }
 
-hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
-                              int32_t first, int32_t count, uint32_t* hist, hipStream_t st) {
+hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
+                              int32_t count, int32_t xoff, uint32_t* hist, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_index_count, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk,
-                     cent_seqno, first, count, hist);
+  hipLaunchKernelGGL(k_index_count, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk, map, first, count, xoff,
+                     hist);
   return hipGetLastError();
 }
-hipError_t launch_index_scan(uint32_t* hist_to_off, hipStream_t st) {
-  // hist_to_off: [65536] histogram followed by [65537] offsets
-  hipLaunchKernelGGL(k_index_scan, dim3(1), dim3(1024), 0, st, hist_to_off, hist_to_off + 65536);
+hipError_t launch_index_scan(uint32_t* hist, uint32_t* partial, uint32_t* off, uint32_t* cursor, uint16_t* post,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(256), 0, st, hist, partial);
+  hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(256), 0, st, hist, partial, off, cursor, post);
   return hipGetLastError();
 }
-hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
-                             int32_t first, int32_t count, const uint32_t* off, uint32_t* cursor,
+hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
+                             int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod, uint32_t* cursor,
                              uint16_t* post, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_index_fill, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk,
-                     cent_seqno, first, count, off, cursor, post);
+  hipLaunchKernelGGL(k_index_fill, dim3((count + 3) / 4), dim3(256), 0, st, kmers, nk, map, first, count, xoff,
+                     vbase, seg_mod, cursor, post);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ K2: prefilter
-// One 512-thread workgroup per (query, strand).  Per index tile: u8 counters (4 per u32) for up to
-// 65536 centroids in 64 KiB of LDS.
-//  count: the query's <= 65 posting lists are walked as one flat sequence of 16-byte chunks (8 u16
-//         postings); each thread keeps 4 chunk loads in flight, then issues fire-and-forget
-//         ds_add_u32 for the postings inside its list range (the memory system, not the atomics,
-//         must be kept busy: one dependent 2-byte load per atomic was latency-bound);
-//  scan:  the counters are read back 16 bytes per lane and a SWAR test finds every byte >= the
-//         threshold min(12, #kmers) (searchcore.cc search_topscores' `count >= minmatches`);
-//  top:   candidates get 30-bit keys (count desc, length asc, id asc), are bitonic-sorted and
-//         merged into the running top-41 (u64 keys over all tiles; minheap.cc order).
-// A threshold of 0, or more candidates than the LDS buffer holds, switches the tile to a chunked
-// exact path, so the result is exact in every case.
-constexpr int kPfThreads = 512;
-constexpr int kPfUnroll = 4;
-constexpr int kRankSel = 1024;  // candidate counts up to this are selected by rank
+// vsearch searchcore.cc search_topscores: for a (query, strand), count the query's unique 8-mers
+// shared with every centroid (u8 counters), keep counters >= min(minwordmatches, #kmers) and take
+// the top 41 by (count desc, length asc, seqno asc) (minheap.cc order).
+//
+// One 256-thread workgroup per (query-strand, part): blockIdx.x = qs * kParts + part, so the
+// hardware's round-robin dispatch puts every part-p workgroup on one XCD, whose L2 then serves only
+// part p's postings and offsets (~1/8 of the index).  Per counter segment (normally one):
+//  lists: the (tile, k-mer) posting lists of the query (centroid tiles of the segment, then the two
+//         peer tiles of the in-block window) are laid end to end as one stream of 16-byte chunks
+//         (lists are padded to whole chunks by the index build, so no bounds are needed);
+//  count: each wave streams a contiguous range of 64-chunk windows, lane l taking chunk 64w + l;
+//         the list of every lane's chunk comes from one LDS read of the next 64 list starts, an OR
+//         of one-hot start bits across the wave and a popcount.  A posting is its counter index,
+//         so each of the chunk's 8 postings is one fire-and-forget ds_add_u32 on packed u8 counters;
+//  scan:  counters are read back 16 per lane, a SWAR test finds every byte >= the threshold;
+//  top:   candidates get 30-bit keys (count desc, length asc, sub-id asc = seqno asc within a
+//         part), are selected by rank (few) or bitonic sort and merged into the part's running
+//         top-41 (u64 keys); peers keep every candidate (<= kPeerCap), sorted by key.
+// A threshold of 0, or more candidates than the LDS buffer holds, switches a segment to a chunked
+// exact path.  The second kernel merges the kParts sorted part lists of each query-strand into the
+// exact top-41 (the top-41 of a union is the top-41 of the parts' top-41s) and concatenates the
+// peer lists.
+constexpr int kPfThreads = 256;
+constexpr int kPfWaves = kPfThreads / 64;
+constexpr int kPfCand = 1024;   // LDS candidate buffer (centroids)
+constexpr int kRankSel = 512;   // candidate counts up to this are selected by rank
+constexpr int kPfTiles = 12;    // tiles per counter segment: 7 sealed + base + delta + 2 peer (+1)
+constexpr int kPfLists = kMaxKmers * kPfTiles;
+constexpr int kPfSlots = (kPfLists + kPfThreads - 1) / kPfThreads;  // list-table slots per thread
 
 struct PfShared {
-  uint32_t cnt[kTile / 4];        // 64 KiB packed u8 counters
-  uint32_t cand[kCandCap];        // candidate local ids, then 30-bit keys
+  uint32_t lstart[kPfLists + 66];   // first chunk of each non-empty list, then the chunk total
+  uint32_t lbias[kPfLists];         // posting index of chunk g of list L: lbias[L] + 8 g
+  uint32_t cand[kPfCand];           // candidate sub-ids, then 30-bit keys
+  uint32_t pcand[kPeerCap + 1];     // peer keys
   unsigned long long top[kTopHits];
   unsigned long long merged[kTopHits];
-  uint32_t best[kPeerCap + 1];    // the tile's best keys in order
   unsigned long long bestk[kTopHits];
-  uint32_t kbeg[kMaxKmers + 3];   // posting range [kbeg, kend) of each query k-mer in this tile
-  uint32_t kend[kMaxKmers + 3];
-  uint32_t kchunk[kMaxKmers + 4]; // prefix sum of 16-byte chunks per list
+  unsigned long long wsum[kPfWaves];
+  uint32_t best[kPeerCap + 1];
   uint16_t km[kMaxKmers + 3];
   uint32_t ncand;
+  uint32_t npc;
   uint32_t overflow;
-  int32_t ntop;
   uint32_t post_local;
+  int32_t ntop;
 };
+// the u8 counters follow in dynamic LDS (16-byte aligned offset)
+constexpr int kPfSharedBytes = (int)((sizeof(PfShared) + 15) & ~(size_t)15);
 
 __device__ __forceinline__ uint32_t cnt_get(const uint32_t* cnt, uint32_t c) {
   return (cnt[c >> 2] >> ((c & 3) * 8)) & 0xffu;
@@ -349,26 +410,78 @@ __device__ void bitonic_u32(uint32_t* a, int n) {
   }
 }
 
-__device__ __forceinline__ void pf_add(uint32_t* cnt, uint32_t c) {
-  atomicAdd(&cnt[c >> 2], 1u << ((c & 3) * 8));  // result unused -> ds_add_u32 (no return)
+// wave-uniform pointer (both halves through readfirstlane), so a descriptor built from it is scalar
+template <typename T>
+__device__ __forceinline__ const T* uniform_ptr(const T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (const T*)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ void pf_chunk(uint32_t* cnt, const uint4& v, uint32_t base, uint32_t lo,
-                                         uint32_t hi) {
+// postings are read with buffer loads (counted on vmcnt only): flat loads also count on lgkmcnt, so
+// every wait for them would drain the fire-and-forget LDS atomics too
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t arena_rsrc(const uint16_t* uniform_base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(uniform_base), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint4 ld_chunk(__amdgpu_buffer_rsrc_t r, uint32_t idx) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 2u), 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// the 8 postings of a chunk: one counter increment each
+__device__ __forceinline__ void pf_chunk(uint32_t* cnt, const uint4& v) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 8; e++) {
-    const uint32_t idx = base + (uint32_t)e;
     const uint32_t c = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-    if (idx >= lo && idx < hi) pf_add(cnt, c);
+    atomicAdd(&cnt[c >> 2], 1u << ((c & 3) * 8));  // result unused -> ds_add_u32 (no return)
   }
 }
 
-__global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    lo |= (uint32_t)__shfl_xor((int)lo, d, 64);
+    hi |= (uint32_t)__shfl_xor((int)hi, d, 64);
+  }
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// exclusive scan over the workgroup (every thread must call it)
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* wsum,
+                                                              unsigned long long& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  unsigned long long base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kPfWaves; w++) {
+    const unsigned long long x = wsum[w];
+    base += (w < wave) ? x : 0ull;
+    tot += x;
+  }
+  total = tot;
+  __syncthreads();
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
-  const int tid = threadIdx.x;
-  const int qs = blockIdx.x;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem + kPfSharedBytes);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int part = (int)(blockIdx.x & (kParts - 1));
+  const int qs = (int)(blockIdx.x >> kPartShift);
   const int qlocal = qs / a.both;
   const int strand = qs % a.both;
   const int32_t q = a.q0 + qlocal;
@@ -381,139 +494,176 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
     S.post_local = 0;
   }
   __syncthreads();
-  int npeer = 0;
-  for (int t = 0; t < a.ntiles + 2; t++) {
-    const bool peer = (t >= a.ntiles);
-    TileView tv;
-    if (peer) tv = a.peer[t - a.ntiles];
-    else tv = a.tiles[t];
-    // peers: only the window queries before q (a peer tile's base is its first seqno)
-    const int limit = peer ? min(tv.n, q - tv.base) : tv.n;
-    if (limit <= 0) continue;
-    // zero the counters (whole uint4 groups: the scan reads 16 counters per lane)
-    const int nq4 = (tv.n + 15) >> 4;
-    uint4* cnt4 = reinterpret_cast<uint4*>(S.cnt);
-    for (int x = tid; x < nq4; x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid < nk) {
-      const uint32_t b = tv.off[S.km[tid]], e = tv.off[S.km[tid] + 1];
-      S.kbeg[tid] = b;
-      S.kend[tid] = e;
-    }
+  const int64_t pq_ = (int64_t)qs * kParts + part;
+  const int npass = a.nseg > 0 ? a.nseg : 1;
+  uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
+  for (int sg = 0; sg < npass; sg++) {
+    const bool last = sg == npass - 1;
+    const int t0 = a.nseg > 0 ? a.seg_tile[sg] : 0;
+    const int nct = a.nseg > 0 ? a.seg_tile[sg + 1] - t0 : 0;  // centroid tiles of this segment
+    const int ntl = nct + (last ? 2 : 0);                       // + the peer tiles in the last pass
+    const int seg0 = sg * kSegCentroids;
+    const int segn = min(a.ncent - seg0, kSegCentroids);
+    const int nsubC = segn > part ? (segn - part + kParts - 1) >> kPartShift : 0;
+    const int ncnt = kCentBase + ((nsubC + 15) & ~15);         // counter bytes in use
+    // the pass's postings are addressed from its lowest arena slot (32-bit buffer offsets)
+    const uint64_t pbase = a.seg_base[sg];
+    const __amdgpu_buffer_rsrc_t arena = arena_rsrc(uniform_ptr(a.arena + pbase));
+    for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
       S.ncand = 0;
+      S.npc = 0;
       S.overflow = 0;
     }
-    __syncthreads();
-    if (tid < 64) {
-      // exclusive prefix of 16-byte chunk counts over the <= 65 lists (wave 0, shuffles)
-      uint32_t carry = 0, touched = 0;
-      for (int k0 = 0; k0 < nk; k0 += 64) {
-        const int k = k0 + tid;
-        uint32_t nch = 0;
-        if (k < nk) {
-          const uint32_t b = S.kbeg[k], e = S.kend[k];
-          touched += e - b;
-          nch = (e > b) ? ((e - (b & ~7u) + 7u) >> 3) : 0u;
-        }
-        uint32_t inc = nch;
+    // list table: the (tile, k-mer) grid, kPfSlots consecutive slots per thread, compacted to the
+    // non-empty lists
+    const int nl = thr > 0 ? ntl * nk : 0;
+    uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t v = __shfl_up(inc, d, 64);
-          if (tid >= d) inc += v;
+    for (int j = 0; j < kPfSlots; j++) {
+      nch[j] = 0;
+      bse[j] = 0;
+      const int L = kPfSlots * tid + j;
+      if (L < nl) {
+        const int ti = L / nk, k = L - ti * nk;
+        const TileView tv = ti < nct ? a.tiles[t0 + ti] : (ti == nct ? a.peer[0] : a.peer[1]);
+        if (tv.n > 0) {
+          const uint32_t* op = tv.off + ((uint32_t)part << 16) + S.km[k];
+          const uint32_t lo = op[0], hi = op[1];
+          nch[j] = (hi - lo) >> 3;
+          bse[j] = (uint32_t)(tv.post_base - pbase) + lo;
         }
-        if (k < nk) S.kchunk[k] = carry + inc - nch;
-        carry += __shfl(inc, 63, 64);
       }
+      sum_ch += nch[j];
+      sum_ne += nch[j] ? 1u : 0u;
+    }
+    unsigned long long tot;
+    const unsigned long long ex = block_excl_scan(((unsigned long long)sum_ch << 16) | sum_ne, S.wsum, tot);
+    const uint32_t T = (uint32_t)(tot >> 16), nlc = (uint32_t)(tot & 0xffffu);
+    {
+      uint32_t li = (uint32_t)(ex & 0xffffu), ci = (uint32_t)(ex >> 16);
 #pragma unroll
-      for (int d = 32; d > 0; d >>= 1) touched += __shfl_xor(touched, d, 64);
-      if (tid == 0) {
-        S.kchunk[nk] = carry;
-        S.post_local += touched;
+      for (int j = 0; j < kPfSlots; j++)
+        if (nch[j]) {
+          S.lstart[li] = ci;
+          S.lbias[li] = bse[j] - 8u * ci;
+          li++;
+          ci += nch[j];
+        }
+      if (tid < 66) S.lstart[nlc + tid] = T;
+    }
+    __syncthreads();
+    // count
+    if (T > 0) {
+      const uint32_t nwin = (T + 63u) >> 6;
+      const uint32_t per = (nwin + kPfWaves - 1) / kPfWaves;
+      const uint32_t wb = (uint32_t)wave * per, we = min(nwin, wb + per);
+      if (wb < we) {
+        // m = the list holding chunk 64 wb (the last list starting at or before it)
+        int lo = 0, hi = (int)nlc - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (S.lstart[mid] <= (wb << 6)) lo = mid;
+          else hi = mid - 1;
+        }
+        uint32_t m = (uint32_t)lo;
+        const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
+        for (uint32_t w = wb; w < we; w++) {
+          const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
+          const uint32_t ck = S.lstart[m + 1 + lane];
+          const unsigned long long sm = wave_or64(ck < g0 + 64u ? (1ull << (ck - g0)) : 0ull);
+          const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
+          m += (uint32_t)__builtin_popcountll(sm);
+          if (g < T) pf_chunk(cnt, ld_chunk(arena, S.lbias[L0] + 8u * g));
+        }
       }
     }
     __syncthreads();
-    if (thr > 0) {
-      const uint32_t total = S.kchunk[nk];
-      int k = 0;
-      for (uint32_t g0 = (uint32_t)tid; g0 < total; g0 += kPfThreads * kPfUnroll) {
-        uint4 v[kPfUnroll];
-        uint32_t base[kPfUnroll], lo[kPfUnroll], hi[kPfUnroll];
-#pragma unroll
-        for (int u = 0; u < kPfUnroll; u++) {
-          const uint32_t g = g0 + (uint32_t)(u * kPfThreads);
-          lo[u] = hi[u] = base[u] = 0;
-          if (g < total) {
-            while (S.kchunk[k + 1] <= g) k++;
-            base[u] = (S.kbeg[k] & ~7u) + 8u * (g - S.kchunk[k]);
-            lo[u] = S.kbeg[k];
-            hi[u] = S.kend[k];
-            v[u] = *reinterpret_cast<const uint4*>(tv.post + base[u]);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < kPfUnroll; u++)
-          if (hi[u] > lo[u]) pf_chunk(S.cnt, v[u], base[u], lo[u], hi[u]);
-      }
+    if (wave == 0) {
+      // postings touched (stats): every chunk posting minus the padding ones, counted by the spare
+      // counters (<= 7 pads per list spread over 64 counters: no u8 overflow in practice)
+      const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
+      const uint32_t pads = wave_sum((uint32_t)cb[kDummy + lane]);
+      if (lane == 0) S.post_local += 8u * T - pads;
     }
-    __syncthreads();
-    // scan: every counter >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
+    // scan: centroid counters >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
     if (thr > 0) {
       const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
-      const int lim4 = (limit + 15) >> 4;
+      const int lim4 = (nsubC + 15) >> 4;
+      const uint4* c4 = cnt4 + kCentBase / 16;
       for (int x = tid; x < lim4; x += kPfThreads) {
-        const uint4 v = cnt4[x];
+        const uint4 v = c4[x];
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          uint32_t m = (w[j] + add) & 0x80808080u;
-          while (m) {
-            const uint32_t byte = (uint32_t)__builtin_ctz(m) >> 3;
-            m &= m - 1u;
+          uint32_t mk = (w[j] + add) & 0x80808080u;
+          while (mk) {
+            const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
+            mk &= mk - 1u;
             const uint32_t c = (uint32_t)x * 16u + (uint32_t)j * 4u + byte;
-            if ((int)c < limit) {
+            if ((int)c < nsubC) {
               const uint32_t slot = atomicAdd(&S.ncand, 1u);
-              if (slot < (uint32_t)kCandCap) S.cand[slot] = c;
+              if (slot < (uint32_t)kPfCand) S.cand[slot] = c;
               else S.overflow = 1;
             }
           }
         }
       }
     }
+    if (last) {
+      // peers: the window queries before q, every count >= thr (all of them when thr == 0)
+      const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
+#pragma unroll
+      for (int v = 0; v < 2; v++) {
+        const TileView pv = v == 0 ? a.peer[0] : a.peer[1];
+        if (pv.n <= 0) continue;
+        const int lim = min(pv.n, q - pv.base);
+        const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
+        for (int s = tid; s < nsubP; s += kPfThreads) {
+          const uint32_t cv = cb[pv.seg * kPeerRegion + s];
+          if ((int)cv >= thr) {
+            const int32_t sq = pv.base + (s << kPartShift) + part;
+            const uint32_t key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) |
+                                 (uint32_t)(sq - a.peer_base);
+            const uint32_t slot = atomicAdd(&S.npc, 1u);
+            if (slot <= (uint32_t)kPeerCap) S.pcand[slot] = key;
+          }
+        }
+      }
+    }
     __syncthreads();
     const bool scan_mode = (thr == 0) || S.overflow;
-    const int nchunks = scan_mode ? (limit + kCandCap - 1) / kCandCap : 1;
+    const int nchunks = scan_mode ? (nsubC + kPfCand - 1) / kPfCand : 1;
     for (int ch = 0; ch < nchunks; ch++) {
-      int nc;
       if (scan_mode) {
         __syncthreads();
         if (tid == 0) S.ncand = 0;
         __syncthreads();
-        const int c0 = ch * kCandCap;
-        const int c1 = min(limit, c0 + kCandCap);
+        const int c0 = ch * kPfCand;
+        const int c1 = min(nsubC, c0 + kPfCand);
         for (int c = c0 + tid; c < c1; c += kPfThreads)
-          if ((int)cnt_get(S.cnt, (uint32_t)c) >= thr) S.cand[atomicAdd(&S.ncand, 1u)] = (uint32_t)c;
+          if ((int)cnt_get(cnt, (uint32_t)(kCentBase + c)) >= thr) S.cand[atomicAdd(&S.ncand, 1u)] = (uint32_t)c;
         __syncthreads();
       }
-      nc = (int)min(S.ncand, (uint32_t)kCandCap);
-      // keys: (127-count) << 23 | len << 16 | local id   (30 bits, unique within a tile; local-id
-      // order is seqno order, so key order is (count desc, length asc, seqno asc))
+      const int nc = (int)min(S.ncand, (uint32_t)kPfCand);
+      // keys: (127-count) << 23 | len << 16 | sub-id   (30 bits, unique within the part of a segment;
+      // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc))
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
-        const uint32_t cntv = cnt_get(S.cnt, c);
-        const int32_t sq = peer ? (tv.base + (int32_t)c) : a.cent_seqno[tv.base + (int32_t)c];
+        const uint32_t cntv = cnt_get(cnt, kCentBase + c);
+        const int32_t sq = a.cent_seqno[seg0 + (int32_t)(c << kPartShift) + part];
         S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
       }
       __syncthreads();
-      // best K of the tile in key order: by rank (all-pairs count, broadcast LDS reads) when the
-      // candidate set is small, by a bitonic sort otherwise
-      const int K = peer ? kPeerCap + 1 : kTopHits;
-      int nbest = nc < K ? nc : K;
+      // best 41 of the segment part in key order: by rank (all-pairs count, broadcast LDS reads)
+      // when the candidate set is small, by a bitonic sort otherwise
+      const int nbest = nc < kTopHits ? nc : kTopHits;
       if (nc <= kRankSel) {
         for (int x = tid; x < nc; x += kPfThreads) {
           const uint32_t kx = S.cand[x];
           int r = 0;
           for (int y = 0; y < nc; y++) r += S.cand[y] < kx;
-          if (r < K) S.best[r] = kx;
+          if (r < kTopHits) S.best[r] = kx;
         }
       } else {
         int np2 = 1;
@@ -524,78 +674,162 @@ __global__ __launch_bounds__(kPfThreads) void k_prefilter(PrefilterArgs a) {
         for (int x = tid; x < nbest; x += kPfThreads) S.best[x] = S.cand[x];
       }
       __syncthreads();
-      if (peer) {
-        if (tid < nbest && npeer + tid < kPeerCap) {
-          const uint32_t key = S.best[tid];
-          a.peer_id[(int64_t)qs * kPeerCap + npeer + tid] =
-              (uint16_t)(tv.base + (int32_t)(key & 0xffffu) - a.peer_base);
-          a.peer_count[(int64_t)qs * kPeerCap + npeer + tid] = (uint8_t)(127u - (key >> 23));
-        }
-        npeer += nc;
-      } else {
-        // merge the tile's best into the running top-41 (u64 keys, unique seqnos): every element
-        // of either sorted list finds its merged position by binary search in the other list
-        const int ntop = S.ntop;
-        if (tid < nbest) {
-          const uint32_t key = S.best[tid];
-          S.bestk[tid] = ((unsigned long long)(key >> 23) << 56) |
-                         ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
-                         (unsigned long long)(uint32_t)a.cent_seqno[tv.base + (int32_t)(key & 0xffffu)];
-        }
-        __syncthreads();
-        if (tid < nbest) {
-          const unsigned long long kj = S.bestk[tid];
-          int lo = 0, hi = ntop;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (S.top[mid] < kj) lo = mid + 1;
-            else hi = mid;
-          }
-          if (tid + lo < kTopHits) S.merged[tid + lo] = kj;
-        } else if (tid >= 64 && tid - 64 < ntop) {
-          const int i = tid - 64;
-          const unsigned long long ki = S.top[i];
-          int lo = 0, hi = nbest;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (S.bestk[mid] < ki) lo = mid + 1;
-            else hi = mid;
-          }
-          if (i + lo < kTopHits) S.merged[i + lo] = ki;
-        }
-        __syncthreads();
-        const int nm = min(kTopHits, ntop + nbest);
-        if (tid < nm) S.top[tid] = S.merged[tid];
-        __syncthreads();
-        if (tid == 0) S.ntop = nm;
+      // merge into the running top-41 (u64 keys, unique seqnos): every element of either sorted
+      // list finds its merged position by binary search in the other list
+      const int ntop = S.ntop;
+      if (tid < nbest) {
+        const uint32_t key = S.best[tid];
+        const int32_t ord = seg0 + (int32_t)((key & 0xffffu) << kPartShift) + part;
+        S.bestk[tid] = ((unsigned long long)(key >> 23) << 56) | ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
+                       (unsigned long long)(uint32_t)a.cent_seqno[ord];
       }
+      __syncthreads();
+      if (tid < nbest) {
+        const unsigned long long kj = S.bestk[tid];
+        int lo = 0, hi = ntop;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (S.top[mid] < kj) lo = mid + 1;
+          else hi = mid;
+        }
+        if (tid + lo < kTopHits) S.merged[tid + lo] = kj;
+      } else if (tid >= 64 && tid - 64 < ntop) {
+        const int i = tid - 64;
+        const unsigned long long ki = S.top[i];
+        int lo = 0, hi = nbest;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (S.bestk[mid] < ki) lo = mid + 1;
+          else hi = mid;
+        }
+        if (i + lo < kTopHits) S.merged[i + lo] = ki;
+      }
+      __syncthreads();
+      const int nm = min(kTopHits, ntop + nbest);
+      if (tid < nm) S.top[tid] = S.merged[tid];
+      __syncthreads();
+      if (tid == 0) S.ntop = nm;
       __syncthreads();
     }
   }
-  if (tid == 0) {
-    const int ntop = S.ntop;
-    for (int x = 0; x < ntop; x++) {
-      a.top_seqno[(int64_t)qs * kTopHits + x] = (uint32_t)(S.top[x] & 0xffffffffull);
-      a.top_count[(int64_t)qs * kTopHits + x] = (uint8_t)(127u - (uint32_t)(S.top[x] >> 56));
+  // peers in key order (<= kPeerCap, else the query-strand overflows)
+  const int np = (int)S.npc;
+  if (np <= kPeerCap) {
+    for (int x = tid; x < np; x += kPfThreads) {
+      const uint32_t kx = S.pcand[x];
+      int r = 0;
+      for (int y = 0; y < np; y++) r += S.pcand[y] < kx;
+      a.ppeer_id[pq_ * kPeerCap + r] = (uint16_t)(kx & 0xffffu);
+      a.ppeer_count[pq_ * kPeerCap + r] = (uint8_t)(127u - (kx >> 23));
     }
-    a.ntop[qs] = (uint8_t)ntop;
-    a.npeer[qs] = (uint8_t)(npeer > kPeerCap ? 255 : npeer);
-    if (a.postings_touched) atomicAdd(a.postings_touched, S.post_local);
+  }
+  const int ntop = S.ntop;
+  if (tid < ntop) a.ptop[pq_ * kTopHits + tid] = S.top[tid];
+  if (tid == 0) {
+    a.pntop[pq_] = (uint8_t)ntop;
+    a.pnpeer[pq_] = (uint8_t)(np > kPeerCap ? 255 : np);
+    if (a.postings_touched && S.post_local) atomicAdd(a.postings_touched, S.post_local);
+  }
+}
+
+// One wave per query-strand: the kParts sorted part lists (distinct seqnos, so distinct keys) are
+// staged in LDS and every key finds its rank in the union by binary search in the other lists;
+// ranks < 41 are the exact top-41.  Peer lists are concatenated in part order.
+constexpr int kMergeWaves = 4;
+__global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs) {
+  __shared__ unsigned long long keys[kMergeWaves][kParts * kTopHits];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qs = (int)blockIdx.x * kMergeWaves + wave;
+  const bool live = qs < nqs;
+  unsigned long long* K = keys[wave];
+  const int64_t p0 = (int64_t)qs * kParts;
+  // list sizes and offsets (lanes 0..kParts-1)
+  int n_l = (live && lane < kParts) ? (int)a.pntop[p0 + lane] : 0;
+  int inc = n_l;
+#pragma unroll
+  for (int d = 1; d < kParts; d <<= 1) {
+    const int u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  const int o_l = inc - n_l;
+  const int total = __shfl(inc, kParts - 1, 64);
+  // list sizes / offsets as wave-uniform values (shuffles only with every lane active)
+  int ln[kParts], lo[kParts];
+#pragma unroll
+  for (int l = 0; l < kParts; l++) {
+    ln[l] = __shfl(n_l, l, 64);
+    lo[l] = __shfl(o_l, l, 64);
+  }
+#pragma unroll
+  for (int l = 0; l < kParts; l++)
+    for (int x = lane; x < ln[l]; x += 64) K[lo[l] + x] = a.ptop[(p0 + l) * kTopHits + x];
+  __syncthreads();
+  for (int e = lane; e < total; e += 64) {
+    const unsigned long long key = K[e];
+    int rank = 0;
+#pragma unroll
+    for (int l = 0; l < kParts; l++) {
+      const int n = ln[l], o = lo[l];
+      if (e >= o && e < o + n) {
+        rank += e - o;  // own list: its position
+        continue;
+      }
+      int b0 = 0, b1 = n;
+      while (b0 < b1) {
+        const int mid = (b0 + b1) >> 1;
+        if (K[o + mid] < key) b0 = mid + 1;
+        else b1 = mid;
+      }
+      rank += b0;
+    }
+    if (rank < kTopHits) {
+      a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)(key & 0xffffffffull);
+      a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
+    }
+  }
+  // peers
+  int np_l = (live && lane < kParts) ? (int)a.pnpeer[p0 + lane] : 0;
+  const bool over = __any(np_l == 255);
+  int pinc = np_l;
+#pragma unroll
+  for (int d = 1; d < kParts; d <<= 1) {
+    const int u = __shfl_up(pinc, d, 64);
+    if (lane >= d) pinc += u;
+  }
+  const int ptotal = __shfl(pinc, kParts - 1, 64);
+  const int po_l = pinc - np_l;
+  if (!live) return;
+  const bool povf = over || ptotal > kPeerCap;
+  if (lane == 0) {
+    a.ntop[qs] = (uint8_t)min(total, kTopHits);
+    a.npeer[qs] = (uint8_t)(povf ? 255 : ptotal);
+  }
+  if (povf) return;
+  for (int l = 0; l < kParts; l++) {
+    const int n = __shfl(np_l, l, 64), o = __shfl(po_l, l, 64);
+    if (lane < n) {
+      a.peer_id[(int64_t)qs * kPeerCap + o + lane] = a.ppeer_id[(p0 + l) * kPeerCap + lane];
+      a.peer_count[(int64_t)qs * kPeerCap + o + lane] = a.ppeer_count[(p0 + l) * kPeerCap + lane];
+    }
   }
 }
 
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
-  const size_t smem = sizeof(PfShared);
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_prefilter,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    const int most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
+    hipError_t e = hipFuncSetAttribute((const void*)k_prefilter, hipFuncAttributeMaxDynamicSharedMemorySize, most);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_prefilter, dim3(nqs), dim3(kPfThreads), smem, st, a);
+  // LDS: the fixed part + counters for the peer regions, the spares and one segment's centroids
+  const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
+  const size_t smem = (size_t)kPfSharedBytes + kCentBase + ((((segn + kParts - 1) >> kPartShift) + 15) & ~15);
+  hipLaunchKernelGGL(k_prefilter, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+  hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st,
+                     a, nqs);
   return hipGetLastError();
 }
 

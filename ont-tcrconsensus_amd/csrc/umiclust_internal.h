@@ -11,12 +11,32 @@ constexpr int kMinTplLen = 32;       // shortest query length with a compiled al
 constexpr int kCodeWords = kMaxLen / 8;  // 4-bit codes, 8 residues per u32
 constexpr int kMaxKmers = kMaxLen - 8 + 1;  // unique 8-mers per strand <= 65
 constexpr int kKmerStride = 68;     // u16 slots per (sequence, strand) k-mer list
-constexpr int kTile = 65536;        // centroids per index tile (u16 local ids)
+constexpr int kTile = 65536;        // centroids per sealed index tile
+// Index layout.  Every posting list is split into kParts parts by the ordinal of its sequence
+// (centroid ordinal, or seqno for the per-block peer tiles): part = x % kParts.  The prefilter runs
+// one workgroup per (query-strand, part) and the launch maps part p to XCD p (workgroups are dealt
+// to the 8 XCDs round-robin), so each XCD's L2 holds only its part of the index.  CSR bins are
+// part-major (bin = part << 16 | k-mer) and every list is padded to a multiple of 8 postings
+// (16-byte chunks; padding postings hit spare counters), so the counting loop needs no bounds.
+// A posting IS its LDS counter index:
+//   [0, kPeerRegion)              peer tiles of even blocks   (x - base) / kParts
+//   [kPeerRegion, 2*kPeerRegion)  peer tiles of odd blocks
+//   [kDummy, kDummy + 64)         padding postings
+//   [kCentBase, ...)              centroids: kCentBase + (ordinal % kSegCentroids) / kParts
+// Centroids beyond kSegCentroids live in further counter segments, processed one after another.
+constexpr int kParts = 8;
+constexpr int kPartShift = 3;
+constexpr int kBins = kParts << 16;
+constexpr int kMaxBlock = 8192;                     // queries per greedy block
+constexpr int kPeerRegion = kMaxBlock / kParts;     // counter slots per part of a peer tile
+constexpr int kDummy = 2 * kPeerRegion;
+constexpr int kCentBase = kDummy + 64;
+constexpr int kSegCentroids = 7 * kTile;            // counter indexes stay below 65536
+constexpr int kMaxSegs = 16;
 constexpr int kTopHits = 41;        // maxaccepts + maxrejects + MAXDELAYED (searchcore.cc)
 constexpr int kBatch = 8;           // MAXDELAYED: alignment batch of search_onequery
 constexpr int kWalk = 32;           // maxaccepts + maxrejects - 1: most candidates ever aligned
 constexpr int kPeerCap = 64;        // in-block peer candidates kept per query-strand
-constexpr int kCandCap = 2048;      // LDS candidate buffer of the prefilter
 constexpr int kOpsStride = 2 * kMaxLen;  // alignment ops per member (<= qlen + tlen)
 constexpr int kConsCap = 2 * kMaxLen;    // consensus bytes reserved per cluster
 constexpr int kMsaCols = 2048;      // LDS profile columns of the consensus kernel
@@ -27,12 +47,13 @@ struct Scoring {
   int32_t boundary_open;
 };
 
-// One index tile: CSR over 4^8 k-mers of up to kTile centroids, u16 local ids.
+// One index tile: CSR over bins (part << 16 | k-mer); postings live in one arena shared by all tiles.
 struct TileView {
-  const uint32_t* off;     // [65537]
-  const uint16_t* post;    // postings
-  int32_t n;               // centroids in tile
-  int32_t base;            // centroid ordinal of local id 0
+  const uint32_t* off;     // [kBins + 1] tile-relative, each list a multiple of 8 postings
+  uint64_t post_base;      // arena index of the tile's first posting
+  int32_t n;               // sequences in the tile
+  int32_t base;            // first centroid ordinal / first seqno (peer tiles)
+  int32_t seg;             // counter segment (centroid tiles) / peer region 0|1 (peer tiles)
 };
 
 struct DevSeqs {
@@ -46,27 +67,44 @@ struct DevSeqs {
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
                        char* masked, uint32_t* ambig, hipStream_t st);
-hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
-                              int32_t first, int32_t count, uint32_t* hist, hipStream_t st);
-// hist_to_off: [65536] histogram followed by [65537] offsets
-hipError_t launch_index_scan(uint32_t* hist_to_off, hipStream_t st);
-hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* cent_seqno,
-                             int32_t first, int32_t count, const uint32_t* off, uint32_t* cursor,
+// index tile build over sequences c in [0, count) with seqno map[first + c] and ordinal
+// x = xoff + c (centroid tiles: the centroid ordinal; peer tiles: c): count (hist[kBins], all zero
+// on entry), scan (padded offsets off[kBins+1], fill cursors, padding postings written into post,
+// hist re-zeroed), fill (posting = vbase + (x % seg_mod) / kParts)
+constexpr int kScanPer = 1024;
+constexpr int kScanBlocks = kBins / kScanPer;
+hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
+                              int32_t count, int32_t xoff, uint32_t* hist, hipStream_t st);
+hipError_t launch_index_scan(uint32_t* hist, uint32_t* partial, uint32_t* off, uint32_t* cursor, uint16_t* post,
+                             hipStream_t st);
+hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
+                             int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod, uint32_t* cursor,
                              uint16_t* post, hipStream_t st);
 // prefilter: for query-strands qs in [0, nqs): query seqno = q0 + qs/2 (or qs if !both), strand.
 struct PrefilterArgs {
   DevSeqs seqs;
-  const TileView* tiles;   // device array
+  const uint16_t* arena;   // postings of every tile
+  const TileView* tiles;   // device array, centroid tiles in segment order
   int32_t ntiles;
+  int32_t nseg;            // counter segments holding centroids (0 if none)
+  int32_t seg_tile[kMaxSegs + 1];  // tiles of segment s: [seg_tile[s], seg_tile[s+1])
+  uint64_t seg_base[kMaxSegs];     // lowest arena index a pass of segment s reads (peers: last pass)
+  int32_t ncent;           // centroid ordinals [0, ncent) are indexed
   const int32_t* cent_seqno;  // centroid ordinal -> sorted seqno
   int32_t q0, nq;          // block of queries (sorted seqnos)
   int32_t both;            // strands per query (1 or 2)
   int32_t minwordmatches;
   // peer tiles: mini indexes over the + strand k-mers of the previous block and of this block
-  // (base = first seqno, local id c = seqno - base; n = 0 if absent); together they cover the peer
-  // window [peer_base, q0+nq), and a query sees the window entries before it
+  // (base = first seqno, n = 0 if absent); together they cover the peer window [peer_base, q0+nq),
+  // and a query sees the window entries before it
   TileView peer[2];
   int32_t peer_base;
+  // per-(query-strand, part) outputs, merged by launch_prefilter's second kernel
+  unsigned long long* ptop;  // [nqs*kParts*kTopHits] keys (127-count)<<56 | len<<48 | seqno, sorted
+  uint8_t* pntop;            // [nqs*kParts]
+  uint16_t* ppeer_id;        // [nqs*kParts*kPeerCap]
+  uint8_t* ppeer_count;      // [nqs*kParts*kPeerCap]
+  uint8_t* pnpeer;           // [nqs*kParts] (255 = overflow)
   // outputs
   uint32_t* top_seqno;     // [nqs*kTopHits]
   uint8_t* top_count;      // [nqs*kTopHits]
@@ -76,6 +114,7 @@ struct PrefilterArgs {
   uint8_t* npeer;          // [nqs] (255 = overflow)
   uint32_t* postings_touched;  // [1] atomic counter (stats)
 };
+// two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st);
 
 // alignment of pairs whose queries all have length qlen; pq = (query seqno << 1) | strand, pt = target seqno (plus strand)
