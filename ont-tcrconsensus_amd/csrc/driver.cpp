@@ -194,6 +194,8 @@ struct umiclust_ctx {
   Tile base_tile, delta_tile;
   int32_t sealed_end = 0, base_end = 0;
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
+  DevBuf<uint8_t> d_cent_len;     // ordinal -> length
+  std::vector<uint8_t> cent_len;
   // two passes in flight (software pipeline over blocks) + round B on a side stream
   Pass pass[2];
   Tile blk_tile[3], solo_tile;    // per-block peer tiles (ring), overflow re-runs
@@ -485,6 +487,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     }
   }
   a.cent_seqno = c->d_cent.p;
+  a.cent_len = c->d_cent_len.p;
   a.q0 = q0;
   a.nq = nq;
   a.both = both;
@@ -747,10 +750,16 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   if (new_cents.empty()) return;
   hipStream_t st = c->st;
   const int32_t ord0 = (int32_t)c->cent.size();
-  for (int32_t q : new_cents) c->cent.push_back(q);  // capacity reserved: no reallocation
+  for (int32_t q : new_cents) {  // capacity reserved: no reallocation
+    c->cent.push_back(q);
+    c->cent_len.push_back(c->hlen[q]);
+  }
   c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4, hipMemcpyHostToDevice,
                         st),
          "h2d cent");
+  c->hip(hipMemcpyAsync(c->d_cent_len.p + ord0, c->cent_len.data() + ord0, new_cents.size(), hipMemcpyHostToDevice,
+                        st),
+         "h2d cent len");
   const int32_t ordend = (int32_t)c->cent.size();
   if (c->nix >= c->ix_events.size()) {
     hipEvent_t e0, e1;
@@ -798,6 +807,8 @@ void cluster_all(umiclust_ctx* c) {
   c->target.assign(n, -1);
   c->cent.clear();
   c->cent.reserve((size_t)n + 1);
+  c->cent_len.clear();
+  c->cent_len.reserve((size_t)n + 1);
   c->nclusters = 0;
   c->hip(hipStreamSynchronize(c->st), "sync");  // no queued work may still read the old tiles
   for (Tile* t : c->tiles) delete t;
@@ -810,6 +821,7 @@ void cluster_all(umiclust_ctx* c) {
   c->stats.n_input = c->n_input;
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
+  c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
   std::vector<uint8_t> state(n, ST_UNDET);
   double t_pf = 0, t_al = 0, t_host = 0;
   // blocks of at most B queries of one length (the aligner is compiled per query length); a block's

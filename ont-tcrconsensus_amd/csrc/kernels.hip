@@ -364,7 +364,8 @@ constexpr int kPfCand = 1024;   // LDS candidate buffer (centroids)
 constexpr int kRankSel = 512;   // candidate counts up to this are selected by rank
 constexpr int kPfTiles = 12;    // tiles per counter segment: 7 sealed + base + delta + 2 peer (+1)
 constexpr int kPfLists = kMaxKmers * kPfTiles;
-constexpr int kPfSlots = (kPfLists + kPfThreads - 1) / kPfThreads;  // list-table slots per thread
+constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
+constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
 struct PfShared {
   uint32_t lstart[kPfLists + 66];   // first chunk of each non-empty list, then the chunk total
@@ -376,7 +377,6 @@ struct PfShared {
   unsigned long long bestk[kTopHits];
   unsigned long long wsum[kPfWaves];
   uint32_t best[kPeerCap + 1];
-  uint16_t km[kMaxKmers + 3];
   uint32_t ncand;
   uint32_t npc;
   uint32_t overflow;
@@ -429,6 +429,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t arena_rsrc(const uint16_t* uni
 __device__ __forceinline__ uint4 ld_chunk(__amdgpu_buffer_rsrc_t r, uint32_t idx) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 2u), 0, 0);
   return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// a tile view through scalar loads (the address is wave-uniform and the views are read-only)
+__device__ __forceinline__ TileView load_view(const TileView* p) {
+  const __attribute__((address_space(4))) u32x4* q = (const __attribute__((address_space(4))) u32x4*)p;
+  struct Raw {
+    u32x4 a, b;
+  } r{q[0], q[1]};
+  return __builtin_bit_cast(TileView, r);
 }
 
 // the 8 postings of a chunk: one counter increment each
@@ -488,12 +497,13 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
   const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
   const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
   const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
-  for (int x = tid; x < nk; x += kPfThreads) S.km[x] = qk[x];
+  // every wave keeps the query's k-mers in registers: lane l holds k-mers l and l + 64
+  const uint32_t km0 = lane < nk ? qk[lane] : 0u, km1 = lane + 64 < nk ? qk[lane + 64] : 0u;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
   if (tid == 0) {
     S.ntop = 0;
     S.post_local = 0;
   }
-  __syncthreads();
   const int64_t pq_ = (int64_t)qs * kParts + part;
   const int npass = a.nseg > 0 ? a.nseg : 1;
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
@@ -515,25 +525,34 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       S.npc = 0;
       S.overflow = 0;
     }
-    // list table: the (tile, k-mer) grid, kPfSlots consecutive slots per thread, compacted to the
-    // non-empty lists
-    const int nl = thr > 0 ? ntl * nk : 0;
+    // list table: wave w takes tiles w, w + kPfWaves, ... (the tile view is wave-uniform: scalar
+    // loads) and lane l the query's k-mers l and l + 64; compacted to the non-empty lists
     uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
 #pragma unroll
-    for (int j = 0; j < kPfSlots; j++) {
-      nch[j] = 0;
-      bse[j] = 0;
-      const int L = kPfSlots * tid + j;
-      if (L < nl) {
-        const int ti = L / nk, k = L - ti * nk;
-        const TileView tv = ti < nct ? a.tiles[t0 + ti] : (ti == nct ? a.peer[0] : a.peer[1]);
+    for (int it = 0; it < kPfTilesPerWave; it++) {
+      const int ti = wv + it * kPfWaves;
+      nch[2 * it] = nch[2 * it + 1] = 0u;
+      bse[2 * it] = bse[2 * it + 1] = 0u;
+      if (thr > 0 && ti < ntl) {
+        const TileView tv = ti < nct ? load_view(a.tiles + t0 + ti) : (ti == nct ? a.peer[0] : a.peer[1]);
         if (tv.n > 0) {
-          const uint32_t* op = tv.off + ((uint32_t)part << 16) + S.km[k];
-          const uint32_t lo = op[0], hi = op[1];
-          nch[j] = (hi - lo) >> 3;
-          bse[j] = (uint32_t)(tv.post_base - pbase) + lo;
+          const uint32_t* op = tv.off + ((uint32_t)part << 16);
+          const uint32_t tb = (uint32_t)(tv.post_base - pbase);
+          if (lane < nk) {
+            const uint32_t lo = op[km0], hi = op[km0 + 1];
+            nch[2 * it] = (hi - lo) >> 3;
+            bse[2 * it] = tb + lo;
+          }
+          if (lane + 64 < nk) {
+            const uint32_t lo = op[km1], hi = op[km1 + 1];
+            nch[2 * it + 1] = (hi - lo) >> 3;
+            bse[2 * it + 1] = tb + lo;
+          }
         }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < kPfSlots; j++) {
       sum_ch += nch[j];
       sum_ne += nch[j] ? 1u : 0u;
     }
@@ -651,8 +670,8 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(cnt, kCentBase + c);
-        const int32_t sq = a.cent_seqno[seg0 + (int32_t)(c << kPartShift) + part];
-        S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | c;
+        const uint32_t len = a.cent_len[seg0 + (int32_t)(c << kPartShift) + part];
+        S.cand[x] = ((127u - cntv) << 23) | (len << 16) | c;
       }
       __syncthreads();
       // best 41 of the segment part in key order: by rank (all-pairs count, broadcast LDS reads)

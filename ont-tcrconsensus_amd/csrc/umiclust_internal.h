@@ -91,6 +91,7 @@ struct PrefilterArgs {
   uint64_t seg_base[kMaxSegs];     // lowest arena index a pass of segment s reads (peers: last pass)
   int32_t ncent;           // centroid ordinals [0, ncent) are indexed
   const int32_t* cent_seqno;  // centroid ordinal -> sorted seqno
+  const uint8_t* cent_len;    // centroid ordinal -> length
   int32_t q0, nq;          // block of queries (sorted seqnos)
   int32_t both;            // strands per query (1 or 2)
   int32_t minwordmatches;
