@@ -86,11 +86,15 @@ struct PinBuf {
     p = nullptr;
     n = 0;
   }
+  // Kernels write these buffers directly (pinned host memory is device-accessible); the host reads
+  // them only after the writing kernel's completion event, and copies what it scans into pageable
+  // vectors first.
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
     release();
     size_t c = count ? count : 1;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), c * sizeof(T), hipHostMallocDefault);
+    const unsigned flags = hipHostMallocDefault;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), c * sizeof(T), flags);
     if (e == hipSuccess) n = c;
     return e;
   }
@@ -140,11 +144,13 @@ struct Pass {
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
   DevBuf<WalkState> d_ws;
   DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
-  PinBuf<WalkState> h_ws;
-  PinBuf<uint8_t> h_ntop, h_npeer, h_peer_count, h_top_count;
-  PinBuf<uint16_t> h_peer_id;
-  PinBuf<uint32_t> h_counters, h_peer_res, h_top_seqno, h_res;
-  hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, download done
+  DevBuf<uint32_t> d_reccount;
+  // written by k_pack into host memory: per query-strand outcomes, records, counters
+  PinBuf<HostQs> h_hq;
+  PinBuf<uint32_t> h_rec, h_counters;
+  std::vector<HostQs> hq_copy;
+  std::vector<uint32_t> rec_copy;
+  hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   ~Pass() {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
@@ -409,20 +415,14 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_outidx.ensure(nqs * kBatch), "alloc");
   c->hip(P.d_res.ensure(nqs * kWalk), "alloc");
   c->hip(P.d_ws.ensure(nqs), "alloc");
-  c->hip(P.h_ws.ensure(nqs), "pin");
-  c->hip(P.h_ntop.ensure(nqs), "pin");
-  c->hip(P.h_npeer.ensure(nqs), "pin");
-  c->hip(P.h_peer_count.ensure(nqs * kPeerCap), "pin");
-  c->hip(P.h_peer_id.ensure(nqs * kPeerCap), "pin");
+  c->hip(P.d_reccount.ensure(1), "alloc");
+  c->hip(P.h_hq.ensure(nqs), "pin");
+  c->hip(P.h_rec.ensure(nqs * kRecWords), "pin");
   c->hip(P.h_counters.ensure(16), "pin");
   c->hip(P.d_ppq.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_ppt.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_poutidx.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_res.ensure(nqs * kPeerCap), "alloc");
-  c->hip(P.h_peer_res.ensure(nqs * kPeerCap), "pin");
-  c->hip(P.h_top_seqno.ensure(nqs * kTopHits), "pin");
-  c->hip(P.h_top_count.ensure(nqs * kTopHits), "pin");
-  c->hip(P.h_res.ensure(nqs * kWalk), "pin");
   // fixed capacities, so a pass never frees memory a queued pass still reads
   c->hip(P.h_tiles.ensure(64), "pin");
   c->hip(P.d_tiles.ensure(64), "alloc");
@@ -525,41 +525,33 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
                        st),
            "walk");
   }
-  c->hip(launch_peer_pairs(q0, w0, nqs, both, P.d_peer_id.p, P.d_npeer.p, P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p,
-                           P.d_counters.p + 8, st),
+  c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
+                           P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p, P.d_counters.p + 8, st),
          "peer pairs");
   c->hip(launch_align(ds, qlen, c->ambig, P.d_ppq.p, P.d_ppt.p, nqs * kPeerCap, P.d_counters.p + 8,
                       P.d_poutidx.p, c->sc, P.d_peer_res.p, st),
          "align peers");
   c->hip(hipEventRecord(P.ev[3], st), "event");
-  // the download runs on the copy stream, overlapping the next queued pass's kernels; the pass
-  // that next reuses these buffers is enqueued only after the host has waited for ev[4]
-  hipStream_t sc = c->st_copy;
-  c->hip(hipStreamWaitEvent(sc, P.ev[3], 0), "wait");
-  auto d2h = [&](void* dst, const void* src, size_t bytes) {
-    c->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, sc), "d2h");
-  };
-  d2h(P.h_ws.p, P.d_ws.p, (size_t)nqs * sizeof(WalkState));
-  d2h(P.h_ntop.p, P.d_ntop.p, (size_t)nqs);
-  d2h(P.h_npeer.p, P.d_npeer.p, (size_t)nqs);
-  d2h(P.h_peer_id.p, P.d_peer_id.p, (size_t)nqs * kPeerCap * 2);
-  d2h(P.h_peer_count.p, P.d_peer_count.p, (size_t)nqs * kPeerCap);
-  d2h(P.h_peer_res.p, P.d_peer_res.p, (size_t)nqs * kPeerCap * 4);
-  d2h(P.h_top_seqno.p, P.d_top_seqno.p, (size_t)nqs * kTopHits * 4);
-  d2h(P.h_top_count.p, P.d_top_count.p, (size_t)nqs * kTopHits);
-  d2h(P.h_res.p, P.d_res.p, (size_t)nqs * kWalk * 4);
-  d2h(P.h_counters.p, P.d_counters.p, 16 * 4);
-  c->hip(hipEventRecord(P.ev[4], sc), "event");
+  // what the host needs goes straight to pinned host memory; the pass that next reuses these
+  // buffers is enqueued only after the host has waited for ev[4]
+  c->hip(hipMemsetAsync(P.d_reccount.p, 0, 4, st), "memset");
+  c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
+                     P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_peer_res.p, P.d_reccount.p, P.h_hq.p,
+                     P.h_rec.p, P.d_counters.p, P.h_counters.p, st),
+         "pack");
+  c->hip(hipEventRecord(P.ev[4], st), "event");
 }
 
 // Wait for a pass and resolve its block on the host in sorted order.  Returns false if a peer
 // list overflowed (the caller re-runs the block in smaller pieces).  Every query of the peer
 // window before the block is already resolved, so peers are final or earlier in this block.
 //
-// A (query, strand) without centroid peers that could change its walk takes the device walk;
-// otherwise the host runs the exact merged walk over T_old u (peers that are centroids).  Only a
-// merged walk that needs a T_old entry the device did not align is deferred to round B (and
-// queries whose peers are deferred).
+// A (query, strand) without a record (no relevant peer: k_pack) takes the device walk.  With one,
+// its outcome depends on the peers' states: a relevant peer still undetermined blocks it; a
+// relevant peer that is a centroid makes the host run the exact merged walk over T_old u (peers
+// that are centroids) -- every such peer now matters, so an undetermined one blocks too.  A merged
+// walk that needs an alignment the pass did not compute (a T_old entry past the device walk, or a
+// peer that was not relevant) is deferred to round B, and so are queries blocked by deferred ones.
 bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::vector<int32_t>& new_cents,
                   double& t_pf, double& t_al, double& t_host) {
   const int both = c->both;
@@ -576,71 +568,118 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
   t_al += ms * 1e-3;
   c->stats.kmer_postings += P.h_counters.p[0];
   c->stats.pairs_peer += P.h_counters.p[8];
+  // pageable copies of the pass's outcomes and records: the scans below revisit them many times
+  const double tc0 = now_s();
+  P.hq_copy.assign(P.h_hq.p, P.h_hq.p + nqs);
+  uint32_t last = 0xffffffffu;
+  for (int32_t qs = 0; qs < nqs; qs++) {
+    const uint32_t r = P.hq_copy[qs].rec;
+    if (r != 0xffffffffu && (last == 0xffffffffu || r > last)) last = r;
+  }
+  uint32_t nrec = 0;
+  if (last != 0xffffffffu) {
+    const uint32_t h0 = P.h_rec.p[last], nt = h0 & 0xffu, np = (h0 >> 8) & 0xffu;
+    nrec = last + 1 + 2 * nt + ((nt + 3) >> 2) + 2 * np;
+  }
+  const double tc1 = now_s();
+  P.rec_copy.assign(P.h_rec.p, P.h_rec.p + nrec);
+  if (getenv("UMICLUST_DEBUG")) {
+    static double t_hq = 0, t_rec = 0, words = 0, qss = 0;
+    t_hq += tc1 - tc0;
+    t_rec += now_s() - tc1;
+    words += nrec;
+    qss += nqs;
+    fprintf(stderr, "copy: qs %.0f hq %.3fs rec words %.0f %.3fs\n", qss, t_hq, words, t_rec);
+  }
+  c->stats.t_sync_s += now_s() - tc0;
+  const HostQs* hq = P.hq_copy.data();
   for (int32_t qs = 0; qs < nqs; qs++)
-    if (P.h_npeer.p[qs] == 255) return false;
+    if (hq[qs].flags & 2u) return false;
   new_cents.clear();
   const double th0 = now_s();
-  const WalkState* ws = P.h_ws.p;
+  constexpr int kSlots = kWalk + kPeerCap;  // round-B result slots per query-strand: T_old, peers
   std::vector<int32_t> deferred;
   std::vector<MCand> L;
   std::vector<std::pair<unsigned long long, int>> cp;
-  std::vector<uint32_t> extra_res;   // [row*kWalk + x] results of round B (valid if flag)
+  std::vector<uint32_t> extra_res;   // [row*kSlots + slot] results of round B (valid if flag)
   std::vector<uint8_t> extra_have;
   std::vector<int32_t> extra_row;    // qs -> row of the round-B arrays (-1: none)
+  struct Rec {
+    int nt, np;
+    const uint32_t *seq, *res, *cw, *peer, *pres;
+    uint32_t count(int x) const { return (cw[x >> 2] >> ((x & 3) * 8)) & 0xffu; }
+  };
+  auto rec_of = [&](const HostQs& h) {
+    const uint32_t* r = P.rec_copy.data() + h.rec;
+    Rec R;
+    R.nt = (int)(r[0] & 0xffu);
+    R.np = (int)((r[0] >> 8) & 0xffu);
+    R.seq = r + 1;
+    R.res = R.seq + R.nt;
+    R.cw = R.res + R.nt;
+    R.peer = R.cw + ((R.nt + 3) >> 2);
+    R.pres = R.peer + R.np;
+    return R;
+  };
+  auto device_outcome = [](const HostQs& h, Outcome& o) {
+    o.acc = (h.flags & 1u) != 0;
+    o.rank = h.best_rank;
+    o.t = h.best_t;
+    o.walked = h.w;
+    o.cells = h.cells;
+  };
   auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o) -> int {
-    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs T_old entries not aligned
-    const int np = P.h_npeer.p[qs];
-    const WalkState& w = ws[qs];
-    // a centroid peer changes the device walk only if it ranks among the walked candidates, or the
-    // last walked batch was not full (the list ended mid-batch: the peer would join that batch), or
-    // the walk ended because the list ran out
-    const bool open_batch = (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
-    bool affects = false;
-    const uint16_t* pid = P.h_peer_id.p + (size_t)qs * kPeerCap;
-    const uint8_t* pcnt = P.h_peer_count.p + (size_t)qs * kPeerCap;
-    for (int x = 0; x < np; x++) {
-      const uint32_t ps = (uint32_t)(w0 + pid[x]);
-      const uint8_t s = state[ps];
-      if (s == ST_UNDET) return 1;
-      if (s == ST_CENT) affects |= open_batch || cand_key(pcnt[x], c->hlen[ps], ps) < w.lastkey;
-    }
-    if (!affects) {
-      o.acc = w.acc;
-      o.rank = w.best_rank;
-      o.t = w.best_t;
-      o.walked = w.w;
-      o.cells = w.cells;
+    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed
+    const HostQs& h = hq[qs];
+    if (h.rec == 0xffffffffu) {
+      device_outcome(h, o);
       return 0;
     }
+    const Rec R = rec_of(h);
+    bool affects = false, undet = false;
+    for (int y = 0; y < R.np; y++) {
+      const uint32_t pw = R.peer[y];
+      const uint8_t st = state[(uint32_t)w0 + (pw & 0xffffu)];
+      if (pw >> 24) {
+        if (st == ST_UNDET) return 1;
+        affects |= st == ST_CENT;
+      } else {
+        undet |= st == ST_UNDET;
+      }
+    }
+    if (!affects) {
+      device_outcome(h, o);
+      return 0;
+    }
+    if (undet) return 1;
     c->stats.n_merged_walks++;
     const double tm0 = now_s();
     struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{&c->stats.t_merged_s, tm0};
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
+    const int32_t row = allow_extra ? extra_row[qs] : -1;
     cp.clear();
-    for (int y = 0; y < np; y++) {
-      const uint32_t ps = (uint32_t)(w0 + pid[y]);
-      if (state[ps] == ST_CENT) cp.push_back({cand_key(pcnt[y], c->hlen[ps], ps), y});
+    for (int y = 0; y < R.np; y++) {
+      const uint32_t pw = R.peer[y];
+      const uint32_t ps = (uint32_t)w0 + (pw & 0xffffu);
+      if (state[ps] == ST_CENT) cp.push_back({cand_key((pw >> 16) & 0xffu, c->hlen[ps], ps), y});
     }
     std::sort(cp.begin(), cp.end());
     L.clear();
-    const int nt = std::min<int>(P.h_ntop.p[qs], kWalk);
-    const uint32_t* ts = P.h_top_seqno.p + (size_t)qs * kTopHits;
-    const uint8_t* tc = P.h_top_count.p + (size_t)qs * kTopHits;
     int i = 0;
     size_t x = 0;
-    while ((int)L.size() < kWalk && (i < nt || x < cp.size())) {
-      const unsigned long long kt = (i < nt) ? cand_key(tc[i], c->hlen[ts[i]], ts[i]) : ~0ull;
+    while ((int)L.size() < kWalk && (i < R.nt || x < cp.size())) {
+      const unsigned long long kt = (i < R.nt) ? cand_key(R.count(i), c->hlen[R.seq[i]], R.seq[i]) : ~0ull;
       const unsigned long long kp = (x < cp.size()) ? cp[x].first : ~0ull;
       MCand m;
       if (kt < kp) {
         m.key = kt;
-        m.seqno = ts[i];
-        if (i < w.w) {
-          m.res = P.h_res.p[(size_t)qs * kWalk + i];
+        m.seqno = R.seq[i];
+        if (i < h.w) {
+          m.res = R.res[i];
           m.have = true;
-        } else if (allow_extra && extra_row[qs] >= 0 && extra_have[(size_t)extra_row[qs] * kWalk + i]) {
-          m.res = extra_res[(size_t)extra_row[qs] * kWalk + i];
+        } else if (row >= 0 && extra_have[(size_t)row * kSlots + i]) {
+          m.res = extra_res[(size_t)row * kSlots + i];
           m.have = true;
         } else {
           m.res = 0;
@@ -650,9 +689,17 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
       } else {
         const int y = cp[x].second;
         m.key = kp;
-        m.seqno = (uint32_t)(w0 + pid[y]);
-        m.res = P.h_peer_res.p[(size_t)qs * kPeerCap + y];
-        m.have = true;
+        m.seqno = (uint32_t)w0 + (R.peer[y] & 0xffffu);
+        if (R.peer[y] >> 24) {
+          m.res = R.pres[y];
+          m.have = true;
+        } else if (row >= 0 && extra_have[(size_t)row * kSlots + kWalk + y]) {
+          m.res = extra_res[(size_t)row * kSlots + kWalk + y];
+          m.have = true;
+        } else {
+          m.res = 0;
+          m.have = false;
+        }
         x++;
       }
       L.push_back(m);
@@ -688,20 +735,29 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
   t_host += now_s() - th0;
   c->stats.t_host_pass1_s += now_s() - th0;
   c->stats.n_deferred += (int64_t)deferred.size();
-  // --- round B (side stream, so the queued pass keeps the device busy): align every T_old entry a
-  // deferred query could still need, then resolve the deferred queries in order
+  // --- round B (side stream, so the queued pass keeps the device busy): align every T_old entry and
+  // every peer a deferred query could still need, then resolve the deferred queries in order
   if (!deferred.empty()) {
     const double th1 = now_s();
     std::vector<uint32_t> bpq, bpt, bidx;
     for (int32_t ql : deferred)
       for (int s = 0; s < both; s++) {
         const int32_t qs = ql * both + s;
-        const int nt = std::min<int>(P.h_ntop.p[qs], kWalk);
-        for (int x = ws[qs].w; x < nt; x++) {
-          bpq.push_back(((uint32_t)(q0 + ql) << 1) | (uint32_t)s);
-          bpt.push_back(P.h_top_seqno.p[(size_t)qs * kTopHits + x]);
-          bidx.push_back((uint32_t)(qs * kWalk + x));
+        const HostQs& h = hq[qs];
+        if (h.rec == 0xffffffffu) continue;
+        const Rec R = rec_of(h);
+        const uint32_t qv = ((uint32_t)(q0 + ql) << 1) | (uint32_t)s;
+        for (int x = h.w; x < R.nt; x++) {
+          bpq.push_back(qv);
+          bpt.push_back(R.seq[x]);
+          bidx.push_back((uint32_t)(qs * kSlots + x));
         }
+        for (int y = 0; y < R.np; y++)
+          if (!(R.peer[y] >> 24)) {
+            bpq.push_back(qv);
+            bpt.push_back((uint32_t)w0 + (R.peer[y] & 0xffffu));
+            bidx.push_back((uint32_t)(qs * kSlots + kWalk + y));
+          }
       }
     t_host += now_s() - th1;
     const int32_t nb = (int32_t)bpq.size();
@@ -728,12 +784,12 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
     extra_row.assign((size_t)nqs, -1);
     for (size_t r = 0; r < deferred.size(); r++)
       for (int s = 0; s < both; s++) extra_row[(size_t)deferred[r] * both + s] = (int32_t)(r * both + s);
-    extra_res.assign(deferred.size() * both * kWalk, 0);
-    extra_have.assign(deferred.size() * both * kWalk, 0);
+    extra_res.assign(deferred.size() * both * kSlots, 0);
+    extra_have.assign(deferred.size() * both * kSlots, 0);
     for (int32_t x = 0; x < nb; x++) {
-      const int32_t qs = (int32_t)(bidx[x] / kWalk), e = (int32_t)(bidx[x] % kWalk);
-      extra_res[(size_t)extra_row[qs] * kWalk + e] = bres[x];
-      extra_have[(size_t)extra_row[qs] * kWalk + e] = 1;
+      const int32_t qs = (int32_t)(bidx[x] / kSlots), e = (int32_t)(bidx[x] % kSlots);
+      extra_res[(size_t)extra_row[qs] * kSlots + e] = bres[x];
+      extra_have[(size_t)extra_row[qs] * kSlots + e] = 1;
     }
     for (int32_t ql : deferred)
       if (!resolve(ql, true))

@@ -1303,12 +1303,24 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
   return hipGetLastError();
 }
 
-// every peer pair (query vs an earlier query of the peer window [w0, q) that passed the k-mer
-// threshold) is aligned speculatively in the same pass, so the host can run the exact merged walk
-// without another round trip whichever peers turn out to be centroids
-__global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* __restrict__ peer_id,
-                             const uint8_t* __restrict__ npeer, uint32_t* __restrict__ pq,
-                             uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
+__device__ __forceinline__ unsigned long long cand_key_dev(uint32_t count, uint32_t len, uint32_t seqno) {
+  return ((unsigned long long)(127u - count) << 56) | ((unsigned long long)len << 48) | seqno;
+}
+// the device walk's last batch is still open: a candidate inserted anywhere could join it
+__device__ __forceinline__ bool walk_open(const WalkState& w) {
+  return (w.w % kBatch) != 0 || w.w == 0 || (!w.acc && w.w < kWalk);
+}
+// a peer (an earlier query of the peer window [w0, q) passing the k-mer threshold) can change the
+// query-strand's walk only if it is a centroid AND it ranks before the walk's last candidate, or
+// the last batch is open; exactly those peers are aligned here, speculatively, in the same pass
+__device__ __forceinline__ bool peer_relevant(const WalkState& w, uint32_t count, uint32_t len, uint32_t seqno) {
+  return walk_open(w) || cand_key_dev(count, len, seqno) < w.lastkey;
+}
+
+__global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* __restrict__ lens,
+                             const WalkState* __restrict__ ws, const uint16_t* __restrict__ peer_id,
+                             const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
+                             uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
                              uint32_t* __restrict__ npairs) {
   // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
   // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
@@ -1316,21 +1328,110 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
   if (qs >= nqs) return;
   const int np = npeer[qs];
   if (np == 255 || np == 0) return;
-  const uint32_t base = atomicAdd(npairs, (uint32_t)np);
-  const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  const WalkState w = ws[qs];
+  unsigned long long rel = 0;
   for (int x = 0; x < np; x++) {
-    pq[base + x] = qv;
-    pt[base + x] = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
-    outidx[base + x] = (uint32_t)(qs * kPeerCap + x);
+    const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
+    if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps)) rel |= 1ull << x;
+  }
+  if (!rel) return;
+  uint32_t k = atomicAdd(npairs, (uint32_t)__builtin_popcountll(rel));
+  const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  for (int x = 0; x < np; x++)
+    if ((rel >> x) & 1ull) {
+      pq[k] = qv;
+      pt[k] = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
+      outidx[k] = (uint32_t)(qs * kPeerCap + x);
+      k++;
+    }
+}
+
+hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
+                             const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
+                             hipStream_t st) {
+  if (nqs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
+                     peer_count, npeer, pq, pt, outidx, npairs);
+  return hipGetLastError();
+}
+
+// What the host needs of a pass, written straight into pinned host memory (no copies): per
+// query-strand the device walk's outcome (HostQs), and -- only for query-strands with a relevant
+// peer, whose outcome depends on which peers turn out to be centroids -- a record with the walk's
+// candidate list (seqno, k-mer count, result of the walked ones) and every peer (window id, count,
+// relevant flag, result of the aligned ones).  One wave per query-strand, lanes writing consecutive
+// words.  Record layout (u32 words): nt | np << 8, seqno[nt], res[nt], counts[(nt+3)/4] (u8 x4),
+// peer[np] (id | count << 16 | relevant << 24), peer_res[np].
+__global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uint8_t* __restrict__ lens,
+                                              const WalkState* __restrict__ ws, const uint8_t* __restrict__ ntop,
+                                              const uint32_t* __restrict__ top_seqno,
+                                              const uint8_t* __restrict__ top_count, const uint32_t* __restrict__ res,
+                                              const uint8_t* __restrict__ npeer, const uint16_t* __restrict__ peer_id,
+                                              const uint8_t* __restrict__ peer_count,
+                                              const uint32_t* __restrict__ peer_res, uint32_t* __restrict__ reccount,
+                                              HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
+                                              const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
+  const int lane = threadIdx.x & 63;
+  const int qs = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x < 16) hcounters[threadIdx.x] = counters[threadIdx.x];
+  if (qs >= nqs) return;
+  const WalkState w = ws[qs];
+  const int np = npeer[qs];
+  bool rel = false;
+  uint32_t pw = 0;
+  if (np != 255 && lane < np) {
+    const uint32_t id = peer_id[(int64_t)qs * kPeerCap + lane];
+    const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + lane];
+    const uint32_t ps = (uint32_t)w0 + id;
+    rel = peer_relevant(w, cnt, lens[ps], ps);
+    pw = id | (cnt << 16) | (rel ? 1u << 24 : 0u);
+  }
+  uint32_t base = 0xffffffffu;
+  if (__any(rel)) {
+    const int nt = min((int)ntop[qs], kWalk);
+    const int ncw = (nt + 3) >> 2;
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(reccount, (uint32_t)(1 + 2 * nt + ncw + 2 * np));
+    base = (uint32_t)__shfl((int)b, 0, 64);
+    uint32_t* r = rec + base;
+    if (lane == 0) r[0] = (uint32_t)nt | ((uint32_t)np << 8);
+    if (lane < nt) {
+      r[1 + lane] = top_seqno[(int64_t)qs * kTopHits + lane];
+      r[1 + nt + lane] = lane < w.w ? res[(int64_t)qs * kWalk + lane] : 0u;
+    }
+    if (lane < ncw) {
+      uint32_t cw = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (4 * lane + e < nt) cw |= (uint32_t)top_count[(int64_t)qs * kTopHits + 4 * lane + e] << (8 * e);
+      r[1 + 2 * nt + lane] = cw;
+    }
+    if (lane < np) {
+      r[1 + 2 * nt + ncw + lane] = pw;
+      r[1 + 2 * nt + ncw + np + lane] = rel ? peer_res[(int64_t)qs * kPeerCap + lane] : 0u;
+    }
+  }
+  if (lane == 0) {
+    HostQs h;
+    h.best_t = w.best_t;
+    h.cells = w.cells;
+    h.rec = base;
+    h.best_rank = w.best_rank;
+    h.w = w.w;
+    h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
+    hq[qs] = h;
   }
 }
 
-hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* peer_id,
-                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
-                             uint32_t* npairs, hipStream_t st) {
+hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
+                       const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
+                       const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
+                       const uint32_t* peer_res, uint32_t* reccount, HostQs* hq, uint32_t* rec,
+                       const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, peer_id, npeer,
-                     pq, pt, outidx, npairs);
+  hipLaunchKernelGGL(k_pack, dim3((nqs + 3) / 4), dim3(256), 0, st, nqs, w0, lens, ws, ntop, top_seqno, top_count,
+                     res, npeer, peer_id, peer_count, peer_res, reccount, hq, rec, counters, hcounters);
   return hipGetLastError();
 }
 

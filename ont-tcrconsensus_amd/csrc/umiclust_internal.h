@@ -143,9 +143,25 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
                        uint32_t* outidx, uint32_t* npairs, hipStream_t st);
-hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint16_t* peer_id,
-                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx,
-                             uint32_t* npairs, hipStream_t st);
+hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
+                             const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
+                             hipStream_t st);
+// per query-strand outcome of the device walk, as the host reads it (pinned host memory)
+struct HostQs {
+  uint32_t best_t;      // best accepted target seqno
+  uint32_t cells;       // sum of qlen*tlen over walked candidates
+  uint32_t rec;         // word offset of the record (relevant peers), 0xffffffff if none
+  uint16_t best_rank;   // id rank of the best accepted hit
+  uint8_t w;            // candidates walked
+  uint8_t flags;        // bit 0: an accepted hit exists; bit 1: peer list overflow
+};
+constexpr int kRecWords = 1 + 2 * kWalk + kWalk / 4 + 2 * kPeerCap;  // largest record
+hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
+                       const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
+                       const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
+                       const uint32_t* peer_res, uint32_t* reccount, HostQs* hq, uint32_t* rec,
+                       const uint32_t* counters, uint32_t* hcounters, hipStream_t st);
 // traceback: ops[k*kOpsStride...] ('M','D','I' in alignment order), nops[k]
 hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
                             int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,
