@@ -112,6 +112,7 @@ struct Tile {
   int32_t n = 0;              // sequences
   int32_t base = 0;           // first centroid ordinal / first seqno (peer tiles)
   int32_t seg = 0;            // counter segment / peer region
+  int32_t len = 0;            // peer tiles: the block's query length
   int32_t built_n = -1;       // n at last build
 };
 
@@ -171,6 +172,7 @@ struct umiclust_ctx {
   bool ambig = false;             // some kept sequence holds a non-ACGT (IUPAC) symbol
   bool loaded = false;
   bool clustered = false;
+  DevBuf<unsigned long long> pf_prof;  // prefilter phase clocks (UMICLUST_PFPROF)
 
   // input (host copies kept only for the file path outputs)
   int64_t n_input = 0;
@@ -202,6 +204,7 @@ struct umiclust_ctx {
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
   DevBuf<uint8_t> d_cent_len;     // ordinal -> length
   std::vector<uint8_t> cent_len;
+  int32_t cnt_ge[kMaxLen + 1] = {};  // centroids of length >= L
   // two passes in flight (software pipeline over blocks) + round B on a side stream
   Pass pass[2];
   Tile blk_tile[3], solo_tile;    // per-block peer tiles (ring), overflow re-runs
@@ -335,6 +338,7 @@ TileView view_of(const Tile& t) {
   v.n = t.n;
   v.base = t.base;
   v.seg = t.seg;
+  v.len = t.len;
   return v;
 }
 
@@ -447,6 +451,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   build_tile(c, own, c->d_iota.p, q0, nq, 0, region * kPeerRegion, 1 << 30);
   own.base = q0;
   own.seg = region;
+  own.len = c->hlen[q0];  // blocks hold one query length
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -487,7 +492,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     }
   }
   a.cent_seqno = c->d_cent.p;
-  a.cent_len = c->d_cent_len.p;
+  for (int L = 0; L <= kMaxLen; L++) a.cnt_ge[L] = c->cnt_ge[L];
   a.q0 = q0;
   a.nq = nq;
   a.both = both;
@@ -507,6 +512,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.peer_count = P.d_peer_count.p;
   a.npeer = P.d_npeer.p;
   a.postings_touched = P.d_counters.p;
+  a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
   c->hip(hipEventRecord(P.ev[0], st), "event");
   c->hip(launch_prefilter(a, st), "prefilter");
   c->hip(hipEventRecord(P.ev[1], st), "event");
@@ -809,6 +815,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   for (int32_t q : new_cents) {  // capacity reserved: no reallocation
     c->cent.push_back(q);
     c->cent_len.push_back(c->hlen[q]);
+    for (int L = 0; L <= c->hlen[q]; L++) c->cnt_ge[L]++;
   }
   c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4, hipMemcpyHostToDevice,
                         st),
@@ -864,6 +871,7 @@ void cluster_all(umiclust_ctx* c) {
   c->cent.clear();
   c->cent.reserve((size_t)n + 1);
   c->cent_len.clear();
+  std::fill(c->cnt_ge, c->cnt_ge + kMaxLen + 1, 0);
   c->cent_len.reserve((size_t)n + 1);
   c->nclusters = 0;
   c->hip(hipStreamSynchronize(c->st), "sync");  // no queued work may still read the old tiles
@@ -1085,6 +1093,15 @@ void cluster_all(umiclust_ctx* c) {
   c->stats.t_align_s = t_al;
   c->stats.t_consensus_s = t_cons;
   c->stats.t_host_s = t_host;
+  if (c->pf_prof.p) {
+    unsigned long long h[9];
+    c->hip(hipMemcpy(h, c->pf_prof.p, sizeof(h), hipMemcpyDeviceToHost), "d2h");
+    const double nwg = h[8] ? (double)h[8] : 1.0;
+    fprintf(stderr,
+            "prefilter phase clocks per workgroup (%llu): query %.0f views %.0f offsets %.0f table %.0f count %.0f "
+            "scan %.0f select %.0f out %.0f\n",
+            h[8], h[5] / nwg, h[6] / nwg, h[7] / nwg, h[0] / nwg, h[1] / nwg, h[2] / nwg, h[3] / nwg, h[4] / nwg);
+  }
   c->stats.t_total_s = now_s() - t0;
   c->clustered = true;
 }
@@ -1512,6 +1529,13 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     return nullptr;
   }
   if (const char* b = getenv("UMICLUST_BLOCK")) c->block_size = std::max(1, std::min(kTile, atoi(b)));
+  if (getenv("UMICLUST_PFPROF")) {
+    if (c->pf_prof.ensure(9) != hipSuccess || hipMemset(c->pf_prof.p, 0, 9 * sizeof(unsigned long long)) != hipSuccess) {
+      delete c;
+      if (err) *err = UMICLUST_EDEVICE;
+      return nullptr;
+    }
+  }
   if (err) *err = UMICLUST_OK;
   return c;
 }

@@ -367,15 +367,22 @@ constexpr int kPfLists = kMaxKmers * kPfTiles;
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
+constexpr int kPfWinBase = 1024;  // windows whose base list is tabulated (the rest: binary search)
 struct PfShared {
-  uint32_t lstart[kPfLists + 66];   // first chunk of each non-empty list, then the chunk total
-  uint32_t lbias[kPfLists];         // posting index of chunk g of list L: lbias[L] + 8 g
-  uint32_t cand[kPfCand];           // candidate sub-ids, then 30-bit keys
+  union {
+    struct {                        // list table (count phase)
+      uint32_t lstart[kPfLists + 66];  // first chunk of each non-empty list, then the chunk total
+      uint32_t lbias[kPfLists];        // posting index of chunk g of list L: lbias[L] + 8 g
+      uint16_t wbase[kPfWinBase];      // the list holding chunk 64 w
+    };
+    uint32_t cand[kPfCand];         // candidate sub-ids, then 30-bit keys (scan / select phases)
+  };
   uint32_t pcand[kPeerCap + 1];     // peer keys
   unsigned long long top[kTopHits];
   unsigned long long merged[kTopHits];
   unsigned long long bestk[kTopHits];
-  unsigned long long wsum[kPfWaves];
+  uint32_t wsum[kPfWaves];
+  int32_t cge[kMaxLen + 1];         // a.cnt_ge
   uint32_t best[kPeerCap + 1];
   uint32_t ncand;
   uint32_t npc;
@@ -431,6 +438,15 @@ __device__ __forceinline__ uint4 ld_chunk(__amdgpu_buffer_rsrc_t r, uint32_t idx
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// two consecutive list offsets of a tile (wave-uniform base): a buffer load, so nothing waits on
+// lgkmcnt for it and the loads of all slots are in flight together
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 ld_off2(const uint32_t* uniform_off, uint32_t idx) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(uniform_off), (short)0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b64(r, (int)(idx * 4u), 0, 0);
+}
+
 // a tile view through scalar loads (the address is wave-uniform and the views are read-only)
 __device__ __forceinline__ TileView load_view(const TileView* p) {
   const __attribute__((address_space(4))) u32x4* q = (const __attribute__((address_space(4))) u32x4*)p;
@@ -450,33 +466,69 @@ __device__ __forceinline__ void pf_chunk(uint32_t* cnt, const uint4& v) {
   }
 }
 
-__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    lo |= (uint32_t)__shfl_xor((int)lo, d, 64);
-    hi |= (uint32_t)__shfl_xor((int)hi, d, 64);
+// Inclusive wave scans on the VALU through DPP (no LDS traffic, unlike ds_bpermute shuffles, whose
+// lgkmcnt waits would also drain the counting loop's LDS atomics): Hillis-Steele over rows of 16
+// lanes (row_shr 1, 2, 4, 8; lanes shifted in from outside the row read 0), then lane 15 of rows 0/2
+// into rows 1/3 (row_bcast:15) and lane 31 into rows 2/3 (row_bcast:31).  All 64 lanes must be active.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v, Op op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+// two independent OR scans interleaved (fills the DPP read-after-write wait states)
+__device__ __forceinline__ void wave_or2_dpp(uint32_t& a, uint32_t& b) {
+#define UC_DPP2(ctrl, rmask, bc)                                                    \
+  {                                                                                 \
+    const uint32_t ta = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, ctrl, rmask, 0xf, bc); \
+    const uint32_t tb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, ctrl, rmask, 0xf, bc); \
+    a |= ta;                                                                        \
+    b |= tb;                                                                        \
   }
-  return ((unsigned long long)hi << 32) | lo;
+  UC_DPP2(0x111, 0xf, true)
+  UC_DPP2(0x112, 0xf, true)
+  UC_DPP2(0x114, 0xf, true)
+  UC_DPP2(0x118, 0xf, true)
+  UC_DPP2(0x142, 0xa, false)
+  UC_DPP2(0x143, 0xc, false)
+#undef UC_DPP2
+}
+struct OpAdd {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+struct OpOr {
+  __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; }
+};
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+// wave-aggregated allocation of n slots per lane from an LDS counter (all 64 lanes active): one
+// atomic per wave; returns the lane's first slot
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t n, uint32_t* counter) {
+  const uint32_t inc = wave_scan_dpp(n, OpAdd());
+  const uint32_t tot = lane63(inc);
+  uint32_t b = 0;
+  if (tot) {
+    if ((threadIdx.x & 63) == 0) b = atomicAdd(counter, tot);
+    b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+  }
+  return b + inc - n;
 }
 
-// exclusive scan over the workgroup (every thread must call it)
-__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* wsum,
-                                                              unsigned long long& total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long inc = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned long long u = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += u;
-  }
-  if (lane == 63) wsum[wave] = inc;
+// exclusive scan over the workgroup (every thread must call it); one DPP scan per wave
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+  const int wave = threadIdx.x >> 6;
+  const uint32_t inc = wave_scan_dpp(v, OpAdd());
+  if ((threadIdx.x & 63) == 63) wsum[wave] = inc;
   __syncthreads();
-  unsigned long long base = 0, tot = 0;
+  uint32_t base = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < kPfWaves; w++) {
-    const unsigned long long x = wsum[w];
-    base += (w < wave) ? x : 0ull;
+    const uint32_t x = wsum[w];
+    base += (w < wave) ? x : 0u;
     tot += x;
   }
   total = tot;
@@ -484,26 +536,40 @@ __device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long
   return base + inc - v;
 }
 
-__global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
+__global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem + kPfSharedBytes);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // optional phase timing (a.prof != nullptr): thread 0's shader-clock deltas between barriers
+  const bool prof = a.prof != nullptr && tid == 0 && blockIdx.x % 61u == 0;  // sampled workgroups
+  unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PF_MARK(i)                                              \
+  if (prof) {                                                   \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    tacc[i] += t_ - tprev;                                      \
+    tprev = t_;                                                 \
+  }
   const int part = (int)(blockIdx.x & (kParts - 1));
   const int qs = (int)(blockIdx.x >> kPartShift);
   const int qlocal = qs / a.both;
   const int strand = qs % a.both;
   const int32_t q = a.q0 + qlocal;
+  // every wave keeps the query's k-mers in registers: lane l holds k-mers l and l + 64 (the k-mer
+  // slots are loaded unconditionally, together with their count, and masked afterwards)
   const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
   const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
+  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane & 3)];
   const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
-  // every wave keeps the query's k-mers in registers: lane l holds k-mers l and l + 64
-  const uint32_t km0 = lane < nk ? qk[lane] : 0u, km1 = lane + 64 < nk ? qk[lane + 64] : 0u;
+  const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
+  PF_MARK(5)
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   if (tid == 0) {
     S.ntop = 0;
     S.post_local = 0;
   }
+  if (tid <= kMaxLen) S.cge[tid] = a.cnt_ge[tid];
   const int64_t pq_ = (int64_t)qs * kParts + part;
   const int npass = a.nseg > 0 ? a.nseg : 1;
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
@@ -519,85 +585,131 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
     // the pass's postings are addressed from its lowest arena slot (32-bit buffer offsets)
     const uint64_t pbase = a.seg_base[sg];
     const __amdgpu_buffer_rsrc_t arena = arena_rsrc(uniform_ptr(a.arena + pbase));
+    // list table: wave w takes tiles w, w + kPfWaves, ... (the tile view is wave-uniform: scalar
+    // loads, issued before anything waits) and lane l the query's k-mers l and l + 64; compacted to
+    // the non-empty lists below
+    TileView tvs[kPfTilesPerWave];
+#pragma unroll
+    for (int it = 0; it < kPfTilesPerWave; it++) {
+      const int ti = wv + it * kPfWaves;
+      if (ti < nct) tvs[it] = load_view(a.tiles + t0 + ti);
+      else if (ti < ntl) tvs[it] = ti == nct ? a.peer[0] : a.peer[1];
+      else tvs[it].n = 0;
+    }
+    PF_MARK(6)
     for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
       S.ncand = 0;
       S.npc = 0;
       S.overflow = 0;
     }
-    // list table: wave w takes tiles w, w + kPfWaves, ... (the tile view is wave-uniform: scalar
-    // loads) and lane l the query's k-mers l and l + 64; compacted to the non-empty lists
+    // every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's
+    // offsets, a k-mer slot past nk reads list 0) and masked afterwards
     uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
+    u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
 #pragma unroll
     for (int it = 0; it < kPfTilesPerWave; it++) {
-      const int ti = wv + it * kPfWaves;
-      nch[2 * it] = nch[2 * it + 1] = 0u;
-      bse[2 * it] = bse[2 * it + 1] = 0u;
-      if (thr > 0 && ti < ntl) {
-        const TileView tv = ti < nct ? load_view(a.tiles + t0 + ti) : (ti == nct ? a.peer[0] : a.peer[1]);
-        if (tv.n > 0) {
-          const uint32_t* op = tv.off + ((uint32_t)part << 16);
-          const uint32_t tb = (uint32_t)(tv.post_base - pbase);
-          if (lane < nk) {
-            const uint32_t lo = op[km0], hi = op[km0 + 1];
-            nch[2 * it] = (hi - lo) >> 3;
-            bse[2 * it] = tb + lo;
-          }
-          if (lane + 64 < nk) {
-            const uint32_t lo = op[km1], hi = op[km1 + 1];
-            nch[2 * it + 1] = (hi - lo) >> 3;
-            bse[2 * it + 1] = tb + lo;
-          }
-        }
-      }
+      const bool live = thr > 0 && tvs[it].n > 0;
+      const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[1].off) + ((uint32_t)part << 16));
+      o0[it] = ld_off2(op, km0);
+      o1[it] = ld_off2(op, km1);
     }
+#pragma unroll
+    for (int it = 0; it < kPfTilesPerWave; it++) {
+      const bool live = thr > 0 && tvs[it].n > 0;
+      const uint32_t tb = (uint32_t)(tvs[it].post_base - pbase);
+      nch[2 * it] = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
+      bse[2 * it] = tb + o0[it].x;
+      nch[2 * it + 1] = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
+      bse[2 * it + 1] = tb + o1[it].x;
+    }
+    PF_MARK(7)
 #pragma unroll
     for (int j = 0; j < kPfSlots; j++) {
       sum_ch += nch[j];
       sum_ne += nch[j] ? 1u : 0u;
     }
-    unsigned long long tot;
-    const unsigned long long ex = block_excl_scan(((unsigned long long)sum_ch << 16) | sum_ne, S.wsum, tot);
-    const uint32_t T = (uint32_t)(tot >> 16), nlc = (uint32_t)(tot & 0xffffu);
+    // packed scan: chunks << 10 | lists (lists <= kPfLists < 1024; chunks per tile part < 2^12 per
+    // list, so the chunk total stays below 2^22)
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan((sum_ch << 10) | sum_ne, S.wsum, tot);
+    const uint32_t T = tot >> 10, nlc = tot & 1023u;
     {
-      uint32_t li = (uint32_t)(ex & 0xffffu), ci = (uint32_t)(ex >> 16);
+      uint32_t li = ex & 1023u, ci = ex >> 10;
 #pragma unroll
       for (int j = 0; j < kPfSlots; j++)
         if (nch[j]) {
           S.lstart[li] = ci;
           S.lbias[li] = bse[j] - 8u * ci;
+          // windows whose first chunk lies in this list
+          for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch[j] && w < (uint32_t)kPfWinBase; w++)
+            S.wbase[w] = (uint16_t)li;
           li++;
           ci += nch[j];
         }
       if (tid < 66) S.lstart[nlc + tid] = T;
     }
     __syncthreads();
+    PF_MARK(0)
     // count
     if (T > 0) {
       const uint32_t nwin = (T + 63u) >> 6;
-      const uint32_t per = (nwin + kPfWaves - 1) / kPfWaves;
-      const uint32_t wb = (uint32_t)wave * per, we = min(nwin, wb + per);
-      if (wb < we) {
-        // m = the list holding chunk 64 wb (the last list starting at or before it)
-        int lo = 0, hi = (int)nlc - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (S.lstart[mid] <= (wb << 6)) lo = mid;
-          else hi = mid - 1;
+      const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
+      // arena index of this lane's chunk of window w (~0u past the stream's end).  The window's
+      // base list m (the one holding chunk 64 w) comes from the table; the lists that start inside
+      // the window (lstart[m + 1 + l] - 64 w < 64) set one bit each of a wave-uniform mask, and the
+      // lane's list is m + the starts at or before it.  Windows are independent, so the address
+      // chains of a batch overlap.
+      auto window = [&](uint32_t w) -> uint32_t {
+        if (w >= nwin) return 0xffffffffu;
+        const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
+        uint32_t m;
+        if (w < (uint32_t)kPfWinBase) {
+          m = S.wbase[w];
+        } else {
+          int lo = 0, hi = (int)nlc - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.lstart[mid] <= g0) lo = mid;
+            else hi = mid - 1;
+          }
+          m = (uint32_t)lo;
         }
-        uint32_t m = (uint32_t)lo;
-        const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
-        for (uint32_t w = wb; w < we; w++) {
-          const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
-          const uint32_t ck = S.lstart[m + 1 + lane];
-          const unsigned long long sm = wave_or64(ck < g0 + 64u ? (1ull << (ck - g0)) : 0ull);
-          const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
-          m += (uint32_t)__builtin_popcountll(sm);
-          if (g < T) pf_chunk(cnt, ld_chunk(arena, S.lbias[L0] + 8u * g));
-        }
+        const uint32_t bit = S.lstart[m + 1 + lane] - g0;
+        uint32_t lo32 = bit < 32u ? 1u << bit : 0u, hi32 = bit - 32u < 32u ? 1u << (bit - 32u) : 0u;
+        wave_or2_dpp(lo32, hi32);
+        const unsigned long long sm = ((unsigned long long)lane63(hi32) << 32) | lane63(lo32);
+        const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
+        return g < T ? S.lbias[L0] + 8u * g : 0xffffffffu;
+      };
+      // wave v counts windows v, v + 4, v + 8, ... in batches of two, one batch of loads in flight
+      // ahead of the batch being counted.  Two register sets are used alternately (a copy between
+      // them would wait for the loads in flight) and the loop body has no exit between the halves:
+      // every load and counter update is unconditional, so the compiler neither sinks a prefetch
+      // below the other batch's updates nor waits for more than the oldest loads.  A lane past the
+      // end of the stream reads chunk 0 and counts into its own trash counter word.
+      const uint32_t tw = (uint32_t)(kTrash + 4 * lane), tr = tw | (tw << 16);
+      const uint4 trash = make_uint4(tr, tr, tr, tr);
+      auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
+      constexpr uint32_t S1 = kPfWaves;
+      uint32_t w = (uint32_t)wave;
+      uint32_t a0 = window(w), a1 = window(w + S1);
+      uint4 v0 = ldv(a0), v1 = ldv(a1);
+      for (; w < nwin; w += 4 * S1) {
+        const uint32_t b0 = window(w + 2 * S1), b1 = window(w + 3 * S1);
+        const uint4 u0 = ldv(b0), u1 = ldv(b1);
+        pf_chunk(cnt, a0 != 0xffffffffu ? v0 : trash);
+        pf_chunk(cnt, a1 != 0xffffffffu ? v1 : trash);
+        a0 = window(w + 4 * S1);
+        a1 = window(w + 5 * S1);
+        v0 = ldv(a0);
+        v1 = ldv(a1);
+        pf_chunk(cnt, b0 != 0xffffffffu ? u0 : trash);
+        pf_chunk(cnt, b1 != 0xffffffffu ? u1 : trash);
       }
     }
     __syncthreads();
+    PF_MARK(1)
     if (wave == 0) {
       // postings touched (stats): every chunk posting minus the padding ones, counted by the spare
       // counters (<= 7 pads per list spread over 64 counters: no u8 overflow in practice)
@@ -605,52 +717,62 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       const uint32_t pads = wave_sum((uint32_t)cb[kDummy + lane]);
       if (lane == 0) S.post_local += 8u * T - pads;
     }
-    // scan: centroid counters >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr)
+    // scan: centroid counters >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr);
+    // each wave sweeps 64 counter vectors per step and takes LDS slots with one atomic per step
+    const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
     if (thr > 0) {
-      const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
-      const int lim4 = (nsubC + 15) >> 4;
+      const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
       const uint4* c4 = cnt4 + kCentBase / 16;
-      for (int x = tid; x < lim4; x += kPfThreads) {
-        const uint4 v = c4[x];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (int x0 = wave * 64; x0 < lim4; x0 += kPfThreads) {
+        const int x = x0 + lane;
+        const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t mk[4] = {(v.x + add) & 0x80808080u, (v.y + add) & 0x80808080u, (v.z + add) & 0x80808080u,
+                          (v.w + add) & 0x80808080u};
+        const uint32_t n = (uint32_t)(__builtin_popcount(mk[0]) + __builtin_popcount(mk[1]) +
+                                      __builtin_popcount(mk[2]) + __builtin_popcount(mk[3]));
+        uint32_t slot = wave_alloc(n, &S.ncand);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          uint32_t mk = (w[j] + add) & 0x80808080u;
-          while (mk) {
-            const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
-            mk &= mk - 1u;
-            const uint32_t c = (uint32_t)x * 16u + (uint32_t)j * 4u + byte;
-            if ((int)c < nsubC) {
-              const uint32_t slot = atomicAdd(&S.ncand, 1u);
-              if (slot < (uint32_t)kPfCand) S.cand[slot] = c;
-              else S.overflow = 1;
-            }
+          while (mk[j]) {
+            const uint32_t byte = (uint32_t)__builtin_ctz(mk[j]) >> 3;
+            mk[j] &= mk[j] - 1u;
+            if (slot < (uint32_t)kPfCand) S.cand[slot] = (uint32_t)x * 16u + (uint32_t)j * 4u + byte;
+            else S.overflow = 1;
+            slot++;
           }
         }
       }
     }
     if (last) {
       // peers: the window queries before q, every count >= thr (all of them when thr == 0)
-      const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
 #pragma unroll
       for (int v = 0; v < 2; v++) {
         const TileView pv = v == 0 ? a.peer[0] : a.peer[1];
         if (pv.n <= 0) continue;
         const int lim = min(pv.n, q - pv.base);
         const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
-        for (int s = tid; s < nsubP; s += kPfThreads) {
-          const uint32_t cv = cb[pv.seg * kPeerRegion + s];
-          if ((int)cv >= thr) {
-            const int32_t sq = pv.base + (s << kPartShift) + part;
-            const uint32_t key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) |
-                                 (uint32_t)(sq - a.peer_base);
-            const uint32_t slot = atomicAdd(&S.npc, 1u);
+        const int nwords = (nsubP + 3) >> 2;
+        const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
+        for (int x0 = wave * 64; x0 < nwords; x0 += kPfThreads) {
+          const int x = x0 + lane;
+          const uint32_t w = x < nwords ? pw[x] : 0u;
+          const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
+          uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
+          uint32_t slot = wave_alloc((uint32_t)__builtin_popcount(mk), &S.npc);
+          while (mk) {
+            const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
+            mk &= mk - 1u;
+            const uint32_t cv = (w >> (8 * byte)) & 0xffu;
+            const int32_t sq = pv.base + ((4 * x + (int)byte) << kPartShift) + part;
+            const uint32_t key = ((127u - cv) << 23) | ((uint32_t)pv.len << 16) | (uint32_t)(sq - a.peer_base);
             if (slot <= (uint32_t)kPeerCap) S.pcand[slot] = key;
+            slot++;
           }
         }
       }
     }
     __syncthreads();
+    PF_MARK(2)
     const bool scan_mode = (thr == 0) || S.overflow;
     const int nchunks = scan_mode ? (nsubC + kPfCand - 1) / kPfCand : 1;
     for (int ch = 0; ch < nchunks; ch++) {
@@ -666,12 +788,19 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       }
       const int nc = (int)min(S.ncand, (uint32_t)kPfCand);
       // keys: (127-count) << 23 | len << 16 | sub-id   (30 bits, unique within the part of a segment;
-      // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc))
+      // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc));
+      // the length is the largest L with cnt_ge[L] > ordinal (binary search in LDS, no HBM read)
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(cnt, kCentBase + c);
-        const uint32_t len = a.cent_len[seg0 + (int32_t)(c << kPartShift) + part];
-        S.cand[x] = ((127u - cntv) << 23) | (len << 16) | c;
+        const int32_t ord = seg0 + (int32_t)(c << kPartShift) + part;
+        int lo = 0, hi = kMaxLen;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (S.cge[mid] > ord) lo = mid;
+          else hi = mid - 1;
+        }
+        S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)lo << 16) | c;
       }
       __syncthreads();
       // best 41 of the segment part in key order: by rank (all-pairs count, broadcast LDS reads)
@@ -698,9 +827,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       const int ntop = S.ntop;
       if (tid < nbest) {
         const uint32_t key = S.best[tid];
+        // the ordinal stands in for the seqno (same order); k_pf_merge maps it
         const int32_t ord = seg0 + (int32_t)((key & 0xffffu) << kPartShift) + part;
         S.bestk[tid] = ((unsigned long long)(key >> 23) << 56) | ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
-                       (unsigned long long)(uint32_t)a.cent_seqno[ord];
+                       (unsigned long long)(uint32_t)ord;
       }
       __syncthreads();
       if (tid < nbest) {
@@ -730,6 +860,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
       if (tid == 0) S.ntop = nm;
       __syncthreads();
     }
+    PF_MARK(3)
   }
   // peers in key order (<= kPeerCap, else the query-strand overflows)
   const int np = (int)S.npc;
@@ -749,6 +880,13 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_prefilter(PrefilterArgs a) {
     a.pnpeer[pq_] = (uint8_t)(np > kPeerCap ? 255 : np);
     if (a.postings_touched && S.post_local) atomicAdd(a.postings_touched, S.post_local);
   }
+  PF_MARK(4)
+  if (prof) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) atomicAdd(&a.prof[i], tacc[i]);
+    atomicAdd(&a.prof[8], 1ull);
+  }
+#undef PF_MARK
 }
 
 // One wave per query-strand: the kParts sorted part lists (distinct seqnos, so distinct keys) are
@@ -802,7 +940,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       rank += b0;
     }
     if (rank < kTopHits) {
-      a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)(key & 0xffffffffull);
+      a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)a.cent_seqno[(uint32_t)(key & 0xffffffffull)];
       a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
     }
   }

@@ -22,6 +22,7 @@ constexpr int kTile = 65536;        // centroids per sealed index tile
 //   [0, kPeerRegion)              peer tiles of even blocks   (x - base) / kParts
 //   [kPeerRegion, 2*kPeerRegion)  peer tiles of odd blocks
 //   [kDummy, kDummy + 64)         padding postings
+//   [kTrash, kTrash + 256)        lanes past the end of the posting stream, one word per lane (never read)
 //   [kCentBase, ...)              centroids: kCentBase + (ordinal % kSegCentroids) / kParts
 // Centroids beyond kSegCentroids live in further counter segments, processed one after another.
 constexpr int kParts = 8;
@@ -30,7 +31,8 @@ constexpr int kBins = kParts << 16;
 constexpr int kMaxBlock = 8192;                     // queries per greedy block
 constexpr int kPeerRegion = kMaxBlock / kParts;     // counter slots per part of a peer tile
 constexpr int kDummy = 2 * kPeerRegion;
-constexpr int kCentBase = kDummy + 64;
+constexpr int kTrash = kDummy + 64;
+constexpr int kCentBase = kTrash + 256;
 constexpr int kSegCentroids = 7 * kTile;            // counter indexes stay below 65536
 constexpr int kMaxSegs = 16;
 constexpr int kTopHits = 41;        // maxaccepts + maxrejects + MAXDELAYED (searchcore.cc)
@@ -54,6 +56,7 @@ struct TileView {
   int32_t n;               // sequences in the tile
   int32_t base;            // first centroid ordinal / first seqno (peer tiles)
   int32_t seg;             // counter segment (centroid tiles) / peer region 0|1 (peer tiles)
+  int32_t len;             // peer tiles: the block's query length (one length per block)
 };
 
 struct DevSeqs {
@@ -91,7 +94,10 @@ struct PrefilterArgs {
   uint64_t seg_base[kMaxSegs];     // lowest arena index a pass of segment s reads (peers: last pass)
   int32_t ncent;           // centroid ordinals [0, ncent) are indexed
   const int32_t* cent_seqno;  // centroid ordinal -> sorted seqno
-  const uint8_t* cent_len;    // centroid ordinal -> length
+  // centroids of length >= L, for L = 0..kMaxLen: lengths never increase with the ordinal (queries
+  // are length-sorted, centroids appended in query order), so ordinal o has the largest L with
+  // cnt_ge[L] > o
+  int32_t cnt_ge[kMaxLen + 1];
   int32_t q0, nq;          // block of queries (sorted seqnos)
   int32_t both;            // strands per query (1 or 2)
   int32_t minwordmatches;
@@ -101,7 +107,7 @@ struct PrefilterArgs {
   TileView peer[2];
   int32_t peer_base;
   // per-(query-strand, part) outputs, merged by launch_prefilter's second kernel
-  unsigned long long* ptop;  // [nqs*kParts*kTopHits] keys (127-count)<<56 | len<<48 | seqno, sorted
+  unsigned long long* ptop;  // [nqs*kParts*kTopHits] keys (127-count)<<56 | len<<48 | ordinal, sorted
   uint8_t* pntop;            // [nqs*kParts]
   uint16_t* ppeer_id;        // [nqs*kParts*kPeerCap]
   uint8_t* ppeer_count;      // [nqs*kParts*kPeerCap]
@@ -114,6 +120,7 @@ struct PrefilterArgs {
   uint8_t* peer_count;     // [nqs*kPeerCap]
   uint8_t* npeer;          // [nqs] (255 = overflow)
   uint32_t* postings_touched;  // [1] atomic counter (stats)
+  unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
 };
 // two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st);
