@@ -367,7 +367,8 @@ constexpr int kPfLists = kMaxKmers * kPfTiles;
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
-constexpr int kPfWinBase = 1024;  // windows whose base list is tabulated (the rest: binary search)
+constexpr int kPfWinBase = 1024;
+constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors  // windows whose base list is tabulated (the rest: binary search)
 struct PfShared {
   union {
     struct {                        // list table (count phase)
@@ -382,7 +383,7 @@ struct PfShared {
   unsigned long long merged[kTopHits];
   unsigned long long bestk[kTopHits];
   uint32_t wsum[kPfWaves];
-  int32_t cge[kMaxLen + 1];         // a.cnt_ge
+  alignas(16) int32_t cge[kCge];    // a.cnt_ge, zero-padded
   uint32_t best[kPeerCap + 1];
   uint32_t ncand;
   uint32_t npc;
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
     S.ntop = 0;
     S.post_local = 0;
   }
-  if (tid <= kMaxLen) S.cge[tid] = a.cnt_ge[tid];
+  if (tid < kCge) S.cge[tid] = tid <= kMaxLen ? a.cnt_ge[tid] : 0;
   const int64_t pq_ = (int64_t)qs * kParts + part;
   const int npass = a.nseg > 0 ? a.nseg : 1;
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
@@ -714,7 +715,7 @@ __global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
       // postings touched (stats): every chunk posting minus the padding ones, counted by the spare
       // counters (<= 7 pads per list spread over 64 counters: no u8 overflow in practice)
       const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
-      const uint32_t pads = wave_sum((uint32_t)cb[kDummy + lane]);
+      const uint32_t pads = lane63(wave_scan_dpp((uint32_t)cb[kDummy + lane], OpAdd()));
       if (lane == 0) S.post_local += 8u * T - pads;
     }
     // scan: centroid counters >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr);
@@ -789,29 +790,43 @@ __global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
       const int nc = (int)min(S.ncand, (uint32_t)kPfCand);
       // keys: (127-count) << 23 | len << 16 | sub-id   (30 bits, unique within the part of a segment;
       // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc));
-      // the length is the largest L with cnt_ge[L] > ordinal (binary search in LDS, no HBM read)
+      // the length is the largest L with cnt_ge[L] > ordinal = #{L >= 1 : cnt_ge[L] > ordinal}
+      // (broadcast 16-byte LDS reads, no HBM read)
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(cnt, kCentBase + c);
         const int32_t ord = seg0 + (int32_t)(c << kPartShift) + part;
-        int lo = 0, hi = kMaxLen;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (S.cge[mid] > ord) lo = mid;
-          else hi = mid - 1;
+        uint32_t len = 0;
+        const int4* g4 = reinterpret_cast<const int4*>(S.cge);
+#pragma unroll
+        for (int i = 0; i < kCge / 4; i++) {
+          const int4 g = g4[i];
+          len += (uint32_t)(g.x > ord) + (uint32_t)(g.y > ord) + (uint32_t)(g.z > ord) + (uint32_t)(g.w > ord);
         }
-        S.cand[x] = ((127u - cntv) << 23) | ((uint32_t)lo << 16) | c;
+        S.cand[x] = ((127u - cntv) << 23) | ((len - 1u) << 16) | c;
       }
       __syncthreads();
       // best 41 of the segment part in key order: by rank (all-pairs count, broadcast LDS reads)
-      // when the candidate set is small, by a bitonic sort otherwise
+      // when the candidate set is small, by a bitonic sort otherwise.  With one pass (one counter
+      // segment, no chunked scan) they are the part's final list and go straight to HBM.
+      const bool direct = npass == 1 && !scan_mode;
+      // u64 key: (127-count) << 56 | len << 48 | ordinal (the ordinal stands in for the seqno: same
+      // order; k_pf_merge maps it)
+      auto key64 = [&](uint32_t key) {
+        const int32_t ord = seg0 + (int32_t)((key & 0xffffu) << kPartShift) + part;
+        return ((unsigned long long)(key >> 23) << 56) | ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
+               (unsigned long long)(uint32_t)ord;
+      };
       const int nbest = nc < kTopHits ? nc : kTopHits;
       if (nc <= kRankSel) {
         for (int x = tid; x < nc; x += kPfThreads) {
           const uint32_t kx = S.cand[x];
           int r = 0;
           for (int y = 0; y < nc; y++) r += S.cand[y] < kx;
-          if (r < kTopHits) S.best[r] = kx;
+          if (r < kTopHits) {
+            if (direct) a.ptop[pq_ * kTopHits + r] = key64(kx);
+            else S.best[r] = kx;
+          }
         }
       } else {
         int np2 = 1;
@@ -819,19 +834,20 @@ __global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
         for (int x = nc + tid; x < np2; x += kPfThreads) S.cand[x] = 0xffffffffu;
         __syncthreads();
         bitonic_u32(S.cand, np2);
-        for (int x = tid; x < nbest; x += kPfThreads) S.best[x] = S.cand[x];
+        for (int x = tid; x < nbest; x += kPfThreads) {
+          if (direct) a.ptop[pq_ * kTopHits + x] = key64(S.cand[x]);
+          else S.best[x] = S.cand[x];
+        }
+      }
+      if (direct) {
+        if (tid == 0) S.ntop = -1 - nbest;  // written already
+        break;
       }
       __syncthreads();
       // merge into the running top-41 (u64 keys, unique seqnos): every element of either sorted
       // list finds its merged position by binary search in the other list
       const int ntop = S.ntop;
-      if (tid < nbest) {
-        const uint32_t key = S.best[tid];
-        // the ordinal stands in for the seqno (same order); k_pf_merge maps it
-        const int32_t ord = seg0 + (int32_t)((key & 0xffffu) << kPartShift) + part;
-        S.bestk[tid] = ((unsigned long long)(key >> 23) << 56) | ((unsigned long long)((key >> 16) & 0x7fu) << 48) |
-                       (unsigned long long)(uint32_t)ord;
-      }
+      if (tid < nbest) S.bestk[tid] = key64(S.best[tid]);
       __syncthreads();
       if (tid < nbest) {
         const unsigned long long kj = S.bestk[tid];
@@ -873,10 +889,11 @@ __global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
       a.ppeer_count[pq_ * kPeerCap + r] = (uint8_t)(127u - (kx >> 23));
     }
   }
-  const int ntop = S.ntop;
+  __syncthreads();
+  const int ntop = S.ntop;  // < 0: -1 - (entries written directly)
   if (tid < ntop) a.ptop[pq_ * kTopHits + tid] = S.top[tid];
   if (tid == 0) {
-    a.pntop[pq_] = (uint8_t)ntop;
+    a.pntop[pq_] = (uint8_t)(ntop < 0 ? -1 - ntop : ntop);
     a.pnpeer[pq_] = (uint8_t)(np > kPeerCap ? 255 : np);
     if (a.postings_touched && S.post_local) atomicAdd(a.postings_touched, S.post_local);
   }
