@@ -150,7 +150,6 @@ struct Pass {
   PinBuf<HostQs> h_hq;
   PinBuf<uint32_t> h_rec, h_counters;
   std::vector<HostQs> hq_copy;
-  std::vector<uint32_t> rec_copy;
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   ~Pass() {
     for (hipEvent_t e : ev)
@@ -213,6 +212,7 @@ struct umiclust_ctx {
   int32_t index_end = 0;          // centroid ordinals [0, index_end) are indexed
   int32_t pass_B = 0;
   hipStream_t st_b = nullptr, st_copy = nullptr;
+  hipStream_t st_al = nullptr;    // walk / alignment rounds / packing of the passes
   hipEvent_t evb[2] = {nullptr, nullptr};
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ix_events;  // index rebuild timing
@@ -516,6 +516,11 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipEventRecord(P.ev[0], st), "event");
   c->hip(launch_prefilter(a, st), "prefilter");
   c->hip(hipEventRecord(P.ev[1], st), "event");
+  // The walk, its alignment rounds and the packing run on the align stream: they read only this
+  // pass's buffers and the sequences, so the main stream goes on with the index append of the block
+  // being resolved and the next pass's prefilter while these small launches run.
+  c->hip(hipStreamWaitEvent(c->st_al, P.ev[1], 0), "wait");
+  st = c->st_al;
   DevSeqs ds = dev_seqs(c);
   const int32_t qlen = c->hlen[q0];
   c->hip(launch_walk(-1, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
@@ -574,29 +579,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
   t_al += ms * 1e-3;
   c->stats.kmer_postings += P.h_counters.p[0];
   c->stats.pairs_peer += P.h_counters.p[8];
-  // pageable copies of the pass's outcomes and records: the scans below revisit them many times
+  // a pageable copy of the per-query-strand outcomes (sequential, revisited below); the records
+  // are read in place, only for the query-strands whose relevant peers include a centroid
   const double tc0 = now_s();
   P.hq_copy.assign(P.h_hq.p, P.h_hq.p + nqs);
-  uint32_t last = 0xffffffffu;
-  for (int32_t qs = 0; qs < nqs; qs++) {
-    const uint32_t r = P.hq_copy[qs].rec;
-    if (r != 0xffffffffu && (last == 0xffffffffu || r > last)) last = r;
-  }
-  uint32_t nrec = 0;
-  if (last != 0xffffffffu) {
-    const uint32_t h0 = P.h_rec.p[last], nt = h0 & 0xffu, np = (h0 >> 8) & 0xffu;
-    nrec = last + 1 + 2 * nt + ((nt + 3) >> 2) + 2 * np;
-  }
-  const double tc1 = now_s();
-  P.rec_copy.assign(P.h_rec.p, P.h_rec.p + nrec);
-  if (getenv("UMICLUST_DEBUG")) {
-    static double t_hq = 0, t_rec = 0, words = 0, qss = 0;
-    t_hq += tc1 - tc0;
-    t_rec += now_s() - tc1;
-    words += nrec;
-    qss += nqs;
-    fprintf(stderr, "copy: qs %.0f hq %.3fs rec words %.0f %.3fs\n", qss, t_hq, words, t_rec);
-  }
   c->stats.t_sync_s += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
   for (int32_t qs = 0; qs < nqs; qs++)
@@ -616,7 +602,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
     uint32_t count(int x) const { return (cw[x >> 2] >> ((x & 3) * 8)) & 0xffu; }
   };
   auto rec_of = [&](const HostQs& h) {
-    const uint32_t* r = P.rec_copy.data() + h.rec;
+    const uint32_t* r = P.h_rec.p + h.rec;
     Rec R;
     R.nt = (int)(r[0] & 0xffu);
     R.np = (int)((r[0] >> 8) & 0xffu);
@@ -640,6 +626,18 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
     if (h.rec == 0xffffffffu) {
       device_outcome(h, o);
       return 0;
+    }
+    if (h.nrel <= (uint32_t)kInlineRel) {
+      bool cent = false;
+      for (uint32_t i = 0; i < h.nrel; i++) {
+        const uint8_t st = state[(uint32_t)w0 + h.rel[i]];
+        if (st == ST_UNDET) return 1;
+        cent |= st == ST_CENT;
+      }
+      if (!cent) {
+        device_outcome(h, o);
+        return 0;
+      }
     }
     const Rec R = rec_of(h);
     bool affects = false, undet = false;
@@ -968,6 +966,7 @@ void cluster_all(umiclust_ctx* c) {
     c->stats.n_blocks++;
     if (k + 2 < nb) enqueue(k + 2, true);
   }
+  c->hip(hipStreamSynchronize(c->st_al), "sync");
   c->hip(hipStreamSynchronize(c->st), "sync");
   for (size_t i = 0; i < c->nix; i++) {
     float ms = 0;
@@ -1517,6 +1516,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_b, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->st_al, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
       hipEventCreate(&c->pass[0].ev[0]) != hipSuccess || hipEventCreate(&c->pass[0].ev[1]) != hipSuccess ||
@@ -1555,6 +1555,7 @@ void umiclust_destroy(umiclust_ctx* c) {
   }
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
+  if (c->st_al) (void)hipStreamDestroy(c->st_al);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }

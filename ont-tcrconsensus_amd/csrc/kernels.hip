@@ -1567,6 +1567,20 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
       r[1 + 2 * nt + ncw + np + lane] = rel ? peer_res[(int64_t)qs * kPeerCap + lane] : 0u;
     }
   }
+  // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform mask)
+  unsigned long long rm = __ballot(rel);
+  const uint32_t nrel = (uint32_t)__builtin_popcountll(rm);
+  uint16_t ids[kInlineRel];
+#pragma unroll
+  for (int i = 0; i < kInlineRel; i++) {
+    uint32_t id = 0;
+    if (rm) {
+      const int l = __builtin_ctzll(rm);
+      rm &= rm - 1ull;
+      id = (uint32_t)__builtin_amdgcn_readlane((int)(pw & 0xffffu), l);
+    }
+    ids[i] = (uint16_t)id;
+  }
   if (lane == 0) {
     HostQs h;
     h.best_t = w.best_t;
@@ -1575,6 +1589,9 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     h.best_rank = w.best_rank;
     h.w = w.w;
     h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
+    h.nrel = nrel;
+#pragma unroll
+    for (int i = 0; i < kInlineRel; i++) h.rel[i] = ids[i];
     hq[qs] = h;
   }
 }

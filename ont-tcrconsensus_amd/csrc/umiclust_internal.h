@@ -155,6 +155,7 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
                              hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
+constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {
   uint32_t best_t;      // best accepted target seqno
   uint32_t cells;       // sum of qlen*tlen over walked candidates
@@ -162,7 +163,11 @@ struct HostQs {
   uint16_t best_rank;   // id rank of the best accepted hit
   uint8_t w;            // candidates walked
   uint8_t flags;        // bit 0: an accepted hit exists; bit 1: peer list overflow
+  uint32_t nrel;        // relevant peers
+  uint16_t rel[kInlineRel];  // the first kInlineRel of them (window ids), so the host reads the
+                             // record only when one turns out to be a centroid (or nrel is larger)
 };
+static_assert(sizeof(HostQs) == 32, "HostQs layout");
 constexpr int kRecWords = 1 + 2 * kWalk + kWalk / 4 + 2 * kPeerCap;  // largest record
 hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
