@@ -537,7 +537,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return base + inc - v;
 }
 
-__global__ __launch_bounds__(kPfThreads, 6) void k_prefilter(PrefilterArgs a) {
+__global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem + kPfSharedBytes);
