@@ -33,7 +33,7 @@ extern "C" {
 #define UMICLUST_ESTATE (-77)   /* call out of order (e.g. cluster before load) */
 #define UMICLUST_ERANGE (-34)   /* a sequence exceeds the supported length (UMICLUST_MAX_LEN) */
 
-#define UMICLUST_MAX_LEN 72     /* longest sequence the kernels are compiled for */
+#define UMICLUST_MAX_LEN 112    /* longest sequence the kernels are compiled for */
 
 /* gap slots (vsearch --gapopen/--gapext letters): Q = gap in the query (CIGAR I, consumes the
  * target), T = gap in the target (CIGAR D, consumes the query); L/I/R = left end, interior,

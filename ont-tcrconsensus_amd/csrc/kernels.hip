@@ -17,6 +17,7 @@
 
 #include <cstdlib>
 
+#include "align_kernels.h"
 #include "umiclust_internal.h"
 
 namespace uc {
@@ -121,10 +122,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ 
   int len = (int)(offs[r + 1] - b);
   for (int x = 0; x < len; x++) P.ch[x] = (uint8_t)ascii[b + x];
   // lower-case mask bits (bit x set = masked), 3 words
-  uint32_t mk0 = 0, mk1 = 0, mk2 = 0;
+  uint32_t mk[kMaskWords];
+#pragma unroll
+  for (int w = 0; w < kMaskWords; w++) mk[w] = 0;
   if (dust) {
     // dust(): the whole sequence upper-cased, masked intervals lower-cased
-    uint8_t* codes2 = reinterpret_cast<uint8_t*>(P.km);  // >= 72 bytes available (136)
+    uint8_t* codes2 = reinterpret_cast<uint8_t*>(P.km);  // >= kMaxLen bytes available (2 * kMaxKmers + 6)
     for (int x = 0; x < len; x++) codes2[x] = (uint8_t)code2_of4(c_map4[P.ch[x]]);
     for (int i = 0; i < len; i += 32) {
       int l = (len > i + 64) ? 64 : len - i;
@@ -132,15 +135,19 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ 
       int v = dust_wo(codes2 + i, l, &a, &e, P.words, P.counts);
       if (v > 20) {
         for (int j = a + i; j <= e + i; j++) {
-          if (j < 32) mk0 |= 1u << j;
-          else if (j < 64) mk1 |= 1u << (j - 32);
-          else mk2 |= 1u << (j - 64);
+#pragma unroll
+          for (int w = 0; w < kMaskWords; w++)
+            if ((j >> 5) == w) mk[w] |= 1u << (j & 31);
         }
       }
     }
   }
   auto masked_at = [&](int x) -> uint32_t {
-    return x < 32 ? (mk0 >> x) & 1u : (x < 64 ? (mk1 >> (x - 32)) & 1u : (mk2 >> (x - 64)) & 1u);
+    uint32_t b = 0;
+#pragma unroll
+    for (int w = 0; w < kMaskWords; w++)
+      if ((x >> 5) == w) b = (mk[w] >> (x & 31)) & 1u;
+    return b;
   };
   lens[s] = (uint8_t)len;
   // masked ASCII (what vsearch prints) and 4-bit codes for both strands
@@ -364,6 +371,12 @@ constexpr int kPfCand = 1024;   // LDS candidate buffer (centroids)
 constexpr int kRankSel = 512;   // candidate counts up to this are selected by rank
 constexpr int kPfTiles = 12;    // tiles per counter segment: 7 sealed + base + delta + 2 peer (+1)
 constexpr int kPfLists = kMaxKmers * kPfTiles;
+// the list-table scan packs (chunks << kListBits | lists) into 32 bits; a list holds <= kTile / kParts
+// postings (<= 1024 chunks + padding), so the chunk total stays below 2^(32 - kListBits)
+constexpr int kListBits = kPfLists < 1024 ? 10 : 11;
+constexpr uint32_t kListMask = (1u << kListBits) - 1u;
+static_assert(kPfLists < (1 << kListBits) && (uint64_t)kPfLists * (kTile / kParts / 8 + 1) < (1ull << (32 - kListBits)),
+              "list-table scan overflows");
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
   // slots are loaded unconditionally, together with their count, and masked afterwards)
   const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
   const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
-  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane & 3)];
+  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane < kKmerStride - 64 ? lane : 0)];
   const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
   const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
   PF_MARK(5)
@@ -630,13 +643,13 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
       sum_ch += nch[j];
       sum_ne += nch[j] ? 1u : 0u;
     }
-    // packed scan: chunks << 10 | lists (lists <= kPfLists < 1024; chunks per tile part < 2^12 per
+    // packed scan: chunks << kListBits | lists (see kListBits)
     // list, so the chunk total stays below 2^22)
     uint32_t tot;
-    const uint32_t ex = block_excl_scan((sum_ch << 10) | sum_ne, S.wsum, tot);
-    const uint32_t T = tot >> 10, nlc = tot & 1023u;
+    const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, S.wsum, tot);
+    const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
     {
-      uint32_t li = ex & 1023u, ci = ex >> 10;
+      uint32_t li = ex & kListMask, ci = ex >> kListBits;
 #pragma unroll
       for (int j = 0; j < kPfSlots; j++)
         if (nch[j]) {
@@ -1007,375 +1020,33 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ K3: alignment (stats)
-__device__ __forceinline__ int sx16(uint32_t v) { return (int)(int16_t)(v & 0xffffu); }
-__device__ __forceinline__ uint32_t pack_hf(int h, int f) {
-  return ((uint32_t)f << 16) | ((uint32_t)h & 0xffffu);
+static AlignFn g_align[3 * (kMaxLen + 1)];
+static TraceFn g_trace[kMaxLen + 1];
+static void init_align_tables() {
+  static bool init = false;
+  if (init) return;
+  fill_align_part0(g_align, g_trace);
+  fill_align_part1(g_align, g_trace);
+  fill_align_part2(g_align, g_trace);
+  fill_align_part3(g_align, g_trace);
+  fill_align_part4(g_align, g_trace);
+  fill_align_part5(g_align, g_trace);
+  init = true;
 }
-
-constexpr int kNegInf = -16000;  // below any reachable score (|score| <= 72*40 + gaps)
-
-// Query rows are unrolled: QL is a compile-time constant (the driver cuts greedy blocks at length
-// changes, so every pair of a launch has the same query length) and the per-row state lives in
-// VGPRs with compile-time indices.  Target columns run as a runtime loop (lanes may have different
-// target lengths); the target's last column takes the target-right gap penalties (one select per
-// column, shared by all rows).
-//
-// Forward-carried traceback (no direction matrix).  vsearch's acceptance needs, along the path
-// backtrack16 picks, the matches m and internal_len = columns - leading gap run - trailing gap run
-// (align_trim).  For every real DP cell the leading CIGAR run is exactly the boundary run (row -1
-// or column -1) the path starts with, so columns - leading run = the number of moves INTO real
-// cells, a.  Each DP state carries the summary a | m << 8 of the path the traceback would follow
-// from it (boundary states carry 0), selected with backtrack16's strict priorities
-// (diagonal > up/D > left/I; a gap extends only if strictly better than reopening).
-// The trailing gap run is backtrack16's first run from the end cell (last row, last column):
-//  * an I run walks left along the last row; with Lext(j) = run length when arriving at column j in
-//    an I run: Lh(j) = left(j) ? 1 + Lext(j-1) : 0, Lext(j) = extleft(j) ? 1 + Lext(j-1) : Lh(j);
-//  * a D run walks up the last column: the F state's summary carries the length of its trailing D
-//    run in bits 16-23 (opening from H inherits H's run, so consecutive D runs merge exactly as
-//    CIGAR runs do); H inherits it only when it takes F.
-// Per row: HE[i] = H(i, j-1) | E(i, j) << 16 and SS[i] = S_H(i, j-1) | S_E(i, j) << 16, 16 bits each.
-template <int QL, bool AMB>
-__device__ __forceinline__ void align_column(uint32_t (&HE)[QL], uint32_t (&SS)[QL],
-                                             const uint32_t (&qw)[(QL + 7) / 8], uint32_t tcode,
-                                             int j, const Scoring& sc, int QRt, int Rt, int& Lext,
-                                             int& trail) {
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  const bool tamb = AMB && ((tcode & (tcode - 1u)) != 0u || tcode == 0u);
-  // row -1 of this column: H(-1, j-1) (diagonal of row 0) and F(0, j); boundary summaries are 0
-  int Hd = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-  uint32_t SHd = 0;
-  int F = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - QRt : kNegInf;
-  uint32_t SF = 0x10001u;  // one real D move, trailing D run 1
-#pragma unroll
-  for (int i = 0; i < QL; i++) {
-    const uint32_t qcode = (qw[i >> 3] >> ((i & 7) * 4)) & 15u;
-    int sub;
-    uint32_t e;
-    if (AMB) {
-      // IUPAC: any ambiguous symbol scores 0; a match is a non-empty code intersection
-      const bool amb = tamb || (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-      sub = amb ? 0 : (qcode == tcode ? sc.match : sc.mismatch);
-      e = (qcode & tcode) ? (1u << 8) : 0u;
-    } else {
-      const bool eq = qcode == tcode;
-      sub = eq ? sc.match : sc.mismatch;
-      e = eq ? (1u << 8) : 0u;
-    }
-    const uint32_t he = HE[i];
-    const uint32_t ss = SS[i];
-    const int Hl = sx16(he);
-    const int E = (int)he >> 16;
-    const uint32_t SE = ss >> 16;
-    int h = Hd + sub;
-    uint32_t sh = SHd + 1u + e;
-    const bool fb = F > h;  // up: D chosen
-    h = fb ? F : h;
-    sh = fb ? SF : sh;
-    const bool eb = E > h;  // left: I chosen
-    h = eb ? E : h;
-    sh = eb ? SE : sh;
-    const int fo = h - QRt, fe = F - Rt;
-    const bool fx = fe > fo;  // extup
-    SF = (fx ? SF : sh) + 0x10001u;
-    const int qrq = (i == QL - 1) ? QRqr : QRqi;
-    const int rq = (i == QL - 1) ? Rqr : Rqi;
-    const int eo = h - qrq, ee = E - rq;
-    const bool ex = ee > eo;  // extleft
-    const uint32_t sen = (ex ? SE : sh) + 1u;
-    if (i == QL - 1) {
-      // last row: I-run counters; the value left by the last column is the end cell's
-      const int lh = eb ? 1 + Lext : 0;
-      Lext = ex ? 1 + Lext : lh;
-      trail = eb ? lh : (int)(sh >> 16);
-    }
-    F = fx ? fe : fo;
-    Hd = Hl;
-    SHd = ss & 0xffffu;
-    // materialise the next row's diagonal now: otherwise SDWA folding reads the old packed words
-    // in row i+1, both generations stay live and every column ends in a 2*QL-register copy
-    asm volatile("" : "+v"(Hd), "+v"(SHd));
-    HE[i] = pack_hf(h, ex ? ee : eo);
-    SS[i] = (sh & 0xffffu) | (sen << 16);
-  }
-}
-
-template <int QL, bool AMB>
-__global__ __launch_bounds__(64) void k_align(DevSeqs s, const uint32_t* __restrict__ pq,
-                                              const uint32_t* __restrict__ pt, int32_t npairs,
-                                              const uint32_t* __restrict__ dev_npairs,
-                                              const uint32_t* __restrict__ outidx, Scoring sc,
-                                              uint32_t* __restrict__ out) {
-  constexpr int CW = (QL + 7) / 8;
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  if (dev_npairs && k >= (int)*dev_npairs) return;
-  const uint32_t qv = pq[k];
-  const int32_t q = (int32_t)(qv >> 1);
-  const int qstr = (int)(qv & 1u);
-  const int32_t t = (int32_t)pt[k];
-  const int tl = s.lens[t];
-  uint32_t qw[CW];
-#pragma unroll
-  for (int w = 0; w < CW; w++) qw[w] = s.codes[((int64_t)q * 2 + qstr) * kCodeWords + w];
-  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
-  uint32_t HE[QL], SS[QL];
-  {
-    // boundary column -1: H(i,-1) = -(GO_TL + (i+1) GE_TL), E(i,0) opened from it; built
-    // incrementally in VGPRs (an opaque zero keeps the compiler from materialising 2*QL scalars)
-    int vz;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-    int hleft = vz - sc.go[1];
-    const int QRqi = sc.go[2] + sc.ge[2], QRqr = sc.go[4] + sc.ge[4];
-#pragma unroll
-    for (int i = 0; i < QL; i++) {
-      hleft -= sc.ge[1];
-      const int qrq = (i == QL - 1) ? QRqr : QRqi;
-      HE[i] = pack_hf(hleft, sc.boundary_open ? hleft - qrq : kNegInf);
-      SS[i] = 1u << 16;  // S_H(i,-1) = 0 (boundary), S_E(i,0) = one real move
-    }
-  }
-  int Lext = 0, trail = 0;
-  uint32_t tword = 0;
-  for (int j = 0; j < tl; j++) {
-    if ((j & 7) == 0) tword = tcp[j >> 3];
-    const uint32_t tcode = tword & 15u;
-    tword >>= 4;
-    // keep the per-row query codes from being hoisted out of the column loop (that would pin
-    // QL extra VGPRs); re-extracting them is one v_bfe per cell
-#pragma unroll
-    for (int w = 0; w < CW; w++) asm volatile("" : "+v"(qw[w]));
-    const bool lc = (j == tl - 1);
-    align_column<QL, AMB>(HE, SS, qw, tcode, j, sc, lc ? QRtr : QRti, lc ? Rtr : Rti, Lext, trail);
-  }
-  const int H = sx16(HE[QL - 1]);
-  const uint32_t S = SS[QL - 1] & 0xffffu;
-  const uint32_t m = S >> 8, acols = S & 0xffu;
-  const uint32_t internal = acols - (uint32_t)trail;
-  out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
-}
-
-// ------------------------------------------------------------------ K3P: packed 16-bit alignment
-// The same recurrences, summaries and strict priorities as k_align, two DP cells per 32-bit VALU
-// op (VOP3P v_pk_* on int16 halves).  A column is split into a top half (rows [0, TOP)) and a
-// bottom half (rows [TOP, QL)) that runs one column behind: register k holds row k of column j in
-// its low half and row TOP+k of column j-1 in its high half.  Within a step the rows are
-// processed in order, so the bottom half's upper neighbour (row TOP-1 of column j-1) is the top
-// half's carry-out of the previous step; one step costs one pass over TOP packed rows.
-// Branch-free selection: for |values| well inside int16, (a - b) >> 15 (arithmetic, per half) is
-// the mask of "b > a", which drives v_bfi for the summaries and v_pk_max for the scores.
-// Substitution: per 16-row group a match bit-mask of the column's target base, selected per step
-// from per-base masks built once per pair (non-ambiguous sequences only: one-hot codes).
-typedef short v2s __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ v2s as_v2(uint32_t x) { return __builtin_bit_cast(v2s, x); }
-__device__ __forceinline__ uint32_t as_u(v2s x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)hi << 16) | ((uint32_t)lo & 0xffffu); }
-// mask of (b > a) per half
-// (opaque to the compiler, which otherwise rewrites it into per-half compares and selects)
-__device__ __forceinline__ uint32_t gt_mask(v2s b, v2s a) {
-  uint32_t d;
-  // op_sel_hi:[0,1]: the inline constant's low half serves both halves (its high half is 0)
-  asm("v_pk_sub_i16 %0, %1, %2\n\tv_pk_ashrrev_i16 %0, 15, %0 op_sel_hi:[0,1]" : "=&v"(d) : "v"(a), "v"(b));
-  return d;
-}
-
-template <int QL>
-__global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __restrict__ pq,
-                                                 const uint32_t* __restrict__ pt, int32_t npairs,
-                                                 const uint32_t* __restrict__ dev_npairs,
-                                                 const uint32_t* __restrict__ outidx, Scoring sc,
-                                                 uint32_t* __restrict__ out) {
-  constexpr int TOP = (QL + 1) / 2, BOT = QL - TOP;  // BOT == TOP or TOP - 1
-  constexpr int NG = (TOP + 15) / 16;
-  constexpr int KL = BOT - 1;                        // register holding row QL-1 (high half)
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  if (dev_npairs && k >= (int)*dev_npairs) return;
-  const uint32_t qv = pq[k];
-  const int32_t q = (int32_t)(qv >> 1);
-  const int qstr = (int)(qv & 1u);
-  const int32_t t = (int32_t)pt[k];
-  const int tl = s.lens[t];
-  // per-base row masks: MT[g] / MB[g] hold, for base b at bits [16b, 16b+16), the rows of group g
-  // (top half / bottom half) whose query base is b
-  uint64_t MT[NG], MB[NG];
-#pragma unroll
-  for (int g = 0; g < NG; g++) MT[g] = MB[g] = 0;
-  {
-    const uint32_t* qc = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
-    uint32_t w = 0;
-#pragma unroll
-    for (int i = 0; i < QL; i++) {
-      if ((i & 7) == 0) w = qc[i >> 3];
-      const uint32_t b = (uint32_t)__builtin_ctz((w & 15u) | 16u) & 3u;
-      w >>= 4;
-      if (i < TOP) MT[i >> 4] |= 1ull << (16 * b + (i & 15));
-      else MB[(i - TOP) >> 4] |= 1ull << (16 * b + ((i - TOP) & 15));
-    }
-  }
-  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  const v2s MM = as_v2(pk2(sc.mismatch, sc.mismatch));
-  const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
-  v2s H[TOP], E[TOP];
-  uint32_t SH[TOP], SE[TOP];  // summaries; SH stored +1 (every consumer adds the move)
-  auto init_rows = [&](uint32_t keep_mask) {
-    // boundary column -1: H(i,-1) = -(GO_TL + (i+1) GE_TL), E(i,0) opened from it, S_H = 0,
-    // S_E = one real move; keep_mask selects the halves to (re)initialise
-    int vz;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-#pragma unroll
-    for (int kk = 0; kk < TOP; kk++) {
-      const int i0 = kk, i1 = TOP + kk;
-      const int h0 = vz - sc.go[1] - (i0 + 1) * sc.ge[1];
-      const int h1 = vz - sc.go[1] - (i1 + 1) * sc.ge[1];
-      const int q1 = (i1 == QL - 1) ? QRqr : QRqi;
-      const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
-      const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
-      H[kk] = as_v2(bfi(keep_mask, pk2(h0, h1), as_u(H[kk])));
-      E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
-      SH[kk] = bfi(keep_mask, 0x00010001u, SH[kk]);
-      SE[kk] = bfi(keep_mask, 0x00010001u, SE[kk]);
-    }
-  };
-#pragma unroll
-  for (int kk = 0; kk < TOP; kk++) {
-    H[kk] = as_v2(0u);
-    E[kk] = as_v2(0u);
-    SH[kk] = SE[kk] = 0;
-  }
-  init_rows(0xffffffffu);
-  // carries of the top half's last row, consumed by the bottom half in the next step
-  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDF = 0;
-  int Lext = 0, trail = 0;
-  uint32_t tword = 0, tprev = 1;
-  for (int j = 0; j <= tl; j++) {
-    if ((j & 7) == 0) tword = tcp[j >> 3];
-    const uint32_t tcode = tword & 15u;
-    tword >>= 4;
-    const uint32_t bl = (uint32_t)__builtin_ctz(tcode | 16u) & 3u, bh = (uint32_t)__builtin_ctz(tprev | 16u) & 3u;
-    tprev = tcode;
-    uint32_t M[NG];
-#pragma unroll
-    for (int g = 0; g < NG; g++)
-      M[g] = ((uint32_t)(MT[g] >> (16 * bl)) & 0xffffu) | ((uint32_t)(MB[g] >> (16 * bh)) << 16);
-    const bool lc0 = (j == tl - 1), lc1 = (j == tl);
-    const uint32_t QRt = pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti);
-    const uint32_t Rt = pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti);
-    // row -1 (top half, column j) | carry (bottom half, column j-1)
-    const int hd0 = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
-    v2s Hd = as_v2(pk2(hd0, (int)cHd));
-    uint32_t SHd = pk2(1, (int)cSHd);
-    v2s F = as_v2(pk2(f0, (int)cF));
-    uint32_t SF = pk2(1, (int)cSF);
-    uint32_t DF = pk2(-1, (int)cDF);  // row the current D run opened from (-1: boundary)
-#pragma unroll
-    for (int kk = 0; kk < TOP; kk++) {
-      const uint32_t e = (M[kk >> 4] >> (kk & 15)) & 0x00010001u;
-      v2s h = Hd + MM + as_v2(e) * DELTA;
-      uint32_t sh = SHd + (e << 8);
-      const uint32_t mF = gt_mask(F, h);
-      h = __builtin_elementwise_max(h, F);
-      sh = bfi(mF, SF, sh);
-      const v2s Ec = E[kk];
-      const uint32_t mE = gt_mask(Ec, h);
-      h = __builtin_elementwise_max(h, Ec);
-      sh = bfi(mE, SE[kk], sh);
-      const uint32_t sh1 = sh + 0x00010001u;
-      int dr_last = 0;
-      bool eb_last = false;
-      if (kk == KL) {
-        // last row (high half): D run of the chosen F = rows since it opened (before DF moves on)
-        eb_last = (mE >> 31) != 0;
-        dr_last = (mF >> 31) != 0 ? (QL - 1) - (int)(short)(DF >> 16) : 0;
-      }
-      const v2s fo = h - as_v2(QRt), fe = F - as_v2(Rt);
-      const uint32_t mfx = gt_mask(fe, fo);
-      F = __builtin_elementwise_max(fo, fe);
-      // a new D run opened from H continues H's own D run when H took F
-      DF = bfi(mfx | (mF & ~mE), DF, pk2(kk, TOP + kk));
-      SF = bfi(mfx, SF + 0x00010001u, sh1);
-      const uint32_t qrq = pk2(QRqi, (TOP + kk == QL - 1) ? QRqr : QRqi);
-      const uint32_t rq = pk2(Rqi, (TOP + kk == QL - 1) ? Rqr : Rqi);
-      const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
-      const uint32_t mex = gt_mask(ee, eo);
-      if (kk == KL) {
-        // trailing I-run counters along the last row; the value left by the last column is the
-        // end cell's (vsearch align_trim's trailing run)
-        const bool ex = (mex >> 31) != 0;
-        const int lh = eb_last ? 1 + Lext : 0;
-        trail = eb_last ? lh : dr_last;
-        Lext = ex ? 1 + Lext : lh;
-      }
-      E[kk] = __builtin_elementwise_max(eo, ee);
-      SE[kk] = bfi(mex, SE[kk] + 0x00010001u, sh1);
-      Hd = H[kk];
-      SHd = SH[kk];
-      H[kk] = h;
-      SH[kk] = sh1;
-    }
-    // carry the top half's outputs into the bottom half of the next step
-    cHd = as_u(Hd) & 0xffffu;
-    cSHd = SHd & 0xffffu;
-    cF = as_u(F) & 0xffffu;
-    cSF = SF & 0xffffu;
-    cDF = DF & 0xffffu;
-    if (j == 0) {
-      // the bottom half processed column -1 in this step: restore the boundary column
-      init_rows(0xffff0000u);
-      Lext = 0;
-      trail = 0;
-    }
-  }
-  const int Hend = (int)(short)(as_u(H[KL]) >> 16);
-  const uint32_t S = ((SH[KL] >> 16) - 1u) & 0xffffu;
-  const uint32_t m = S >> 8, acols = S & 0xffu;
-  const uint32_t internal = acols - (uint32_t)trail;
-  out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
-}
-
-typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
-                        const uint32_t*, Scoring, uint32_t*);
-
-template <int L>
-struct AlignTable {
-  static void fill(AlignFn* t) {
-    t[3 * L] = k_align_pk<L>;
-    t[3 * L + 1] = k_align<L, false>;
-    t[3 * L + 2] = k_align<L, true>;
-    AlignTable<L - 1>::fill(t);
-  }
-};
-template <>
-struct AlignTable<kMinTplLen - 1> {
-  static void fill(AlignFn*) {}
-};
 
 hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq,
                         const uint32_t* pt, int32_t npairs, const uint32_t* dev_npairs,
                         const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st) {
-  static AlignFn table[3 * (kMaxLen + 1)] = {};
-  static bool init = false;
-  static int variant0 = 0;
-  if (!init) {
-    AlignTable<kMaxLen>::fill(table);
+  static int variant0 = -1;
+  init_align_tables();
+  if (variant0 < 0) {
     // UMICLUST_ALIGN=scalar selects the one-cell-per-op kernel (cross-checks / benchmarks)
     const char* v = getenv("UMICLUST_ALIGN");
     variant0 = (v && v[0] == 's') ? 1 : 0;
-    init = true;
   }
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(table[3 * qlen + (ambig ? 2 : variant0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
+  hipLaunchKernelGGL(g_align[3 * qlen + (ambig ? 2 : variant0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
                      pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
 }
@@ -1607,155 +1278,13 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ K3T: traceback
-// Same DP (rows unrolled) without summaries; the direction nibble of every cell (bit0 up = D
-// chosen, bit1 left = I chosen, bit2 D-extension, bit3 I-extension) goes to HBM as one column of
-// CW words per step, laid out [column][word][pair] so a wave's stores are coalesced; then each lane
-// runs backtrack16 over its own matrix.
-template <int QL>
-__global__ __launch_bounds__(64) void k_traceback(DevSeqs s, const uint32_t* __restrict__ pq,
-                                                  const uint32_t* __restrict__ pt, int32_t npairs,
-                                                  Scoring sc, uint32_t* __restrict__ dirbuf,
-                                                  uint8_t* __restrict__ ops,
-                                                  uint16_t* __restrict__ nops,
-                                                  uint32_t* __restrict__ out) {
-  constexpr int CW = (QL + 7) / 8;
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  const uint32_t qv = pq[k];
-  const int32_t q = (int32_t)(qv >> 1);
-  const int qstr = (int)(qv & 1u);
-  const int32_t t = (int32_t)pt[k];
-  const int tl = s.lens[t];
-  uint32_t qw[CW];
-#pragma unroll
-  for (int w = 0; w < CW; w++) qw[w] = s.codes[((int64_t)q * 2 + qstr) * kCodeWords + w];
-  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  uint32_t HE[QL];
-#pragma unroll
-  for (int i = 0; i < QL; i++) {
-    const int hleft = -(sc.go[1] + (i + 1) * sc.ge[1]);
-    const int qrq = (i == QL - 1) ? QRqr : QRqi;
-    HE[i] = pack_hf(hleft, sc.boundary_open ? hleft - qrq : kNegInf);
-  }
-  uint32_t tword = 0;
-  for (int j = 0; j < tl; j++) {
-    if ((j & 7) == 0) tword = tcp[j >> 3];
-    const uint32_t tcode = tword & 15u;
-    tword >>= 4;
-    const bool tamb = (tcode & (tcode - 1u)) != 0u || tcode == 0u;
-    // keep the per-row query codes from being hoisted out of the column loop (that would pin
-    // QL extra VGPRs); re-extracting them is one v_bfe per cell
-#pragma unroll
-    for (int w = 0; w < CW; w++) asm volatile("" : "+v"(qw[w]));
-    const bool lc = (j == tl - 1);
-    const int QRt = lc ? QRtr : QRti;
-    const int Rt = lc ? Rtr : Rti;
-    int Hd = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-    int F = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - QRt : kNegInf;
-    uint32_t dw[CW];
-#pragma unroll
-    for (int w = 0; w < CW; w++) dw[w] = 0;
-#pragma unroll
-    for (int i = 0; i < QL; i++) {
-      const uint32_t qcode = (qw[i >> 3] >> ((i & 7) * 4)) & 15u;
-      const bool amb = tamb || (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-      const int sub = amb ? 0 : (qcode == tcode ? sc.match : sc.mismatch);
-      const uint32_t he = HE[i];
-      const int Hl = sx16(he);
-      const int E = (int)he >> 16;
-      int h = Hd + sub;
-      uint32_t d = 0;
-      if (F > h) { h = F; d |= 1u; }
-      if (E > h) { h = E; d |= 2u; }
-      const int fo = h - QRt, fe = F - Rt;
-      if (fe > fo) { F = fe; d |= 4u; } else F = fo;
-      const int qrq = (i == QL - 1) ? QRqr : QRqi;
-      const int rq = (i == QL - 1) ? Rqr : Rqi;
-      const int eo = h - qrq, ee = E - rq;
-      int En = eo;
-      if (ee > eo) { En = ee; d |= 8u; }
-      dw[i >> 3] |= d << ((i & 7) * 4);
-      Hd = Hl;
-      HE[i] = pack_hf(h, En);
-    }
-#pragma unroll
-    for (int w = 0; w < CW; w++) dirbuf[((int64_t)j * CW + w) * npairs + k] = dw[w];
-  }
-  const int H = sx16(HE[QL - 1]);
-  // backtrack16
-  uint8_t* o = ops + (int64_t)k * kOpsStride;
-  int n = 0;
-  int i = QL - 1, j = tl - 1;
-  int aligned = 0, matches = 0;
-  uint32_t op = 0;  // 0 none, 'M','D','I'
-  while (i >= 0 && j >= 0) {
-    aligned++;
-    const uint32_t d = (dirbuf[((int64_t)j * CW + (i >> 3)) * npairs + k] >> ((i & 7) * 4)) & 15u;
-    if (op == 'I' && (d & 8u)) {
-      j--;
-    } else if (op == 'D' && (d & 4u)) {
-      i--;
-    } else if (d & 2u) {
-      j--;
-      op = 'I';
-    } else if (d & 1u) {
-      i--;
-      op = 'D';
-    } else {
-      const uint32_t qcode = (s.codes[((int64_t)q * 2 + qstr) * kCodeWords + (i >> 3)] >> ((i & 7) * 4)) & 15u;
-      const uint32_t tcode = (tcp[j >> 3] >> ((j & 7) * 4)) & 15u;
-      if (qcode & tcode) matches++;
-      i--;
-      j--;
-      op = 'M';
-    }
-    o[kOpsStride - 1 - n] = (uint8_t)op;
-    n++;
-  }
-  while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
-  while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
-  nops[k] = (uint16_t)n;
-  // align_trim on the op string (alignment order = o[kOpsStride-n .. kOpsStride-1])
-  const uint8_t* a0 = o + kOpsStride - n;
-  int tlft = 0, trgt = 0;
-  if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
-  if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
-  if (tlft >= aligned) trgt = 0;
-  const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
-  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
-}
-
-typedef void (*TraceFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, Scoring, uint32_t*,
-                        uint8_t*, uint16_t*, uint32_t*);
-template <int L>
-struct TraceTable {
-  static void fill(TraceFn* t) {
-    t[L] = k_traceback<L>;
-    TraceTable<L - 1>::fill(t);
-  }
-};
-template <>
-struct TraceTable<kMinTplLen - 1> {
-  static void fill(TraceFn*) {}
-};
-
 hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
                             int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,
                             uint16_t* nops, uint32_t* out, hipStream_t st) {
-  static TraceFn table[kMaxLen + 1] = {};
-  static bool init = false;
-  if (!init) {
-    TraceTable<kMaxLen>::fill(table);
-    init = true;
-  }
+  init_align_tables();
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(table[qlen], dim3((npairs + 63) / 64), dim3(64), 0, st, s, pq, pt, npairs, sc,
+  hipLaunchKernelGGL(g_trace[qlen], dim3((npairs + 63) / 64), dim3(64), 0, st, s, pq, pt, npairs, sc,
                      dirbuf, ops, nops, out);
   return hipGetLastError();
 }

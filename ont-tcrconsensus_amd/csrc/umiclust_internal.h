@@ -6,11 +6,15 @@
 
 namespace uc {
 
-constexpr int kMaxLen = 72;          // longest supported UMI (UMICLUST_MAX_LEN)
+constexpr int kMaxLen = 112;         // longest supported UMI (UMICLUST_MAX_LEN; config 5 needs 110)
+constexpr int kShortLen = 72;        // longest length with the one-cell-per-op cross-check aligner
 constexpr int kMinTplLen = 32;       // shortest query length with a compiled aligner
 constexpr int kCodeWords = kMaxLen / 8;  // 4-bit codes, 8 residues per u32
-constexpr int kMaxKmers = kMaxLen - 8 + 1;  // unique 8-mers per strand <= 65
-constexpr int kKmerStride = 68;     // u16 slots per (sequence, strand) k-mer list
+constexpr int kMaxKmers = kMaxLen - 8 + 1;  // unique 8-mers per strand <= 105
+constexpr int kKmerStride = (kMaxKmers + 3) & ~3;  // u16 slots per (sequence, strand) k-mer list
+constexpr int kMaskWords = (kMaxLen + 31) / 32;    // DUST mask bits per sequence
+static_assert(kMaxKmers <= 128, "k-mer slots are lanes l and l + 64");
+static_assert(kMaxLen % 8 == 0 && kMaxLen <= 120, "summaries and keys hold lengths in 7 bits");
 constexpr int kTile = 65536;        // centroids per sealed index tile
 // Index layout.  Every posting list is split into kParts parts by the ordinal of its sequence
 // (centroid ordinal, or seqno for the per-block peer tiles): part = x % kParts.  The prefilter runs

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libumiclust.so")
 QL, TL, QI, TI, QR, TR = range(6)
 PRESET_ROUND1 = 1
 PRESET_VSEARCH_DEFAULT = 2
-MAX_LEN = 72
+MAX_LEN = 112
 
 ERRORS = {-22: "EINVAL", -5: "EIO", -12: "ENOMEM", -19: "EDEVICE", -77: "ESTATE", -34: "ERANGE"}
 
@@ -268,7 +268,7 @@ class Context:
         b, o = _pack(seqs)
         n = len(o) - 1
         masked = np.zeros(len(b), np.uint8)
-        kst = 68
+        kst = MAX_LEN - 7  # >= unique 8-mers per strand
         km = np.zeros(max(n, 1) * 2 * kst, np.uint16)
         nk = np.zeros(max(n, 1) * 2, np.int32)
         P = C.POINTER

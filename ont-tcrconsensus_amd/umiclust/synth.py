@@ -137,12 +137,25 @@ def make_umis(n_molecules: int, seed: int, mean_reads: float = 20.0, dispersion:
     return UmiSet(seq=seq, off=off, molecule=mol, strand=strand, fwd_dist=f_ed, rev_dist=r_ed)
 
 
+# BASELINE config -> (minseqlength, maxseqlength) of the vsearch run
+CONFIG_LENGTHS = {1: (58, 68), 2: (58, 68), 5: (80, 110)}
+# config 5 stress UMIs: each pattern concatenated x1.5 (48-nt halves, ~96-nt combined UMI)
+UMI_FWD_LONG = UMI_FWD + UMI_FWD[:16]
+UMI_REV_LONG = UMI_REV + UMI_REV[:16]
+
+
 def config_umis(config: int, scale: float = 1.0) -> UmiSet:
-    """BASELINE.json configs: 1 = 100k reads (seed 1001), 2 = 2M reads (seed 1002)."""
+    """BASELINE.json configs: 1 = 100k reads (seed 1001), 2 = 2M reads (seed 1002), 5 = the high-error
+    stress bin (seed 1005): ~96-nt UMIs, 15 % indels (insertion : deletion = 1 : 1, up to 4 per half, as the UMI extraction caps edits),
+    deep clusters (NegBin mean 1,500 reads per molecule), 300k reads at scale 1."""
     if config == 1:
         return make_umis(int(5000 * scale), seed=1001, max_reads=int(100_000 * scale))
     if config == 2:
         return make_umis(int(100_000 * scale), seed=1002, max_reads=int(2_000_000 * scale))
+    if config == 5:
+        return make_umis(max(1, int(200 * scale)), seed=1005, mean_reads=1500.0, error_rate=0.15,
+                         split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=UMI_FWD_LONG,
+                         pattern_rev=UMI_REV_LONG, max_reads=int(300_000 * scale))
     raise ValueError(config)
 
 

@@ -1,8 +1,9 @@
 """Generate tests/golden/oracle_config<N>.json: digests of the CPU oracle's clustering of the synthetic
-BASELINE config-1 bin (100k reads, the reference's CPU-runnable case), so the GPU parity test can check a
-full config-1-sized bin without re-running the ~1 min CPU oracle on the GPU box.
+BASELINE config-1 bin (100k reads, the reference's CPU-runnable case) and of samples of the config-5
+stress bin (~96-nt UMIs, 15 % indels, clusters of >1k members), so the GPU parity test can check them
+without re-running the CPU oracle (~1 min per config-1 case) on the GPU box.
 
-Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py
+Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py [config ...]
 """
 import hashlib
 import json
@@ -31,24 +32,34 @@ CASES = {
     "config1_round1_id093": (1, 1.0, 1, 0.93),
     "config1_round1_id090": (1, 1.0, 1, 0.90),
     "config1_round2_id097": (1, 1.0, 2, 0.97),
+    # config 5: at id 0.75 the deep clusters form (2 clusters > 1k members at scale 0.1); at id 0.90
+    # almost every read is a centroid (long candidate lists, many new-centroid alignments)
+    "config5_round1_id075": (5, 0.1, 1, 0.75),
+    "config5_round1_id090": (5, 0.02, 1, 0.90),
+    "config5_round2_id075": (5, 0.02, 2, 0.75),
 }
 
 
-def main():
+def main(configs):
     import orc
     from umiclust import synth
     out = {}
     for name, (cfg, scale, preset, idn) in CASES.items():
+        if cfg not in configs:
+            continue
+        lo, hi = synth.CONFIG_LENGTHS[cfg]
         seqs = synth.config_umis(cfg, scale).as_list()
-        r = orc.cluster(orc.params(preset, idn, 58, 68), seqs)
+        r = orc.cluster(orc.params(preset, idn, lo, hi), seqs)
         d = digest(r)
-        d.update(config=cfg, scale=scale, preset=preset, identity=idn, n_reads=len(seqs),
-                 alignments=r["stats"]["alignments"], cells=r["stats"]["cells"])
-        out[name] = d
+        d.update(config=cfg, scale=scale, preset=preset, identity=idn, minlen=lo, maxlen=hi, n_reads=len(seqs),
+                 alignments=r["stats"]["alignments"], cells=r["stats"]["cells"],
+                 max_cluster=int(np.bincount(np.asarray(r["cluster"])).max()) if len(seqs) else 0)
+        out.setdefault(cfg, {})[name] = d
         print(name, d, flush=True)
-    with open(os.path.join(HERE, "oracle_config1.json"), "w") as f:
-        json.dump(out, f, indent=1, sort_keys=True)
+    for cfg, cases in out.items():
+        with open(os.path.join(HERE, f"oracle_config{cfg}.json"), "w") as f:
+            json.dump(cases, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main()
+    main([int(a) for a in sys.argv[1:]] or sorted({c[0] for c in CASES.values()}))

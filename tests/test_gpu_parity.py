@@ -54,11 +54,14 @@ def _pairs(seed, n, qlens, tl_lo=16, tl_hi=72, ambig=False):
     return qs, ts
 
 
-@pytest.mark.parametrize("preset,ambig", [(1, False), (2, False), (1, True), (2, True)])
-def test_align_pairs_vs_oracle(gpu_ctx, preset, ambig):
-    p = _lib.params(preset, 0.93, 32, 72)
-    op = orc.params(preset, 0.93, 32, 72)
-    qs, ts = _pairs(100 + preset + 10 * ambig, 3000, list(range(32, 73)), ambig=ambig)
+@pytest.mark.parametrize("preset,ambig,hi", [(1, False, 72), (2, False, 72), (1, True, 72), (2, True, 72),
+                                             (1, False, _lib.MAX_LEN), (2, False, _lib.MAX_LEN),
+                                             (1, True, _lib.MAX_LEN)])
+def test_align_pairs_vs_oracle(gpu_ctx, preset, ambig, hi):
+    """Every query length 32..hi (one kernel instantiation each), targets 16..hi."""
+    p = _lib.params(preset, 0.93, 32, hi)
+    op = orc.params(preset, 0.93, 32, hi)
+    qs, ts = _pairs(100 + preset + 10 * ambig + hi, 3000, list(range(32, hi + 1)), tl_hi=hi, ambig=ambig)
     r = gpu_ctx.align_pairs(p, qs, ts)
     tb = gpu_ctx.align_pairs(p, qs, ts, with_ops=True)
     for k, (q, t) in enumerate(zip(qs, ts)):
@@ -91,7 +94,12 @@ def test_prep_vs_oracle(gpu_ctx):
     seqs += synth.make_umis(50, seed=9, max_reads=400).as_list()
     seqs += ["".join(rng.choice("AC") for _ in range(rng.randint(16, 72))) for _ in range(100)]
     seqs += ["".join(rng.choice("ACGTN") for _ in range(rng.randint(16, 72))) for _ in range(100)]
-    p = _lib.params(1, 0.93, 1, 72)
+    # long UMIs (config 5): DUST over three 64-nt windows, up to 105 k-mers per strand
+    seqs += synth.config_umis(5, 0.002).as_list()[:300]
+    seqs += ["".join(rng.choice("AC") for _ in range(rng.randint(73, _lib.MAX_LEN))) for _ in range(50)]
+    seqs += ["ACG" * 20 + "".join(rng.choice("ACGT") for _ in range(rng.randint(13, _lib.MAX_LEN - 60)))
+             for _ in range(50)]
+    p = _lib.params(1, 0.93, 1, _lib.MAX_LEN)
     out = gpu_ctx.prep(p, seqs)
     from pyref import revcomp
     for s, m, km in zip(seqs, out["masked"], out["kmers"]):
@@ -118,6 +126,29 @@ CASES = [
     (100, 5, 3000, 1, 0.93, 0.2, 0.06),
     (1500, 6, 30000, 1, 0.93, 0.0, 0.015),
 ]
+# config-5 style: long UMIs (~96 nt), 15 % indels, (min, max) length 80..110
+LONG_CASES = [
+    # (n_molecules, seed, max_reads, preset, identity, orient_mix)
+    (8, 11, 2000, 1, 0.75, 0.3),
+    (30, 12, 1500, 1, 0.90, 0.0),
+    (8, 13, 2000, 2, 0.80, 0.2),
+]
+
+
+@pytest.mark.parametrize("case", LONG_CASES, ids=[f"long_m{c[0]}_s{c[1]}_p{c[3]}_id{c[4]}" for c in LONG_CASES])
+def test_cluster_long_vs_oracle(gpu_ctx, case):
+    nm, seed, mr, preset, idn, mix = case
+    u = synth.make_umis(nm, seed=seed, max_reads=mr, orient_mix=mix, mean_reads=1500.0, error_rate=0.15,
+                        split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                        pattern_rev=synth.UMI_REV_LONG)
+    seqs = u.as_list()
+    gpu_ctx.load(_lib.params(preset, idn, 80, 110), seqs)
+    st = gpu_ctx.cluster()
+    g = gpu_ctx.fetch()
+    o = orc.cluster(orc.params(preset, idn, 80, 110), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"]
+    assert st["cells"] == o["stats"]["cells"]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"m{c[0]}_s{c[1]}_p{c[3]}_id{c[4]}" for c in CASES])
@@ -257,20 +288,26 @@ def _check_consensus_cpu(seqs, a, targets, op):
 
 
 def _golden_cases():
+    import glob
     import json
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_config1.json")
-    return sorted(json.load(open(path)).items())
+    out = {}
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                              "oracle_config*.json"))):
+        out.update(json.load(open(path)))
+    return sorted(out.items())
 
 
 @pytest.mark.parametrize("name,gold", _golden_cases(), ids=[n for n, _ in _golden_cases()])
-def test_config1_vs_oracle_golden(gpu_ctx, name, gold):
-    """BASELINE config 1 (100k reads, one bin) at full size: digests of membership, strands, centroids and
-    consensus equal the CPU oracle's (committed by tests/golden/make_oracle_golden.py)."""
+def test_config_vs_oracle_golden(gpu_ctx, name, gold):
+    """BASELINE config 1 (100k reads, one bin) at full size and config-5 stress samples (long UMIs, 15 %
+    indels, clusters of >1k members): digests of membership, strands, centroids and consensus equal the
+    CPU oracle's (committed by tests/golden/make_oracle_golden.py)."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     from make_oracle_golden import digest
     u = synth.config_umis(gold["config"], gold["scale"])
-    gpu_ctx.load(_lib.params(gold["preset"], gold["identity"], 58, 68), buf=u.seq, off=u.off)
+    gpu_ctx.load(_lib.params(gold["preset"], gold["identity"], gold.get("minlen", 58), gold.get("maxlen", 68)),
+                 buf=u.seq, off=u.off)
     st = gpu_ctx.cluster()
     d = digest(gpu_ctx.fetch())
     assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]

@@ -128,6 +128,23 @@ def test_cluster_matches_python_restatement(preset, identity):
     assert r["consensus"] == cons
 
 
+@pytest.mark.parametrize("preset,identity", [(1, 0.75), (2, 0.80)])
+def test_cluster_long_matches_python_restatement(preset, identity):
+    """Config-5 style: ~96-nt UMIs, 15 % indels, DUST over several windows, up to ~100 k-mers."""
+    u = synth.make_umis(3, seed=31 + preset, max_reads=150, mean_reads=1500.0, error_rate=0.15,
+                        split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                        pattern_rev=synth.UMI_REV_LONG, orient_mix=0.3)
+    seqs = u.as_list()
+    seqs += ["ACG" * 30 + "TTGCA", "AC" * 50]  # low-complexity long records
+    r = orc.cluster(orc.params(preset, identity, 80, 110), seqs)
+    c, s, cons = pyref.cluster(pyref.P(preset, identity, 80, 110), seqs)
+    assert list(r["cluster"]) == c
+    assert list(r["strand"]) == s
+    assert r["consensus"] == cons
+    for x in seqs[-2:] + seqs[:20]:
+        assert orc.dust(x) == pyref.dust(x)
+
+
 def test_cluster_invariants():
     u = synth.make_umis(200, seed=5, max_reads=3000)
     seqs = u.as_list()
