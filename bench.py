@@ -25,13 +25,13 @@ METRIC = "UMIs clustered/sec + banded-NW GCUPS (whole node, 1/2/4/8 MI355X)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def cpu_baseline(umis, n_sample: int, identity: float) -> dict:
+def cpu_baseline(umis, n_sample: int, identity: float, lens=(58, 68)) -> dict:
     """The C oracle (oracle/, 1 thread) on the first n_sample reads of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
     seqs = umis.as_list()[:n_sample]
     t0 = time.perf_counter()
-    r = orc.cluster(orc.params(1, identity, 58, 68), seqs)
+    r = orc.cluster(orc.params(1, identity, *lens), seqs)
     dt = time.perf_counter() - t0
     return dict(value=r["stats"]["kept"] / dt, unit="UMIs/s", cores=1, kind="port",
                 sample=f"first {n_sample} reads of the rank-0 bin ({r['stats']['kept']} kept, "
@@ -45,8 +45,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the 2M-read bin (testing only)")
-    ap.add_argument("--identity", type=float, default=0.90)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
+                    help="2: the headline bin (default); 5: the long-UMI high-error stress bin")
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the bin (testing only)")
+    ap.add_argument("--identity", type=float, default=None, help="default 0.90 (config 2), 0.75 (config 5)")
     ap.add_argument("--cpu-sample", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -67,11 +69,23 @@ def main() -> None:
     torch.cuda.set_device(local_rank)
 
     from umiclust import _lib, synth
-    seed = 1002 if rank == 0 else 1002 * 1_000_003 + rank
-    n_mol = int(100_000 * args.scale)
-    umis = synth.make_umis(n_mol, seed=seed, max_reads=int(2_000_000 * args.scale))
+    if args.identity is None:
+        args.identity = 0.90 if args.config == 2 else 0.75
+    lens = synth.CONFIG_LENGTHS[args.config]
+    seed = (1000 + args.config) if rank == 0 else (1000 + args.config) * 1_000_003 + rank
+    if args.config == 2:
+        umis = synth.make_umis(int(100_000 * args.scale), seed=seed, max_reads=int(2_000_000 * args.scale))
+        workload = ("BASELINE config 2: synthetic 2M dual-UMI reads per GPU, one region bin, "
+                    f"--id {args.identity:.2f}, round-1 scoring (match 10, mismatch -40, gapopen 0E/40I)")
+    else:
+        umis = synth.make_umis(max(1, int(200 * args.scale)), seed=seed, mean_reads=1500.0, error_rate=0.15,
+                               split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                               pattern_rev=synth.UMI_REV_LONG, max_reads=int(300_000 * args.scale))
+        workload = ("BASELINE config 5 stress: synthetic 300k long (~96-nt) UMIs per GPU, 15% indels, deep "
+                    f"clusters (NegBin mean 1500 reads/molecule), --id {args.identity:.2f}, "
+                    f"--minseqlength {lens[0]} --maxseqlength {lens[1]}, round-1 scoring")
     ctx = _lib.Context(local_rank)
-    params = _lib.params(_lib.PRESET_ROUND1, args.identity, 58, 68)
+    params = _lib.params(_lib.PRESET_ROUND1, args.identity, *lens)
     ctx.load(params, buf=umis.seq, off=umis.off)
 
     def barrier():
@@ -125,13 +139,12 @@ def main() -> None:
                           cells_per_step=cells, cells_computed=st["cells_computed"])
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(umis, args.cpu_sample, args.identity)
+            cpu = cpu_baseline(umis, args.cpu_sample, args.identity, lens)
         out = {
             "metric": METRIC, "value": value, "unit": "UMIs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": "BASELINE config 2: synthetic 2M dual-UMI reads per GPU, one region bin, "
-                                   "--id 0.90, round-1 scoring (match 10, mismatch -40, gapopen 0E/40I)",
+            "config": {"workload": workload,
                        "reads_per_gpu": int(umis.n), "umis_kept_per_gpu": int(n_kept), "clusters": st["n_clusters"],
                        "parallelism": f"{world} independent bins (1 per GPU), no data-path collective"},
             "gcups": gcups,

@@ -122,6 +122,41 @@ int64_t umiclust_run_fasta(umiclust_ctx *ctx, const umiclust_params *p, const ch
 int64_t umiclust_run_argv(umiclust_ctx *ctx, int32_t argc, const char *const *argv,
                           umiclust_stats *stats);
 
+/* ---- in-process consumer ---- */
+/* Parameters of the reference's parse_umi_clusters / polish_cluster
+ * (/root/reference/ont_tcr_consensus/parse_umi_clusters.py:10-21, :143-151). */
+typedef struct umiclust_parse_params {
+  int32_t min_reads_per_cluster;  /* min_reads_per_cluster (20) */
+  int32_t max_reads_per_cluster;  /* max_reads_per_cluster (60) */
+  int32_t balance_strands;        /* balance_strands (0) */
+  int32_t max_clusters;           /* max_clusters; 0 = no limit (the reference's None) */
+} umiclust_parse_params;
+
+typedef struct umiclust_parse_result {
+  int64_t n_clusters;     /* consout records */
+  int64_t n_written;      /* clusters written to clusters_fa/ */
+  int64_t reads_found;    /* the reference's running total as it computes it (last cluster's count x 2) */
+  int64_t reads_written;  /* likewise */
+  int32_t empty_region;   /* 1: n_written == 0 or reads_found == 0 -- the caller appends the region to
+                             regions_wo_clusters_txt (parse_umi_clusters.py:222-231) and no log is written */
+  int32_t pad;
+} umiclust_parse_result;
+
+/* umiclust_run_fasta followed by parse_umi_clusters' outputs straight from the in-memory clusters:
+ * <work_dir>/clusters_fa/cluster<N>.fasta, <work_dir>/smolecule_clusters.fa,
+ * <work_dir>/vsearch_cluster_stats.tsv and <work_dir>/parse_cluster.log, byte-identical to running
+ * the reference's parse_umi_clusters on the files umiclust_run_fasta writes (work_dir = the consout's
+ * directory; clusterout_sort and clusterout_id must be set).  clusters_prefix may be NULL: the
+ * per-cluster vsearch files, which the consumer only re-reads, are then not written at all.
+ * <work_dir>/clusters_fa must not exist (UMICLUST_EEXIST).  A record header without the 7
+ * `;`-separated fields or a strand other than + / - is UMICLUST_EFORMAT (the reference raises). */
+#define UMICLUST_EEXIST (-17)   /* output directory already exists */
+#define UMICLUST_EFORMAT (-74)  /* a record header does not follow the extract_umis format */
+int64_t umiclust_run_fasta_parse(umiclust_ctx *ctx, const umiclust_params *p, const char *in_fasta,
+                                 const char *clusters_prefix, const char *consout, const char *log_path,
+                                 const umiclust_parse_params *pp, const char *work_dir,
+                                 umiclust_parse_result *result, umiclust_stats *stats);
+
 /* ---- session API (in-memory, inputs resident in HBM) ---- */
 /* Stage n sequences (concatenated ASCII `seqs`, record i at [offsets[i], offsets[i+1])) into
  * device memory.  Length-filters, sorts and encodes on the device side of the boundary. */

@@ -1262,9 +1262,175 @@ bool write_file(const std::string& path, const std::string& data) {
   return ok;
 }
 
+// ---------------------------------------------------------------- in-process parse (§8f f2)
+// parse_umi_clusters / polish_cluster (/root/reference/ont_tcr_consensus/parse_umi_clusters.py:10-242)
+// evaluated on the in-memory clusters instead of re-reading consout and the cluster<N> files.  Every
+// string operation restates the Python it replaces; the comments cite the lines.
+std::string pjoin(const std::string& a, const std::string& b) {  // os.path.join(a, b), b relative
+  if (a.empty()) return b;
+  return a.back() == '/' ? a + b : a + "/" + b;
+}
+
+struct Sv {
+  const char* p;
+  size_t n;
+  std::string str() const { return std::string(p, n); }
+  bool operator==(const char* s) const { return n == strlen(s) && !memcmp(p, s, n); }
+};
+
+// Python `s.split(sep)[1]`: the text between the first and the second occurrence of sep
+bool split1(Sv s, const char* sep, Sv& out) {
+  const size_t m = strlen(sep);
+  const char* e = s.p + s.n;
+  const char* a = std::search(s.p, e, sep, sep + m);
+  if (a == e) return false;
+  a += m;
+  const char* b = std::search(a, e, sep, sep + m);
+  out = Sv{a, (size_t)(b - a)};
+  return true;
+}
+
+void split_fields(Sv name, std::vector<Sv>& f) {  // name.split(";")
+  f.clear();
+  size_t st = 0;
+  for (size_t i = 0; i <= name.n; i++)
+    if (i == name.n || name.p[i] == ';') {
+      f.push_back(Sv{name.p + st, i - st});
+      st = i + 1;
+    }
+}
+
+void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp, const char* work_dir_c,
+                umiclust_parse_result* pr) {
+  if (!c->p.clusterout_sort || !c->p.clusterout_id)
+    c->fail(UMICLUST_EINVAL, "in-process parse needs --clusterout_sort and --clusterout_id numbering");
+  const int64_t min_reads = pp->min_reads_per_cluster, max_reads = pp->max_reads_per_cluster;
+  const std::string work_dir = work_dir_c ? work_dir_c : "";
+  const std::string fa_dir = pjoin(work_dir, "clusters_fa");  // :177
+  struct stat sb;
+  if (stat(fa_dir.c_str(), &sb) == 0) c->fail(UMICLUST_EEXIST, "%s should not exist yet but does exist!", fa_dir.c_str());
+  if (mkdir(fa_dir.c_str(), 0777) != 0) c->fail(UMICLUST_EIO, "cannot create %s", fa_dir.c_str());
+  const int32_t K = c->nclusters;
+  std::string stats_out = "id_cluster\tn_fwd\tn_rev\twritten_fwd\twritten_rev\tn\twritten\tcluster_written\n";
+  std::string smol, log, lines, fn;
+  int64_t n_written = 0, reads_found = 0, reads_written = 0;
+  std::vector<Sv> fields;
+  // kept[strand]: insertion-ordered dict read id -> record (:61-65); ids of one cluster
+  std::vector<std::pair<Sv, int32_t>> kept[2];
+  std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position), per cluster
+  for (int32_t k = 0; k < K; k++) {  // consout in file order; clusterid = k (:197-200)
+    const std::string out_fasta = pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta");  // :34
+    kept[0].clear();
+    kept[1].clear();
+    index.clear();
+    int64_t seen[2] = {0, 0}, found = 0;
+    for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {  // cluster<N> file order (:36)
+      const int32_t i = c->perm[c->omemb[x]];
+      const Sv name{f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]};
+      split_fields(name, fields);
+      if (fields.size() != 7)  // :38-47
+        c->fail(UMICLUST_EFORMAT, "cluster %d: header has %d cols while it should contain 7: %s", k,
+                (int)fields.size(), name.str().c_str());
+      Sv strand;
+      if (!split1(fields[1], "strand=", strand)) c->fail(UMICLUST_EFORMAT, "no strand= field: %s", name.str().c_str());
+      found++;
+      int st = 0;
+      if (strand == "+") st = 0;
+      else if (strand == "-") st = 1;
+      else c->fail(UMICLUST_EFORMAT, "Strand annotation is %s but only - or + are allowed!", strand.str().c_str());
+      if (seen[st] < max_reads) {  // kept[strand][id] = rec: a repeated id keeps its first position
+        std::string key = fields[0].str();
+        key.push_back((char)('0' + st));
+        int32_t pos = -1;
+        for (auto& e : index)
+          if (e.first == key) { pos = e.second; break; }
+        if (pos < 0) {
+          index.emplace_back(std::move(key), (int32_t)kept[st].size());
+          kept[st].emplace_back(fields[0], i);
+        } else {
+          kept[st][pos].second = i;
+        }
+      }
+      seen[st]++;
+    }
+    // strand caps (:66-87)
+    const int64_t n_fwd = seen[0], n_rev = seen[1];
+    int64_t min_fwd, min_rev, max_fwd, max_rev;
+    if (pp->balance_strands) {
+      min_fwd = min_rev = min_reads / 2;
+      const int64_t capped = std::min(std::min(n_fwd * 2, n_rev * 2), max_reads);
+      max_fwd = max_rev = capped / 2;
+    } else if (n_fwd > n_rev) {
+      min_fwd = min_rev = 0;
+      max_rev = std::min(n_rev, max_reads / 2);
+      max_fwd = std::min(max_reads - max_rev, n_fwd);
+    } else {
+      min_fwd = min_rev = 0;
+      max_fwd = std::min(n_fwd, max_reads / 2);
+      max_rev = std::min(max_reads - max_fwd, n_rev);
+    }
+    const int64_t n_reads = max_fwd + max_rev;
+    if (n_reads > max_reads) c->fail(UMICLUST_EINVAL, "n_reads is higher than max_reads_per_cluster");  // :89-92
+    log += "Cluster: " + out_fasta + " has " + std::to_string(n_fwd) + "/" + std::to_string(max_fwd) + " fwd and " +
+           std::to_string(n_rev) + "/" + std::to_string(max_rev) + " rev reads\n";
+    int64_t w_fwd = 0, w_rev = 0, w_all = 0, written = 0;
+    if (n_fwd >= min_fwd && n_rev >= min_rev && n_reads >= min_reads) {  // :95-120
+      w_fwd = std::min<int64_t>((int64_t)kept[0].size(), max_fwd);
+      w_rev = std::min<int64_t>((int64_t)kept[1].size(), max_rev);
+      w_all = std::min<int64_t>(w_fwd + w_rev, max_reads);
+      written = 1;
+      lines.clear();
+      for (int64_t y = 0; y < w_all; y++) {
+        const auto& e = y < w_fwd ? kept[0][y] : kept[1][y - w_fwd];
+        const int32_t i = e.second;
+        split_fields(Sv{f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]}, fields);
+        Sv read;
+        if (!split1(fields[6], "seq=", read)) c->fail(UMICLUST_EFORMAT, "no seq= field in record %d", i);
+        lines.push_back('>');
+        lines.append(fields[0].p, fields[0].n);
+        lines.push_back('\n');
+        lines.append(read.p, read.n);
+        lines.push_back('\n');
+        smol += ">" + std::to_string(k) + "\n";
+        smol.append(read.p, read.n);
+        smol.push_back('\n');
+      }
+      if (!write_file(out_fasta, lines)) c->fail(UMICLUST_EIO, "cannot write %s", out_fasta.c_str());
+    } else {
+      log += "Cluster " + std::to_string(k) + " skipped\n";
+    }
+    log += "Cluster: " + out_fasta + " has " + std::to_string(w_all) + " reads written: " + std::to_string(w_fwd) +
+           " fwd - " + std::to_string(w_rev) + " rev\n";
+    stats_out += "cluster" + std::to_string(k) + "\t" + std::to_string(n_fwd) + "\t" + std::to_string(n_rev) + "\t" +
+                 std::to_string(w_fwd) + "\t" + std::to_string(w_rev) + "\t" + std::to_string(found) + "\t" +
+                 std::to_string(w_all) + "\t" + std::to_string(written) + "\n";
+    n_written += written;
+    // the reference's quirk (:206, :219-221): the totals are overwritten by this cluster's counts, then doubled
+    reads_found = 2 * found;
+    reads_written = 2 * w_all;
+    if (pp->max_clusters > 0 && n_written > pp->max_clusters) break;  // :222-223
+  }
+  if (!write_file(pjoin(work_dir, "vsearch_cluster_stats.tsv"), stats_out))
+    c->fail(UMICLUST_EIO, "cannot write the stats table");
+  if (!write_file(pjoin(work_dir, "smolecule_clusters.fa"), smol)) c->fail(UMICLUST_EIO, "cannot write smolecule_clusters.fa");
+  pr->n_clusters = K;
+  pr->n_written = n_written;
+  pr->reads_found = reads_found;
+  pr->reads_written = reads_written;
+  pr->empty_region = (n_written == 0 || reads_found == 0) ? 1 : 0;
+  pr->pad = 0;
+  if (pr->empty_region) return;  // :224-231 (the caller appends the region: it may need the JSON map)
+  log += "Clusters: " + std::to_string((int64_t)(n_written * 100.0 / K)) + "% written (" + std::to_string(n_written) +
+         ")\n";
+  log += "Reads: " + std::to_string(reads_found) + " found\n";
+  log += "Reads: " + std::to_string((int64_t)(reads_written * 100.0 / reads_found)) + "% in written clusters\n";
+  if (!write_file(pjoin(work_dir, "parse_cluster.log"), log)) c->fail(UMICLUST_EIO, "cannot write parse_cluster.log");
+}
+
 int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
                        const char* clusters_prefix, const char* consout, const char* log_path,
-                       umiclust_stats* stats) {
+                       umiclust_stats* stats, const umiclust_parse_params* pp = nullptr,
+                       const char* work_dir = nullptr, umiclust_parse_result* pr = nullptr) {
   const double t0 = now_s();
   Fasta f;
   if (!in_fasta || !read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
@@ -1347,6 +1513,7 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
              t_read, s.t_total_s, s.t_prefilter_s, s.t_align_s, s.t_consensus_s, s.t_host_s, t_write);
     if (!write_file(log_path, buf)) c->fail(UMICLUST_EIO, "cannot write %s", log_path);
   }
+  if (pp) parse_impl(c, f, pp, work_dir, pr);
   if (stats) *stats = c->stats;
   return K;
 }
@@ -1585,6 +1752,19 @@ int64_t umiclust_run_fasta(umiclust_ctx* c, const umiclust_params* p, const char
   UC_GUARD(c, {
     if (!p) c->fail(UMICLUST_EINVAL, "null params");
     return run_fasta_impl(c, p, in_fasta, clusters_prefix, consout, log_path, stats);
+  });
+}
+
+int64_t umiclust_run_fasta_parse(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
+                                 const char* clusters_prefix, const char* consout, const char* log_path,
+                                 const umiclust_parse_params* pp, const char* work_dir,
+                                 umiclust_parse_result* result, umiclust_stats* stats) {
+  UC_GUARD(c, {
+    if (!p || !pp || !result) c->fail(UMICLUST_EINVAL, "null params");
+    if (!p->clusterout_sort || !p->clusterout_id)
+      c->fail(UMICLUST_EINVAL, "in-process parse needs --clusterout_sort and --clusterout_id numbering");
+    if (pp->max_reads_per_cluster < 0 || pp->min_reads_per_cluster < 0) c->fail(UMICLUST_EINVAL, "read caps");
+    return run_fasta_impl(c, p, in_fasta, clusters_prefix, consout, log_path, stats, pp, work_dir, result);
   });
 }
 

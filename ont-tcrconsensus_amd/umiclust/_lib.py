@@ -17,7 +17,8 @@ PRESET_ROUND1 = 1
 PRESET_VSEARCH_DEFAULT = 2
 MAX_LEN = 112
 
-ERRORS = {-22: "EINVAL", -5: "EIO", -12: "ENOMEM", -19: "EDEVICE", -77: "ESTATE", -34: "ERANGE"}
+ERRORS = {-22: "EINVAL", -5: "EIO", -12: "ENOMEM", -19: "EDEVICE", -77: "ESTATE", -34: "ERANGE", -17: "EEXIST",
+          -74: "EFORMAT"}
 
 
 class UmiclustError(RuntimeError):
@@ -78,10 +79,23 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class ParseParams(C.Structure):
+    _fields_ = [("min_reads_per_cluster", C.c_int32), ("max_reads_per_cluster", C.c_int32),
+                ("balance_strands", C.c_int32), ("max_clusters", C.c_int32)]
+
+
+class ParseResult(C.Structure):
+    _fields_ = [("n_clusters", C.c_int64), ("n_written", C.c_int64), ("reads_found", C.c_int64),
+                ("reads_written", C.c_int64), ("empty_region", C.c_int32), ("pad", C.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
 # every symbol include/umiclust.h declares
 EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
-    "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv",
+    "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
     "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_align_pairs", "umiclust_prep",
 ]
 
@@ -112,6 +126,9 @@ def lib() -> C.CDLL:
     L.umiclust_run_fasta.restype = C.c_int64
     L.umiclust_run_fasta.argtypes = [C.c_void_p, P(Params), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
                                      P(Stats)]
+    L.umiclust_run_fasta_parse.restype = C.c_int64
+    L.umiclust_run_fasta_parse.argtypes = [C.c_void_p, P(Params), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                           P(ParseParams), C.c_char_p, P(ParseResult), P(Stats)]
     L.umiclust_run_argv.restype = C.c_int64
     L.umiclust_run_argv.argtypes = [C.c_void_p, C.c_int32, P(C.c_char_p), P(Stats)]
     L.umiclust_load.restype = C.c_int32
@@ -205,6 +222,16 @@ class Context:
                                      enc(log), C.byref(st))
         self._check(k, "run_fasta")
         return st.as_dict()
+
+    def run_fasta_parse(self, p: Params, in_fasta: str, clusters_prefix: str | None, consout: str | None,
+                        log: str | None, pp: ParseParams, work_dir: str) -> tuple[dict, dict]:
+        """Clustering + parse_umi_clusters' outputs from memory (include/umiclust.h)."""
+        st, pr = Stats(), ParseResult()
+        enc = lambda x: x.encode() if x else None  # noqa: E731
+        k = lib().umiclust_run_fasta_parse(self._h, C.byref(p), enc(in_fasta), enc(clusters_prefix), enc(consout),
+                                           enc(log), C.byref(pp), work_dir.encode(), C.byref(pr), C.byref(st))
+        self._check(k, "run_fasta_parse")
+        return st.as_dict(), pr.as_dict()
 
     def run_argv(self, argv: list[str]) -> dict:
         st = Stats()

@@ -173,11 +173,68 @@ def _parse_umi_clusters(
     return smolecule_fa
 
 
+def _append_empty_region(regions_wo_clusters_txt, work_dir, region_cluster_dict_json) -> None:
+    """parse_umi_clusters.py:224-231: record a region that produced no written cluster."""
+    region = os.path.basename(work_dir)
+    with open(regions_wo_clusters_txt, "a") as fh:
+        if region_cluster_dict_json:
+            with open(region_cluster_dict_json) as jf:
+                mapping = json.load(jf)
+            by_cluster = collections.defaultdict(list)
+            for reg, rc in mapping.items():
+                by_cluster[rc].append(reg)
+            fh.write(f"{region} {by_cluster[int(region.split('region_cluster')[1])]}\n")
+        else:
+            fh.write(f"{region}\n")
+
+
+def _vsearch_cluster_and_parse(
+    umi_fasta: Union[str, os.PathLike[str]],
+    clustering_out_dir: Union[str, os.PathLike[str]],
+    threads: int,
+    regions_wo_clusters_txt: Union[str, os.PathLike[str]],
+    min_umi_length: int = 50,
+    max_umi_length: int = 60,
+    identity: float = 0.94,
+    min_reads_per_cluster: int = 20,
+    max_reads_per_cluster: int = 60,
+    region_cluster_dict_json: Union[str, os.PathLike[str]] = None,
+    balance_strands: bool = False,
+    max_clusters: int = None,
+    round_: int = 1,
+    write_cluster_files: bool = True,
+):
+    """`vsearch_cluster` (round_=1) or `vsearch_cluster_consensus` (round_=2) followed by
+    `parse_umi_clusters` on its consout (tcr_consensus.py:237-265 round 1, :419-444 round 2), fused:
+    the consumer's outputs (clusters_fa/, smolecule_clusters.fa, vsearch_cluster_stats.tsv,
+    parse_cluster.log) are written by the native library straight from the in-memory clusters, byte-
+    identical to the two-step path.  With write_cluster_files=False the per-cluster `cluster<N>` files,
+    which the consumer only re-reads, are skipped.  Returns the
+    smolecule_clusters.fa path, or None for a region without written clusters, like parse_umi_clusters."""
+    from . import _lib
+    from .vsearch_umi_cluster import context, round1_argv, round2_argv
+    build = round1_argv if round_ == 1 else round2_argv
+    argv = build(os.fspath(umi_fasta), os.fspath(clustering_out_dir), threads, min_umi_length, max_umi_length,
+                 identity)
+    p, paths = _lib.params_from_argv(argv)
+    pp = _lib.ParseParams(min_reads_per_cluster, max_reads_per_cluster, int(bool(balance_strands)),
+                          int(max_clusters) if max_clusters else 0)
+    work_dir = os.path.dirname(paths["consout"])
+    _, res = context().run_fasta_parse(p, paths["in_fasta"], paths["clusters_prefix"] if write_cluster_files else None,
+                                       paths["consout"], paths["log"], pp, work_dir)
+    if res["empty_region"]:
+        _append_empty_region(regions_wo_clusters_txt, work_dir, region_cluster_dict_json)
+        return None
+    return os.path.join(work_dir, "smolecule_clusters.fa")
+
+
 try:  # pragma: no cover - ray is not installed in this image
     import ray as _ray
 
     parse_umi_clusters = _ray.remote(_parse_umi_clusters)
+    vsearch_cluster_and_parse = _ray.remote(_vsearch_cluster_and_parse)
 except ImportError:
     from .vsearch_umi_cluster import _LocalRemote
 
     parse_umi_clusters = _LocalRemote(_parse_umi_clusters)
+    vsearch_cluster_and_parse = _LocalRemote(_vsearch_cluster_and_parse)

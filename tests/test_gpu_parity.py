@@ -229,6 +229,72 @@ def test_dropin_files_vs_oracle(tmp_path, round_):
     assert sm and os.path.exists(sm)
 
 
+def _tree(d):
+    out = {}
+    for root, _, files in os.walk(d):
+        for fn in files:
+            if not fn.endswith(".log") or fn == "parse_cluster.log":
+                p = os.path.join(root, fn)
+                out[os.path.relpath(p, d)] = open(p, "rb").read()
+    return out
+
+
+PARSE_CASES = [
+    # (round, min_reads, max_reads, balance, max_clusters, dup_ids)
+    (1, 4, 60, False, None, False),
+    (1, 2, 5, True, None, True),
+    (1, 3, 8, False, 5, True),
+    (2, 1, 4, False, None, False),
+    (1, 100000, 60, False, None, False),  # nothing written: the empty-region branch
+]
+
+
+@pytest.mark.parametrize("case", PARSE_CASES, ids=[f"r{c[0]}_min{c[1]}_max{c[2]}_b{int(c[3])}_mc{c[4]}_d{int(c[5])}"
+                                                  for c in PARSE_CASES])
+def test_fused_parse_matches_two_step(tmp_path, case):
+    """§8f f2: vsearch_cluster_and_parse writes the same bytes as vsearch_cluster followed by the
+    (reference-pinned, tests/test_parse_golden.py) parse_umi_clusters restatement, with and without the
+    intermediate cluster<N> files."""
+    from umiclust.parse_umi_clusters import parse_umi_clusters, vsearch_cluster_and_parse
+    from umiclust.vsearch_umi_cluster import vsearch_cluster, vsearch_cluster_consensus
+    round_, mn, mx, bal, mc, dup = case
+    u = synth.make_umis(120, seed=41 + mn, max_reads=2000, orient_mix=0.1, error_rate=0.015 if round_ == 1 else 0.002)
+    fa = tmp_path / "in.fasta"
+    synth.write_umi_fasta(str(fa), u)
+    if dup:  # repeated read ids (kept once per strand, at the first position, with the last record)
+        lines = fa.read_text().splitlines(True)
+        hdrs = [i for i, ln in enumerate(lines) if ln.startswith(">")]
+        rng = random.Random(5)
+        for i in rng.sample(hdrs, len(hdrs) // 4):
+            j = rng.choice(hdrs)
+            lines[i] = lines[j].split(";", 1)[0] + ";" + lines[i].split(";", 1)[1]
+        fa.write_text("".join(lines))
+    idn = 0.93 if round_ == 1 else 0.97
+    kw = dict(min_reads_per_cluster=mn, max_reads_per_cluster=mx, balance_strands=bal, max_clusters=mc)
+    a = tmp_path / "region_cluster3"
+    a.mkdir()
+    if round_ == 1:
+        cons = vsearch_cluster.remote(str(fa), str(a), 25, 58, 68, idn)
+    else:
+        cons = vsearch_cluster_consensus.remote(str(fa), str(a), 25, 58, 68, idn)
+    ra = parse_umi_clusters.remote(cons, str(tmp_path / "wo_a.txt"), **kw)
+    for write in (True, False):
+        b = tmp_path / f"fused{int(write)}" / "region_cluster3"
+        b.mkdir(parents=True)
+        rb = vsearch_cluster_and_parse.remote(str(fa), str(b), 25, str(tmp_path / f"wo_b{int(write)}.txt"), 58, 68, idn,
+                                              round_=round_, write_cluster_files=write, **kw)
+        assert (ra is None) == (rb is None)
+        ta, tb = _tree(a), _tree(b)
+        if not write:
+            ta = {k: v for k, v in ta.items() if not (k.startswith("cluster") and "/" not in k)}
+        assert sorted(ta) == sorted(tb)
+        for k in ta:
+            # paths inside the log name the work dir
+            assert ta[k].replace(str(a).encode(), b"@") == tb[k].replace(str(b).encode(), b"@"), k
+        if ra is None:
+            assert open(tmp_path / "wo_a.txt").read() == open(tmp_path / f"wo_b{int(write)}.txt").read()
+
+
 def test_run_argv_matches_reference_argv(tmp_path):
     """umiclust_run_argv consumes the exact argv the reference passes to vsearch."""
     from umiclust.vsearch_umi_cluster import context, round1_argv
