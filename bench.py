@@ -126,7 +126,9 @@ def main() -> None:
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                traffic = tj.get("prefilter_hbm_bytes_per_launch")
+                # PMC traffic is per workload: only report it for the config it was counted on
+                if tj.get("config", 2) == args.config:
+                    traffic = tj.get("prefilter_hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         achieved = pf_bytes / n_launch / (t_pf / n_launch) / 1e9 if t_pf > 0 else 0.0
