@@ -142,7 +142,9 @@ typedef struct umiclust_parse_result {
   int32_t pad;
 } umiclust_parse_result;
 
-/* umiclust_run_fasta followed by parse_umi_clusters' outputs straight from the in-memory clusters:
+/* Replaces the vsearch_cluster -> parse_umi_clusters task pair (tcr_consensus.py:237-265 round 1,
+ * :419-444 round 2; consumer parse_umi_clusters.py:10-242).
+ * umiclust_run_fasta followed by parse_umi_clusters' outputs straight from the in-memory clusters:
  * <work_dir>/clusters_fa/cluster<N>.fasta, <work_dir>/smolecule_clusters.fa,
  * <work_dir>/vsearch_cluster_stats.tsv and <work_dir>/parse_cluster.log, byte-identical to running
  * the reference's parse_umi_clusters on the files umiclust_run_fasta writes (work_dir = the consout's
