@@ -1,13 +1,20 @@
 """Benchmark: UMIs clustered/s (+ GCUPS) of the vsearch --cluster_fast drop-in on MI355X.
 
-Workload (BASELINE.json configs[1]): one synthetic region bin of 2M dual-UMI reads per
-GPU (seed 1002 for rank 0, 1002*1_000_003 + rank for other ranks: weak scaling, one independent bin
-per GPU, no collective on the data path), --id 0.90, round-1 scoring (vsearch_umi_cluster.py:44-50).
-A step = one full pass of the hot path over the bin, with the sequences already resident in HBM:
-K1 prep/DUST/k-mers, greedy blocks of K2 prefilter + K3 walk alignment + host resolution, K3T
-traceback for members, K4 consensus, and the result download.
+Workloads (BASELINE.json configs):
+  --config 2 (default; the headline): one synthetic region bin of 2M dual-UMI reads per GPU (seed 1002 on
+      rank 0, 1002*1_000_003 + rank on other ranks: weak scaling, one independent bin per GPU, no collective
+      on the data path), --id 0.90, round-1 scoring (vsearch_umi_cluster.py:44-50).
+  --config 3: 10M reads over 24 barcodes x 40 Zipf(1.1) region bins, LPT-sharded over the ranks (strong
+      scaling: the node clusters the fixed 10M), round 1 (--id 0.93, run_config.json:16).
+  --config 4: 70M reads, 24 barcodes x 40 Zipf bins, both rounds: round 1 on every bin, round 2 (default
+      scoring, --id 0.97) on the round-1 consensus UMIs of every bin (tcr_consensus.py:190-267, :376-446).
+  --config 5: the long-UMI high-error stress bin (300k ~96-nt UMIs, 15 % indels, >1k-member clusters).
+A step = one full pass of the hot path over the rank's bins with the sequences already resident in HBM:
+K1 prep/DUST/k-mers, greedy blocks of K2 prefilter + K3 walk alignment + host resolution, K3T traceback
+for members, K4 consensus, and the result download.  --e2e adds the file leg: the same config-2 bin
+written as a FASTA with 1,500-nt `seq=` reads, then read FASTA -> cluster -> files written, timed end to end.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W [--config 2|3|4|5] [--e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -22,22 +29,103 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ont-tcrconsensus_amd"))
 
 METRIC = "UMIs clustered/sec + banded-NW GCUPS (whole node, 1/2/4/8 MI355X)"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+L2_GATHER_GBS = 18800.0    # MI355X_MICROARCH.md "Indexed rows: gather into LDS", L2-served rows, upper end
+# integer VALU issue ceiling: 256 CUs x 4 SIMDs x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md
+# "v_fma_f32 (wave64) 2 cyc (SIMD-32)"); lane-instructions per second
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# VALU wave-instructions per alignment cell of k_align_pk, measured: SQ_INSTS_VALU x 64 / cells computed
+# (profiles/); updated with the kernel
+ALIGN_VALU_PER_CELL = 15.7
 
 
-def cpu_baseline(umis, n_sample: int, identity: float, lens=(58, 68)) -> dict:
-    """The C oracle (oracle/, 1 thread) on the first n_sample reads of the same workload."""
+def cpu_baseline_bins(bins, identity: float, lens, budget_s: float = 20.0, preset: int = 1) -> dict:
+    """The C oracle (oracle/, 1 thread) over whole bins, largest first, until ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    done, kept, t = [], 0, 0.0
+    for b in sorted(bins, key=lambda b: -b.umis.n):
+        if t > budget_s:
+            break
+        seqs = b.umis.as_list()
+        t0 = time.perf_counter()
+        r = orc.cluster(orc.params(preset, identity, *lens), seqs)
+        t += time.perf_counter() - t0
+        kept += r["stats"]["kept"]
+        done.append(b.umis.n)
+    return dict(value=kept / t if t else 0.0, unit="UMIs/s", cores=1, kind="port",
+                sample=f"{len(done)} whole bins (largest first, {sum(done)} reads, sizes {done[:5]}...) clustered "
+                       f"by the C oracle restatement, 1 thread, {t:.1f} s",
+                seconds=t, n_kept=kept)
+
+
+def cpu_baseline_prefix(umis, n_sample: int, identity: float, lens, preset: int = 1) -> dict:
+    """The C oracle (oracle/, 1 thread) on the first n_sample reads of the bin."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
     seqs = umis.as_list()[:n_sample]
     t0 = time.perf_counter()
-    r = orc.cluster(orc.params(1, identity, *lens), seqs)
+    r = orc.cluster(orc.params(preset, identity, *lens), seqs)
     dt = time.perf_counter() - t0
     return dict(value=r["stats"]["kept"] / dt, unit="UMIs/s", cores=1, kind="port",
                 sample=f"first {n_sample} reads of the rank-0 bin ({r['stats']['kept']} kept, "
                        f"{r['n_clusters']} clusters) clustered by the C oracle restatement, 1 thread, "
-                       f"{dt:.1f} s; CPU cost grows ~N*C so a full 2M-read bin is slower per UMI",
+                       f"{dt:.1f} s; CPU cost grows ~N*C, so the full bin is slower per UMI (full-bin oracle "
+                       f"time: tests/golden/oracle_config2.json oracle_seconds)",
                 seconds=dt, n_kept=r["stats"]["kept"])
+
+
+def full_bin_cpu_reference(config: int) -> dict | None:
+    """The oracle's measured wall time over the whole config-2 bin (tests/golden/make_oracle_golden.py)."""
+    path = os.path.join(ROOT, "tests", "golden", f"oracle_config{config}.json")
+    if not os.path.exists(path):
+        return None
+    for name, g in json.load(open(path)).items():
+        if g.get("scale") == 1.0 and "oracle_seconds" in g:
+            return dict(case=name, seconds=g["oracle_seconds"], umis_per_s=g["n_reads"] / g["oracle_seconds"],
+                        threads=g.get("oracle_threads", 1), host_cpu=g.get("host_cpu"))
+    return None
+
+
+def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
+    """k_prefilter against the L2-served gather rate (its postings stay L2-resident: parts = XCDs), with
+    the HBM fraction as a side figure; k_align against the integer VALU issue ceiling."""
+    t_pf = sum(s["t_prefilter_s"] for s in stats)
+    t_al = sum(s["t_align_s"] for s in stats)
+    n_launch = sum(s["n_blocks"] for s in stats)
+    pf_bytes = sum(s["kmer_postings"] for s in stats) * 2
+    traffic = None
+    if os.path.exists(traffic_json):
+        try:
+            tj = json.load(open(traffic_json))
+            if tj.get("config", 2) == config:  # PMC traffic is per workload
+                traffic = tj.get("prefilter_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    achieved = pf_bytes / t_pf / 1e9 if t_pf > 0 else 0.0
+    roof = dict(kernel="k_prefilter", bound="l2", achieved=achieved, peak=L2_GATHER_GBS, unit="GB/s",
+                frac=achieved / L2_GATHER_GBS, traffic=traffic,
+                hbm_frac=achieved / HBM_PEAK_GBS, hbm_peak=HBM_PEAK_GBS,
+                bytes_per_launch=pf_bytes / max(1, n_launch), launches=n_launch,
+                avg_launch_ms=1e3 * t_pf / max(1, n_launch),
+                note="2 B per u16 posting streamed (postings served from the XCD-partitioned L2; measured HBM "
+                     "traffic is `traffic`); peak = L2-served gather rate, MI355X_MICROARCH.md")
+    cells = sum(s["cells"] for s in stats)
+    cells_c = sum(s["cells_computed"] for s in stats)
+    g_alg = cells / t_al / 1e9 if t_al else 0.0
+    g_cmp = cells_c / t_al / 1e9 if t_al else 0.0
+    ceiling = VALU_LANE_OPS / ALIGN_VALU_PER_CELL / 1e9
+    align = dict(kernel="k_align_pk", bound="valu", seconds=t_al, cells=cells, cells_computed=cells_c,
+                 gcups_kernel=g_alg, gcups_computed=g_cmp, valu_per_cell=ALIGN_VALU_PER_CELL,
+                 ceiling_gcups=ceiling, frac=g_alg / ceiling, frac_computed=g_cmp / ceiling,
+                 speculative_ratio=cells_c / cells if cells else None)
+    return roof, align
+
+
+def breakdown(stats: list) -> dict:
+    k = ["t_total_s", "t_prefilter_s", "t_align_s", "t_consensus_s", "t_index_s", "t_host_s",
+         "t_host_pass1_s", "t_sync_s", "t_merged_s"]
+    return {x: sum(s[x] for s in stats) for x in k}
 
 
 def main() -> None:
@@ -45,12 +133,13 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
-                    help="2: the headline bin (default); 5: the long-UMI high-error stress bin")
-    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the bin (testing only)")
-    ap.add_argument("--identity", type=float, default=None, help="default 0.90 (config 2), 0.75 (config 5)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
+    ap.add_argument("--scale", type=float, default=1.0, help="fraction of the workload (testing only)")
+    ap.add_argument("--identity", type=float, default=None,
+                    help="default 0.90 (config 2), 0.93 (configs 3, 4 round 1), 0.75 (config 5)")
     ap.add_argument("--cpu-sample", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time FASTA read -> cluster -> files written")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -58,6 +147,14 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from umiclust import _lib, binset, shard, synth
+    # multi-bin inputs are generated before anything touches the GPU (spawned workers)
+    bins = None
+    if args.config in (3, 4):
+        all_bins = synth.config_bins(args.config, args.scale, workers=min(16, os.cpu_count() or 4))
+        costs = [shard.bin_cost(b.umis.n) for b in all_bins]
+        plan = shard.lpt_assign(costs, world)
+        bins = synth.concat_bins([all_bins[i] for i in plan[rank]])
     import torch
     dist = None
     if world > 1:
@@ -68,104 +165,180 @@ def main() -> None:
         raise SystemExit("bench.py needs a HIP device (there is no CPU backend)")
     torch.cuda.set_device(local_rank)
 
-    from umiclust import _lib, synth
     if args.identity is None:
-        args.identity = 0.90 if args.config == 2 else 0.75
+        args.identity = {2: 0.90, 3: 0.93, 4: 0.93, 5: 0.75}[args.config]
     lens = synth.CONFIG_LENGTHS[args.config]
-    seed = (1000 + args.config) if rank == 0 else (1000 + args.config) * 1_000_003 + rank
+    ctx = _lib.Context(local_rank)
+    ctx2 = None
+    umis = None
     if args.config == 2:
+        seed = 1002 if rank == 0 else 1002 * 1_000_003 + rank
         umis = synth.make_umis(int(100_000 * args.scale), seed=seed, max_reads=int(2_000_000 * args.scale))
         workload = ("BASELINE config 2: synthetic 2M dual-UMI reads per GPU, one region bin, "
                     f"--id {args.identity:.2f}, round-1 scoring (match 10, mismatch -40, gapopen 0E/40I)")
-    else:
+    elif args.config == 5:
+        seed = 1005 if rank == 0 else 1005 * 1_000_003 + rank
         umis = synth.make_umis(max(1, int(200 * args.scale)), seed=seed, mean_reads=1500.0, error_rate=0.15,
                                split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
                                pattern_rev=synth.UMI_REV_LONG, max_reads=int(300_000 * args.scale))
         workload = ("BASELINE config 5 stress: synthetic 300k long (~96-nt) UMIs per GPU, 15% indels, deep "
                     f"clusters (NegBin mean 1500 reads/molecule), --id {args.identity:.2f}, "
                     f"--minseqlength {lens[0]} --maxseqlength {lens[1]}, round-1 scoring")
-    ctx = _lib.Context(local_rank)
-    params = _lib.params(_lib.PRESET_ROUND1, args.identity, *lens)
-    ctx.load(params, buf=umis.seq, off=umis.off)
+    elif args.config == 3:
+        workload = (f"BASELINE config 3: synthetic {int(10_000_000 * args.scale)} reads over 24 barcodes x 40 "
+                    f"Zipf(1.1) region bins, LPT-sharded over {world} GPU(s), round 1 --id {args.identity:.2f}")
+    else:
+        workload = (f"BASELINE config 4: synthetic {int(70_000_000 * args.scale)} reads over 24 barcodes x 40 "
+                    f"Zipf(1.1) region bins, LPT-sharded over {world} GPU(s); round 1 --id {args.identity:.2f} "
+                    "on every bin, round 2 (default scoring, --id 0.97) on the round-1 consensus UMIs of every "
+                    "bin, consensus emitted")
+
+    runners = []
+    if umis is not None:
+        params = _lib.params(_lib.PRESET_ROUND1, args.identity, *lens)
+        ctx.load(params, buf=umis.seq, off=umis.off)
+
+        def step():
+            return [ctx.cluster()]
+    else:
+        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens)
+        runners.append(r1)
+        if args.config == 4:
+            # round-2 inputs come from the round-1 results (deterministic): built once, resident like round 1
+            r1.cluster_all()
+            bins2 = binset.round2_binset(bins, r1.results())
+            ctx2 = _lib.Context(local_rank)
+            runners.append(binset.BinRunner(ctx2, bins2, binset.ROUND2["preset"], binset.ROUND2["identity"], *lens))
+
+        def step():
+            out = []
+            for r in runners:
+                out += r.cluster_all()
+            return out
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        ctx.cluster()
+        step()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stats = []
     for _ in range(args.steps):
-        stats.append(ctx.cluster())
+        stats.append(step())
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     t_max = elapsed
+    my_umis = sum(s["n_kept"] for s in stats[-1])
+    tot_umis = my_umis
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-    st = stats[-1]
-    n_kept = st["n_kept"]
-    total_umis = n_kept * world * args.steps
-    cells = st["cells"]
+        t = torch.tensor([elapsed, float(my_umis)], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        tm = t.clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t_max = float(tm[0].item())
+        tot_umis = int(t[1].item())
+    total_umis = tot_umis * args.steps
+    last = stats[-1]
+    cells = sum(s["cells"] for s in last)
     value = total_umis / t_max
-    gcups = cells * world * args.steps / t_max / 1e9
+    gcups = cells * (world if args.config in (2, 5) else 1) * args.steps / t_max / 1e9
 
     if rank == 0:
-        # roofline of the dominant kernel, from HIP-event kernel times accumulated by the driver
-        t_pf = sum(s["t_prefilter_s"] for s in stats) / args.steps
-        t_al = sum(s["t_align_s"] for s in stats) / args.steps
-        n_launch = st["n_blocks"]
-        # prefilter algorithmic bytes: u16 postings streamed + 2 CSR offsets per (k-mer, tile)
-        pf_bytes = st["kmer_postings"] * 2
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                # PMC traffic is per workload: only report it for the config it was counted on
-                if tj.get("config", 2) == args.config:
-                    traffic = tj.get("prefilter_hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        achieved = pf_bytes / n_launch / (t_pf / n_launch) / 1e9 if t_pf > 0 else 0.0
-        roof = dict(kernel="k_prefilter", bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=achieved / HBM_PEAK_GBS, traffic=traffic,
-                    bytes_per_launch=pf_bytes / max(1, n_launch), launches=n_launch,
-                    avg_launch_ms=1e3 * t_pf / max(1, n_launch))
-        # the alignment kernel is integer-VALU bound (no MFMA): reported beside the roofline
-        align_info = dict(kernel="k_align", seconds_per_step=t_al, gcups_kernel=cells / t_al / 1e9 if t_al else 0,
-                          cells_per_step=cells, cells_computed=st["cells_computed"])
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(umis, args.cpu_sample, args.identity, lens)
+        flat = [s for st in stats for s in st]
+        roof, align = roofline(flat, args.config, args.traffic_json)
+        # per-step averages for the breakdown
+        bd = {k: v / args.steps for k, v in breakdown(flat).items()}
+        bd["wall"] = t_max / args.steps
+        cfg = {"workload": workload, "parallelism": (f"{world} independent bins (1 per GPU), no data-path collective"
+                                                      if args.config in (2, 5) else
+                                                      f"LPT over {world} GPU(s) of the bins, no data-path collective")}
+        if umis is not None:
+            cfg.update(reads_per_gpu=int(umis.n), umis_kept_per_gpu=int(last[0]["n_kept"]),
+                       clusters=int(last[0]["n_clusters"]))
+        else:
+            cfg.update(bins_rank0=sum(r.nbins for r in runners), reads_rank0=int(sum(r.binset.n for r in runners)),
+                       umis_kept_rank0=int(my_umis), clusters_rank0=int(sum(s["n_clusters"] for s in last)))
         out = {
             "metric": METRIC, "value": value, "unit": "UMIs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": workload,
-                       "reads_per_gpu": int(umis.n), "umis_kept_per_gpu": int(n_kept), "clusters": st["n_clusters"],
-                       "parallelism": f"{world} independent bins (1 per GPU), no data-path collective"},
-            "gcups": gcups,
-            "breakdown_s_per_step": {"total": t_max / args.steps, "prefilter_kernels": t_pf, "align_kernels": t_al,
-                                     "consensus_kernels": st["t_consensus_s"], "index_kernels": st["t_index_s"],
-                                     "host_resolve": st["t_host_s"], "host_pass1": st["t_host_pass1_s"],
-                                     "host_wait_d2h": st["t_sync_s"]},
-            "merged_walks": st["n_merged_walks"], "t_merged_walks": st["t_merged_s"],
-            "deferred_queries": st["n_deferred"], "pairs_round_b": st["pairs_round_b"],
-            "pairs_peer": st["pairs_peer"],
-            "alignments_per_step": st["n_alignments"],
-            "roofline": roof,
-            "align": align_info,
-            "cpu_baseline": cpu,
+            "scaling": "weak" if args.config in (2, 5) else "strong", "vs_baseline": None, "dtype": "int16/int32",
+            "data": "synthetic", "config": cfg, "gcups": gcups,
+            "breakdown_s_per_step": bd,
+            "merged_walks": sum(s["n_merged_walks"] for s in last), "deferred_queries": sum(s["n_deferred"] for s in last),
+            "pairs_round_b": sum(s["pairs_round_b"] for s in last), "pairs_peer": sum(s["pairs_peer"] for s in last),
+            "alignments_per_step": sum(s["n_alignments"] for s in last),
+            "roofline": roof, "align": align,
         }
+        if args.config in (3, 4) and world == 1:
+            # per-bin wall times of the last step -> the LPT makespan of the same bins on 2/4/8 GPUs (model:
+            # bins are independent, so a rank's time is the sum of its bins' times)
+            per_bin = [s["t_total_s"] for s in last]
+            nb1 = runners[0].nbins
+            costs = [shard.bin_cost(b.umis.n) for b in runners[0].binset.bins]
+            model = {}
+            for g in (2, 4, 8):
+                plan = shard.lpt_assign(costs, g)
+                span = 0.0
+                for p in plan:
+                    tt = sum(per_bin[i] for i in p)
+                    if len(runners) > 1:
+                        tt += sum(per_bin[nb1 + i] for i in p)
+                    span = max(span, tt)
+                model[str(g)] = dict(makespan_s=span, umis_per_s=tot_umis / span if span else None,
+                                     efficiency=(sum(per_bin) / g) / span if span else None)
+            out["lpt_model_from_measured_bins"] = model
+            out["largest_bin_s"] = max(per_bin) if per_bin else 0.0
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            if umis is not None:
+                cpu = cpu_baseline_prefix(umis, args.cpu_sample, args.identity, lens)
+                full = full_bin_cpu_reference(args.config)
+                if full:
+                    cpu["full_bin_oracle"] = full
+            else:
+                cpu = cpu_baseline_bins(runners[0].binset.bins, args.identity, lens)
+        out["cpu_baseline"] = cpu
+        if args.e2e and args.config == 2 and world == 1:
+            out["e2e"] = e2e_leg(ctx, umis, args.identity, lens)
         print(json.dumps(out), flush=True)
     ctx.close()
+    if ctx2 is not None:
+        ctx2.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
+    """§8d's UMIs/s: read FASTA -> cluster -> cluster<N> files + consout written (the drop-in's file
+    boundary, umiclust_run_fasta), on the same bin written with 1,500-nt `seq=` reads."""
+    import shutil
+    import tempfile
+    from umiclust import _lib, synth
+    d = tempfile.mkdtemp(prefix="umiclust_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        fa = os.path.join(d, "region_cluster0_detected_umis.fasta")
+        t0 = time.perf_counter()
+        synth.write_umi_fasta_fast(fa, umis, read_len=read_len)
+        t_gen = time.perf_counter() - t0
+        size = os.path.getsize(fa)
+        out = os.path.join(d, "out")
+        os.mkdir(out)
+        p = _lib.params(_lib.PRESET_ROUND1, identity, *lens)
+        t0 = time.perf_counter()
+        st = ctx.run_fasta(p, fa, os.path.join(out, "cluster"), os.path.join(out, "umi_clusters_consensus.fasta"),
+                           os.path.join(out, "vsearch_cluster.log"))
+        t_run = time.perf_counter() - t0
+        return dict(umis_per_s=st["n_kept"] / t_run, seconds=t_run, fasta_bytes=size, n_kept=st["n_kept"],
+                    clusters=st["n_clusters"], cluster_files=st["n_clusters"], t_read_s=st.get("t_read_s"),
+                    t_cluster_s=st["t_total_s"], t_write_s=st.get("t_write_s"), fasta_write_s=t_gen,
+                    note="page-cache-warm input; outputs on the box's local disk")
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 if __name__ == "__main__":

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 1
+#define UMICLUST_ABI_VERSION 2
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -89,6 +89,9 @@ typedef struct umiclust_stats {
   double t_host_pass1_s;  /* host first in-order pass of every block */
   int64_t n_merged_walks; /* (query, strand) walks the host re-ran with in-block centroids */
   double t_merged_s;      /* host time inside those merged walks */
+  double t_read_s;        /* file path: FASTA read + parse (umiclust_run_fasta*) */
+  double t_write_s;       /* file path: cluster<N> / consout (+ in-process parse) writing */
+  double t_run_s;         /* file path: the whole call, read to files written */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;
@@ -129,7 +132,8 @@ typedef struct umiclust_parse_params {
   int32_t min_reads_per_cluster;  /* min_reads_per_cluster (20) */
   int32_t max_reads_per_cluster;  /* max_reads_per_cluster (60) */
   int32_t balance_strands;        /* balance_strands (0) */
-  int32_t max_clusters;           /* max_clusters; 0 = no limit (the reference's None) */
+  int32_t max_clusters;           /* max_clusters; 0 = no limit (the reference's None); any other value
+                                     stops once n_written > max_clusters, as Python's truthiness does */
 } umiclust_parse_params;
 
 typedef struct umiclust_parse_result {
@@ -175,6 +179,20 @@ int64_t umiclust_cluster(umiclust_ctx *ctx, umiclust_stats *stats);
  * n_clusters+1 entries; cons capacity cons_cap bytes). Any pointer may be NULL. */
 int64_t umiclust_fetch(umiclust_ctx *ctx, int32_t *cluster, uint8_t *strand, uint8_t *centroid,
                        char *cons, int64_t cons_cap, int64_t *cons_off);
+
+/* ---- many region bins per load (BASELINE configs 3 and 4) ---- */
+/* The reference runs one vsearch process per (library x region bin) (tcr_consensus.py:231-245 round 1,
+ * :411-427 round 2).  A load may hold many such bins resident in HBM at once: bin b is input records
+ * [bin_start[b], bin_start[b+1]) (bin_start has nbins+1 entries, bin_start[0] = 0, bin_start[nbins] = n).
+ * Every bin is length-filtered, sorted and clustered on its own, exactly as its own vsearch run would
+ * be; umiclust_load / umiclust_cluster / umiclust_fetch are the nbins = 1 case. */
+int32_t umiclust_load_bins(umiclust_ctx *ctx, const umiclust_params *p, const char *seqs,
+                           const int64_t *offsets, int64_t n, const int64_t *bin_start, int32_t nbins);
+/* cluster one bin of the load; returns its number of clusters */
+int64_t umiclust_cluster_bin(umiclust_ctx *ctx, int32_t bin, umiclust_stats *stats);
+/* umiclust_fetch for one clustered bin: arrays over the bin's input records (bin-local index) */
+int64_t umiclust_fetch_bin(umiclust_ctx *ctx, int32_t bin, int32_t *cluster, uint8_t *strand,
+                           uint8_t *centroid, char *cons, int64_t cons_cap, int64_t *cons_off);
 
 /* ---- kernel-level entry points (parity tests) ---- */
 /* Align npairs (query, target) pairs with the production alignment kernel.  Sequences are

@@ -36,6 +36,7 @@
 #include <string>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <thread>
 #include <unistd.h>
 #include <vector>
 
@@ -141,7 +142,8 @@ struct Pass {
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
-  DevBuf<uint32_t> d_counters;  // [0] postings, [1..5] npairs per walk round, [8] peer pairs
+  DevBuf<uint32_t> d_counters;  // [0] postings, [1..5] npairs per walk round, [8] peer pairs,
+                                // [9] target residues of walk pairs, [10] of peer pairs
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
   DevBuf<WalkState> d_ws;
   DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
@@ -173,11 +175,17 @@ struct umiclust_ctx {
   bool clustered = false;
   DevBuf<unsigned long long> pf_prof;  // prefilter phase clocks (UMICLUST_PFPROF)
 
-  // input (host copies kept only for the file path outputs)
+  // input (host copies kept only for the file path outputs).  A load holds one or more independent
+  // region bins (umiclust_load_bins): bin b is input records [bin_in[b], bin_in[b+1]) and sorted
+  // seqnos [bin_s[b], bin_s[b+1]) -- every bin is length-sorted on its own and clustered on its own,
+  // with absolute seqnos on the device.
   int64_t n_input = 0;
-  int32_t n = 0;                  // kept sequences
+  int32_t n = 0;                  // kept sequences (all bins)
   std::vector<int32_t> perm;      // sorted -> input index
   std::vector<uint8_t> hlen;      // sorted lengths
+  std::vector<int64_t> bin_in;    // [nbins + 1] input record boundaries
+  std::vector<int32_t> bin_s;     // [nbins + 1] sorted seqno boundaries
+  int32_t cur_bin = -1;           // bin of the last umiclust_cluster* call
 
   // device: sequences
   DevBuf<char> d_ascii;
@@ -218,19 +226,35 @@ struct umiclust_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ix_events;  // index rebuild timing
   size_t nix = 0;
 
-  // results (sorted order)
-  std::vector<int32_t> cno;       // creation cluster number
+  // results (sorted order, absolute seqnos; each bin's range is rewritten when it is clustered)
+  std::vector<int32_t> cno;       // creation cluster number (within the bin)
   std::vector<uint8_t> strand;
   std::vector<int32_t> target;    // centroid seqno a member aligned to (-1 for centroids)
-  std::vector<int32_t> cent;      // ordinal -> seqno
-  int32_t nclusters = 0;
-  // outputs (output-cluster numbering)
+  std::vector<int32_t> ocl;       // output cluster number (within the bin)
+  std::vector<int32_t> cent;      // ordinal -> seqno (current bin)
+  int32_t nclusters = 0;          // current bin
+  // outputs of the current bin (output-cluster numbering)
   std::vector<int32_t> rank_of;   // creation number -> output number
   std::vector<int32_t> ostart, omemb;  // members per output cluster (centroid first)
   std::vector<char> cons;
   std::vector<int64_t> cons_off;
+  // per-bin results kept for umiclust_fetch_bin
+  struct BinOut {
+    bool done = false;
+    int32_t K = 0;
+    std::vector<char> cons;
+    std::vector<int64_t> cons_off;
+  };
+  std::vector<BinOut> bout;
   umiclust_stats stats{};
   int32_t block_size = 8192;
+  // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
+  DevBuf<uint32_t> t_mpq, t_mpt, t_mout, t_dir;
+  DevBuf<uint8_t> t_ops, t_mstrand;
+  DevBuf<uint16_t> t_nops, t_conslen;
+  DevBuf<int32_t> t_cstart, t_mseq, t_mops, t_over;
+  DevBuf<char> t_cons;
+  hipEvent_t tev[2] = {nullptr, nullptr};
 
   void fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -400,6 +424,13 @@ inline bool better(const Outcome& a, const Outcome& b) {
 
 enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
 
+// greedy state of the sorted seqnos [s0, s0 + n) of the bin being clustered, indexed by absolute seqno
+struct StateView {
+  uint8_t* p = nullptr;
+  int32_t s0 = 0;
+  uint8_t& operator[](int64_t i) const { return p[i - s0]; }
+};
+
 void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   const size_t nqs = (size_t)B * c->both;
   c->hip(P.d_top_seqno.ensure(nqs * kTopHits), "alloc");
@@ -524,7 +555,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   DevSeqs ds = dev_seqs(c);
   const int32_t qlen = c->hlen[q0];
   c->hip(launch_walk(-1, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
-                     c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 1, st),
+                     c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 1,
+                     P.d_counters.p + 9, st),
          "walk");
   c->hip(hipEventRecord(P.ev[2], st), "event");
   for (int r = 0; r < kWalk / kBatch; r++) {
@@ -533,11 +565,11 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
            "align");
     c->hip(launch_walk(r, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
                        c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2 + r,
-                       st),
+                       P.d_counters.p + 9, st),
            "walk");
   }
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
-                           P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p, P.d_counters.p + 8, st),
+                           P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p, P.d_counters.p + 8, P.d_counters.p + 10, st),
          "peer pairs");
   c->hip(launch_align(ds, qlen, c->ambig, P.d_ppq.p, P.d_ppt.p, nqs * kPeerCap, P.d_counters.p + 8,
                       P.d_poutidx.p, c->sc, P.d_peer_res.p, st),
@@ -563,7 +595,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
 // that are centroids) -- every such peer now matters, so an undetermined one blocks too.  A merged
 // walk that needs an alignment the pass did not compute (a T_old entry past the device walk, or a
 // peer that was not relevant) is deferred to round B, and so are queries blocked by deferred ones.
-bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::vector<int32_t>& new_cents,
+bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<int32_t>& new_cents,
                   double& t_pf, double& t_al, double& t_host) {
   const int both = c->both;
   const int32_t q0 = P.q0, nq = P.nq, w0 = P.w0;
@@ -579,6 +611,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
   t_al += ms * 1e-3;
   c->stats.kmer_postings += P.h_counters.p[0];
   c->stats.pairs_peer += P.h_counters.p[8];
+  // every alignment the device computed for this pass (walk rounds + speculative peers)
+  c->stats.cells_computed += (int64_t)c->hlen[q0] * ((int64_t)P.h_counters.p[9] + (int64_t)P.h_counters.p[10]);
   // a pageable copy of the per-query-strand outcomes (sequential, revisited below); the records
   // are read in place, only for the query-strands whose relevant peers include a centroid
   const double tc0 = now_s();
@@ -766,6 +800,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, std::vector<uint8_t>& state, std::ve
     t_host += now_s() - th1;
     const int32_t nb = (int32_t)bpq.size();
     c->stats.pairs_round_b += nb;
+    for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[q0] * c->hlen[bpt[x]];
     std::vector<uint32_t> bres(nb);
     if (nb > 0) {
       hipStream_t sb = c->st_b;
@@ -860,12 +895,16 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   c->hip(hipEventRecord(ev.second, st), "event");
 }
 
-void cluster_all(umiclust_ctx* c) {
+void cluster_all(umiclust_ctx* c, int32_t bin) {
   const double t0 = now_s();
-  const int32_t n = c->n;
-  c->cno.assign(n, -1);
-  c->strand.assign(n, 0);
-  c->target.assign(n, -1);
+  if (bin < 0 || bin + 1 >= (int32_t)c->bin_s.size()) c->fail(UMICLUST_EINVAL, "bin %d out of range", bin);
+  // one bin = the sorted seqnos [s0, s1); seqnos stay absolute everywhere
+  const int32_t s0 = c->bin_s[bin], s1 = c->bin_s[bin + 1];
+  const int32_t n = s1 - s0;
+  c->cur_bin = bin;
+  std::fill(c->cno.begin() + s0, c->cno.begin() + s1, -1);
+  std::fill(c->strand.begin() + s0, c->strand.begin() + s1, 0);
+  std::fill(c->target.begin() + s0, c->target.begin() + s1, -1);
   c->cent.clear();
   c->cent.reserve((size_t)n + 1);
   c->cent_len.clear();
@@ -880,11 +919,12 @@ void cluster_all(umiclust_ctx* c) {
   c->index_end = 0;
   c->nix = 0;
   c->stats = umiclust_stats{};
-  c->stats.n_input = c->n_input;
+  c->stats.n_input = c->bin_in[bin + 1] - c->bin_in[bin];
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
-  std::vector<uint8_t> state(n, ST_UNDET);
+  std::vector<uint8_t> state_buf((size_t)n, ST_UNDET);
+  StateView state{state_buf.data(), s0};
   double t_pf = 0, t_al = 0, t_host = 0;
   // blocks of at most B queries of one length (the aligner is compiled per query length); a block's
   // peer tile fills one kPeerRegion of the prefilter counters, so B <= kMaxBlock
@@ -910,9 +950,9 @@ void cluster_all(umiclust_ctx* c) {
     c->hip(c->arena.ensure((size_t)off + 64), "alloc arena");
   }
   std::vector<std::pair<int32_t, int32_t>> blocks;
-  for (int32_t q0 = 0; q0 < n;) {
+  for (int32_t q0 = s0; q0 < s1;) {
     int32_t same = 1;
-    while (q0 + same < n && same < B && c->hlen[q0 + same] == c->hlen[q0]) same++;
+    while (q0 + same < s1 && same < B && c->hlen[q0 + same] == c->hlen[q0]) same++;
     blocks.push_back({q0, same});
     q0 += same;
   }
@@ -976,12 +1016,12 @@ void cluster_all(umiclust_ctx* c) {
   // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's
   c->nclusters = (int32_t)c->cent.size();
   for (int32_t k = 0; k < c->nclusters; k++) c->cno[c->cent[k]] = k;
-  for (int32_t s = 0; s < n; s++)
+  for (int32_t s = s0; s < s1; s++)
     if (c->target[s] >= 0) c->cno[s] = c->cno[c->target[s]];
   // --- output numbering: --clusterout_sort orders clusters by size desc, creation order
   const int32_t K = c->nclusters;
   std::vector<int32_t> size(K, 0);
-  for (int32_t s = 0; s < n; s++) size[c->cno[s]]++;
+  for (int32_t s = s0; s < s1; s++) size[c->cno[s]]++;
   std::vector<int32_t> order(K);
   for (int32_t k = 0; k < K; k++) order[k] = k;
   if (c->p.clusterout_sort)
@@ -989,53 +1029,52 @@ void cluster_all(umiclust_ctx* c) {
   c->rank_of.assign(K, 0);
   for (int32_t k = 0; k < K; k++) c->rank_of[order[k]] = k;
   c->ostart.assign((size_t)K + 1, 0);
-  for (int32_t s = 0; s < n; s++) c->ostart[c->rank_of[c->cno[s]] + 1]++;
+  for (int32_t s = s0; s < s1; s++) {
+    c->ocl[s] = c->rank_of[c->cno[s]];
+    c->ostart[c->ocl[s] + 1]++;
+  }
   for (int32_t k = 0; k < K; k++) c->ostart[k + 1] += c->ostart[k];
   c->omemb.assign(n, 0);
   {
     std::vector<int32_t> fill(c->ostart.begin(), c->ostart.end() - 1);
-    for (int32_t s = 0; s < n; s++) c->omemb[fill[c->rank_of[c->cno[s]]]++] = s;
+    for (int32_t s = s0; s < s1; s++) c->omemb[fill[c->ocl[s]]++] = s;
   }
   // --- traceback for members, then consensus
   double t_cons = 0;
   {
     std::vector<uint32_t> mpq, mpt;
     std::vector<int32_t> opsidx(n, -1);
-    for (int32_t s = 0; s < n; s++)
+    for (int32_t s = s0; s < s1; s++)
       if (c->target[s] >= 0) {
-        opsidx[s] = (int32_t)mpq.size();
+        opsidx[s - s0] = (int32_t)mpq.size();
         mpq.push_back(((uint32_t)s << 1) | c->strand[s]);
         mpt.push_back((uint32_t)c->target[s]);
       }
     const int32_t nm = (int32_t)mpq.size();
-    DevBuf<uint32_t> d_mpq, d_mpt, d_mout, d_dir;
-    DevBuf<uint8_t> d_ops, d_mstrand;
-    DevBuf<uint16_t> d_nops, d_conslen;
-    DevBuf<int32_t> d_cstart, d_mseq, d_mops, d_over;
-    DevBuf<char> d_cons;
-    c->hip(d_mpq.ensure(nm), "alloc");
-    c->hip(d_mpt.ensure(nm), "alloc");
-    c->hip(d_mout.ensure(nm), "alloc");
-    c->hip(d_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
-    c->hip(d_nops.ensure(nm), "alloc");
-    const int32_t chunk = 1 << 18;
-    c->hip(d_dir.ensure((size_t)chunk * kMaxLen * kCodeWords), "alloc");
+    c->hip(c->t_mpq.ensure(nm), "alloc");
+    c->hip(c->t_mpt.ensure(nm), "alloc");
+    c->hip(c->t_mout.ensure(nm), "alloc");
+    c->hip(c->t_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
+    c->hip(c->t_nops.ensure(nm), "alloc");
+    const int32_t chunk = std::max(1, std::min(nm, 1 << 18));
+    c->hip(c->t_dir.ensure((size_t)chunk * kMaxLen * kCodeWords), "alloc");
     if (nm > 0) {
-      c->hip(hipMemcpyAsync(d_mpq.p, mpq.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(d_mpt.p, mpt.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mpq.p, mpq.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mpt.p, mpt.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
     }
-    hipEvent_t e0, e1;
-    c->hip(hipEventCreate(&e0), "event");
-    c->hip(hipEventCreate(&e1), "event");
-    c->hip(hipEventRecord(e0, c->st), "event");
+    if (!c->tev[0]) {
+      c->hip(hipEventCreate(&c->tev[0]), "event");
+      c->hip(hipEventCreate(&c->tev[1]), "event");
+    }
+    c->hip(hipEventRecord(c->tev[0], c->st), "event");
     DevSeqs ds = dev_seqs(c);
     // members are in sorted (length-descending) order: one launch per query length and chunk
     for (int32_t b = 0; b < nm;) {
       const int32_t ql = c->hlen[mpq[b] >> 1];
       int32_t e = b + 1;
       while (e < nm && e - b < chunk && c->hlen[mpq[e] >> 1] == ql) e++;
-      c->hip(launch_traceback(ds, ql, d_mpq.p + b, d_mpt.p + b, e - b, c->sc, d_dir.p,
-                              d_ops.p + (size_t)b * kOpsStride, d_nops.p + b, d_mout.p + b, c->st),
+      c->hip(launch_traceback(ds, ql, c->t_mpq.p + b, c->t_mpt.p + b, e - b, c->sc, c->t_dir.p,
+                              c->t_ops.p + (size_t)b * kOpsStride, c->t_nops.p + b, c->t_mout.p + b, c->st),
              "traceback");
       b = e;
     }
@@ -1045,41 +1084,39 @@ void cluster_all(umiclust_ctx* c) {
     for (int32_t x = 0; x < n; x++) {
       const int32_t s = c->omemb[x];
       mseq[x] = s;
-      mops[x] = opsidx[s];
+      mops[x] = opsidx[s - s0];
       mstr[x] = c->strand[s];
     }
-    c->hip(d_cstart.ensure((size_t)K + 1), "alloc");
-    c->hip(d_mseq.ensure(n), "alloc");
-    c->hip(d_mops.ensure(n), "alloc");
-    c->hip(d_mstrand.ensure(n), "alloc");
-    c->hip(d_cons.ensure((size_t)std::max(K, 1) * kConsCap), "alloc");
-    c->hip(d_conslen.ensure((size_t)std::max(K, 1)), "alloc");
-    c->hip(d_over.ensure(1), "alloc");
-    c->hip(hipMemsetAsync(d_over.p, 0, 4, c->st), "memset");
-    c->hip(hipMemcpyAsync(d_cstart.p, c->ostart.data(), ((size_t)K + 1) * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(c->t_cstart.ensure((size_t)K + 1), "alloc");
+    c->hip(c->t_mseq.ensure(n), "alloc");
+    c->hip(c->t_mops.ensure(n), "alloc");
+    c->hip(c->t_mstrand.ensure(n), "alloc");
+    c->hip(c->t_cons.ensure((size_t)std::max(K, 1) * kConsCap), "alloc");
+    c->hip(c->t_conslen.ensure((size_t)std::max(K, 1)), "alloc");
+    c->hip(c->t_over.ensure(1), "alloc");
+    c->hip(hipMemsetAsync(c->t_over.p, 0, 4, c->st), "memset");
+    c->hip(hipMemcpyAsync(c->t_cstart.p, c->ostart.data(), ((size_t)K + 1) * 4, hipMemcpyHostToDevice, c->st), "h2d");
     if (n > 0) {
-      c->hip(hipMemcpyAsync(d_mseq.p, mseq.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(d_mops.p, mops.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(d_mstrand.p, mstr.data(), (size_t)n, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mseq.p, mseq.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mops.p, mops.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mstrand.p, mstr.data(), (size_t)n, hipMemcpyHostToDevice, c->st), "h2d");
     }
-    c->hip(launch_consensus(ds, d_cstart.p, K, d_mseq.p, d_mops.p, d_mstrand.p, d_ops.p, d_nops.p,
-                            d_cons.p, d_conslen.p, d_over.p, c->st),
+    c->hip(launch_consensus(ds, c->t_cstart.p, K, c->t_mseq.p, c->t_mops.p, c->t_mstrand.p, c->t_ops.p, c->t_nops.p,
+                            c->t_cons.p, c->t_conslen.p, c->t_over.p, c->st),
            "consensus");
-    c->hip(hipEventRecord(e1, c->st), "event");
+    c->hip(hipEventRecord(c->tev[1], c->st), "event");
     std::vector<uint16_t> clen(K);
     std::vector<char> craw((size_t)K * kConsCap);
     int32_t over = 0;
     if (K > 0) {
-      c->hip(hipMemcpyAsync(clen.data(), d_conslen.p, (size_t)K * 2, hipMemcpyDeviceToHost, c->st), "d2h");
-      c->hip(hipMemcpyAsync(craw.data(), d_cons.p, (size_t)K * kConsCap, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(clen.data(), c->t_conslen.p, (size_t)K * 2, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(craw.data(), c->t_cons.p, (size_t)K * kConsCap, hipMemcpyDeviceToHost, c->st), "d2h");
     }
-    c->hip(hipMemcpyAsync(&over, d_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipMemcpyAsync(&over, c->t_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
     c->hip(hipStreamSynchronize(c->st), "sync");
     float ms = 0;
-    c->hip(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+    c->hip(hipEventElapsedTime(&ms, c->tev[0], c->tev[1]), "elapsed");
     t_cons = ms * 1e-3;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     if (over) c->fail(UMICLUST_ERANGE, "consensus: %d clusters exceed the MSA column budget", over);
     c->cons_off.assign((size_t)K + 1, 0);
     for (int32_t k = 0; k < K; k++) c->cons_off[k + 1] = c->cons_off[k] + clen[k];
@@ -1087,6 +1124,11 @@ void cluster_all(umiclust_ctx* c) {
     for (int32_t k = 0; k < K; k++)
       memcpy(c->cons.data() + c->cons_off[k], craw.data() + (size_t)k * kConsCap, clen[k]);
   }
+  auto& bo = c->bout[bin];
+  bo.done = true;
+  bo.K = K;
+  bo.cons = c->cons;
+  bo.cons_off = c->cons_off;
   c->stats.n_clusters = K;
   c->stats.t_prefilter_s = t_pf;
   c->stats.t_align_s = t_al;
@@ -1106,43 +1148,76 @@ void cluster_all(umiclust_ctx* c) {
 }
 
 // ---------------------------------------------------------------- load
-void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs, int64_t n) {
-  if (!p || (!seqs && n > 0) || !offs || n < 0) c->fail(UMICLUST_EINVAL, "null argument");
+// bin_in: nbins + 1 input record boundaries (NULL: one bin of all n records)
+void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs, int64_t n,
+               const int64_t* bin_in = nullptr, int32_t nbins = 1) {
+  if (!p || (!seqs && n > 0) || !offs || n < 0 || nbins < 1) c->fail(UMICLUST_EINVAL, "null argument");
   validate(c, *p);
+  c->loaded = false;
+  c->clustered = false;
   c->p = *p;
   c->sc = to_scoring(*p);
   c->both = p->strand_both ? 2 : 1;
   build_tables(c);
   c->n_input = n;
-  // length filter + stable sort by length desc (db_sortbylength; ties keep input order, O1)
+  c->bin_in.assign((size_t)nbins + 1, 0);
+  if (bin_in) {
+    if (bin_in[0] != 0 || bin_in[nbins] != n) c->fail(UMICLUST_EINVAL, "bin boundaries must span [0, n]");
+    for (int32_t b = 0; b < nbins; b++)
+      if (bin_in[b + 1] < bin_in[b]) c->fail(UMICLUST_EINVAL, "bin boundaries must not decrease");
+    for (int32_t b = 0; b <= nbins; b++) c->bin_in[b] = bin_in[b];
+  } else {
+    c->bin_in[1] = n;
+  }
+  // length filter + stable sort by length desc within every bin (db_sortbylength; ties keep input
+  // order, O1): one counting sort per bin, bins laid out one after another
   const int64_t maxlen = std::min<int64_t>(p->maxseqlength, kMaxLen);
   for (int64_t i = 0; i < n; i++) {
     const int64_t L = offs[i + 1] - offs[i];
     if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
   }
-  std::vector<int64_t> cnt(kMaxLen + 2, 0);
+  int64_t kept = 0;
   for (int64_t i = 0; i < n; i++) {
     const int64_t L = offs[i + 1] - offs[i];
-    if (L >= p->minseqlength && L <= maxlen) cnt[kMaxLen - L]++;
+    kept += (L >= p->minseqlength && L <= maxlen) ? 1 : 0;
   }
-  int64_t acc = 0;
-  for (int L = 0; L <= kMaxLen; L++) {
-    const int64_t t = cnt[L];
-    cnt[L] = acc;
-    acc += t;
-  }
-  if (acc > (int64_t)INT32_MAX / 2) c->fail(UMICLUST_ERANGE, "too many sequences in one bin");
-  c->n = (int32_t)acc;
+  if (kept > (int64_t)INT32_MAX / 2) c->fail(UMICLUST_ERANGE, "too many sequences in one load");
+  c->n = (int32_t)kept;
   c->perm.assign(c->n, 0);
   c->hlen.assign(c->n, 0);
-  for (int64_t i = 0; i < n; i++) {
-    const int64_t L = offs[i + 1] - offs[i];
-    if (L >= p->minseqlength && L <= maxlen) {
-      const int64_t s = cnt[kMaxLen - L]++;
-      c->perm[s] = (int32_t)i;
-      c->hlen[s] = (uint8_t)L;
+  c->bin_s.assign((size_t)nbins + 1, 0);
+  {
+    std::vector<int64_t> cnt(kMaxLen + 2, 0);
+    int64_t acc = 0;
+    for (int32_t b = 0; b < nbins; b++) {
+      c->bin_s[b] = (int32_t)acc;
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (int64_t i = c->bin_in[b]; i < c->bin_in[b + 1]; i++) {
+        const int64_t L = offs[i + 1] - offs[i];
+        if (L >= p->minseqlength && L <= maxlen) cnt[kMaxLen - L]++;
+      }
+      for (int L = 0; L <= kMaxLen; L++) {
+        const int64_t t = cnt[L];
+        cnt[L] = acc;
+        acc += t;
+      }
+      for (int64_t i = c->bin_in[b]; i < c->bin_in[b + 1]; i++) {
+        const int64_t L = offs[i + 1] - offs[i];
+        if (L >= p->minseqlength && L <= maxlen) {
+          const int64_t s = cnt[kMaxLen - L]++;
+          c->perm[s] = (int32_t)i;
+          c->hlen[s] = (uint8_t)L;
+        }
+      }
     }
+    c->bin_s[nbins] = (int32_t)acc;
   }
+  c->cno.assign(c->n, -1);
+  c->strand.assign(c->n, 0);
+  c->target.assign(c->n, -1);
+  c->ocl.assign(c->n, -1);
+  c->bout.assign(nbins, umiclust_ctx::BinOut());
+  c->cur_bin = -1;
   const int64_t bytes = n > 0 ? offs[n] - offs[0] : 0;
   c->hip(c->d_ascii.ensure((size_t)bytes + 1), "alloc ascii");
   c->hip(c->d_offs.ensure((size_t)n + 1), "alloc offs");
@@ -1181,13 +1256,79 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
 }
 
 // ---------------------------------------------------------------- FASTA I/O
+// Host threads for file I/O (the box gives a GPU process ~16 cores; UMICLUST_IO_THREADS overrides).
+int io_threads() {
+  static int n = 0;
+  if (n == 0) {
+    const char* e = getenv("UMICLUST_IO_THREADS");
+    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    n = std::max(1, std::min(v > 0 ? v : 1, 16));
+  }
+  return n;
+}
+
+// run f(t) for t in [0, T) on T threads (the caller's thread runs t = 0)
+template <typename F>
+void parallel_for(int T, F&& f) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
+  f(0);
+  for (auto& x : th) x.join();
+}
+
+// The input FASTA, memory-mapped; records are parsed by io_threads() threads, each taking the records
+// that start in its slice of the file.
 struct Fasta {
-  std::vector<char> raw;          // file contents
+  const char* data = nullptr;     // file contents (mapping)
+  size_t size = 0;
+  void* map = nullptr;
   std::vector<int64_t> hdr_off;   // label start (after '>')
   std::vector<int32_t> hdr_len;   // label length (truncated at whitespace)
   std::vector<char> seq;          // concatenated sequences
   std::vector<int64_t> seq_off;   // n+1
+  Fasta() = default;
+  Fasta(const Fasta&) = delete;
+  Fasta& operator=(const Fasta&) = delete;
+  ~Fasta() {
+    if (map) munmap(map, size);
+  }
 };
+
+struct FastaPart {
+  std::vector<int64_t> hdr_off;
+  std::vector<int32_t> hdr_len;
+  std::vector<char> seq;
+  std::vector<int64_t> seq_off;
+};
+
+// records starting in [a, b) (a is a record start or 0): headers are truncated at the first whitespace
+// (vsearch without --notrunclabels); sequence lines keep letters only; lines before the first '>' are
+// ignored
+void parse_fasta_range(const char* d, size_t a, size_t b, FastaPart& P) {
+  size_t i = a;
+  bool in = false;
+  P.seq_off.push_back(0);
+  while (i < b) {
+    const char* nl = (const char*)memchr(d + i, '\n', b - i);
+    const size_t e = nl ? (size_t)(nl - d) : b;
+    if (d[i] == '>') {
+      if (in) P.seq_off.push_back((int64_t)P.seq.size());
+      const size_t j = i + 1;
+      size_t k = j;
+      while (k < e && d[k] != '\r' && d[k] != ' ' && d[k] != '\t') k++;
+      P.hdr_off.push_back((int64_t)j);
+      P.hdr_len.push_back((int32_t)(k - j));
+      in = true;
+    } else if (in) {
+      for (size_t k = i; k < e; k++) {
+        const char ch = d[k];
+        if ((ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z')) P.seq.push_back(ch);
+      }
+    }
+    i = e + 1;
+  }
+  if (in) P.seq_off.push_back((int64_t)P.seq.size());
+}
 
 bool read_fasta(const char* path, Fasta& f) {
   int fd = open(path, O_RDONLY);
@@ -1197,47 +1338,53 @@ bool read_fasta(const char* path, Fasta& f) {
     close(fd);
     return false;
   }
-  f.raw.resize((size_t)sb.st_size + 1);
-  size_t got = 0;
-  while (got < (size_t)sb.st_size) {
-    ssize_t r = read(fd, f.raw.data() + got, (size_t)sb.st_size - got);
-    if (r <= 0) {
+  f.size = (size_t)sb.st_size;
+  if (f.size > 0) {
+    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (f.map == MAP_FAILED) {
+      f.map = nullptr;
       close(fd);
       return false;
     }
-    got += (size_t)r;
+    f.data = (const char*)f.map;
   }
   close(fd);
-  f.raw[got] = '\n';
-  const char* d = f.raw.data();
-  const size_t N = got;
-  f.seq.reserve(N / 8);
-  f.seq_off.push_back(0);
-  size_t i = 0;
-  bool in = false;
-  while (i < N) {
-    if (d[i] == '>') {
-      if (in) f.seq_off.push_back((int64_t)f.seq.size());
-      size_t j = i + 1;
-      size_t e = j;
-      while (e < N && d[e] != '\n' && d[e] != '\r' && d[e] != ' ' && d[e] != '\t') e++;
-      f.hdr_off.push_back((int64_t)j);
-      f.hdr_len.push_back((int32_t)(e - j));
-      while (e < N && d[e] != '\n') e++;
-      i = e + 1;
-      in = true;
-    } else {
-      size_t e = i;
-      while (e < N && d[e] != '\n') e++;
-      if (in)
-        for (size_t k = i; k < e; k++) {
-          const char ch = d[k];
-          if ((ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z')) f.seq.push_back(ch);
-        }
-      i = e + 1;
+  const char* d = f.data;
+  const size_t N = f.size;
+  const int T = N < (1u << 20) ? 1 : io_threads();
+  // slice starts: the first record start at or after t*N/T
+  std::vector<size_t> cut(T + 1, N);
+  cut[0] = 0;
+  for (int t = 1; t < T; t++) {
+    size_t p = std::max(cut[t - 1], N / T * t);
+    while (p < N && !(d[p] == '>' && d[p - 1] == '\n')) {
+      const char* q = (const char*)memchr(d + p, '>', N - p);
+      if (!q) { p = N; break; }
+      p = (size_t)(q - d);
+      if (d[p - 1] != '\n') p++;
     }
+    cut[t] = p;
   }
-  if (in) f.seq_off.push_back((int64_t)f.seq.size());
+  std::vector<FastaPart> parts(T);
+  parallel_for(T, [&](int t) { parse_fasta_range(d, cut[t], cut[t + 1], parts[t]); });
+  size_t nrec = 0, nseq = 0;
+  for (auto& P : parts) {
+    nrec += P.hdr_off.size();
+    nseq += P.seq.size();
+  }
+  f.hdr_off.reserve(nrec);
+  f.hdr_len.reserve(nrec);
+  f.seq.reserve(nseq);
+  f.seq_off.reserve(nrec + 1);
+  f.seq_off.push_back(0);
+  for (auto& P : parts) {
+    const int64_t base = (int64_t)f.seq.size();
+    f.hdr_off.insert(f.hdr_off.end(), P.hdr_off.begin(), P.hdr_off.end());
+    f.hdr_len.insert(f.hdr_len.end(), P.hdr_len.begin(), P.hdr_len.end());
+    f.seq.insert(f.seq.end(), P.seq.begin(), P.seq.end());
+    for (size_t r = 1; r < P.seq_off.size(); r++) f.seq_off.push_back(base + P.seq_off[r]);
+  }
+  if (f.seq_off.size() != f.hdr_off.size() + 1) return false;
   return true;
 }
 
@@ -1254,12 +1401,39 @@ void put_wrapped(std::string& out, const char* s, int64_t len, int width) {
   }
 }
 
+bool write_all(int fd, const char* p, size_t n) {
+  while (n > 0) {
+    const ssize_t w = write(fd, p, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
 bool write_file(const std::string& path, const std::string& data) {
-  FILE* fp = fopen(path.c_str(), "wb");
-  if (!fp) return false;
-  bool ok = fwrite(data.data(), 1, data.size(), fp) == data.size();
-  ok = (fclose(fp) == 0) && ok;
+  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) return false;
+  bool ok = write_all(fd, data.data(), data.size());
+  ok = (close(fd) == 0) && ok;
   return ok;
+}
+
+// clusters [0, K) split over T threads by member count
+std::vector<int32_t> cluster_slices(const std::vector<int32_t>& ostart, int32_t K, int T) {
+  std::vector<int32_t> cut(T + 1, K);
+  cut[0] = 0;
+  const int64_t tot = ostart[K];
+  int32_t k = 0;
+  for (int t = 1; t < T; t++) {
+    const int64_t want = tot * t / T;
+    while (k < K && ostart[k] < want) k++;
+    cut[t] = std::max(k, cut[t - 1]);
+  }
+  return cut;
 }
 
 // ---------------------------------------------------------------- in-process parse (§8f f2)
@@ -1326,7 +1500,7 @@ void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp
     int64_t seen[2] = {0, 0}, found = 0;
     for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {  // cluster<N> file order (:36)
       const int32_t i = c->perm[c->omemb[x]];
-      const Sv name{f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]};
+      const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
       split_fields(name, fields);
       if (fields.size() != 7)  // :38-47
         c->fail(UMICLUST_EFORMAT, "cluster %d: header has %d cols while it should contain 7: %s", k,
@@ -1383,7 +1557,7 @@ void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp
       for (int64_t y = 0; y < w_all; y++) {
         const auto& e = y < w_fwd ? kept[0][y] : kept[1][y - w_fwd];
         const int32_t i = e.second;
-        split_fields(Sv{f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]}, fields);
+        split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, fields);
         Sv read;
         if (!split1(fields[6], "seq=", read)) c->fail(UMICLUST_EFORMAT, "no seq= field in record %d", i);
         lines.push_back('>');
@@ -1408,7 +1582,8 @@ void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp
     // the reference's quirk (:206, :219-221): the totals are overwritten by this cluster's counts, then doubled
     reads_found = 2 * found;
     reads_written = 2 * w_all;
-    if (pp->max_clusters > 0 && n_written > pp->max_clusters) break;  // :222-223
+    // `if max_clusters and n_written > max_clusters` (:222-223): any non-zero value applies, as in Python
+    if (pp->max_clusters != 0 && n_written > pp->max_clusters) break;
   }
   if (!write_file(pjoin(work_dir, "vsearch_cluster_stats.tsv"), stats_out))
     c->fail(UMICLUST_EIO, "cannot write the stats table");
@@ -1441,45 +1616,64 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   }
   const double t_read = now_s() - t0;
   load_impl(c, p, f.seq.data(), f.seq_off.data(), n);
-  cluster_all(c);
+  if (c->bin_s.size() != 2) c->fail(UMICLUST_EINVAL, "file path: one bin per load");
+  cluster_all(c, 0);
   const double t1 = now_s();
-  // masked sequences (vsearch prints the DUST-masked db sequence)
-  std::vector<char> masked((size_t)c->n * kMaxLen);
-  if (c->n > 0)
-    c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
   const int32_t K = c->nclusters;
   const int width = p->fasta_width;
+  // both writers build and write disjoint cluster ranges on io_threads() threads
+  const int T = K < 256 ? 1 : io_threads();
+  const std::vector<int32_t> cut = cluster_slices(c->ostart, K, T);
   if (consout) {
-    std::string out;
-    out.reserve((size_t)K * 256);
-    for (int32_t k = 0; k < K; k++) {
-      const int32_t cs = c->omemb[c->ostart[k]];
-      const int32_t ci = c->perm[cs];
-      out += ">centroid=";
-      out.append(f.raw.data() + f.hdr_off[ci], (size_t)f.hdr_len[ci]);
-      out += ";seqs=" + std::to_string(c->ostart[k + 1] - c->ostart[k]);
-      if (p->clusterout_id) out += ";clusterid=" + std::to_string(k);
-      out.push_back('\n');
-      put_wrapped(out, c->cons.data() + c->cons_off[k], c->cons_off[k + 1] - c->cons_off[k], width);
-    }
-    if (!write_file(consout, out)) c->fail(UMICLUST_EIO, "cannot write %s", consout);
+    std::vector<std::string> part(T);
+    parallel_for(T, [&](int t) {
+      std::string& out = part[t];
+      out.reserve((size_t)(cut[t + 1] - cut[t]) * 256);
+      for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
+        const int32_t cs = c->omemb[c->ostart[k]];
+        const int32_t ci = c->perm[cs];
+        out += ">centroid=";
+        out.append(f.data + f.hdr_off[ci], (size_t)f.hdr_len[ci]);
+        out += ";seqs=" + std::to_string(c->ostart[k + 1] - c->ostart[k]);
+        if (p->clusterout_id) out += ";clusterid=" + std::to_string(k);
+        out.push_back('\n');
+        put_wrapped(out, c->cons.data() + c->cons_off[k], c->cons_off[k + 1] - c->cons_off[k], width);
+      }
+    });
+    const int fd = open(consout, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    bool ok = fd >= 0;
+    for (int t = 0; ok && t < T; t++) ok = write_all(fd, part[t].data(), part[t].size());
+    if (fd >= 0) ok = (close(fd) == 0) && ok;
+    if (!ok) c->fail(UMICLUST_EIO, "cannot write %s", consout);
   }
   if (clusters_prefix) {
-    std::string fn, out;
-    for (int32_t k = 0; k < K; k++) {
-      out.clear();
-      for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {
-        const int32_t s = c->omemb[x];
-        const int32_t i = c->perm[s];
-        out.push_back('>');
-        out.append(f.raw.data() + f.hdr_off[i], (size_t)f.hdr_len[i]);
-        out.push_back('\n');
-        put_wrapped(out, masked.data() + (size_t)s * kMaxLen, c->hlen[s], width);
+    // masked sequences (vsearch prints the DUST-masked db sequence): only the cluster<N> files need them
+    std::vector<char> masked((size_t)c->n * kMaxLen);
+    if (c->n > 0)
+      c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
+    std::vector<int32_t> bad(T, -1);
+    parallel_for(T, [&](int t) {
+      std::string fn, out;
+      for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
+        out.clear();
+        for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {
+          const int32_t s = c->omemb[x];
+          const int32_t i = c->perm[s];
+          out.push_back('>');
+          out.append(f.data + f.hdr_off[i], (size_t)f.hdr_len[i]);
+          out.push_back('\n');
+          put_wrapped(out, masked.data() + (size_t)s * kMaxLen, c->hlen[s], width);
+        }
+        fn = clusters_prefix;
+        fn += std::to_string(k);
+        if (!write_file(fn, out)) {
+          bad[t] = k;
+          return;
+        }
       }
-      fn = clusters_prefix;
-      fn += std::to_string(k);
-      if (!write_file(fn, out)) c->fail(UMICLUST_EIO, "cannot write %s", fn.c_str());
-    }
+    });
+    for (int t = 0; t < T; t++)
+      if (bad[t] >= 0) c->fail(UMICLUST_EIO, "cannot write %s%d", clusters_prefix, bad[t]);
   }
   const double t_write = now_s() - t1;
   if (log_path) {
@@ -1514,6 +1708,9 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
     if (!write_file(log_path, buf)) c->fail(UMICLUST_EIO, "cannot write %s", log_path);
   }
   if (pp) parse_impl(c, f, pp, work_dir, pr);
+  c->stats.t_read_s = t_read;
+  c->stats.t_write_s = t_write + (pp ? now_s() - t1 - t_write : 0.0);
+  c->stats.t_run_s = now_s() - t0;
   if (stats) *stats = c->stats;
   return K;
 }
@@ -1794,7 +1991,8 @@ int32_t umiclust_load(umiclust_ctx* c, const umiclust_params* p, const char* seq
 int64_t umiclust_cluster(umiclust_ctx* c, umiclust_stats* stats) {
   UC_GUARD(c, {
     if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster before umiclust_load");
-    cluster_all(c);
+    if (c->bin_s.size() != 2) c->fail(UMICLUST_EINVAL, "umiclust_cluster: the load holds several bins");
+    cluster_all(c, 0);
     if (stats) *stats = c->stats;
     return c->nclusters;
   });
@@ -1802,27 +2000,58 @@ int64_t umiclust_cluster(umiclust_ctx* c, umiclust_stats* stats) {
 
 int64_t umiclust_fetch(umiclust_ctx* c, int32_t* cluster, uint8_t* strand, uint8_t* centroid, char* cons,
                        int64_t cons_cap, int64_t* cons_off) {
+  if (!c) return UMICLUST_EINVAL;
+  if (c->bin_s.size() != 2) {
+    c->err = "umiclust_fetch: the load holds several bins (umiclust_fetch_bin)";
+    return UMICLUST_EINVAL;
+  }
+  return umiclust_fetch_bin(c, 0, cluster, strand, centroid, cons, cons_cap, cons_off);
+}
+
+int64_t umiclust_fetch_bin(umiclust_ctx* c, int32_t bin, int32_t* cluster, uint8_t* strand, uint8_t* centroid,
+                           char* cons, int64_t cons_cap, int64_t* cons_off) {
   UC_GUARD(c, {
-    if (!c->clustered) c->fail(UMICLUST_ESTATE, "umiclust_fetch before umiclust_cluster");
-    const int64_t n = c->n_input;
+    if (!c->loaded || bin < 0 || bin >= (int32_t)c->bout.size())
+      c->fail(c->loaded ? UMICLUST_EINVAL : UMICLUST_ESTATE, "umiclust_fetch_bin: no such bin");
+    const auto& bo = c->bout[bin];
+    if (!bo.done) c->fail(UMICLUST_ESTATE, "umiclust_fetch_bin before the bin was clustered");
+    const int64_t i0 = c->bin_in[bin], n = c->bin_in[bin + 1] - i0;
     if (cluster)
       for (int64_t i = 0; i < n; i++) cluster[i] = -1;
     if (strand) memset(strand, 0, (size_t)n);
     if (centroid) memset(centroid, 0, (size_t)n);
-    for (int32_t s = 0; s < c->n; s++) {
-      const int32_t i = c->perm[s];
-      if (cluster) cluster[i] = c->rank_of[c->cno[s]];
+    for (int32_t s = c->bin_s[bin]; s < c->bin_s[bin + 1]; s++) {
+      const int64_t i = c->perm[s] - i0;
+      if (cluster) cluster[i] = c->ocl[s];
       if (strand) strand[i] = c->strand[s];
       if (centroid) centroid[i] = c->target[s] < 0 ? 1 : 0;
     }
-    const int32_t K = c->nclusters;
+    const int32_t K = bo.K;
     if (cons_off)
-      for (int32_t k = 0; k <= K; k++) cons_off[k] = c->cons_off[k];
+      for (int32_t k = 0; k <= K; k++) cons_off[k] = bo.cons_off[k];
     if (cons) {
-      if ((int64_t)c->cons.size() > cons_cap) c->fail(UMICLUST_EINVAL, "consensus buffer too small");
-      memcpy(cons, c->cons.data(), c->cons.size());
+      if ((int64_t)bo.cons.size() > cons_cap) c->fail(UMICLUST_EINVAL, "consensus buffer too small");
+      memcpy(cons, bo.cons.data(), bo.cons.size());
     }
     return K;
+  });
+}
+
+int32_t umiclust_load_bins(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs,
+                           int64_t n, const int64_t* bin_start, int32_t nbins) {
+  UC_GUARD(c, {
+    if (!bin_start || nbins < 1) c->fail(UMICLUST_EINVAL, "bin boundaries");
+    load_impl(c, p, seqs, offs, n, bin_start, nbins);
+    return UMICLUST_OK;
+  });
+}
+
+int64_t umiclust_cluster_bin(umiclust_ctx* c, int32_t bin, umiclust_stats* stats) {
+  UC_GUARD(c, {
+    if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster_bin before umiclust_load_bins");
+    cluster_all(c, bin);
+    if (stats) *stats = c->stats;
+    return c->nclusters;
   });
 }
 

@@ -22,6 +22,22 @@
 
 namespace uc {
 
+// ------------------------------------------------------------------ per-device launch attributes
+// hipFuncSetAttribute acts on the current device; one process may hold contexts on several GPUs
+// (vsearch_umi_cluster.context(device)), so the "already set" flags are kept per device.
+enum { k_attr_prefilter = 0, k_attr_consensus = 1, k_attr_count = 2 };
+constexpr int kAttrDevices = 64;
+static bool g_attr_set[kAttrDevices][k_attr_count];
+static bool attr_set_on_device(int which) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kAttrDevices) return false;  // set it every time
+  return g_attr_set[d][which];
+}
+static void mark_attr_set(int which) {
+  int d = 0;
+  if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kAttrDevices) g_attr_set[d][which] = true;
+}
+
 // ------------------------------------------------------------------ character maps
 // 4-bit IUPAC code (vsearch chrmap_4bit): A1 C2 G4 T/U8, ambiguity codes OR-ed, N15.
 __constant__ uint8_t c_map4[256];
@@ -1004,12 +1020,11 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
+  if (!attr_set_on_device(k_attr_prefilter)) {
     const int most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
     hipError_t e = hipFuncSetAttribute((const void*)k_prefilter, hipFuncAttributeMaxDynamicSharedMemorySize, most);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    mark_attr_set(k_attr_prefilter);
   }
   // LDS: the fixed part + counters for the peer regions, the spares and one segment's centroids
   const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
@@ -1064,7 +1079,8 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint32_t* __restrict__ res, const uint8_t* __restrict__ acc_tab,
                        const uint16_t* __restrict__ rank_tab, WalkState* __restrict__ ws,
                        uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
-                       uint32_t* __restrict__ outidx, uint32_t* __restrict__ npairs) {
+                       uint32_t* __restrict__ outidx, uint32_t* __restrict__ npairs,
+                       uint32_t* __restrict__ tsum) {
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   if (qs >= nqs) return;
   const int32_t q = q0 + qs / both;
@@ -1108,12 +1124,16 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
   if (!w.done) {
     const int b0 = w.w, b1 = min(nt, b0 + kBatch);
     const uint32_t base = atomicAdd(npairs, (uint32_t)(b1 - b0));
+    uint32_t tl = 0;
     for (int x = b0; x < b1; x++) {
       const uint32_t k = base + (uint32_t)(x - b0);
+      const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
       pq[k] = ((uint32_t)q << 1) | strand;
-      pt[k] = top_seqno[(int64_t)qs * kTopHits + x];
+      pt[k] = t;
       outidx[k] = (uint32_t)qs * kWalk + (uint32_t)x;
+      tl += lens[t];
     }
+    atomicAdd(tsum, tl);  // target residues of the pairs emitted (cells computed = qlen * this)
   }
 }
 
@@ -1121,11 +1141,11 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
-                       uint32_t* outidx, uint32_t* npairs, hipStream_t st) {
+                       uint32_t* outidx, uint32_t* npairs, uint32_t* tsum, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_walk, dim3((nqs + 255) / 256), dim3(256), 0, st, round, q0, nqs, both,
                      top_seqno, top_count, ntop, lens, res, acc_tab, rank_tab, ws, pq, pt, outidx,
-                     npairs);
+                     npairs, tsum);
   return hipGetLastError();
 }
 
@@ -1147,7 +1167,7 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* __restrict__ ws, const uint16_t* __restrict__ peer_id,
                              const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
                              uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
-                             uint32_t* __restrict__ npairs) {
+                             uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum) {
   // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
   // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1163,22 +1183,26 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
   if (!rel) return;
   uint32_t k = atomicAdd(npairs, (uint32_t)__builtin_popcountll(rel));
   const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  uint32_t tl = 0;
   for (int x = 0; x < np; x++)
     if ((rel >> x) & 1ull) {
+      const uint32_t t = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       pq[k] = qv;
-      pt[k] = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
+      pt[k] = t;
       outidx[k] = (uint32_t)(qs * kPeerCap + x);
+      tl += lens[t];
       k++;
     }
+  atomicAdd(tsum, tl);
 }
 
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             hipStream_t st) {
+                             uint32_t* tsum, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, npairs);
+                     peer_count, npeer, pq, pt, outidx, npairs, tsum);
   return hipGetLastError();
 }
 
@@ -1437,12 +1461,11 @@ hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t ncl
                             int32_t* overflow, hipStream_t st) {
   if (nclusters <= 0) return hipSuccess;
   const size_t smem = sizeof(ConsShared);
-  static bool attr_set = false;
-  if (!attr_set) {
+  if (!attr_set_on_device(k_attr_consensus)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_consensus,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    mark_attr_set(k_attr_consensus);
   }
   hipLaunchKernelGGL(k_consensus, dim3(nclusters), dim3(kConsThreads), smem, st, s, cstart,
                      nclusters, member_seqno, member_opsidx, member_strand, ops, nops, cons,

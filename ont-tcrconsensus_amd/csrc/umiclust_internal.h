@@ -136,8 +136,8 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
                         const uint32_t* dev_npairs, const uint32_t* outidx, const Scoring& sc,
                         uint32_t* out, hipStream_t st);
 
-constexpr int kTabL = 2 * kMaxLen + 1;  // internal alignment length 0..144
-constexpr int kTabM = kMaxLen + 1;      // matches 0..72
+constexpr int kTabL = 2 * kMaxLen + 1;  // internal alignment length 0..2*kMaxLen
+constexpr int kTabM = kMaxLen + 1;      // matches 0..kMaxLen
 struct WalkState {
   unsigned long long lastkey;  // key of the last walked candidate
   uint32_t best_t;             // best accepted target seqno
@@ -153,11 +153,12 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
-                       uint32_t* outidx, uint32_t* npairs, hipStream_t st);
+                       uint32_t* outidx, uint32_t* npairs, uint32_t* tsum, hipStream_t st);
+// tsum accumulates the target lengths of the pairs emitted (cells computed = qlen * sum)
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             hipStream_t st);
+                             uint32_t* tsum, hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
 constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {

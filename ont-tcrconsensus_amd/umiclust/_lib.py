@@ -73,6 +73,9 @@ class Stats(C.Structure):
         ("t_host_pass1_s", C.c_double),
         ("n_merged_walks", C.c_int64),
         ("t_merged_s", C.c_double),
+        ("t_read_s", C.c_double),
+        ("t_write_s", C.c_double),
+        ("t_run_s", C.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -96,7 +99,8 @@ class ParseResult(C.Structure):
 EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
-    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_align_pairs", "umiclust_prep",
+    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin",
+    "umiclust_fetch_bin", "umiclust_align_pairs", "umiclust_prep",
 ]
 
 _lib = None
@@ -138,6 +142,14 @@ def lib() -> C.CDLL:
     L.umiclust_fetch.restype = C.c_int64
     L.umiclust_fetch.argtypes = [C.c_void_p, P(C.c_int32), P(C.c_uint8), P(C.c_uint8), C.c_void_p, C.c_int64,
                                  P(C.c_int64)]
+    L.umiclust_load_bins.restype = C.c_int32
+    L.umiclust_load_bins.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64),
+                                     C.c_int32]
+    L.umiclust_cluster_bin.restype = C.c_int64
+    L.umiclust_cluster_bin.argtypes = [C.c_void_p, C.c_int32, P(Stats)]
+    L.umiclust_fetch_bin.restype = C.c_int64
+    L.umiclust_fetch_bin.argtypes = [C.c_void_p, C.c_int32, P(C.c_int32), P(C.c_uint8), P(C.c_uint8), C.c_void_p,
+                                     C.c_int64, P(C.c_int64)]
     L.umiclust_align_pairs.restype = C.c_int32
     L.umiclust_align_pairs.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_void_p, P(C.c_int64),
                                        C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_int32,
@@ -246,6 +258,7 @@ class Context:
         n = len(off) - 1
         self._check(lib().umiclust_load(self._h, C.byref(p), buf.ctypes.data, _i64(off), n), "load")
         self._n = n
+        self._bins = None
 
     def cluster(self) -> dict:
         st = Stats()
@@ -253,18 +266,42 @@ class Context:
         return st.as_dict()
 
     def fetch(self) -> dict:
-        n = self._n
+        return self.fetch_bin(0) if getattr(self, "_bins", None) is not None else self._fetch(None, self._n)
+
+    def load_bins(self, p: Params, buf: np.ndarray, off: np.ndarray, bin_start) -> None:
+        """Many region bins resident at once: bin b = records [bin_start[b], bin_start[b+1])."""
+        bs = np.ascontiguousarray(bin_start, np.int64)
+        n = len(off) - 1
+        self._check(lib().umiclust_load_bins(self._h, C.byref(p), buf.ctypes.data, _i64(off), n, _i64(bs),
+                                             len(bs) - 1), "load_bins")
+        self._n = n
+        self._bins = bs
+
+    def cluster_bin(self, b: int) -> dict:
+        st = Stats()
+        self._check(lib().umiclust_cluster_bin(self._h, b, C.byref(st)), "cluster_bin")
+        return st.as_dict()
+
+    def fetch_bin(self, b: int) -> dict:
+        bs = getattr(self, "_bins", None)
+        n = int(bs[b + 1] - bs[b]) if bs is not None else self._n
+        return self._fetch(b, n)
+
+    def _fetch(self, b, n: int) -> dict:
         cl = np.empty(max(n, 1), np.int32)
         sd = np.empty(max(n, 1), np.uint8)
         ce = np.empty(max(n, 1), np.uint8)
-        k = self._check(lib().umiclust_fetch(self._h, None, None, None, None, 0, None), "fetch")
-        off = np.zeros(k + 1, np.int64)
-        self._check(lib().umiclust_fetch(self._h, None, None, None, None, 0, _i64(off)), "fetch")
-        cons = np.zeros(int(off[-1]) + 1, np.uint8)
         P = C.POINTER
-        self._check(lib().umiclust_fetch(self._h, cl.ctypes.data_as(P(C.c_int32)), sd.ctypes.data_as(P(C.c_uint8)),
-                                         ce.ctypes.data_as(P(C.c_uint8)), cons.ctypes.data, len(cons), _i64(off)),
-                    "fetch")
+        if b is None:
+            f = lambda *a: lib().umiclust_fetch(self._h, *a)  # noqa: E731
+        else:
+            f = lambda *a: lib().umiclust_fetch_bin(self._h, b, *a)  # noqa: E731
+        k = self._check(f(None, None, None, None, 0, None), "fetch")
+        off = np.zeros(k + 1, np.int64)
+        self._check(f(None, None, None, None, 0, _i64(off)), "fetch")
+        cons = np.zeros(int(off[-1]) + 1, np.uint8)
+        self._check(f(cl.ctypes.data_as(P(C.c_int32)), sd.ctypes.data_as(P(C.c_uint8)),
+                      ce.ctypes.data_as(P(C.c_uint8)), cons.ctypes.data, len(cons), _i64(off)), "fetch")
         raw = cons.tobytes()
         return dict(n_clusters=int(k), cluster=cl[:n], strand=sd[:n], centroid=ce[:n],
                     consensus=[raw[off[c]:off[c + 1]].decode() for c in range(k)])

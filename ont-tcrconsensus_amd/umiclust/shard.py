@@ -69,6 +69,21 @@ def run_bins(bins: Sequence[tuple[str, str]], worker: Callable[[str, str], dict]
     return out
 
 
+def hip_worker(round_: int = 1, identity: float | None = None, min_len: int = 58, max_len: int = 68):
+    """The per-bin worker on this process's GPU: the reference's exact vsearch argv for the round
+    (vsearch_umi_cluster.py:22-53 / :72-96) through umiclust_run_argv; returns the bin's stats."""
+    from . import vsearch_umi_cluster as v
+    ident = identity if identity is not None else (0.93 if round_ == 1 else 0.97)
+    fn = v.round1_argv if round_ == 1 else v.round2_argv
+
+    def worker(fa, out):
+        os.makedirs(out, exist_ok=True)
+        st = v.context().run_argv(fn(fa, out, 1, min_len, max_len, ident))
+        return dict(n_kept=int(st["n_kept"]), n_clusters=int(st["n_clusters"]), cells=int(st["cells"]),
+                    seconds=float(st["t_run_s"]))
+    return worker
+
+
 def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", type=int, default=1, choices=(1, 2))
@@ -84,14 +99,7 @@ def _main():
     if world > 1:
         dist.init_process_group(backend="gloo")  # host objects only: the data path has no collective
     os.environ.setdefault("UMICLUST_DEVICE", os.environ.get("LOCAL_RANK", "0"))
-    from . import vsearch_umi_cluster as v
-    ident = a.identity if a.identity is not None else (0.93 if a.round == 1 else 0.97)
-    fn = v.round1_argv if a.round == 1 else v.round2_argv
-
-    def worker(fa, out):
-        os.makedirs(out, exist_ok=True)
-        return v.context().run_argv(fn(fa, out, 1, a.min_len, a.max_len, ident))
-
+    worker = hip_worker(a.round, a.identity, a.min_len, a.max_len)
     bins = [tuple(b.split(":", 1)) for b in a.bins]
     res = run_bins(bins, worker, rank, world, gather=dist.all_gather_object if world > 1 else None)
     if rank == 0:

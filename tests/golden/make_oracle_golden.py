@@ -8,7 +8,9 @@ Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py [conf
 import hashlib
 import json
 import os
+import platform
 import sys
+import time
 
 import numpy as np
 
@@ -30,6 +32,9 @@ def digest(res: dict) -> dict:
 CASES = {
     # name: (config, scale, preset, identity)
     "config1_round1_id093": (1, 1.0, 1, 0.93),
+    # the headline bin (BASELINE config 2, 2M reads, id 0.90) at full size; its wall time is also the
+    # full-bin CPU baseline (1 thread, recorded with the host CPU model)
+    "config2_round1_id090": (2, 1.0, 1, 0.90),
     "config1_round1_id090": (1, 1.0, 1, 0.90),
     "config1_round2_id097": (1, 1.0, 2, 0.97),
     # config 5: at id 0.75 the deep clusters form (2 clusters > 1k members at scale 0.1); at id 0.90
@@ -38,6 +43,61 @@ CASES = {
     "config5_round1_id090": (5, 0.02, 1, 0.90),
     "config5_round2_id075": (5, 0.02, 2, 0.75),
 }
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+# multi-bin BASELINE configs at reduced scale: every bin clustered by the oracle, a checksum of the per-bin
+# digests (membership, strands, centroids, consensus) per round; config 4 chains round 2 on the round-1
+# consensus UMIs of every bin (umiclust.binset.round2_binset)
+MULTIBIN_CASES = {
+    # name: (config, scale)
+    "config3_bins_s001": (3, 0.01),
+    "config4_rounds_s0002": (4, 0.002),
+}
+
+
+def multibin_golden(cfg: int, scale: float) -> dict:
+    import orc
+    from umiclust import binset, synth
+    lo, hi = synth.CONFIG_LENGTHS[cfg]
+    bs = synth.concat_bins(synth.config_bins(cfg, scale, workers=4))
+    out = dict(config=cfg, scale=scale, n_bins=len(bs.bins), n_reads=int(bs.n), minlen=lo, maxlen=hi)
+    rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if cfg == 4 else [])
+    t0 = time.perf_counter()
+    for name, prm in rounds:
+        op = orc.params(prm["preset"], prm["identity"], lo, hi)
+        res, alignments, cells = [], 0, 0
+        for b in bs.bins:
+            r = orc.cluster(op, b.umis.as_list())
+            res.append(r)
+            alignments += r["stats"]["alignments"]
+            cells += r["stats"]["cells"]
+        dg = [binset.digest(r) for r in res]
+        out[name] = dict(preset=prm["preset"], identity=prm["identity"], n_reads=int(bs.n),
+                         combined=binset.combine(dg), n_clusters=[d["n_clusters"] for d in dg],
+                         alignments=alignments, cells=cells)
+        print(name, out[name]["combined"], sum(out[name]["n_clusters"]), flush=True)
+        if name == "round1" and len(rounds) > 1:
+            bs = binset.round2_binset(bs, res)
+    out.update(oracle_seconds=round(time.perf_counter() - t0, 2), oracle_threads=1, host_cpu=_cpu_model())
+    return out
+
+
+def main_multibin(names):
+    for name in names:
+        cfg, scale = MULTIBIN_CASES[name]
+        d = multibin_golden(cfg, scale)
+        with open(os.path.join(HERE, f"oracle_{name}.json"), "w") as f:
+            json.dump({name: d}, f, indent=1, sort_keys=True)
 
 
 def main(configs):
@@ -49,11 +109,14 @@ def main(configs):
             continue
         lo, hi = synth.CONFIG_LENGTHS[cfg]
         seqs = synth.config_umis(cfg, scale).as_list()
+        t0 = time.perf_counter()
         r = orc.cluster(orc.params(preset, idn, lo, hi), seqs)
+        dt = time.perf_counter() - t0
         d = digest(r)
         d.update(config=cfg, scale=scale, preset=preset, identity=idn, minlen=lo, maxlen=hi, n_reads=len(seqs),
                  alignments=r["stats"]["alignments"], cells=r["stats"]["cells"],
-                 max_cluster=int(np.bincount(np.asarray(r["cluster"])).max()) if len(seqs) else 0)
+                 max_cluster=int(np.bincount(np.asarray(r["cluster"])).max()) if len(seqs) else 0,
+                 oracle_seconds=round(dt, 2), oracle_threads=1, host_cpu=_cpu_model())
         out.setdefault(cfg, {})[name] = d
         print(name, d, flush=True)
     for cfg, cases in out.items():
@@ -62,4 +125,8 @@ def main(configs):
 
 
 if __name__ == "__main__":
-    main([int(a) for a in sys.argv[1:]] or sorted({c[0] for c in CASES.values()}))
+    args = sys.argv[1:]
+    if args and args[0] == "multibin":
+        main_multibin(args[1:] or sorted(MULTIBIN_CASES))
+    else:
+        main([int(a) for a in args] or sorted({c[0] for c in CASES.values()}))

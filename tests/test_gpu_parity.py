@@ -56,7 +56,7 @@ def _pairs(seed, n, qlens, tl_lo=16, tl_hi=72, ambig=False):
 
 @pytest.mark.parametrize("preset,ambig,hi", [(1, False, 72), (2, False, 72), (1, True, 72), (2, True, 72),
                                              (1, False, _lib.MAX_LEN), (2, False, _lib.MAX_LEN),
-                                             (1, True, _lib.MAX_LEN)])
+                                             (1, True, _lib.MAX_LEN), (2, True, _lib.MAX_LEN)])
 def test_align_pairs_vs_oracle(gpu_ctx, preset, ambig, hi):
     """Every query length 32..hi (one kernel instantiation each), targets 16..hi."""
     p = _lib.params(preset, 0.93, 32, hi)
@@ -360,7 +360,41 @@ def _golden_cases():
     for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
                                               "oracle_config*.json"))):
         out.update(json.load(open(path)))
-    return sorted(out.items())
+    return sorted((k, v) for k, v in out.items() if "n_bins" not in v)
+
+
+def _multibin_cases():
+    import glob
+    import json
+    out = {}
+    for path in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                              "oracle_config*.json"))):
+        out.update(json.load(open(path)))
+    return sorted((k, v) for k, v in out.items() if "n_bins" in v)
+
+
+@pytest.mark.parametrize("name,gold", _multibin_cases(), ids=[n for n, _ in _multibin_cases()])
+def test_multibin_vs_oracle_golden(name, gold):
+    """BASELINE configs 3 (24 barcodes x 40 Zipf bins) and 4 (both rounds, round 2 on the round-1 consensus
+    UMIs) at reduced scale: every bin resident in one load, clustered bin by bin; the checksum of the per-bin
+    digests (membership, strands, centroids, consensus) and every bin's cluster count equal the oracle's."""
+    from umiclust import binset, synth
+    bs = synth.concat_bins(synth.config_bins(gold["config"], gold["scale"], workers=4))
+    assert len(bs.bins) == gold["n_bins"] and bs.n == gold["n_reads"]
+    rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if "round2" in gold else [])
+    for rname, prm in rounds:
+        g = gold[rname]
+        with _lib.Context(0) as ctx:
+            run = binset.BinRunner(ctx, bs, prm["preset"], prm["identity"], gold["minlen"], gold["maxlen"])
+            st = run.cluster_all()
+            res = run.results()
+        assert bs.n == g["n_reads"]
+        dg = [binset.digest(r) for r in res]
+        assert [d["n_clusters"] for d in dg] == g["n_clusters"], rname
+        assert sum(x["n_alignments"] for x in st) == g["alignments"] and sum(x["cells"] for x in st) == g["cells"]
+        assert binset.combine(dg) == g["combined"], rname
+        if rname == "round1":
+            bs = binset.round2_binset(bs, res)
 
 
 @pytest.mark.parametrize("name,gold", _golden_cases(), ids=[n for n, _ in _golden_cases()])
@@ -379,3 +413,22 @@ def test_config_vs_oracle_golden(gpu_ctx, name, gold):
     assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
     for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
         assert d[k] == gold[k], k
+
+
+def test_load_bins_edge_cases(gpu_ctx):
+    """umiclust_load_bins: empty bins, bins whose every record is length-filtered, one-record bins and
+    ordinary bins in one load; each bin equals the oracle run on that bin alone, in any clustering order."""
+    base = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
+    groups = [[], ["ACGT", "ACGTACGT"], [base], synth.make_umis(40, seed=61, max_reads=500, orient_mix=0.2).as_list(),
+              [], synth.make_umis(25, seed=62, max_reads=300).as_list(), [base[:57], base + "A" * 5]]
+    buf, off = _lib._pack([s for g in groups for s in g])
+    starts = np.cumsum([0] + [len(g) for g in groups])
+    op = orc.params(1, 0.93, 58, 68)
+    gpu_ctx.load_bins(_lib.params(1, 0.93, 58, 68), buf, off, starts)
+    for b in [5, 0, 3, 1, 6, 2, 4]:  # out of order: bins are independent
+        gpu_ctx.cluster_bin(b)
+    for b, g in enumerate(groups):
+        got = gpu_ctx.fetch_bin(b)
+        want = orc.cluster(op, g) if g else dict(n_clusters=0, cluster=np.zeros(0, np.int32), strand=np.zeros(0, np.uint8),
+                                                centroid=np.zeros(0, np.uint8), consensus=[])
+        _cmp_cluster(got, want)

@@ -28,8 +28,16 @@ def test_lpt_balances():
     assert abs(loads[0] - loads[1]) <= 1
 
 
-def _make_bins(tmp):
+def _make_bins(tmp, kind="small"):
     bins = []
+    if kind == "config3":
+        # BASELINE config 3's bin structure (Zipf(1.1) sizes over 40 region bins) for two barcodes, scaled
+        # down so the oracle worker runs in seconds
+        for b in synth.config_bins(3, 0.002, barcodes=[0, 5]):
+            fa = os.path.join(tmp, f"bc{b.barcode}_region{b.region}.fasta")
+            synth.write_umi_fasta(fa, b.umis)
+            bins.append(fa)
+        return bins
     for b in range(5):
         u = synth.make_umis(20 + 10 * b, seed=500 + b, max_reads=200 + 100 * b)
         fa = os.path.join(tmp, f"bin{b}.fasta")
@@ -68,10 +76,11 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_matches_single_rank(tmp_path):
+@pytest.mark.parametrize("kind", ["small", "config3"])
+def test_two_rank_gloo_matches_single_rank(tmp_path, kind):
     import json
     tmp = str(tmp_path)
-    bins = _make_bins(tmp)
+    bins = _make_bins(tmp, kind)
     res1 = run_bins([(fa, f"bin{i}") for i, fa in enumerate(bins)], _worker_factory(os.path.join(tmp, "w1")))
     mp.spawn(_rank_main, args=(2, _free_port(), tmp, bins), nprocs=2, join=True)
     res2 = json.load(open(os.path.join(tmp, "res2.json")))
@@ -81,3 +90,16 @@ def test_two_rank_gloo_matches_single_rank(tmp_path):
         assert sorted(os.listdir(d1)) == sorted(os.listdir(d2))
         for fn in os.listdir(d1):
             assert open(os.path.join(d1, fn), "rb").read() == open(os.path.join(d2, fn), "rb").read()
+
+
+def test_config3_lpt_plan_is_balanced():
+    """The Zipf(1.1) bin mix of config 3 on 2/4/8 ranks: every bin once, and the LPT makespan within the
+    classic 4/3 bound of the ideal (sum / world, or the largest bin)."""
+    sizes = synth.zipf_bin_sizes(10_000_000).ravel()
+    costs = [bin_cost(int(n)) for n in sizes]
+    for world in (2, 4, 8):
+        plan = lpt_assign(costs, world)
+        assert sorted(i for p in plan for i in p) == list(range(len(costs)))
+        span = max(sum(costs[i] for i in p) for p in plan)
+        ideal = max(sum(costs) / world, max(costs))
+        assert span <= 4 / 3 * ideal

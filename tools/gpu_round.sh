@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU-box session: parity tests, then bench legs; every step under its own time limit, chained with &&
+# so the first failure (or fault / timeout) ends the call.
+# Usage: bash tools/gpu_round.sh <tag> <steps...>   steps: tests | c2 | c3 | c4 | c5 | e2e | trace
+set -o pipefail
+tag=${1:-run}
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+rc=0
+for st in "$@"; do
+  echo "== $st $(date +%T)"
+  case $st in
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             > "$out/tests.log" 2>&1; rc=$?; tail -3 "$out/tests.log" ;;
+    c2) timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$out/c2.json" 2> "$out/c2.err"; rc=$? ;;
+    c3) timeout -k 10 400 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
+    c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
+    c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
+    e2e) timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e > "$out/e2e.json" 2> "$out/e2e.err"; rc=$? ;;
+    trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
+             python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$out/trace.log" 2>&1; rc=$? ;;
+    *) echo "unknown step $st"; rc=2 ;;
+  esac
+  echo "== $st rc=$rc $(date +%T)"
+  [ $rc -ne 0 ] && break
+done
+for f in "$out"/*.json; do [ -f "$f" ] && { echo "--- $f"; cut -c1-600 "$f"; }; done
+exit $rc
