@@ -115,7 +115,7 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
     g_alg = cells / t_al / 1e9 if t_al else 0.0
     g_cmp = cells_c / t_al / 1e9 if t_al else 0.0
     ceiling = VALU_LANE_OPS / ALIGN_VALU_PER_CELL / 1e9
-    align = dict(kernel="k_align_pk", bound="valu", seconds=t_al, cells=cells, cells_computed=cells_c,
+    align = dict(kernel="k_align_pk", bound="valu", seconds_total=t_al, cells=cells, cells_computed=cells_c,
                  gcups_kernel=g_alg, gcups_computed=g_cmp, valu_per_cell=ALIGN_VALU_PER_CELL,
                  ceiling_gcups=ceiling, frac=g_alg / ceiling, frac_computed=g_cmp / ceiling,
                  speculative_ratio=cells_c / cells if cells else None)
@@ -140,6 +140,8 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time FASTA read -> cluster -> files written")
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="configs 3/4: bins clustered concurrently per GPU (one device context per lane)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -201,14 +203,15 @@ def main() -> None:
         def step():
             return [ctx.cluster()]
     else:
-        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens)
+        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens, lanes=args.lanes, device=local_rank)
         runners.append(r1)
         if args.config == 4:
             # round-2 inputs come from the round-1 results (deterministic): built once, resident like round 1
             r1.cluster_all()
             bins2 = binset.round2_binset(bins, r1.results())
             ctx2 = _lib.Context(local_rank)
-            runners.append(binset.BinRunner(ctx2, bins2, binset.ROUND2["preset"], binset.ROUND2["identity"], *lens))
+            runners.append(binset.BinRunner(ctx2, bins2, binset.ROUND2["preset"], binset.ROUND2["identity"], *lens,
+                                            lanes=args.lanes, device=local_rank))
 
         def step():
             out = []
@@ -272,27 +275,28 @@ def main() -> None:
             "merged_walks": sum(s["n_merged_walks"] for s in last), "deferred_queries": sum(s["n_deferred"] for s in last),
             "pairs_round_b": sum(s["pairs_round_b"] for s in last), "pairs_peer": sum(s["pairs_peer"] for s in last),
             "alignments_per_step": sum(s["n_alignments"] for s in last),
+            "blocks": sum(s["n_blocks"] for s in last), "block_reruns": sum(s["n_reruns"] for s in last),
             "roofline": roof, "align": align,
         }
         if args.config in (3, 4) and world == 1:
-            # per-bin wall times of the last step -> the LPT makespan of the same bins on 2/4/8 GPUs (model:
-            # bins are independent, so a rank's time is the sum of its bins' times)
+            # modelled multi-GPU time of the same bins: the LPT plan bench.py uses for N ranks, each rank's
+            # share weighted by the measured per-bin times of the last step (bins are independent); the
+            # 1-GPU wall scaled by the largest rank's share
             per_bin = [s["t_total_s"] for s in last]
             nb1 = runners[0].nbins
+            w = [per_bin[i] + (per_bin[nb1 + i] if len(runners) > 1 else 0.0) for i in range(nb1)]
             costs = [shard.bin_cost(b.umis.n) for b in runners[0].binset.bins]
+            wall = t_max / args.steps
             model = {}
             for g in (2, 4, 8):
                 plan = shard.lpt_assign(costs, g)
-                span = 0.0
-                for p in plan:
-                    tt = sum(per_bin[i] for i in p)
-                    if len(runners) > 1:
-                        tt += sum(per_bin[nb1 + i] for i in p)
-                    span = max(span, tt)
+                share = max(sum(w[i] for i in p) for p in plan) / max(sum(w), 1e-12)
+                span = wall * share
                 model[str(g)] = dict(makespan_s=span, umis_per_s=tot_umis / span if span else None,
-                                     efficiency=(sum(per_bin) / g) / span if span else None)
+                                     efficiency=1.0 / (g * share) if share else None)
             out["lpt_model_from_measured_bins"] = model
             out["largest_bin_s"] = max(per_bin) if per_bin else 0.0
+            out["lanes"] = args.lanes
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             if umis is not None:

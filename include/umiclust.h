@@ -92,6 +92,7 @@ typedef struct umiclust_stats {
   double t_read_s;        /* file path: FASTA read + parse (umiclust_run_fasta*) */
   double t_write_s;       /* file path: cluster<N> / consout (+ in-process parse) writing */
   double t_run_s;         /* file path: the whole call, read to files written */
+  int64_t n_reruns;       /* block pieces re-run alone after an in-window peer list overflowed */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

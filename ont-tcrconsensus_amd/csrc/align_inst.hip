@@ -9,7 +9,7 @@
 namespace uc {
 #define UC_CAT2(a, b) a##b
 #define UC_CAT(a, b) UC_CAT2(a, b)
-void UC_CAT(fill_align_part, ALIGN_PART)(AlignFn* a, TraceFn* t) {
-  AlignRange<kAlignPartLo[ALIGN_PART + 1] - 1, kAlignPartLo[ALIGN_PART]>::fill(a, t);
+void UC_CAT(fill_align_part, ALIGN_PART)(AlignFn* a) {
+  AlignRange<kAlignPartLo[ALIGN_PART + 1] - 1, kAlignPartLo[ALIGN_PART]>::fill(a);
 }
 }  // namespace uc

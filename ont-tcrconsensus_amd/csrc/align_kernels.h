@@ -345,156 +345,30 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
 }
 
-// ------------------------------------------------------------------ K3T: traceback
-// Same DP (rows unrolled) without summaries; the direction nibble of every cell (bit0 up = D
-// chosen, bit1 left = I chosen, bit2 D-extension, bit3 I-extension) goes to HBM as one column of
-// CW words per step, laid out [column][word][pair] so a wave's stores are coalesced; then each lane
-// runs backtrack16 over its own matrix.
-template <int QL>
-__global__ __launch_bounds__(64) void k_traceback(DevSeqs s, const uint32_t* __restrict__ pq,
-                                                  const uint32_t* __restrict__ pt, int32_t npairs,
-                                                  Scoring sc, uint32_t* __restrict__ dirbuf,
-                                                  uint8_t* __restrict__ ops,
-                                                  uint16_t* __restrict__ nops,
-                                                  uint32_t* __restrict__ out) {
-  constexpr int CW = (QL + 7) / 8;
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  const uint32_t qv = pq[k];
-  const int32_t q = (int32_t)(qv >> 1);
-  const int qstr = (int)(qv & 1u);
-  const int32_t t = (int32_t)pt[k];
-  const int tl = s.lens[t];
-  uint32_t qw[CW];
-#pragma unroll
-  for (int w = 0; w < CW; w++) qw[w] = s.codes[((int64_t)q * 2 + qstr) * kCodeWords + w];
-  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  uint32_t HE[QL];
-#pragma unroll
-  for (int i = 0; i < QL; i++) {
-    const int hleft = -(sc.go[1] + (i + 1) * sc.ge[1]);
-    const int qrq = (i == QL - 1) ? QRqr : QRqi;
-    HE[i] = pack_hf(hleft, sc.boundary_open ? hleft - qrq : kNegInf);
-  }
-  uint32_t tword = 0;
-  for (int j = 0; j < tl; j++) {
-    if ((j & 7) == 0) tword = tcp[j >> 3];
-    const uint32_t tcode = tword & 15u;
-    tword >>= 4;
-    const bool tamb = (tcode & (tcode - 1u)) != 0u || tcode == 0u;
-    // keep the per-row query codes from being hoisted out of the column loop (that would pin
-    // QL extra VGPRs); re-extracting them is one v_bfe per cell
-#pragma unroll
-    for (int w = 0; w < CW; w++) asm volatile("" : "+v"(qw[w]));
-    const bool lc = (j == tl - 1);
-    const int QRt = lc ? QRtr : QRti;
-    const int Rt = lc ? Rtr : Rti;
-    int Hd = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-    int F = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - QRt : kNegInf;
-    uint32_t dw[CW];
-#pragma unroll
-    for (int w = 0; w < CW; w++) dw[w] = 0;
-#pragma unroll
-    for (int i = 0; i < QL; i++) {
-      const uint32_t qcode = (qw[i >> 3] >> ((i & 7) * 4)) & 15u;
-      const bool amb = tamb || (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-      const int sub = amb ? 0 : (qcode == tcode ? sc.match : sc.mismatch);
-      const uint32_t he = HE[i];
-      const int Hl = sx16(he);
-      const int E = (int)he >> 16;
-      int h = Hd + sub;
-      uint32_t d = 0;
-      if (F > h) { h = F; d |= 1u; }
-      if (E > h) { h = E; d |= 2u; }
-      const int fo = h - QRt, fe = F - Rt;
-      if (fe > fo) { F = fe; d |= 4u; } else F = fo;
-      const int qrq = (i == QL - 1) ? QRqr : QRqi;
-      const int rq = (i == QL - 1) ? Rqr : Rqi;
-      const int eo = h - qrq, ee = E - rq;
-      int En = eo;
-      if (ee > eo) { En = ee; d |= 8u; }
-      dw[i >> 3] |= d << ((i & 7) * 4);
-      Hd = Hl;
-      HE[i] = pack_hf(h, En);
-    }
-#pragma unroll
-    for (int w = 0; w < CW; w++) dirbuf[((int64_t)j * CW + w) * npairs + k] = dw[w];
-  }
-  const int H = sx16(HE[QL - 1]);
-  // backtrack16
-  uint8_t* o = ops + (int64_t)k * kOpsStride;
-  int n = 0;
-  int i = QL - 1, j = tl - 1;
-  int aligned = 0, matches = 0;
-  uint32_t op = 0;  // 0 none, 'M','D','I'
-  while (i >= 0 && j >= 0) {
-    aligned++;
-    const uint32_t d = (dirbuf[((int64_t)j * CW + (i >> 3)) * npairs + k] >> ((i & 7) * 4)) & 15u;
-    if (op == 'I' && (d & 8u)) {
-      j--;
-    } else if (op == 'D' && (d & 4u)) {
-      i--;
-    } else if (d & 2u) {
-      j--;
-      op = 'I';
-    } else if (d & 1u) {
-      i--;
-      op = 'D';
-    } else {
-      const uint32_t qcode = (s.codes[((int64_t)q * 2 + qstr) * kCodeWords + (i >> 3)] >> ((i & 7) * 4)) & 15u;
-      const uint32_t tcode = (tcp[j >> 3] >> ((j & 7) * 4)) & 15u;
-      if (qcode & tcode) matches++;
-      i--;
-      j--;
-      op = 'M';
-    }
-    o[kOpsStride - 1 - n] = (uint8_t)op;
-    n++;
-  }
-  while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
-  while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
-  nops[k] = (uint16_t)n;
-  // align_trim on the op string (alignment order = o[kOpsStride-n .. kOpsStride-1])
-  const uint8_t* a0 = o + kOpsStride - n;
-  int tlft = 0, trgt = 0;
-  if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
-  if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
-  if (tlft >= aligned) trgt = 0;
-  const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
-  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)H & 0xffffu) << 16);
-}
-
 typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
                         const uint32_t*, Scoring, uint32_t*);
-typedef void (*TraceFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, Scoring, uint32_t*,
-                        uint8_t*, uint16_t*, uint32_t*);
 
-// launch tables: align[3 L + v] (v: 0 packed, 1 one-cell-per-op, 2 IUPAC), trace[L]
+// launch table: align[3 L + v] (v: 0 packed, 1 one-cell-per-op, 2 IUPAC)
 template <int L, int LO>
 struct AlignRange {
-  static void fill(AlignFn* a, TraceFn* t) {
+  static void fill(AlignFn* a) {
     a[3 * L] = k_align_pk<L>;
     // the one-cell-per-op kernel for one-hot inputs is a cross-check of the packed one (<= kShortLen)
     if constexpr (L <= kShortLen) a[3 * L + 1] = k_align<L, false>;
     else a[3 * L + 1] = k_align_pk<L>;
     a[3 * L + 2] = k_align<L, true>;
-    t[L] = k_traceback<L>;
-    if constexpr (L > LO) AlignRange<L - 1, LO>::fill(a, t);
+    if constexpr (L > LO) AlignRange<L - 1, LO>::fill(a);
   }
 };
 
 // one per translation unit of align_inst.hip (lengths [kAlignPartLo[p], kAlignPartLo[p + 1]))
 constexpr int kAlignParts = 6;
 constexpr int kAlignPartLo[kAlignParts + 1] = {kMinTplLen, 56, 66, 76, 88, 100, kMaxLen + 1};
-void fill_align_part0(AlignFn*, TraceFn*);
-void fill_align_part1(AlignFn*, TraceFn*);
-void fill_align_part2(AlignFn*, TraceFn*);
-void fill_align_part3(AlignFn*, TraceFn*);
-void fill_align_part4(AlignFn*, TraceFn*);
-void fill_align_part5(AlignFn*, TraceFn*);
+void fill_align_part0(AlignFn*);
+void fill_align_part1(AlignFn*);
+void fill_align_part2(AlignFn*);
+void fill_align_part3(AlignFn*);
+void fill_align_part4(AlignFn*);
+void fill_align_part5(AlignFn*);
 
 }  // namespace uc

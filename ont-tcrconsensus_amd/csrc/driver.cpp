@@ -146,7 +146,7 @@ struct Pass {
                                 // [9] target residues of walk pairs, [10] of peer pairs
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
   DevBuf<WalkState> d_ws;
-  DevBuf<uint32_t> d_ppq, d_ppt, d_poutidx, d_peer_res;
+  DevBuf<HostQs> d_hq;              // k_pack's per query-strand outcomes, copied to h_hq by DMA
   DevBuf<uint32_t> d_reccount;
   // written by k_pack into host memory: per query-strand outcomes, records, counters
   PinBuf<HostQs> h_hq;
@@ -248,8 +248,9 @@ struct umiclust_ctx {
   std::vector<BinOut> bout;
   umiclust_stats stats{};
   int32_t block_size = 8192;
+  int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
-  DevBuf<uint32_t> t_mpq, t_mpt, t_mout, t_dir;
+  DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   DevBuf<uint8_t> t_ops, t_mstrand;
   DevBuf<uint16_t> t_nops, t_conslen;
   DevBuf<int32_t> t_cstart, t_mseq, t_mops, t_over;
@@ -445,19 +446,18 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
   c->hip(P.d_counters.ensure(16), "alloc");
-  c->hip(P.d_pq.ensure(nqs * kBatch), "alloc");
-  c->hip(P.d_pt.ensure(nqs * kBatch), "alloc");
-  c->hip(P.d_outidx.ensure(nqs * kBatch), "alloc");
-  c->hip(P.d_res.ensure(nqs * kWalk), "alloc");
+  // pair lists: a launch aligns up to kWalk walk pairs plus kPeerCap peer pairs per query-strand; results
+  // land in d_res: walk candidate x of qs at [qs * kWalk + x], peer y at [nqs * kWalk + qs * kPeerCap + y]
+  c->hip(P.d_pq.ensure(nqs * (kWalk + kPeerCap)), "alloc");
+  c->hip(P.d_pt.ensure(nqs * (kWalk + kPeerCap)), "alloc");
+  c->hip(P.d_outidx.ensure(nqs * (kWalk + kPeerCap)), "alloc");
+  c->hip(P.d_res.ensure(nqs * (kWalk + kPeerCap)), "alloc");
+  c->hip(P.d_hq.ensure(nqs), "alloc");
   c->hip(P.d_ws.ensure(nqs), "alloc");
   c->hip(P.d_reccount.ensure(1), "alloc");
   c->hip(P.h_hq.ensure(nqs), "pin");
   c->hip(P.h_rec.ensure(nqs * kRecWords), "pin");
   c->hip(P.h_counters.ensure(16), "pin");
-  c->hip(P.d_ppq.ensure(nqs * kPeerCap), "alloc");
-  c->hip(P.d_ppt.ensure(nqs * kPeerCap), "alloc");
-  c->hip(P.d_poutidx.ensure(nqs * kPeerCap), "alloc");
-  c->hip(P.d_peer_res.ensure(nqs * kPeerCap), "alloc");
   // fixed capacities, so a pass never frees memory a queued pass still reads
   c->hip(P.h_tiles.ensure(64), "pin");
   c->hip(P.d_tiles.ensure(64), "alloc");
@@ -554,34 +554,42 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   st = c->st_al;
   DevSeqs ds = dev_seqs(c);
   const int32_t qlen = c->hlen[q0];
-  c->hip(launch_walk(-1, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
+  c->hip(launch_walk(-1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
                      c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 1,
                      P.d_counters.p + 9, st),
          "walk");
   c->hip(hipEventRecord(P.ev[2], st), "event");
-  for (int r = 0; r < kWalk / kBatch; r++) {
-    c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * kBatch, P.d_counters.p + 1 + r,
-                        P.d_outidx.p, c->sc, P.d_res.p, st),
-           "align");
-    c->hip(launch_walk(r, q0, nqs, both, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
-                       c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2 + r,
-                       P.d_counters.p + 9, st),
-           "walk");
-  }
+  // two dependent alignment launches: batch 0 (or a speculative whole walk), then the rest of every
+  // unfinished walk together with the relevant in-window peers (their relevance is taken from the walk
+  // state after round 0, which only widens it: a superset of what the final state needs)
+  const uint32_t peer_out0 = (uint32_t)nqs * kWalk;
+  c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * kWalk, P.d_counters.p + 1, P.d_outidx.p, c->sc,
+                      P.d_res.p, st),
+         "align 0");
+  c->hip(launch_walk(0, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
+                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2,
+                     P.d_counters.p + 9, st),
+         "walk 0");
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
-                           P.d_ppq.p, P.d_ppt.p, P.d_poutidx.p, P.d_counters.p + 8, P.d_counters.p + 10, st),
+                           P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2, P.d_counters.p + 10, P.d_counters.p + 8,
+                           peer_out0, st),
          "peer pairs");
-  c->hip(launch_align(ds, qlen, c->ambig, P.d_ppq.p, P.d_ppt.p, nqs * kPeerCap, P.d_counters.p + 8,
-                      P.d_poutidx.p, c->sc, P.d_peer_res.p, st),
-         "align peers");
+  c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * (kWalk + kPeerCap), P.d_counters.p + 2,
+                      P.d_outidx.p, c->sc, P.d_res.p, st),
+         "align 1");
+  c->hip(launch_walk(1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
+                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 3,
+                     P.d_counters.p + 9, st),
+         "walk 1");
   c->hip(hipEventRecord(P.ev[3], st), "event");
   // what the host needs goes straight to pinned host memory; the pass that next reuses these
   // buffers is enqueued only after the host has waited for ev[4]
   c->hip(hipMemsetAsync(P.d_reccount.p, 0, 4, st), "memset");
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
-                     P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_peer_res.p, P.d_reccount.p, P.h_hq.p,
+                     P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_reccount.p, P.d_hq.p,
                      P.h_rec.p, P.d_counters.p, P.h_counters.p, st),
          "pack");
+  c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
   c->hip(hipEventRecord(P.ev[4], st), "event");
 }
 
@@ -713,7 +721,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       if (kt < kp) {
         m.key = kt;
         m.seqno = R.seq[i];
-        if (i < h.w) {
+        if (i < h.e) {
           m.res = R.res[i];
           m.have = true;
         } else if (row >= 0 && extra_have[(size_t)row * kSlots + i]) {
@@ -785,7 +793,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
         if (h.rec == 0xffffffffu) continue;
         const Rec R = rec_of(h);
         const uint32_t qv = ((uint32_t)(q0 + ql) << 1) | (uint32_t)s;
-        for (int x = h.w; x < R.nt; x++) {
+        for (int x = h.e; x < R.nt; x++) {
           bpq.push_back(qv);
           bpt.push_back(R.seq[x]);
           bidx.push_back((uint32_t)(qs * kSlots + x));
@@ -966,6 +974,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     for (int32_t q = q0; q < q0 + nq;) {
       const int32_t m = std::min(piece, q0 + nq - q);
       enqueue_pass(c, P, q, m, nullptr, c->solo_tile, 0);
+      c->stats.n_reruns++;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
         piece = std::max(1, m / 2);
@@ -1056,8 +1065,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     c->hip(c->t_mout.ensure(nm), "alloc");
     c->hip(c->t_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
     c->hip(c->t_nops.ensure(nm), "alloc");
-    const int32_t chunk = std::max(1, std::min(nm, 1 << 18));
-    c->hip(c->t_dir.ensure((size_t)chunk * kMaxLen * kCodeWords), "alloc");
     if (nm > 0) {
       c->hip(hipMemcpyAsync(c->t_mpq.p, mpq.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
       c->hip(hipMemcpyAsync(c->t_mpt.p, mpt.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
@@ -1068,16 +1075,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     }
     c->hip(hipEventRecord(c->tev[0], c->st), "event");
     DevSeqs ds = dev_seqs(c);
-    // members are in sorted (length-descending) order: one launch per query length and chunk
-    for (int32_t b = 0; b < nm;) {
-      const int32_t ql = c->hlen[mpq[b] >> 1];
-      int32_t e = b + 1;
-      while (e < nm && e - b < chunk && c->hlen[mpq[e] >> 1] == ql) e++;
-      c->hip(launch_traceback(ds, ql, c->t_mpq.p + b, c->t_mpt.p + b, e - b, c->sc, c->t_dir.p,
-                              c->t_ops.p + (size_t)b * kOpsStride, c->t_nops.p + b, c->t_mout.p + b, c->st),
-             "traceback");
-      b = e;
-    }
+    // every member's chosen hit in one launch (one wave per alignment, any query length)
+    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st),
+           "traceback");
     // consensus inputs in output-cluster order
     std::vector<int32_t> mseq(n), mops(n);
     std::vector<uint8_t> mstr(n);
@@ -1258,12 +1258,11 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
 // ---------------------------------------------------------------- FASTA I/O
 // Host threads for file I/O (the box gives a GPU process ~16 cores; UMICLUST_IO_THREADS overrides).
 int io_threads() {
-  static int n = 0;
-  if (n == 0) {
+  static const int n = [] {
     const char* e = getenv("UMICLUST_IO_THREADS");
     int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-    n = std::max(1, std::min(v > 0 ? v : 1, 16));
-  }
+    return std::max(1, std::min(v > 0 ? v : 1, 16));
+  }();
   return n;
 }
 
@@ -1893,6 +1892,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     return nullptr;
   }
   if (const char* b = getenv("UMICLUST_BLOCK")) c->block_size = std::max(1, std::min(kTile, atoi(b)));
+  if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
     if (c->pf_prof.ensure(9) != hipSuccess || hipMemset(c->pf_prof.p, 0, 9 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;
@@ -2083,7 +2083,7 @@ int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const ch
     Scoring sc = to_scoring(pp);
     DevBuf<char> d_a;
     DevBuf<int64_t> d_o;
-    DevBuf<uint32_t> d_codes, d_pq, d_pt, d_out, d_dir;
+    DevBuf<uint32_t> d_codes, d_pq, d_pt, d_out;
     DevBuf<uint8_t> d_lens, d_nk, d_ops;
     DevBuf<uint16_t> d_km, d_nops;
     c->hip(d_a.ensure(all.size() + 1), "alloc");
@@ -2133,15 +2133,14 @@ int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const ch
       if (ops_stride < kOpsStride) c->fail(UMICLUST_EINVAL, "ops_stride < %d", kOpsStride);
       c->hip(d_ops.ensure((size_t)npairs * kOpsStride + 1), "alloc");
       c->hip(d_nops.ensure(npairs + 1), "alloc");
-      c->hip(d_dir.ensure((size_t)npairs * kMaxLen * kCodeWords + 1), "alloc");
     }
     for (int64_t b0 = 0; b0 < npairs;) {
       const int32_t ql = (int32_t)(off[ord[b0] + 1] - off[ord[b0]]);
       int64_t e = b0 + 1;
       while (e < npairs && off[ord[e] + 1] - off[ord[e]] == ql) e++;
       if (cigar_ops)
-        c->hip(launch_traceback(ds, ql, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), sc, d_dir.p,
-                                d_ops.p + (size_t)b0 * kOpsStride, d_nops.p + b0, d_out.p + b0, c->st),
+        c->hip(launch_traceback(ds, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), sc, d_ops.p + (size_t)b0 * kOpsStride,
+                                d_nops.p + b0, d_out.p + b0, c->st),
                "traceback");
       else
         c->hip(launch_align(ds, ql, amb != 0, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), nullptr, nullptr, sc,

@@ -15,7 +15,9 @@
 // All integer/byte work: VALU + LDS, no MFMA (not a dense contraction).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
+#include <mutex>
 
 #include "align_kernels.h"
 #include "umiclust_internal.h"
@@ -27,7 +29,9 @@ namespace uc {
 // (vsearch_umi_cluster.context(device)), so the "already set" flags are kept per device.
 enum { k_attr_prefilter = 0, k_attr_consensus = 1, k_attr_count = 2 };
 constexpr int kAttrDevices = 64;
-static bool g_attr_set[kAttrDevices][k_attr_count];
+// contexts on one device may run in different host threads: the flags are atomics (setting an
+// attribute twice is harmless)
+static std::atomic<bool> g_attr_set[kAttrDevices][k_attr_count];
 static bool attr_set_on_device(int which) {
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kAttrDevices) return false;  // set it every time
@@ -43,10 +47,9 @@ static void mark_attr_set(int which) {
 __constant__ uint8_t c_map4[256];
 
 static uint8_t h_map4[256];
-static bool h_maps_init = false;
+static std::once_flag h_maps_once;
 
-static void host_maps() {
-  if (h_maps_init) return;
+static void host_maps_init() {
   const char* iupac = "ACGTURYSWKMBDHVN";
   const uint8_t v4[] = {1, 2, 4, 8, 8, 5, 10, 6, 9, 12, 3, 14, 13, 11, 7, 15};
   for (int i = 0; i < 256; i++) h_map4[i] = 0;
@@ -54,11 +57,10 @@ static void host_maps() {
     h_map4[(uint8_t)iupac[i]] = v4[i];
     h_map4[(uint8_t)(iupac[i] | 0x20)] = v4[i];
   }
-  h_maps_init = true;
 }
 
 static hipError_t ensure_maps(hipStream_t st) {
-  host_maps();
+  std::call_once(h_maps_once, host_maps_init);
   return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_map4), h_map4, 256, 0, hipMemcpyHostToDevice, st);
 }
 
@@ -1036,29 +1038,27 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
 }
 
 static AlignFn g_align[3 * (kMaxLen + 1)];
-static TraceFn g_trace[kMaxLen + 1];
+static int g_align_variant0 = 0;
+static std::once_flag g_align_once;
 static void init_align_tables() {
-  static bool init = false;
-  if (init) return;
-  fill_align_part0(g_align, g_trace);
-  fill_align_part1(g_align, g_trace);
-  fill_align_part2(g_align, g_trace);
-  fill_align_part3(g_align, g_trace);
-  fill_align_part4(g_align, g_trace);
-  fill_align_part5(g_align, g_trace);
-  init = true;
+  std::call_once(g_align_once, [] {
+    fill_align_part0(g_align);
+    fill_align_part1(g_align);
+    fill_align_part2(g_align);
+    fill_align_part3(g_align);
+    fill_align_part4(g_align);
+    fill_align_part5(g_align);
+    // UMICLUST_ALIGN=scalar selects the one-cell-per-op kernel (cross-checks / benchmarks)
+    const char* v = getenv("UMICLUST_ALIGN");
+    g_align_variant0 = (v && v[0] == 's') ? 1 : 0;
+  });
 }
 
 hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq,
                         const uint32_t* pt, int32_t npairs, const uint32_t* dev_npairs,
                         const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st) {
-  static int variant0 = -1;
   init_align_tables();
-  if (variant0 < 0) {
-    // UMICLUST_ALIGN=scalar selects the one-cell-per-op kernel (cross-checks / benchmarks)
-    const char* v = getenv("UMICLUST_ALIGN");
-    variant0 = (v && v[0] == 's') ? 1 : 0;
-  }
+  const int variant0 = g_align_variant0;
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
   hipLaunchKernelGGL(g_align[3 * qlen + (ambig ? 2 : variant0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
@@ -1073,7 +1073,7 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
 // are resolved later by the host): round r evaluates batch r of every unfinished query-strand and
 // emits the pairs of batch r+1.  Acceptance and the id order come from host-built tables, so the
 // IEEE-double test `100.0*matches/internal >= 100.0*id` is exactly vsearch's.
-__global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
+__global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
                        const uint32_t* __restrict__ top_seqno, const uint8_t* __restrict__ top_count,
                        const uint8_t* __restrict__ ntop, const uint8_t* __restrict__ lens,
                        const uint32_t* __restrict__ res, const uint8_t* __restrict__ acc_tab,
@@ -1087,6 +1087,7 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
   const uint32_t strand = (uint32_t)(qs % both);
   const int nt = ntop[qs];
   WalkState w;
+  int emit_to;  // emit candidates [w.e, emit_to)
   if (round < 0) {
     w.w = 0;
     w.done = (nt == 0) ? 1 : 0;
@@ -1095,34 +1096,42 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
     w.best_t = 0xffffffffu;
     w.cells = 0;
     w.lastkey = 0;
+    w.e = 0;
+    const bool spec = nt > 0 && (int)top_count[(int64_t)qs * kTopHits] < spec_thr;
+    emit_to = min(nt, spec ? kWalk : kBatch);
   } else {
     w = ws[qs];
     if (w.done) return;
-    const int b0 = round * kBatch, b1 = min(nt, b0 + kBatch);
     const int ql = lens[q];
-    for (int x = b0; x < b1; x++) {
-      const uint32_t r = res[(int64_t)qs * kWalk + x];
-      const uint32_t m = r & 0xffu, L = (r >> 8) & 0xffu;
-      const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
-      w.cells += (uint32_t)(ql * lens[t]);
-      if (acc_tab[L * kTabM + m]) {
-        const uint16_t rk = rank_tab[L * kTabM + m];
-        if (!w.acc || rk > w.best_rank || (rk == w.best_rank && t < w.best_t)) {
-          w.best_rank = rk;
-          w.best_t = t;
+    // every batch whose results exist, in order
+    while (!w.done && w.w < w.e) {
+      const int b0 = w.w, b1 = min(nt, b0 + kBatch);
+      for (int x = b0; x < b1; x++) {
+        const uint32_t r = res[(int64_t)qs * kWalk + x];
+        const uint32_t m = r & 0xffu, L = (r >> 8) & 0xffu;
+        const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
+        w.cells += (uint32_t)(ql * lens[t]);
+        if (acc_tab[L * kTabM + m]) {
+          const uint16_t rk = rank_tab[L * kTabM + m];
+          if (!w.acc || rk > w.best_rank || (rk == w.best_rank && t < w.best_t)) {
+            w.best_rank = rk;
+            w.best_t = t;
+          }
+          w.acc = 1;
         }
-        w.acc = 1;
       }
+      w.w = (uint8_t)b1;
+      const uint32_t tl = lens[top_seqno[(int64_t)qs * kTopHits + b1 - 1]];
+      w.lastkey = ((unsigned long long)(127u - top_count[(int64_t)qs * kTopHits + b1 - 1]) << 56) |
+                  ((unsigned long long)tl << 48) | top_seqno[(int64_t)qs * kTopHits + b1 - 1];
+      if (w.acc || b1 >= nt || b1 >= kWalk) w.done = 1;
     }
-    w.w = (uint8_t)b1;
-    const uint32_t tl = lens[top_seqno[(int64_t)qs * kTopHits + b1 - 1]];
-    w.lastkey = ((unsigned long long)(127u - top_count[(int64_t)qs * kTopHits + b1 - 1]) << 56) |
-                ((unsigned long long)tl << 48) | top_seqno[(int64_t)qs * kTopHits + b1 - 1];
-    if (w.acc || b1 >= nt || b1 >= kWalk) w.done = 1;
+    // the rest of an unfinished walk is emitted at once (one more align launch instead of up to three
+    // dependent ones); walks are still evaluated batch by batch
+    emit_to = w.done ? (int)w.e : min(nt, kWalk);
   }
-  ws[qs] = w;
-  if (!w.done) {
-    const int b0 = w.w, b1 = min(nt, b0 + kBatch);
+  if (emit_to > (int)w.e) {
+    const int b0 = w.e, b1 = emit_to;
     const uint32_t base = atomicAdd(npairs, (uint32_t)(b1 - b0));
     uint32_t tl = 0;
     for (int x = b0; x < b1; x++) {
@@ -1134,16 +1143,18 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
       tl += lens[t];
     }
     atomicAdd(tsum, tl);  // target residues of the pairs emitted (cells computed = qlen * this)
+    w.e = (uint8_t)b1;
   }
+  ws[qs] = w;
 }
 
-hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
+hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
                        uint32_t* outidx, uint32_t* npairs, uint32_t* tsum, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_walk, dim3((nqs + 255) / 256), dim3(256), 0, st, round, q0, nqs, both,
+  hipLaunchKernelGGL(k_walk, dim3((nqs + 255) / 256), dim3(256), 0, st, round, q0, nqs, both, spec_thr,
                      top_seqno, top_count, ntop, lens, res, acc_tab, rank_tab, ws, pq, pt, outidx,
                      npairs, tsum);
   return hipGetLastError();
@@ -1167,7 +1178,8 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* __restrict__ ws, const uint16_t* __restrict__ peer_id,
                              const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
                              uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
-                             uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum) {
+                             uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum,
+                             uint32_t* __restrict__ nstat, uint32_t out0) {
   // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
   // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1182,6 +1194,7 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
   }
   if (!rel) return;
   uint32_t k = atomicAdd(npairs, (uint32_t)__builtin_popcountll(rel));
+  atomicAdd(nstat, (uint32_t)__builtin_popcountll(rel));
   const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
   uint32_t tl = 0;
   for (int x = 0; x < np; x++)
@@ -1189,7 +1202,7 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
       const uint32_t t = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       pq[k] = qv;
       pt[k] = t;
-      outidx[k] = (uint32_t)(qs * kPeerCap + x);
+      outidx[k] = out0 + (uint32_t)(qs * kPeerCap + x);
       tl += lens[t];
       k++;
     }
@@ -1199,10 +1212,10 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, hipStream_t st) {
+                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, npairs, tsum);
+                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0);
   return hipGetLastError();
 }
 
@@ -1248,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     if (lane == 0) r[0] = (uint32_t)nt | ((uint32_t)np << 8);
     if (lane < nt) {
       r[1 + lane] = top_seqno[(int64_t)qs * kTopHits + lane];
-      r[1 + nt + lane] = lane < w.w ? res[(int64_t)qs * kWalk + lane] : 0u;
+      r[1 + nt + lane] = lane < w.e ? res[(int64_t)qs * kWalk + lane] : 0u;
     }
     if (lane < ncw) {
       uint32_t cw = 0;
@@ -1284,7 +1297,9 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     h.best_rank = w.best_rank;
     h.w = w.w;
     h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
-    h.nrel = nrel;
+    h.nrel = (uint16_t)nrel;
+    h.e = w.e;
+    h.pad = 0;
 #pragma unroll
     for (int i = 0; i < kInlineRel; i++) h.rel[i] = ids[i];
     hq[qs] = h;
@@ -1302,14 +1317,168 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
   return hipGetLastError();
 }
 
-hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
-                            int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,
-                            uint16_t* nops, uint32_t* out, hipStream_t st) {
-  init_align_tables();
+// ------------------------------------------------------------------ K3T: traceback (one wave per alignment)
+// The same DP as k_align / backtrack16 for the one chosen hit of every member (the CIGAR feeding the
+// consensus).  A wave computes one alignment: lane l holds query row 64 s + l of stripe s and sweeps the
+// anti-diagonals, lane l computing column j = step - l; the vertical state (H(i-1, j), F(i, j)) and the
+// target code move one lane down per step by DPP wave_shr:1, the horizontal state (H(i, j-1), E(i, j))
+// stays in the lane, and the diagonal H(i-1, j-1) is what the lane received one step earlier.  Stripe
+// s > 0 takes row 64 s - 1 from LDS (written by lane 63 of stripe s - 1).  Every cell's direction nibble
+// (bit 0 up = D chosen, bit 1 left = I chosen, bit 2 D-extension, bit 3 I-extension) goes to LDS, 8 steps
+// per word, and lane 0 runs backtrack16 over it.  Any query length up to kMaxLen in one launch; latency
+// ~(ql + tl) steps instead of ql * tl serial cells.
+constexpr int kTwWaves = 4;
+constexpr int kTwStripes = (kMaxLen + 63) / 64;
+constexpr int kTwWords = (kMaxLen + 63 + 7) / 8;
+struct TwShared {
+  uint32_t dir[kTwStripes][kTwWords][64];  // cell (64 s + l, t - l): word t / 8 of lane l, nibble t % 8
+  int32_t botH[kMaxLen];                   // H(64 s - 1, j) for the next stripe
+  int32_t botF[kMaxLen];                   // F(64 s, j)
+  uint8_t tcode[kMaxLen + 64];
+  int32_t hend;
+};
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+
+__global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const uint32_t* __restrict__ pq,
+                                                              const uint32_t* __restrict__ pt, int32_t npairs,
+                                                              Scoring sc, uint8_t* __restrict__ ops,
+                                                              uint16_t* __restrict__ nops, uint32_t* __restrict__ out) {
+  __shared__ TwShared SH[kTwWaves];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int k = (int)blockIdx.x * kTwWaves + wave;
+  if (k >= npairs) return;  // wave-uniform
+  TwShared& S = SH[wave];
+  const uint32_t qv = pq[k];
+  const int32_t q = (int32_t)(qv >> 1);
+  const int qstr = (int)(qv & 1u);
+  const int32_t t = (int32_t)pt[k];
+  const int tl = s.lens[t], ql = s.lens[q];
+  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
+  const uint32_t* qcp = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
+  for (int j = lane; j < tl + 64; j += 64) S.tcode[j] = j < tl ? (uint8_t)((tcp[j >> 3] >> ((j & 7) * 4)) & 15u) : 0;
+  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
+  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
+  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int nstripe = (ql + 63) >> 6;
+  for (int st = 0; st < nstripe; st++) {
+    const int i = st * 64 + lane;
+    const int rows = min(64, ql - st * 64);  // live lanes of the stripe
+    const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
+    const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+    const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
+    int Hl = -(sc.go[1] + (i + 1) * sc.ge[1]);  // H(i, -1)
+    int E = sc.boundary_open ? Hl - qrq : kNegInf;
+    int Hd = 0;                                 // H(i-1, j-1) for the next cell
+    int hout = 0, fout = 0;                     // this lane's last cell: H(i, j), F(i+1, j)
+    uint32_t tc = 0, dword = 0;
+    const int nsteps = tl + rows - 1;
+    for (int tt = 0; tt < nsteps; tt++) {
+      const int j = tt - lane;
+      // row above at column tt for lane 0: the top boundary (stripe 0) or the previous stripe's bottom row
+      int hb, fb;
+      if (st == 0) {
+        hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
+        const int qrt = (tt == tl - 1) ? QRtr : QRti;
+        fb = sc.boundary_open ? hb - qrt : kNegInf;
+      } else {
+        hb = tt < tl ? S.botH[tt] : 0;
+        fb = tt < tl ? S.botF[tt] : 0;
+      }
+      const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
+      tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
+      const int Hup = sx16(recv), Fin = (int)recv >> 16;
+      const bool live = j >= 0 && j < tl && i < ql;
+      const int hd = (j == 0) ? (i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1])) : Hd;
+      const bool lc = (j == tl - 1);
+      const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
+      const bool tamb = (tc & (tc - 1u)) != 0u || tc == 0u;
+      const int sub = (tamb || qamb) ? 0 : (qcode == tc ? sc.match : sc.mismatch);
+      int h = hd + sub;
+      uint32_t d = 0;
+      if (Fin > h) { h = Fin; d |= 1u; }
+      if (E > h) { h = E; d |= 2u; }
+      const int fo = h - QRt, fe = Fin - Rt;
+      int Fn = fo;
+      if (fe > fo) { Fn = fe; d |= 4u; }
+      const int eo = h - qrq, ee = E - rq;
+      int En = eo;
+      if (ee > eo) { En = ee; d |= 8u; }
+      if (live) {
+        Hl = h;
+        E = En;
+        hout = h;
+        fout = Fn;
+        if (i == ql - 1 && j == tl - 1) S.hend = h;
+        if (lane == 63 && st + 1 < nstripe) {
+          S.botH[j] = h;
+          S.botF[j] = Fn;
+        }
+      }
+      Hd = Hup;
+      (void)Hl;
+      dword |= d << ((tt & 7) * 4);
+      if ((tt & 7) == 7 || tt == nsteps - 1) {
+        S.dir[st][tt >> 3][lane] = dword;
+        dword = 0;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane != 0) return;
+  // backtrack16 from (ql-1, tl-1): diagonal unless the cell took up (D) / left (I); a run continues while
+  // the cell's extension bit says the gap was extended
+  uint8_t* o = ops + (int64_t)k * kOpsStride;
+  int n = 0, i = ql - 1, j = tl - 1, aligned = 0, matches = 0;
+  uint32_t op = 0;
+  while (i >= 0 && j >= 0) {
+    aligned++;
+    const int l = i & 63, tt = j + l;
+    const uint32_t d = (S.dir[i >> 6][tt >> 3][l] >> ((tt & 7) * 4)) & 15u;
+    if (op == 'I' && (d & 8u)) {
+      j--;
+    } else if (op == 'D' && (d & 4u)) {
+      i--;
+    } else if (d & 2u) {
+      j--;
+      op = 'I';
+    } else if (d & 1u) {
+      i--;
+      op = 'D';
+    } else {
+      const uint32_t qc = (qcp[i >> 3] >> ((i & 7) * 4)) & 15u;
+      if (qc & S.tcode[j]) matches++;
+      i--;
+      j--;
+      op = 'M';
+    }
+    o[kOpsStride - 1 - n] = (uint8_t)op;
+    n++;
+  }
+  while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
+  while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
+  nops[k] = (uint16_t)n;
+  // align_trim: the first and the last op runs, if gaps, are terminal (alignment order)
+  const uint8_t* a0 = o + kOpsStride - n;
+  int tlft = 0, trgt = 0;
+  if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
+  if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
+  if (tlft >= aligned) trgt = 0;
+  const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
+  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)S.hend & 0xffffu) << 16);
+}
+
+hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
+                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(g_trace[qlen], dim3((npairs + 63) / 64), dim3(64), 0, st, s, pq, pt, npairs, sc,
-                     dirbuf, ops, nops, out);
+  hipLaunchKernelGGL(k_trace_wave, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves), 0, st, s, pq, pt,
+                     npairs, sc, ops, nops, out);
   return hipGetLastError();
 }
 

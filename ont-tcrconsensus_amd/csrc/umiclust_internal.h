@@ -146,10 +146,15 @@ struct WalkState {
   uint8_t w;                   // candidates walked (aligned)
   uint8_t done;
   uint8_t acc;                 // an accepted hit exists
-  uint8_t pad[3];
+  uint8_t e;                   // candidates emitted for alignment so far (results exist for [0, e))
+  uint8_t pad[2];
 };
-// round -1 initialises and emits batch 0; round r >= 0 evaluates batch r, emits batch r+1.
-hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
+// round -1 initialises and emits batch 0 -- or, speculatively, every candidate up to kWalk when the best
+// candidate's k-mer count is below spec_thr (junk-like lists walk to the end);
+// round r >= 0 evaluates every batch whose results exist and, if the walk goes on, emits all of its
+// remaining candidates (up to kWalk): a pass has two dependent alignment launches, not five.
+// Speculation changes which alignments are computed, never the walk: batches are evaluated in order.
+hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
@@ -158,7 +163,7 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both,
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, hipStream_t st);
+                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
 constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {
@@ -168,7 +173,9 @@ struct HostQs {
   uint16_t best_rank;   // id rank of the best accepted hit
   uint8_t w;            // candidates walked
   uint8_t flags;        // bit 0: an accepted hit exists; bit 1: peer list overflow
-  uint32_t nrel;        // relevant peers
+  uint16_t nrel;        // relevant peers
+  uint8_t e;            // walk candidates with an alignment result (record res[0, e))
+  uint8_t pad;
   uint16_t rel[kInlineRel];  // the first kInlineRel of them (window ids), so the host reads the
                              // record only when one turns out to be a centroid (or nrel is larger)
 };
@@ -179,10 +186,10 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
                        const uint32_t* peer_res, uint32_t* reccount, HostQs* hq, uint32_t* rec,
                        const uint32_t* counters, uint32_t* hcounters, hipStream_t st);
-// traceback: ops[k*kOpsStride...] ('M','D','I' in alignment order), nops[k]
-hipError_t launch_traceback(const DevSeqs& s, int32_t qlen, const uint32_t* pq, const uint32_t* pt,
-                            int32_t npairs, const Scoring& sc, uint32_t* dirbuf, uint8_t* ops,
-                            uint16_t* nops, uint32_t* out, hipStream_t st);
+// traceback (one wave per pair, any query length): ops[k*kOpsStride...] ('M','D','I' in alignment order,
+// right-aligned in the slot), nops[k], out[k] as launch_align's
+hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
+                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st);
 // consensus: cluster c members member_seqno[cstart[c] .. cstart[c+1]) (centroid first),
 // member_ops index per member (-1 for centroid), member strand.
 hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t nclusters,

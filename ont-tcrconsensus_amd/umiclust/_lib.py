@@ -76,6 +76,7 @@ class Stats(C.Structure):
         ("t_read_s", C.c_double),
         ("t_write_s", C.c_double),
         ("t_run_s", C.c_double),
+        ("n_reruns", C.c_int64),
     ]
 
     def as_dict(self) -> dict:

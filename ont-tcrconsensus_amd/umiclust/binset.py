@@ -41,25 +41,61 @@ def cluster_sizes(res: dict) -> np.ndarray:
 
 
 class BinRunner:
-    """One rank's bins of one round, resident on one device."""
+    """One rank's bins of one round, resident on one device.
 
-    def __init__(self, ctx: _lib.Context, binset: synth.BinSet, preset: int, identity: float,
-                 minlen: int = 58, maxlen: int = 68):
-        self.ctx = ctx
+    Bins are independent, so a rank runs `lanes` of them at once: one device context per lane (its own
+    streams and working buffers), the bins LPT-split over the lanes, one host thread per lane (the C ABI
+    releases the GIL; distinct contexts are re-entrant).  Small bins are launch- and latency-bound on
+    their own; lanes keep the GPU fed.  Results do not depend on the lane count."""
+
+    def __init__(self, ctx, binset: synth.BinSet, preset: int, identity: float, minlen: int = 58,
+                 maxlen: int = 68, lanes: int = 1, device: int = 0):
+        from .shard import bin_cost, lpt_assign
         self.binset = binset
         self.params = _lib.params(preset, identity, minlen, maxlen)
-        ctx.load_bins(self.params, binset.seq, binset.off, binset.bin_start)
+        nb = len(binset.bins)
+        lanes = max(1, min(lanes, nb)) if nb else 1
+        plan = lpt_assign([bin_cost(b.umis.n) for b in binset.bins], lanes)
+        self.ctxs = [ctx] + [_lib.Context(device) for _ in range(lanes - 1)]
+        self._own = self.ctxs[1:]
+        self.plan = plan
+        self.where = {}  # bin -> (lane, index in the lane's load)
+        for lane, idx in enumerate(plan):
+            sub = binset.subset(idx) if lanes > 1 else binset
+            if lanes == 1:
+                idx = list(range(nb))
+                self.plan = [idx]
+            for j, b in enumerate(idx):
+                self.where[b] = (lane, j)
+            self.ctxs[lane].load_bins(self.params, sub.seq, sub.off, sub.bin_start)
 
     @property
     def nbins(self) -> int:
         return len(self.binset.bins)
 
     def cluster_all(self) -> list:
-        """Cluster every bin; per-bin stats."""
-        return [self.ctx.cluster_bin(b) for b in range(self.nbins)]
+        """Cluster every bin; per-bin stats in bin order."""
+        out = [None] * self.nbins
+
+        def run(lane):
+            for j, b in enumerate(self.plan[lane]):
+                out[b] = self.ctxs[lane].cluster_bin(j)
+
+        if len(self.ctxs) == 1:
+            run(0)
+        else:
+            import concurrent.futures as cf
+            with cf.ThreadPoolExecutor(len(self.ctxs)) as ex:
+                list(ex.map(run, range(len(self.ctxs))))
+        return out
 
     def results(self) -> list:
-        return [self.ctx.fetch_bin(b) for b in range(self.nbins)]
+        return [self.ctxs[self.where[b][0]].fetch_bin(self.where[b][1]) for b in range(self.nbins)]
+
+    def close(self):
+        for c in self._own:
+            c.close()
+        self._own = []
 
 
 def round2_binset(binset: synth.BinSet, results: list, min_reads: int = MIN_READS_PER_CLUSTER) -> synth.BinSet:

@@ -21,6 +21,17 @@ for st in "$@"; do
     e2e) timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e > "$out/e2e.json" 2> "$out/e2e.err"; rc=$? ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$out/trace.log" 2>&1; rc=$? ;;
+    pmc_fetch|pmc_write|pmc_sq|pmc_valu)
+       case $st in
+         pmc_fetch) ctr="FETCH_SIZE" ;;
+         pmc_write) ctr="WRITE_SIZE" ;;
+         pmc_sq) ctr="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" ;;
+         pmc_valu) ctr="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY" ;;
+       esac
+       timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d "$out/$st" -o run -- \
+         python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$out/$st.log" 2>&1; rc=$? ;;
+    trace3) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace3" -o run -- \
+             python3 bench.py --config 3 --lanes 1 --steps 1 --warmup 0 --no-cpu-baseline > "$out/trace3.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
