@@ -147,6 +147,7 @@ struct Pass {
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
   DevBuf<WalkState> d_ws;
   DevBuf<HostQs> d_hq;              // k_pack's per query-strand outcomes, copied to h_hq by DMA
+  DevBuf<unsigned long long> d_paligned;  // per query-strand: the peers k_peer_pairs aligned
   DevBuf<uint32_t> d_reccount;
   // written by k_pack into host memory: per query-strand outcomes, records, counters
   PinBuf<HostQs> h_hq;
@@ -195,6 +196,7 @@ struct umiclust_ctx {
   DevBuf<uint8_t> d_lens;
   DevBuf<uint16_t> d_kmers;
   DevBuf<uint8_t> d_nk;
+  DevBuf<uint8_t> d_strong;       // [seqno * 2 + strand] prefilter's near-identical-peer flags (speculation)
   DevBuf<char> d_masked;
   DevBuf<int32_t> d_iota;
   // device: tables
@@ -249,6 +251,9 @@ struct umiclust_ctx {
   umiclust_stats stats{};
   int32_t block_size = 8192;
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
+  bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
+  int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
+  int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -       // skip peers predicted to be members (UMICLUST_PEER_PREDICT=0: align all)
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   DevBuf<uint8_t> t_ops, t_mstrand;
@@ -453,6 +458,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_outidx.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_res.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_hq.ensure(nqs), "alloc");
+  c->hip(P.d_paligned.ensure(nqs), "alloc");
   c->hip(P.d_ws.ensure(nqs), "alloc");
   c->hip(P.d_reccount.ensure(1), "alloc");
   c->hip(P.h_hq.ensure(nqs), "pin");
@@ -542,6 +548,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.peer_id = P.d_peer_id.p;
   a.peer_count = P.d_peer_count.p;
   a.npeer = P.d_npeer.p;
+  a.strong = c->d_strong.p;
+  a.strong_eighths = c->strong_eighths;
   a.postings_touched = P.d_counters.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
   c->hip(hipEventRecord(P.ev[0], st), "event");
@@ -572,7 +580,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
          "walk 0");
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
                            P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2, P.d_counters.p + 10, P.d_counters.p + 8,
-                           peer_out0, st),
+                           peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, st),
          "peer pairs");
   c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * (kWalk + kPeerCap), P.d_counters.p + 2,
                       P.d_outidx.p, c->sc, P.d_res.p, st),
@@ -586,7 +594,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   // buffers is enqueued only after the host has waited for ev[4]
   c->hip(hipMemsetAsync(P.d_reccount.p, 0, 4, st), "memset");
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
-                     P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_reccount.p, P.d_hq.p,
+                     P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_paligned.p, P.d_reccount.p,
+                     P.d_hq.p,
                      P.h_rec.p, P.d_counters.p, P.h_counters.p, st),
          "pack");
   c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
@@ -662,9 +671,15 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     o.walked = h.w;
     o.cells = h.cells;
   };
-  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o) -> int {
+  // Membership can be certain while the walk's outcome is not: a device walk that accepted within its first w
+  // candidates still accepts when at most nrel relevant peers are inserted before them (w + nrel <= kWalk).
+  // Such a query is a member whichever centroid it ends up joining, so later queries that only need to
+  // know "centroid or not" are not held up by it.
+  auto cert_device = [](const HostQs& h) { return (h.flags & 1u) && (int)h.w + (int)h.nrel <= kWalk; };
+  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert) -> int {
     // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed
     const HostQs& h = hq[qs];
+    cert = false;
     if (h.rec == 0xffffffffu) {
       device_outcome(h, o);
       return 0;
@@ -673,7 +688,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       bool cent = false;
       for (uint32_t i = 0; i < h.nrel; i++) {
         const uint8_t st = state[(uint32_t)w0 + h.rel[i]];
-        if (st == ST_UNDET) return 1;
+        if (st == ST_UNDET) {
+          cert = cert_device(h);
+          return 1;
+        }
         cent |= st == ST_CENT;
       }
       if (!cent) {
@@ -686,9 +704,14 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
       const uint8_t st = state[(uint32_t)w0 + (pw & 0xffffu)];
-      if (pw >> 24) {
-        if (st == ST_UNDET) return 1;
+      if ((pw >> 24) & 1u) {
+        if (st == ST_UNDET) {
+          c->dbg[2]++;
+          cert = cert_device(h);
+          return 1;
+        }
         affects |= st == ST_CENT;
+        if (!((pw >> 25) & 1u)) c->dbg[st == ST_CENT ? 0 : 1]++;  // mispredicted / saved
       } else {
         undet |= st == ST_UNDET;
       }
@@ -697,7 +720,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       device_outcome(h, o);
       return 0;
     }
-    if (undet) return 1;
+    if (undet) {
+      cert = cert_device(h);
+      return 1;
+    }
     c->stats.n_merged_walks++;
     const double tm0 = now_s();
     struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{&c->stats.t_merged_s, tm0};
@@ -736,7 +762,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
         const int y = cp[x].second;
         m.key = kp;
         m.seqno = (uint32_t)w0 + (R.peer[y] & 0xffffu);
-        if (R.peer[y] >> 24) {
+        if ((R.peer[y] >> 25) & 1u) {  // aligned by the pass
           m.res = R.pres[y];
           m.have = true;
         } else if (row >= 0 && extra_have[(size_t)row * kSlots + kWalk + y]) {
@@ -750,14 +776,34 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       }
       L.push_back(m);
     }
-    return merged_walk(c, L, c->hlen[q], o) ? 0 : 2;
+    if (merged_walk(c, L, c->hlen[q], o)) return 0;
+    // an accept already known within the first kWalk candidates ends the walk by its batch at the latest
+    for (int x = 0; x < std::min<int>((int)L.size(), kWalk) && !cert; x++)
+      if (L[x].have) {
+        const uint32_t m = L[x].res & 0xffu, Li = (L[x].res >> 8) & 0xffu;
+        cert = c->h_acc[(size_t)Li * kTabM + m] != 0;
+      }
+    return 2;
   };
   auto resolve = [&](int32_t ql, bool allow_extra) -> bool {
     const int32_t q = q0 + ql;
     Outcome best, os[2];
     int bs = 0;
-    for (int s = 0; s < both; s++)
-      if (strand_outcome(ql * both + s, q, allow_extra, os[s]) != 0) return false;
+    bool open = false, member = false;
+    for (int s = 0; s < both; s++) {
+      bool cert = false;
+      if (strand_outcome(ql * both + s, q, allow_extra, os[s], cert) != 0) {
+        open = true;
+        member |= cert;
+      } else {
+        member |= os[s].acc;
+      }
+    }
+    if (open) {
+      // deferred; a certain member is marked so already (its centroid is settled in round B)
+      if (member) state[q] = ST_MEMBER;
+      return false;
+    }
     for (int s = 0; s < both; s++) {
       c->stats.n_alignments += os[s].walked;
       c->stats.cells += os[s].cells;
@@ -799,7 +845,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
           bidx.push_back((uint32_t)(qs * kSlots + x));
         }
         for (int y = 0; y < R.np; y++)
-          if (!(R.peer[y] >> 24)) {
+          if (!((R.peer[y] >> 25) & 1u)) {
             bpq.push_back(qv);
             bpt.push_back((uint32_t)w0 + (R.peer[y] & 0xffffu));
             bidx.push_back((uint32_t)(qs * kSlots + kWalk + y));
@@ -1145,6 +1191,10 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   }
   c->stats.t_total_s = now_s() - t0;
   c->clustered = true;
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: n %d mispredicted %lld saved(seen) %lld blocked %lld deferred %lld\n", bin, n,
+            (long long)c->dbg[0], (long long)c->dbg[1], (long long)c->dbg[2], (long long)c->stats.n_deferred);
+  c->dbg[0] = c->dbg[1] = c->dbg[2] = 0;
 }
 
 // ---------------------------------------------------------------- load
@@ -1234,6 +1284,8 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
   c->hip(c->d_lens.ensure(ns), "alloc");
   c->hip(c->d_kmers.ensure(ns * 2 * kKmerStride), "alloc");
   c->hip(c->d_nk.ensure(ns * 2), "alloc");
+  c->hip(c->d_strong.ensure(ns * 2), "alloc");
+  c->hip(hipMemsetAsync(c->d_strong.p, 0, ns * 2, c->st), "memset");
   c->hip(c->d_masked.ensure(ns * kMaxLen), "alloc");
   c->hip(c->d_iota.ensure(ns), "alloc");
   std::vector<int32_t> iota(ns);
@@ -1893,6 +1945,8 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   }
   if (const char* b = getenv("UMICLUST_BLOCK")) c->block_size = std::max(1, std::min(kTile, atoi(b)));
   if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
   if (getenv("UMICLUST_PFPROF")) {
     if (c->pf_prof.ensure(9) != hipSuccess || hipMemset(c->pf_prof.p, 0, 9 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;

@@ -1005,9 +1005,20 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   const int po_l = pinc - np_l;
   if (!live) return;
   const bool povf = over || ptotal > kPeerCap;
+  // strong[seqno * 2 + strand]: the query has an earlier window query sharing >= 5/8 of its k-mers (it is
+  // then all but surely a member, not a centroid: later queries need not align against it speculatively)
+  int pmax = 0;
+  if (!povf && lane < kParts)
+    for (int x = 0; x < np_l; x++) pmax = max(pmax, (int)a.ppeer_count[(p0 + lane) * kPeerCap + x]);
+#pragma unroll
+  for (int d = 1; d < kParts; d <<= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
   if (lane == 0) {
     a.ntop[qs] = (uint8_t)min(total, kTopHits);
     a.npeer[qs] = (uint8_t)(povf ? 255 : ptotal);
+    const int32_t q = a.q0 + qs / a.both;
+    const int nkq = a.seqs.nk[(int64_t)q * 2 + qs % a.both];
+    a.strong[(int64_t)q * 2 + qs % a.both] =
+        (uint8_t)(!povf && pmax * 8 >= nkq * a.strong_eighths && pmax > a.minwordmatches);
   }
   if (povf) return;
   for (int l = 0; l < kParts; l++) {
@@ -1179,19 +1190,25 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
                              uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
                              uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum,
-                             uint32_t* __restrict__ nstat, uint32_t out0) {
+                             uint32_t* __restrict__ nstat, uint32_t out0, const uint8_t* __restrict__ strong,
+                             unsigned long long* __restrict__ aligned) {
   // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
   // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   if (qs >= nqs) return;
   const int np = npeer[qs];
+  aligned[qs] = 0ull;
   if (np == 255 || np == 0) return;
   const WalkState w = ws[qs];
   unsigned long long rel = 0;
   for (int x = 0; x < np; x++) {
     const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
-    if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps)) rel |= 1ull << x;
+    // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
+    if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
+        !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])))
+      rel |= 1ull << x;
   }
+  aligned[qs] = rel;
   if (!rel) return;
   uint32_t k = atomicAdd(npairs, (uint32_t)__builtin_popcountll(rel));
   atomicAdd(nstat, (uint32_t)__builtin_popcountll(rel));
@@ -1212,10 +1229,11 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, hipStream_t st) {
+                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
+                             unsigned long long* aligned, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0);
+                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0, strong, aligned);
   return hipGetLastError();
 }
 
@@ -1225,14 +1243,16 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
 // candidate list (seqno, k-mer count, result of the walked ones) and every peer (window id, count,
 // relevant flag, result of the aligned ones).  One wave per query-strand, lanes writing consecutive
 // words.  Record layout (u32 words): nt | np << 8, seqno[nt], res[nt], counts[(nt+3)/4] (u8 x4),
-// peer[np] (id | count << 16 | relevant << 24), peer_res[np].
+// peer[np] (id | count << 16 | relevant << 24 | aligned << 25), peer_res[np] (valid if aligned).
 __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uint8_t* __restrict__ lens,
                                               const WalkState* __restrict__ ws, const uint8_t* __restrict__ ntop,
                                               const uint32_t* __restrict__ top_seqno,
                                               const uint8_t* __restrict__ top_count, const uint32_t* __restrict__ res,
                                               const uint8_t* __restrict__ npeer, const uint16_t* __restrict__ peer_id,
                                               const uint8_t* __restrict__ peer_count,
-                                              const uint32_t* __restrict__ peer_res, uint32_t* __restrict__ reccount,
+                                              const uint32_t* __restrict__ peer_res,
+                                              const unsigned long long* __restrict__ aligned,
+                                              uint32_t* __restrict__ reccount,
                                               HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
                                               const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
   const int lane = threadIdx.x & 63;
@@ -1241,14 +1261,15 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
   if (qs >= nqs) return;
   const WalkState w = ws[qs];
   const int np = npeer[qs];
-  bool rel = false;
+  bool rel = false, al = false;
   uint32_t pw = 0;
   if (np != 255 && lane < np) {
     const uint32_t id = peer_id[(int64_t)qs * kPeerCap + lane];
     const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + lane];
     const uint32_t ps = (uint32_t)w0 + id;
     rel = peer_relevant(w, cnt, lens[ps], ps);
-    pw = id | (cnt << 16) | (rel ? 1u << 24 : 0u);
+    al = (aligned[qs] >> lane) & 1ull;
+    pw = id | (cnt << 16) | (rel ? 1u << 24 : 0u) | (al ? 1u << 25 : 0u);
   }
   uint32_t base = 0xffffffffu;
   if (__any(rel)) {
@@ -1272,7 +1293,7 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     }
     if (lane < np) {
       r[1 + 2 * nt + ncw + lane] = pw;
-      r[1 + 2 * nt + ncw + np + lane] = rel ? peer_res[(int64_t)qs * kPeerCap + lane] : 0u;
+      r[1 + 2 * nt + ncw + np + lane] = al ? peer_res[(int64_t)qs * kPeerCap + lane] : 0u;
     }
   }
   // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform mask)
@@ -1309,11 +1330,11 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
 hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
-                       const uint32_t* peer_res, uint32_t* reccount, HostQs* hq, uint32_t* rec,
-                       const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
+                       const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
+                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pack, dim3((nqs + 3) / 4), dim3(256), 0, st, nqs, w0, lens, ws, ntop, top_seqno, top_count,
-                     res, npeer, peer_id, peer_count, peer_res, reccount, hq, rec, counters, hcounters);
+                     res, npeer, peer_id, peer_count, peer_res, aligned, reccount, hq, rec, counters, hcounters);
   return hipGetLastError();
 }
 

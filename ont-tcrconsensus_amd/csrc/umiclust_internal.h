@@ -123,6 +123,8 @@ struct PrefilterArgs {
   uint16_t* peer_id;       // [nqs*kPeerCap] window-local (seqno - peer_base)
   uint8_t* peer_count;     // [nqs*kPeerCap]
   uint8_t* npeer;          // [nqs] (255 = overflow)
+  uint8_t* strong;         // [seqno * 2 + strand] the query has a near-identical earlier window query
+  int32_t strong_eighths;  // ... sharing >= strong_eighths / 8 of its k-mers
   uint32_t* postings_touched;  // [1] atomic counter (stats)
   unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
 };
@@ -163,7 +165,8 @@ hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, hipStream_t st);
+                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
+                             unsigned long long* aligned, hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
 constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {
@@ -184,8 +187,8 @@ constexpr int kRecWords = 1 + 2 * kWalk + kWalk / 4 + 2 * kPeerCap;  // largest 
 hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
-                       const uint32_t* peer_res, uint32_t* reccount, HostQs* hq, uint32_t* rec,
-                       const uint32_t* counters, uint32_t* hcounters, hipStream_t st);
+                       const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
+                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st);
 // traceback (one wave per pair, any query length): ops[k*kOpsStride...] ('M','D','I' in alignment order,
 // right-aligned in the slot), nops[k], out[k] as launch_align's
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
