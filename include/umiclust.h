@@ -93,6 +93,7 @@ typedef struct umiclust_stats {
   double t_write_s;       /* file path: cluster<N> / consout (+ in-process parse) writing */
   double t_run_s;         /* file path: the whole call, read to files written */
   int64_t n_reruns;       /* block pieces re-run alone after an in-window peer list overflowed */
+  int64_t n_overlap_passes; /* overlap hash-table passes (1 + re-seeds after 64-bit hash collisions) */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;
@@ -194,6 +195,23 @@ int64_t umiclust_cluster_bin(umiclust_ctx *ctx, int32_t bin, umiclust_stats *sta
 /* umiclust_fetch for one clustered bin: arrays over the bin's input records (bin-local index) */
 int64_t umiclust_fetch_bin(umiclust_ctx *ctx, int32_t bin, int32_t *cluster, uint8_t *strand,
                            uint8_t *centroid, char *cons, int64_t cons_cap, int64_t *cons_off);
+
+/* ---- region-vs-region UMI overlap ---- */
+/* Replaces the Python string scans of /root/reference/ont_tcr_consensus/extract_umis.py.
+ * umiclust_overlap_counts: count_single_umi_overlaps (:270-290) for every UMI of set 1 at once:
+ *   counts[i] = number of set-2 sequences byte-equal to set-1 sequence i.
+ * umiclust_overlap_regions: count_overlapping_umis_between_2_regions (:293-342) for every region pair of
+ *   count_overlapping_umis_between_all_regions (:345-369): region r = sequences [region_start[r],
+ *   region_start[r+1]); for a < b, total[a * nregions + b] = the pair's summed count (the TSV value) and
+ *   maxcount[a * nregions + b] = the largest count of one region-a UMI (> 1 = the warning).  Entries with
+ *   a >= b are 0.  A GPU hash join: exact (byte comparison; a 64-bit hash collision re-runs with another
+ *   seed). */
+#define UMICLUST_OVERLAP_MAX_REGIONS 4096
+int32_t umiclust_overlap_counts(umiclust_ctx *ctx, const char *seqs1, const int64_t *offsets1, int64_t n1,
+                                const char *seqs2, const int64_t *offsets2, int64_t n2, int64_t *counts);
+int32_t umiclust_overlap_regions(umiclust_ctx *ctx, const char *seqs, const int64_t *offsets, int64_t n,
+                                 const int64_t *region_start, int32_t nregions, int64_t *total,
+                                 int32_t *maxcount);
 
 /* ---- kernel-level entry points (parity tests) ---- */
 /* Align npairs (query, target) pairs with the production alignment kernel.  Sequences are

@@ -2230,6 +2230,121 @@ int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const ch
   });
 }
 
+// ---------------------------------------------------------------- region overlap (§8f f3)
+namespace {
+// n sequences of nreg regions on the device, one table pass (re-seeded on a 64-bit hash collision)
+struct OvRun {
+  DevBuf<char> d_seq;
+  DevBuf<int64_t> d_off, d_rs, d_slot;
+  DevBuf<uint64_t> d_hash;
+  DevBuf<int32_t> d_reg;
+  DevBuf<unsigned long long> d_keys, d_rep;
+  DevBuf<uint32_t> d_cnt, d_start, d_cursor, d_bsum, d_members, d_coll;
+  OvBuffers B{};
+  uint64_t mask = 0;
+};
+
+void overlap_table(umiclust_ctx* c, OvRun& R, const char* seqs, const int64_t* offs, int64_t n,
+                   const int64_t* rstart, int32_t nreg, bool csr) {
+  if (n < 0 || nreg < 1 || (n > 0 && (!seqs || !offs)) || !rstart) c->fail(UMICLUST_EINVAL, "null argument");
+  if (rstart[0] != 0 || rstart[nreg] != n) c->fail(UMICLUST_EINVAL, "region boundaries must span [0, n]");
+  for (int32_t r = 0; r < nreg; r++)
+    if (rstart[r + 1] < rstart[r]) c->fail(UMICLUST_EINVAL, "region boundaries must not decrease");
+  if (n > (int64_t)UINT32_MAX / 2) c->fail(UMICLUST_ERANGE, "too many sequences");
+  uint64_t m = 1024;
+  while (m < (uint64_t)(2 * n)) m <<= 1;
+  R.mask = m - 1;
+  const int64_t bytes = n > 0 ? offs[n] - offs[0] : 0;
+  std::vector<int64_t> rel((size_t)n + 1);
+  for (int64_t i = 0; i <= n; i++) rel[i] = n > 0 ? offs[i] - offs[0] : 0;
+  c->hip(R.d_seq.ensure((size_t)bytes + 1), "alloc");
+  c->hip(R.d_off.ensure((size_t)n + 1), "alloc");
+  c->hip(R.d_rs.ensure((size_t)nreg + 1), "alloc");
+  c->hip(R.d_slot.ensure((size_t)n + 1), "alloc");
+  c->hip(R.d_hash.ensure((size_t)n + 1), "alloc");
+  c->hip(R.d_reg.ensure((size_t)n + 1), "alloc");
+  c->hip(R.d_keys.ensure(m), "alloc");
+  c->hip(R.d_rep.ensure(m), "alloc");
+  c->hip(R.d_cnt.ensure(m), "alloc");
+  c->hip(R.d_start.ensure(m + 1), "alloc");
+  c->hip(R.d_cursor.ensure(m), "alloc");
+  c->hip(R.d_bsum.ensure(m / 1024 + 1), "alloc");
+  c->hip(R.d_members.ensure((size_t)n + 1), "alloc");
+  c->hip(R.d_coll.ensure(1), "alloc");
+  if (bytes > 0) c->hip(hipMemcpyAsync(R.d_seq.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(R.d_off.p, rel.data(), rel.size() * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(R.d_rs.p, rstart, ((size_t)nreg + 1) * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  R.B = OvBuffers{R.d_hash.p, R.d_reg.p, R.d_keys.p, R.d_rep.p, R.d_slot.p, R.d_cnt.p, R.d_start.p, R.d_cursor.p,
+                  R.d_bsum.p, R.d_members.p, R.d_coll.p};
+  // a 64-bit collision between two different sequences is detected exactly; the next seed is tried
+  const uint64_t seeds[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull,
+                             0x082efa98ec4e6c89ull};
+  const bool test_collide = getenv("UMICLUST_OVERLAP_TEST_COLLIDE") != nullptr;  // first pass: 8-bit hashes
+  for (int k = 0; k < 4; k++) {
+    uint32_t coll = 0;
+    const uint64_t hmask = (test_collide && k == 0) ? 0xffull : ~0ull;
+    c->hip(launch_overlap_table(R.d_seq.p, R.d_off.p, n, R.d_rs.p, nreg, seeds[k], hmask, R.mask, R.B, csr, &coll,
+                                c->st),
+           "overlap table");
+    c->stats.n_overlap_passes++;
+    if (!coll) return;
+  }
+  c->fail(UMICLUST_EDEVICE, "overlap: 64-bit hash collisions under four seeds");
+}
+}  // namespace
+
+int32_t umiclust_overlap_counts(umiclust_ctx* c, const char* s1, const int64_t* off1, int64_t n1, const char* s2,
+                                const int64_t* off2, int64_t n2, int64_t* counts) {
+  UC_GUARD(c, {
+    if (n1 < 0 || n2 < 0 || (n1 > 0 && (!s1 || !off1 || !counts)) || (n2 > 0 && (!s2 || !off2)))
+      c->fail(UMICLUST_EINVAL, "null argument");
+    // one buffer: set 1 then set 2
+    std::vector<char> all;
+    std::vector<int64_t> off{0};
+    for (int64_t i = 0; i < n1; i++) {
+      all.insert(all.end(), s1 + off1[i], s1 + off1[i + 1]);
+      off.push_back((int64_t)all.size());
+    }
+    for (int64_t i = 0; i < n2; i++) {
+      all.insert(all.end(), s2 + off2[i], s2 + off2[i + 1]);
+      off.push_back((int64_t)all.size());
+    }
+    const int64_t n = n1 + n2, rs[3] = {0, n1, n};
+    OvRun R;
+    overlap_table(c, R, all.data(), off.data(), n, rs, 2, false);
+    DevBuf<int64_t> d_counts;
+    c->hip(d_counts.ensure((size_t)n1 + 1), "alloc");
+    c->hip(launch_overlap_two(R.B, R.mask, n, n1, d_counts.p, c->st), "overlap counts");
+    if (n1 > 0) c->hip(hipMemcpyAsync(counts, d_counts.p, (size_t)n1 * 8, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    return UMICLUST_OK;
+  });
+}
+
+int32_t umiclust_overlap_regions(umiclust_ctx* c, const char* seqs, const int64_t* offs, int64_t n,
+                                 const int64_t* region_start, int32_t nregions, int64_t* total, int32_t* maxcount) {
+  UC_GUARD(c, {
+    if (nregions < 1 || nregions > UMICLUST_OVERLAP_MAX_REGIONS || !total || !maxcount)
+      c->fail(UMICLUST_EINVAL, "1..%d regions and both outputs required", UMICLUST_OVERLAP_MAX_REGIONS);
+    OvRun R;
+    overlap_table(c, R, seqs, offs, n, region_start, nregions, true);
+    const size_t cells = (size_t)nregions * nregions;
+    DevBuf<unsigned long long> d_total;
+    DevBuf<uint32_t> d_max;
+    c->hip(d_total.ensure(cells), "alloc");
+    c->hip(d_max.ensure(cells), "alloc");
+    c->hip(hipMemsetAsync(d_total.p, 0, cells * 8, c->st), "memset");
+    c->hip(hipMemsetAsync(d_max.p, 0, cells * 4, c->st), "memset");
+    if (n > 0) c->hip(launch_overlap_pairs(R.B, R.mask, nregions, d_total.p, d_max.p, c->st), "overlap pairs");
+    std::vector<uint32_t> mx(cells);
+    c->hip(hipMemcpyAsync(total, d_total.p, cells * 8, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipMemcpyAsync(mx.data(), d_max.p, cells * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    for (size_t x = 0; x < cells; x++) maxcount[x] = (int32_t)mx[x];
+    return UMICLUST_OK;
+  });
+}
+
 int32_t umiclust_prep(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offsets,
                       int64_t n, char* masked, uint16_t* kmers, int32_t kstride, int32_t* nk) {
   UC_GUARD(c, {

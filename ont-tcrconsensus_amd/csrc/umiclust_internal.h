@@ -201,4 +201,31 @@ hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t ncl
                             const uint16_t* nops, char* cons, uint16_t* conslen,
                             int32_t* overflow, hipStream_t st);
 
+// ---- region-vs-region UMI overlap (overlap.hip) ----
+struct OvBuffers {
+  uint64_t* hash;                 // [n]
+  int32_t* region;                // [n]
+  unsigned long long* keys;       // [m] slot hash (~0 = empty)
+  unsigned long long* rep;        // [m] lowest member index
+  int64_t* slot;                  // [n]
+  uint32_t* cnt;                  // [m]
+  uint32_t* start;                // [m + 1]
+  uint32_t* cursor;               // [m]
+  uint32_t* bsum;                 // [m / 1024 + 1]
+  uint32_t* members;              // [n]
+  uint32_t* collision;            // [1]
+};
+// one hash-table pass over n sequences of nreg regions (region r = [rstart[r], rstart[r+1])), table of
+// mask + 1 slots; csr also buckets the members by slot.  Synchronous; *collided != 0 means two different
+// sequences shared a 64-bit hash (re-run with another seed).
+hipError_t launch_overlap_table(const char* seqs, const int64_t* offs, int64_t n, const int64_t* rstart, int32_t nreg,
+                                uint64_t seed, uint64_t hmask, uint64_t mask, const OvBuffers& B, bool csr,
+                                uint32_t* collided, hipStream_t st);
+// total[a * nreg + b] += c_a(s) c_b(s), maxc[a * nreg + b] = max c_b(s) over sequences s held by a and b (a < b)
+hipError_t launch_overlap_pairs(const OvBuffers& B, uint64_t mask, int32_t nreg, unsigned long long* total,
+                                uint32_t* maxc, hipStream_t st);
+// two sets (region 0 = the first n1 sequences, region 1 = the rest): counts[i] = equal sequences in set 2
+hipError_t launch_overlap_two(const OvBuffers& B, uint64_t mask, int64_t n, int64_t n1, int64_t* counts,
+                              hipStream_t st);
+
 }  // namespace uc

@@ -77,6 +77,7 @@ class Stats(C.Structure):
         ("t_write_s", C.c_double),
         ("t_run_s", C.c_double),
         ("n_reruns", C.c_int64),
+        ("n_overlap_passes", C.c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -101,8 +102,10 @@ EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
     "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin",
-    "umiclust_fetch_bin", "umiclust_align_pairs", "umiclust_prep",
+    "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_align_pairs",
+    "umiclust_prep",
 ]
+OVERLAP_MAX_REGIONS = 4096
 
 _lib = None
 
@@ -151,6 +154,12 @@ def lib() -> C.CDLL:
     L.umiclust_fetch_bin.restype = C.c_int64
     L.umiclust_fetch_bin.argtypes = [C.c_void_p, C.c_int32, P(C.c_int32), P(C.c_uint8), P(C.c_uint8), C.c_void_p,
                                      C.c_int64, P(C.c_int64)]
+    L.umiclust_overlap_counts.restype = C.c_int32
+    L.umiclust_overlap_counts.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, C.c_void_p, P(C.c_int64),
+                                          C.c_int64, P(C.c_int64)]
+    L.umiclust_overlap_regions.restype = C.c_int32
+    L.umiclust_overlap_regions.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64), C.c_int32,
+                                           P(C.c_int64), P(C.c_int32)]
     L.umiclust_align_pairs.restype = C.c_int32
     L.umiclust_align_pairs.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_void_p, P(C.c_int64),
                                        C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_int32,
@@ -306,6 +315,30 @@ class Context:
         raw = cons.tobytes()
         return dict(n_clusters=int(k), cluster=cl[:n], strand=sd[:n], centroid=ce[:n],
                     consensus=[raw[off[c]:off[c + 1]].decode() for c in range(k)])
+
+    def overlap_counts(self, seqs1, seqs2) -> np.ndarray:
+        """Per set-1 sequence, the number of byte-equal set-2 sequences (umiclust_overlap_counts)."""
+        b1, o1 = _pack(seqs1)
+        b2, o2 = _pack(seqs2)
+        n1 = len(o1) - 1
+        out = np.zeros(max(n1, 1), np.int64)
+        self._check(lib().umiclust_overlap_counts(self._h, b1.ctypes.data, _i64(o1), n1, b2.ctypes.data, _i64(o2),
+                                                  len(o2) - 1, _i64(out)), "overlap_counts")
+        return out[:n1]
+
+    def overlap_regions(self, regions) -> tuple[np.ndarray, np.ndarray]:
+        """regions: list of sequence lists.  (total, maxcount) R x R matrices, entries [a, b] for a < b."""
+        flat = [s for r in regions for s in r]
+        buf, off = _pack(flat)
+        rs = np.zeros(len(regions) + 1, np.int64)
+        np.cumsum([len(r) for r in regions], out=rs[1:])
+        R = len(regions)
+        tot = np.zeros(R * R, np.int64)
+        mx = np.zeros(R * R, np.int32)
+        self._check(lib().umiclust_overlap_regions(self._h, buf.ctypes.data, _i64(off), len(flat), _i64(rs), R,
+                                                   _i64(tot), mx.ctypes.data_as(C.POINTER(C.c_int32))),
+                    "overlap_regions")
+        return tot.reshape(R, R), mx.reshape(R, R)
 
     def align_pairs(self, p: Params, queries, targets, with_ops: bool = False) -> dict:
         qb, qo = _pack(queries)

@@ -10,8 +10,10 @@ Follows ont_tcr_consensus/extract_umis.py:
 The O(n*m) per-UMI scan becomes a multiset join (count of region-2 sequences equal to each region-1
 sequence), which gives the same per-UMI counts.  Upstream appends TSV rows in Ray completion order;
 here rows follow itertools.combinations order (the only deterministic choice).
-Parity unpinned: the reference ships no fixture for this function; tests pin it against a literal
-pairwise restatement of extract_umis.py:280-288 on seeded inputs.
+Parity pinned: tests/golden/overlap/*.json are the outputs of the reference's own extract_umis.py, run here
+with pass-through stand-ins for the uninstalled ray/pysam/edlib (tests/golden/make_golden_overlap.py);
+tests/test_overlap_cpu.py checks this restatement against them (return list, TSV, warning file, the
+empty-region-1 ValueError) and against a literal pairwise restatement of extract_umis.py:280-288.
 """
 from __future__ import annotations
 

@@ -59,3 +59,44 @@ def test_empty_region_1_raises(tmp_path):
     _write_consout(b, ["ACGT"])
     with pytest.raises(ValueError):
         overlap.count_overlapping_umis_between_2_regions(a, b, str(tmp_path / "t.tsv"), 0)
+
+
+def _golden():
+    import glob
+    import json
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "overlap")
+    return [json.load(open(p)) for p in sorted(glob.glob(os.path.join(d, "*.json")))]
+
+
+def materialize(tmp_path, case):
+    """Write a fixture's regions as <region>/umi_clusters_consensus.fasta (its own wrap width)."""
+    dirs = []
+    for reg in case["regions"]:
+        d = tmp_path / reg["name"]
+        d.mkdir()
+        with open(d / "umi_clusters_consensus.fasta", "w") as fh:
+            for i, s in enumerate(reg["seqs"]):
+                fh.write(f">centroid=r{i};strand=+;seqs={1 + i % 5};clusterid={i}\n")
+                for j in range(0, max(1, len(s)), case["width"]):
+                    fh.write(s[j:j + case["width"]] + "\n")
+        dirs.append(str(d))
+    logs = tmp_path / "logs"
+    logs.mkdir()
+    return [os.path.join(d, "smolecule_filtered.fa") for d in dirs], str(logs)
+
+
+def run_and_compare(fn, tmp_path, case):
+    fas, logs = materialize(tmp_path, case)
+    if case["error"]:
+        with pytest.raises(ValueError):
+            fn(fas, 2, logs)
+    else:
+        assert fn(fas, 2, logs) == case["result"]
+    got = {f: open(os.path.join(logs, f)).read() for f in sorted(os.listdir(logs))}
+    assert got == case["files"]
+
+
+@pytest.mark.parametrize("case", _golden(), ids=[c["name"] for c in _golden()])
+def test_oracle_matches_reference_fixtures(tmp_path, case):
+    """Pinned: tests/golden/overlap/*.json are the reference's own outputs (make_golden_overlap.py)."""
+    run_and_compare(overlap.count_overlapping_umis_between_all_regions, tmp_path, case)
