@@ -213,6 +213,22 @@ int32_t umiclust_overlap_regions(umiclust_ctx *ctx, const char *seqs, const int6
                                  const int64_t *region_start, int32_t nregions, int64_t *total,
                                  int32_t *maxcount);
 
+/* ---- UMI extraction ---- */
+/* Replaces extract_umis (/root/reference/ont_tcr_consensus/extract_umis.py:189-267): per read, the first
+ * adapter_length_5_end and the last adapter_length_3_end bases (:110-126) are searched for umi_fwd / umi_rev
+ * as edlib does (:89-107: mode "HW", task "path", k = max_pattern_dist, the IUPAC additionalEqualities of
+ * :26-87).  umiclust_extract_umis: out[i*6 + 0..2] = (edit distance or -1, start, end) of the 5' UMI in
+ * its window, out[i*6 + 3..5] of the 3' UMI.  umiclust_extract_umis_file: FASTA or FASTQ in, the
+ * <region>_detected_umis.fasta records of write_fasta (:154-186) out, in input order; returns the number
+ * of reads with both UMIs (the reference's n_both_umi).  Patterns of 1..64 symbols.  A record name
+ * without "strand=" is UMICLUST_EFORMAT ("Read strand not annotated!"). */
+int32_t umiclust_extract_umis(umiclust_ctx *ctx, const char *seqs, const int64_t *offsets, int64_t n,
+                              int32_t adapter_length_5_end, int32_t adapter_length_3_end,
+                              int32_t max_pattern_dist, const char *umi_fwd, const char *umi_rev, int32_t *out);
+int64_t umiclust_extract_umis_file(umiclust_ctx *ctx, const char *fastx_file, const char *out_fasta,
+                                   int32_t adapter_length_5_end, int32_t adapter_length_3_end,
+                                   int32_t max_pattern_dist, const char *umi_fwd, const char *umi_rev);
+
 /* ---- kernel-level entry points (parity tests) ---- */
 /* Align npairs (query, target) pairs with the production alignment kernel.  Sequences are
  * ASCII; q/t record k at [q_off[k], q_off[k+1]).  Outputs per pair: score, matches,

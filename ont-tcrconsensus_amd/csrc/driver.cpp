@@ -2345,6 +2345,230 @@ int32_t umiclust_overlap_regions(umiclust_ctx* c, const char* seqs, const int64_
   });
 }
 
+// ---------------------------------------------------------------- UMI extraction (§8f f1)
+namespace {
+// additionalEqualities of extract_umis.py:26-87 (either order), plus identity
+const char* const kIupacEq[] = {"MA", "MC", "RA", "RG", "WA", "WT", "SC", "SG", "YC", "YT", "KG", "KT", "VA", "VC",
+                                "VG", "HA", "HC", "HT", "DA", "DG", "DT", "BC", "BG", "BT", "NA", "NC", "NG", "NT",
+                                "ma", "mc", "ra", "rg", "wa", "wt", "sc", "sg", "yc", "yt", "kg", "kt", "va", "vc",
+                                "vg", "ha", "hc", "ht", "da", "dg", "dt", "bc", "bg", "bt", "na", "nc", "ng", "nt",
+                                "aA", "cC", "tT", "gG"};
+
+void build_patterns(umiclust_ctx* c, const char* fwd, const char* rev, ExtractPatterns& P) {
+  static bool eqt[256][256];
+  static bool init = false;
+  if (!init) {
+    for (int a = 0; a < 256; a++)
+      for (int b = 0; b < 256; b++) eqt[a][b] = a == b;
+    for (const char* e : kIupacEq) {
+      eqt[(uint8_t)e[0]][(uint8_t)e[1]] = true;
+      eqt[(uint8_t)e[1]][(uint8_t)e[0]] = true;
+    }
+    init = true;
+  }
+  memset(&P, 0, sizeof(P));
+  const char* pats[2] = {fwd, rev};
+  for (int w = 0; w < 2; w++) {
+    if (!pats[w]) c->fail(UMICLUST_EINVAL, "null pattern");
+    const int m = (int)strlen(pats[w]);
+    if (m < 1 || m > 64) c->fail(UMICLUST_EINVAL, "UMI patterns of 1..64 symbols are supported (got %d)", m);
+    P.m[w] = m;
+    for (int ch = 0; ch < 256; ch++)
+      for (int i = 0; i < m; i++) {
+        if (eqt[(uint8_t)pats[w][i]][ch]) P.peq[w][ch] |= 1ull << i;
+        if (eqt[(uint8_t)pats[w][m - 1 - i]][ch]) P.peqr[w][ch] |= 1ull << i;
+      }
+  }
+}
+
+void extract_device(umiclust_ctx* c, const char* seqs, const int64_t* offs, int64_t n, int32_t a5, int32_t a3,
+                    int32_t k, const char* fwd, const char* rev, int32_t* out) {
+  if (n < 0 || (n > 0 && (!seqs || !offs || !out)) || a5 < 0 || a3 < 0 || k < 0)
+    c->fail(UMICLUST_EINVAL, "bad argument");
+  ExtractPatterns P;
+  build_patterns(c, fwd, rev, P);
+  if (n == 0) return;
+  const int64_t bytes = offs[n] - offs[0];
+  std::vector<int64_t> rel((size_t)n + 1);
+  for (int64_t i = 0; i <= n; i++) rel[i] = offs[i] - offs[0];
+  DevBuf<char> d_s;
+  DevBuf<int64_t> d_o;
+  DevBuf<ExtractPatterns> d_p;
+  DevBuf<int32_t> d_out;
+  c->hip(d_s.ensure((size_t)bytes + 1), "alloc");
+  c->hip(d_o.ensure((size_t)n + 1), "alloc");
+  c->hip(d_p.ensure(1), "alloc");
+  c->hip(d_out.ensure((size_t)n * 6), "alloc");
+  if (bytes > 0) c->hip(hipMemcpyAsync(d_s.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(d_o.p, rel.data(), rel.size() * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(d_p.p, &P, sizeof(P), hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(launch_extract(d_s.p, d_o.p, n, a5, a3, k, d_p.p, d_out.p, c->st), "extract");
+  c->hip(hipMemcpyAsync(out, d_out.p, (size_t)n * 6 * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+  c->hip(hipStreamSynchronize(c->st), "sync");
+}
+
+// FASTQ records (pysam.FastxFile): '@' header (name up to whitespace), sequence lines up to the '+' line, then
+// as many quality characters as sequence ones
+bool read_fastq(const char* path, Fasta& f) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return false;
+  }
+  f.size = (size_t)sb.st_size;
+  if (f.size > 0) {
+    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (f.map == MAP_FAILED) {
+      f.map = nullptr;
+      close(fd);
+      return false;
+    }
+    f.data = (const char*)f.map;
+  }
+  close(fd);
+  const char* d = f.data;
+  const size_t N = f.size;
+  size_t i = 0;
+  f.seq_off.push_back(0);
+  auto line_end = [&](size_t x) {
+    const char* nl = (const char*)memchr(d + x, '\n', N - x);
+    return nl ? (size_t)(nl - d) : N;
+  };
+  while (i < N) {
+    if (d[i] == '\n' || d[i] == '\r') { i++; continue; }
+    if (d[i] != '@') return false;
+    const size_t e = line_end(i);
+    size_t k = i + 1;
+    while (k < e && d[k] != '\r' && d[k] != ' ' && d[k] != '\t') k++;
+    f.hdr_off.push_back((int64_t)(i + 1));
+    f.hdr_len.push_back((int32_t)(k - i - 1));
+    i = e + 1;
+    size_t nseq = 0;
+    while (i < N && d[i] != '+') {
+      const size_t le = line_end(i);
+      for (size_t x = i; x < le; x++)
+        if (d[x] != '\r') {
+          f.seq.push_back(d[x]);
+          nseq++;
+        }
+      i = le + 1;
+    }
+    if (i >= N) return false;
+    i = line_end(i) + 1;  // the '+' line
+    size_t nq = 0;
+    while (i < N && nq < nseq) {
+      const size_t le = line_end(i);
+      for (size_t x = i; x < le; x++) nq += d[x] != '\r';
+      i = le + 1;
+    }
+    f.seq_off.push_back((int64_t)f.seq.size());
+  }
+  return true;
+}
+
+// the reverse_complement of extract_umis.py:10-12: str.translate("ACTG" -> "TGAC"), reversed
+void revcomp_ref(const char* s, size_t n, std::string& out) {
+  for (size_t x = n; x-- > 0;) {
+    const char ch = s[x];
+    out.push_back(ch == 'A' ? 'T' : ch == 'C' ? 'G' : ch == 'T' ? 'A' : ch == 'G' ? 'C' : ch);
+  }
+}
+}  // namespace
+
+int32_t umiclust_extract_umis(umiclust_ctx* c, const char* seqs, const int64_t* offsets, int64_t n,
+                              int32_t adapter_length_5_end, int32_t adapter_length_3_end, int32_t max_pattern_dist,
+                              const char* umi_fwd, const char* umi_rev, int32_t* out) {
+  UC_GUARD(c, {
+    extract_device(c, seqs, offsets, n, adapter_length_5_end, adapter_length_3_end, max_pattern_dist, umi_fwd,
+                   umi_rev, out);
+    return UMICLUST_OK;
+  });
+}
+
+int64_t umiclust_extract_umis_file(umiclust_ctx* c, const char* fastx_file, const char* out_fasta,
+                                   int32_t adapter_length_5_end, int32_t adapter_length_3_end,
+                                   int32_t max_pattern_dist, const char* umi_fwd, const char* umi_rev) {
+  UC_GUARD(c, {
+    if (!fastx_file || !out_fasta) c->fail(UMICLUST_EINVAL, "null path");
+    Fasta f;
+    bool fastq = false;
+    {
+      FILE* fp = fopen(fastx_file, "rb");
+      if (!fp) c->fail(UMICLUST_EIO, "cannot read %s", fastx_file);
+      int ch;
+      while ((ch = fgetc(fp)) == '\n' || ch == '\r') {}
+      fastq = ch == '@';
+      fclose(fp);
+    }
+    if (!(fastq ? read_fastq(fastx_file, f) : read_fasta(fastx_file, f)))
+      c->fail(UMICLUST_EIO, "cannot parse %s", fastx_file);
+    const int64_t n = (int64_t)f.hdr_off.size();
+    std::vector<int32_t> res((size_t)std::max<int64_t>(n, 1) * 6);
+    extract_device(c, f.seq.data(), f.seq_off.data(), n, adapter_length_5_end, adapter_length_3_end, max_pattern_dist,
+                   umi_fwd, umi_rev, res.data());
+    // records in input order; the reference raises at the first record without a strand annotation, after
+    // writing the records before it: those are written, then the error is returned
+    std::vector<std::string> strand(n), rid(n);
+    int64_t ngood = n;
+    for (int64_t i = 0; i < n; i++) {
+      const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
+      Sv st;
+      if (!split1(name, "strand=", st)) {
+        ngood = i;
+        break;
+      }
+      strand[i] = st.str();
+      const char* semi = (const char*)memchr(name.p, ';', name.n);
+      rid[i] = std::string(name.p, semi ? (size_t)(semi - name.p) : name.n);
+    }
+    const int T = ngood < 4096 ? 1 : io_threads();
+    std::vector<std::string> part(T);
+    std::vector<int64_t> cnt(T, 0);
+    parallel_for(T, [&](int t) {
+      std::string& o = part[t];
+      for (int64_t i = ngood * t / T; i < ngood * (t + 1) / T; i++) {
+        const int32_t* r = res.data() + i * 6;
+        if (r[0] < 0 || r[3] < 0) continue;  // `if not umi_5p or not umi_3p`
+        const char* s = f.seq.data() + f.seq_off[i];
+        const int64_t len = f.seq_off[i + 1] - f.seq_off[i];
+        const int64_t w3 = (adapter_length_3_end == 0 || adapter_length_3_end > len) ? len : adapter_length_3_end;
+        const char* u5 = s + r[1];
+        const size_t l5 = (size_t)(r[2] - r[1] + 1);
+        const char* u3 = s + (len - w3) + r[4];
+        const size_t l3 = (size_t)(r[5] - r[4] + 1);
+        cnt[t]++;
+        o += ">" + rid[i] + ";strand=" + strand[i] + ";umi_fwd_dist=" + std::to_string(r[0]) + ";umi_rev_dist=" +
+             std::to_string(r[3]) + ";umi_fwd_seq=";
+        o.append(u5, l5);
+        o += ";umi_rev_seq=";
+        o.append(u3, l3);
+        o += ";seq=";
+        o.append(s, (size_t)len);
+        o.push_back('\n');
+        if (strand[i] == "+") {
+          o.append(u5, l5);
+          o.append(u3, l3);
+        } else {
+          revcomp_ref(u3, l3, o);
+          revcomp_ref(u5, l5, o);
+        }
+        o.push_back('\n');
+      }
+    });
+    const int fd = open(out_fasta, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    bool ok = fd >= 0;
+    for (int t = 0; ok && t < T; t++) ok = write_all(fd, part[t].data(), part[t].size());
+    if (fd >= 0) ok = (close(fd) == 0) && ok;
+    if (!ok) c->fail(UMICLUST_EIO, "cannot write %s", out_fasta);
+    if (ngood < n) c->fail(UMICLUST_EFORMAT, "Read strand not annotated!");
+    int64_t tot = 0;
+    for (int64_t v : cnt) tot += v;
+    return tot;
+  });
+}
+
 int32_t umiclust_prep(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offsets,
                       int64_t n, char* masked, uint16_t* kmers, int32_t kstride, int32_t* nk) {
   UC_GUARD(c, {

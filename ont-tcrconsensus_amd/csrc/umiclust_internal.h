@@ -228,4 +228,15 @@ hipError_t launch_overlap_pairs(const OvBuffers& B, uint64_t mask, int32_t nreg,
 hipError_t launch_overlap_two(const OvBuffers& B, uint64_t mask, int64_t n, int64_t n1, int64_t* counts,
                               hipStream_t st);
 
+// ---- UMI extraction (extract.hip) ----
+struct ExtractPatterns {
+  uint64_t peq[2][256];   // [fwd | rev pattern][byte]: bit i = pattern[i] equals the byte
+  uint64_t peqr[2][256];  // same for the reversed pattern
+  int32_t m[2];           // pattern lengths (1..64)
+  int32_t pad[2];
+};
+// out[(i * 2 + w) * 3 ...] = (edit distance or -1, start, end) of edlib HW locations[0] in window w of read i
+hipError_t launch_extract(const char* seqs, const int64_t* offs, int64_t n, int32_t a5, int32_t a3, int32_t k,
+                          const ExtractPatterns* P, int32_t* out, hipStream_t st);
+
 }  // namespace uc

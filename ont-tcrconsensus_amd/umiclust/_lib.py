@@ -102,8 +102,8 @@ EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
     "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin",
-    "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_align_pairs",
-    "umiclust_prep",
+    "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
+    "umiclust_extract_umis_file", "umiclust_align_pairs", "umiclust_prep",
 ]
 OVERLAP_MAX_REGIONS = 4096
 
@@ -160,6 +160,12 @@ def lib() -> C.CDLL:
     L.umiclust_overlap_regions.restype = C.c_int32
     L.umiclust_overlap_regions.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64), C.c_int32,
                                            P(C.c_int64), P(C.c_int32)]
+    L.umiclust_extract_umis.restype = C.c_int32
+    L.umiclust_extract_umis.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                        C.c_char_p, C.c_char_p, P(C.c_int32)]
+    L.umiclust_extract_umis_file.restype = C.c_int64
+    L.umiclust_extract_umis_file.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_int32,
+                                             C.c_char_p, C.c_char_p]
     L.umiclust_align_pairs.restype = C.c_int32
     L.umiclust_align_pairs.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_void_p, P(C.c_int64),
                                        C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_int32,
@@ -339,6 +345,20 @@ class Context:
                                                    _i64(tot), mx.ctypes.data_as(C.POINTER(C.c_int32))),
                     "overlap_regions")
         return tot.reshape(R, R), mx.reshape(R, R)
+
+    def extract_umis(self, seqs, a5: int = 73, a3: int = 68, k: int = 3, fwd: str = "", rev: str = "") -> np.ndarray:
+        """[n, 6] int32: (dist, start, end) of the 5' and 3' UMI per read (-1: none), window coordinates."""
+        buf, off = _pack(seqs)
+        n = len(off) - 1
+        out = np.zeros(max(n, 1) * 6, np.int32)
+        self._check(lib().umiclust_extract_umis(self._h, buf.ctypes.data, _i64(off), n, a5, a3, k, fwd.encode(),
+                                                rev.encode(), out.ctypes.data_as(C.POINTER(C.c_int32))),
+                    "extract_umis")
+        return out[:n * 6].reshape(n, 6)
+
+    def extract_umis_file(self, fastx: str, out_fasta: str, a5: int, a3: int, k: int, fwd: str, rev: str) -> int:
+        return int(self._check(lib().umiclust_extract_umis_file(self._h, fastx.encode(), out_fasta.encode(), a5, a3, k,
+                                                                fwd.encode(), rev.encode()), "extract_umis_file"))
 
     def align_pairs(self, p: Params, queries, targets, with_ops: bool = False) -> dict:
         qb, qo = _pack(queries)
