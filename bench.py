@@ -35,28 +35,46 @@ L2_GATHER_GBS = 18800.0    # MI355X_MICROARCH.md "Indexed rows: gather into LDS"
 # "v_fma_f32 (wave64) 2 cyc (SIMD-32)"); lane-instructions per second
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
 # VALU wave-instructions per alignment cell of k_align_pk, measured: SQ_INSTS_VALU x 64 / cells computed
-# (profiles/); updated with the kernel
-ALIGN_VALU_PER_CELL = 15.7
+# (profiles/r02/pmc_c2.json: SQ_INSTS_VALU of every k_align_pk x 64 / cells_computed of the step)
+ALIGN_VALU_PER_CELL = 17.9
 
 
 def cpu_baseline_bins(bins, identity: float, lens, budget_s: float = 20.0, preset: int = 1) -> dict:
-    """The C oracle (oracle/, 1 thread) over whole bins, largest first, until ~budget_s of CPU time."""
+    """The C oracle (oracle/) over whole bins on every host core the process may use (the reference runs one
+    vsearch process per bin, utils.py:56-63): one thread per core pulls bins largest first until ~budget_s of
+    wall time, each bin clustered whole; UMIs/s = the kept UMIs of the finished bins / wall time."""
+    import concurrent.futures as cf
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
-    done, kept, t = [], 0, 0.0
-    for b in sorted(bins, key=lambda b: -b.umis.n):
-        if t > budget_s:
-            break
-        seqs = b.umis.as_list()
-        t0 = time.perf_counter()
-        r = orc.cluster(orc.params(preset, identity, *lens), seqs)
-        t += time.perf_counter() - t0
-        kept += r["stats"]["kept"]
-        done.append(b.umis.n)
-    return dict(value=kept / t if t else 0.0, unit="UMIs/s", cores=1, kind="port",
-                sample=f"{len(done)} whole bins (largest first, {sum(done)} reads, sizes {done[:5]}...) clustered "
-                       f"by the C oracle restatement, 1 thread, {t:.1f} s",
-                seconds=t, n_kept=kept)
+    cores = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
+    order = sorted(bins, key=lambda b: -b.umis.n)
+    orc.cluster(orc.params(preset, identity, *lens), order[-1].umis.as_list())  # library load / tables
+    lock = threading.Lock()
+    state = dict(next=0, kept=0, reads=0, done=0)
+    t0 = time.perf_counter()
+
+    def worker(_):
+        while True:
+            with lock:
+                if state["next"] >= len(order) or time.perf_counter() - t0 > budget_s:
+                    return
+                b = order[state["next"]]
+                state["next"] += 1
+            r = orc.cluster(orc.params(preset, identity, *lens), b.umis.as_list())
+            with lock:
+                state["kept"] += r["stats"]["kept"]
+                state["reads"] += b.umis.n
+                state["done"] += 1
+
+    with cf.ThreadPoolExecutor(cores) as ex:
+        list(ex.map(worker, range(cores)))
+    t = time.perf_counter() - t0
+    return dict(value=state["kept"] / t if t else 0.0, unit="UMIs/s", cores=cores, kind="port",
+                sample=f"{state['done']} of {len(order)} whole bins, largest first ({state['reads']} reads), clustered "
+                       f"by the C oracle restatement on {cores} threads (one bin per thread), {t:.1f} s wall; the "
+                       f"largest bins are the slowest per UMI, so the full set runs faster per UMI on the CPU",
+                seconds=t, n_kept=state["kept"])
 
 
 def cpu_baseline_prefix(umis, n_sample: int, identity: float, lens, preset: int = 1) -> dict:

@@ -229,6 +229,25 @@ int64_t umiclust_extract_umis_file(umiclust_ctx *ctx, const char *fastx_file, co
                                    int32_t adapter_length_5_end, int32_t adapter_length_3_end,
                                    int32_t max_pattern_dist, const char *umi_fwd, const char *umi_rev);
 
+/* ---- region binning ---- */
+/* Replaces the record loop of filter_and_split_reads_by_region_cluster
+ * (/root/reference/ont_tcr_consensus/region_split.py:219-333): BAM in (BGZF inflated on the host threads,
+ * records classified and FASTA records built on the device), every kept primary alignment appended to
+ * <out_dir>/region_cluster<k>.fasta as `>{query_name};strand={+|-}` + its forward sequence, in BAM order.
+ * Regions come from the reference FASTA (names, lengths) and the cluster JSON (region_clusters[r], -1 if the
+ * region is not in it).  counts = {n_unmapped, n_primary_mapped, n_short, n_long} of the records the
+ * reference's loop reaches; reads_per_cluster[k] (ncluster_cap entries); region_detected[r] = 1 if a kept
+ * record aligned to region r.  Returns the number of cluster files appended to.  A record aligned to a
+ * reference missing from the regions (or from the cluster JSON once it passes the filters) stops the loop
+ * as the reference's KeyError does: the records before it are written and UMICLUST_EFORMAT is returned with
+ * the name in missing_name. */
+int64_t umiclust_region_split(umiclust_ctx *ctx, const char *bam_file, int32_t nregions,
+                              const char *const *region_names, const int64_t *region_lengths,
+                              const int32_t *region_clusters, double minimal_region_overlap,
+                              int32_t max_softclip_5_end, int32_t max_softclip_3_end, const char *out_dir,
+                              int64_t *counts, int64_t *reads_per_cluster, int32_t ncluster_cap,
+                              uint8_t *region_detected, char *missing_name, int32_t missing_cap);
+
 /* ---- kernel-level entry points (parity tests) ---- */
 /* Align npairs (query, target) pairs with the production alignment kernel.  Sequences are
  * ASCII; q/t record k at [q_off[k], q_off[k+1]).  Outputs per pair: score, matches,

@@ -38,7 +38,9 @@
 #include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
+#include <unordered_map>
 #include <vector>
+#include <zlib.h>
 
 #include "../../include/umiclust.h"
 #include "umiclust_internal.h"
@@ -2566,6 +2568,223 @@ int64_t umiclust_extract_umis_file(umiclust_ctx* c, const char* fastx_file, cons
     int64_t tot = 0;
     for (int64_t v : cnt) tot += v;
     return tot;
+  });
+}
+
+// ---------------------------------------------------------------- region binning (§8f f4)
+namespace {
+// BGZF (SAM/BAM specification §4.1): gzip members with a BC extra field holding BSIZE; every block is
+// inflated independently, so the blocks are split over the host threads
+bool inflate_bgzf(umiclust_ctx* c, const char* path, std::vector<uint8_t>& raw) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return false;
+  }
+  const size_t N = (size_t)sb.st_size;
+  void* map = N ? mmap(nullptr, N, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0) : nullptr;
+  close(fd);
+  if (N && map == MAP_FAILED) return false;
+  const uint8_t* d = (const uint8_t*)map;
+  std::vector<size_t> boff, bsz;
+  std::vector<uint32_t> isz;
+  size_t o = 0;
+  bool ok = true;
+  while (o + 18 <= N) {
+    if (d[o] != 31 || d[o + 1] != 139 || d[o + 2] != 8 || !(d[o + 3] & 4)) { ok = false; break; }
+    const size_t xlen = (size_t)d[o + 10] | ((size_t)d[o + 11] << 8);
+    size_t bs = 0;
+    for (size_t x = o + 12; x + 4 <= o + 12 + xlen;) {
+      const size_t sl = (size_t)d[x + 2] | ((size_t)d[x + 3] << 8);
+      if (d[x] == 66 && d[x + 1] == 67 && sl == 2) bs = ((size_t)d[x + 4] | ((size_t)d[x + 5] << 8)) + 1;
+      x += 4 + sl;
+    }
+    if (!bs || o + bs > N) { ok = false; break; }
+    boff.push_back(o);
+    bsz.push_back(bs);
+    isz.push_back((uint32_t)d[o + bs - 4] | ((uint32_t)d[o + bs - 3] << 8) | ((uint32_t)d[o + bs - 2] << 16) |
+                  ((uint32_t)d[o + bs - 1] << 24));
+    o += bs;
+  }
+  if (ok && o != N) ok = false;
+  std::vector<size_t> uo(boff.size() + 1, 0);
+  for (size_t b = 0; b < boff.size(); b++) uo[b + 1] = uo[b] + isz[b];
+  if (ok) {
+    raw.resize(uo.back());
+    const int T = std::max(1, std::min<int>(io_threads(), (int)boff.size()));
+    std::vector<int> bad(T, 0);
+    parallel_for(T, [&](int t) {
+      for (size_t b = (size_t)t; b < boff.size(); b += (size_t)T) {
+        if (!isz[b]) continue;
+        const size_t xlen = (size_t)d[boff[b] + 10] | ((size_t)d[boff[b] + 11] << 8);
+        z_stream zs{};
+        if (inflateInit2(&zs, -15) != Z_OK) { bad[t] = 1; return; }
+        zs.next_in = const_cast<Bytef*>(d + boff[b] + 12 + xlen);
+        zs.avail_in = (uInt)(bsz[b] - 12 - xlen - 8);
+        zs.next_out = raw.data() + uo[b];
+        zs.avail_out = isz[b];
+        const int rc = inflate(&zs, Z_FINISH);
+        inflateEnd(&zs);
+        if (rc != Z_STREAM_END || zs.avail_out != 0) { bad[t] = 1; return; }
+      }
+    });
+    for (int v : bad) ok = ok && !v;
+  }
+  if (map) munmap(map, N);
+  (void)c;
+  return ok;
+}
+
+int32_t rd_i32(const uint8_t* p) { int32_t v; memcpy(&v, p, 4); return v; }
+}  // namespace
+
+int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nregions, const char* const* region_names,
+                              const int64_t* region_lengths, const int32_t* region_clusters,
+                              double minimal_region_overlap, int32_t max_softclip_5_end, int32_t max_softclip_3_end,
+                              const char* out_dir, int64_t* counts, int64_t* reads_per_cluster, int32_t ncluster_cap,
+                              uint8_t* region_detected, char* missing_name, int32_t missing_cap) {
+  UC_GUARD(c, {
+    if (!bam_file || !out_dir || nregions < 0 || (nregions > 0 && (!region_names || !region_lengths || !region_clusters)) ||
+        !counts || ncluster_cap < 0 || (ncluster_cap > 0 && !reads_per_cluster))
+      c->fail(UMICLUST_EINVAL, "bad argument");
+    std::vector<uint8_t> raw;
+    if (!inflate_bgzf(c, bam_file, raw)) c->fail(UMICLUST_EIO, "cannot read BGZF/BAM %s", bam_file);
+    if (raw.size() < 12 || memcmp(raw.data(), "BAM\1", 4) != 0) c->fail(UMICLUST_EFORMAT, "%s is not BAM", bam_file);
+    // header: text, then the reference names, matched to the regions of the reference FASTA
+    std::unordered_map<std::string, int32_t> rid;
+    for (int32_t r = 0; r < nregions; r++) rid.emplace(region_names[r], r);
+    size_t o = 4;
+    const int32_t lt = rd_i32(raw.data() + o);
+    o += 4 + (size_t)lt;
+    const int32_t nref = rd_i32(raw.data() + o);
+    o += 4;
+    std::vector<std::string> refname(nref);
+    std::vector<int64_t> rlen(nref, -1);
+    std::vector<int32_t> rclu(nref, -1), rreg(nref, -1);
+    for (int32_t r = 0; r < nref; r++) {
+      const int32_t ln = rd_i32(raw.data() + o);
+      refname[r] = std::string((const char*)raw.data() + o + 4, (size_t)std::max(0, ln - 1));
+      o += 4 + (size_t)ln + 4;
+      auto it = rid.find(refname[r]);
+      if (it != rid.end()) {
+        rreg[r] = it->second;
+        rlen[r] = region_lengths[it->second];
+        rclu[r] = region_clusters[it->second];
+      }
+    }
+    std::vector<int64_t> roff;
+    while (o + 4 <= raw.size()) {
+      roff.push_back((int64_t)o);
+      o += 4 + (size_t)rd_i32(raw.data() + o);
+    }
+    if (o != raw.size()) c->fail(UMICLUST_EFORMAT, "truncated BAM record");
+    const int64_t n = (int64_t)roff.size();
+    // device: classify every record
+    DevBuf<uint8_t> d_raw;
+    DevBuf<int64_t> d_roff, d_rlen, d_outlen, d_pos;
+    DevBuf<int32_t> d_rclu, d_clu;
+    DevBuf<int8_t> d_cls;
+    c->hip(d_raw.ensure(raw.size() + 1), "alloc");
+    c->hip(d_roff.ensure((size_t)n + 1), "alloc");
+    c->hip(d_rlen.ensure((size_t)nref + 1), "alloc");
+    c->hip(d_rclu.ensure((size_t)nref + 1), "alloc");
+    c->hip(d_cls.ensure((size_t)n + 1), "alloc");
+    c->hip(d_clu.ensure((size_t)n + 1), "alloc");
+    c->hip(d_outlen.ensure((size_t)n + 1), "alloc");
+    c->hip(d_pos.ensure((size_t)n + 1), "alloc");
+    c->hip(hipMemcpyAsync(d_raw.p, raw.data(), raw.size(), hipMemcpyHostToDevice, c->st), "h2d");
+    if (n) c->hip(hipMemcpyAsync(d_roff.p, roff.data(), (size_t)n * 8, hipMemcpyHostToDevice, c->st), "h2d");
+    if (nref) {
+      c->hip(hipMemcpyAsync(d_rlen.p, rlen.data(), (size_t)nref * 8, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(d_rclu.p, rclu.data(), (size_t)nref * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    }
+    c->hip(launch_bam_classify(d_raw.p, d_roff.p, n, nref, d_rlen.p, d_rclu.p, minimal_region_overlap,
+                               max_softclip_5_end, max_softclip_3_end, d_cls.p, d_clu.p, d_outlen.p, c->st),
+           "bam classify");
+    std::vector<int8_t> cls(n);
+    std::vector<int32_t> clu(n);
+    std::vector<int64_t> olen(n);
+    if (n) {
+      c->hip(hipMemcpyAsync(cls.data(), d_cls.p, (size_t)n, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(clu.data(), d_clu.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(olen.data(), d_outlen.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->st), "d2h");
+    }
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    // the reference raises KeyError at the first record whose region is unknown, after the records before it
+    int64_t stop = n;
+    for (int64_t r = 0; r < n && stop == n; r++)
+      if (cls[r] == kBamNoRegion || cls[r] == kBamNoCluster) stop = r;
+    int32_t ncl = 0;
+    for (int64_t r = 0; r < stop; r++)
+      if (cls[r] == kBamKept) ncl = std::max(ncl, clu[r] + 1);
+    // output grouped by cluster, records in BAM order within a cluster
+    std::vector<int64_t> cbase((size_t)ncl + 1, 0), pos(n, -1);
+    for (int64_t r = 0; r < stop; r++)
+      if (cls[r] == kBamKept) cbase[clu[r] + 1] += olen[r];
+    for (int32_t k = 0; k < ncl; k++) cbase[k + 1] += cbase[k];
+    {
+      std::vector<int64_t> cur(cbase.begin(), cbase.end() - 1);
+      for (int64_t r = 0; r < stop; r++)
+        if (cls[r] == kBamKept) {
+          pos[r] = cur[clu[r]];
+          cur[clu[r]] += olen[r];
+        }
+    }
+    std::vector<char> outb((size_t)cbase[ncl] + 1);
+    DevBuf<char> d_out;
+    c->hip(d_out.ensure(outb.size()), "alloc");
+    if (stop) {
+      c->hip(hipMemcpyAsync(d_pos.p, pos.data(), (size_t)stop * 8, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(launch_bam_emit(d_raw.p, d_roff.p, stop, d_cls.p, d_pos.p, d_out.p, c->st), "bam emit");
+      c->hip(hipMemcpyAsync(outb.data(), d_out.p, (size_t)cbase[ncl], hipMemcpyDeviceToHost, c->st), "d2h");
+    }
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    // append per cluster (the reference opens region_cluster<k>.fasta with "a" for every record)
+    std::vector<int32_t> used;
+    for (int32_t k = 0; k < ncl; k++)
+      if (cbase[k + 1] > cbase[k]) used.push_back(k);
+    const int T = std::max(1, std::min<int>(io_threads(), (int)used.size()));
+    std::vector<int32_t> bad(T, -1);
+    parallel_for(T, [&](int t) {
+      for (size_t u = (size_t)t; u < used.size(); u += (size_t)T) {
+        const int32_t k = used[u];
+        const std::string fn = pjoin(out_dir, "region_cluster" + std::to_string(k) + ".fasta");
+        const int fd = open(fn.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0666);
+        bool ok = fd >= 0 && write_all(fd, outb.data() + cbase[k], (size_t)(cbase[k + 1] - cbase[k]));
+        if (fd >= 0) ok = (close(fd) == 0) && ok;
+        if (!ok) bad[t] = k;
+      }
+    });
+    for (int32_t v : bad)
+      if (v >= 0) c->fail(UMICLUST_EIO, "cannot append region_cluster%d.fasta", v);
+    // counters of the records the reference reached
+    int64_t cnt[4] = {0, 0, 0, 0};  // unmapped, primary mapped, short, long
+    if (reads_per_cluster) memset(reads_per_cluster, 0, sizeof(int64_t) * (size_t)ncluster_cap);
+    if (region_detected) memset(region_detected, 0, (size_t)nregions);
+    const int64_t last = stop < n ? stop + 1 : n;  // the failing record counts as a primary alignment too
+    for (int64_t r = 0; r < last; r++) {
+      const int8_t k = cls[r];
+      if (k == kBamUnmapped) cnt[0]++;
+      if (k >= kBamShort) cnt[1]++;
+      if (k == kBamShort) cnt[2]++;
+      if (k == kBamLong) cnt[3]++;
+      if (k == kBamKept && r < stop) {
+        if (clu[r] < ncluster_cap) reads_per_cluster[clu[r]]++;
+        const int32_t ref = rd_i32(raw.data() + roff[r] + 4);
+        if (region_detected && rreg[ref] >= 0) region_detected[rreg[ref]] = 1;
+      }
+    }
+    for (int x = 0; x < 4; x++) counts[x] = cnt[x];
+    if (stop < n) {
+      const int32_t ref = rd_i32(raw.data() + roff[stop] + 4);
+      const std::string nm = ref >= 0 && ref < nref ? refname[ref] : std::string("None");
+      if (missing_name && missing_cap > 0) snprintf(missing_name, (size_t)missing_cap, "%s", nm.c_str());
+      c->fail(UMICLUST_EFORMAT, "KeyError: '%s'", nm.c_str());
+    }
+    if (ncl > ncluster_cap) c->fail(UMICLUST_ERANGE, "cluster ids up to %d exceed the counter capacity", ncl - 1);
+    return (int64_t)used.size();
   });
 }
 

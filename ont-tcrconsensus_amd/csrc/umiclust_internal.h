@@ -239,4 +239,15 @@ struct ExtractPatterns {
 hipError_t launch_extract(const char* seqs, const int64_t* offs, int64_t n, int32_t a5, int32_t a3, int32_t k,
                           const ExtractPatterns* P, int32_t* out, hipStream_t st);
 
+// ---- region binning of BAM records (regionsplit.hip) ----
+enum : int8_t { kBamUnmapped = 0, kBamSecondary = 1, kBamShort = 2, kBamLong = 3, kBamKept = 4, kBamNoRegion = 5,
+                kBamNoCluster = 6 };
+// raw: uncompressed BAM, roff[r]: offset of record r's block_size field; ref_len / ref_cluster per BAM reference
+// (-1: not in the reference FASTA / not in the cluster dict)
+hipError_t launch_bam_classify(const uint8_t* raw, const int64_t* roff, int64_t n, int32_t nref, const int64_t* ref_len,
+                               const int32_t* ref_cluster, double minov, int32_t s5, int32_t s3, int8_t* cls,
+                               int32_t* cluster, int64_t* outlen, hipStream_t st);
+hipError_t launch_bam_emit(const uint8_t* raw, const int64_t* roff, int64_t n, const int8_t* cls, const int64_t* pos,
+                           char* out, hipStream_t st);
+
 }  // namespace uc

@@ -103,7 +103,7 @@ EXPORTS = [
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
     "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
-    "umiclust_extract_umis_file", "umiclust_align_pairs", "umiclust_prep",
+    "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
 ]
 OVERLAP_MAX_REGIONS = 4096
 
@@ -166,6 +166,10 @@ def lib() -> C.CDLL:
     L.umiclust_extract_umis_file.restype = C.c_int64
     L.umiclust_extract_umis_file.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int32, C.c_int32, C.c_int32,
                                              C.c_char_p, C.c_char_p]
+    L.umiclust_region_split.restype = C.c_int64
+    L.umiclust_region_split.argtypes = [C.c_void_p, C.c_char_p, C.c_int32, P(C.c_char_p), P(C.c_int64), P(C.c_int32),
+                                        C.c_double, C.c_int32, C.c_int32, C.c_char_p, P(C.c_int64), P(C.c_int64),
+                                        C.c_int32, P(C.c_uint8), C.c_char_p, C.c_int32]
     L.umiclust_align_pairs.restype = C.c_int32
     L.umiclust_align_pairs.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_void_p, P(C.c_int64),
                                        C.c_int64, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_int32,
@@ -359,6 +363,27 @@ class Context:
     def extract_umis_file(self, fastx: str, out_fasta: str, a5: int, a3: int, k: int, fwd: str, rev: str) -> int:
         return int(self._check(lib().umiclust_extract_umis_file(self._h, fastx.encode(), out_fasta.encode(), a5, a3, k,
                                                                 fwd.encode(), rev.encode()), "extract_umis_file"))
+
+    def region_split(self, bam_file: str, names, lengths, clusters, minov: float, s5: int, s3: int, out_dir: str):
+        """umiclust_region_split: (counts[4], reads_per_cluster, region_detected); KeyError(name) as the
+        reference raises it."""
+        R = len(names)
+        nm = (C.c_char_p * max(R, 1))(*[x.encode() for x in names])
+        ln = np.asarray(lengths, np.int64)
+        cl = np.asarray(clusters, np.int32)
+        cap = int(max([0] + [k + 1 for k in clusters]))
+        counts = np.zeros(4, np.int64)
+        rpc = np.zeros(max(cap, 1), np.int64)
+        det = np.zeros(max(R, 1), np.uint8)
+        miss = C.create_string_buffer(4096)
+        P = C.POINTER
+        rc = lib().umiclust_region_split(self._h, bam_file.encode(), R, nm, _i64(ln), cl.ctypes.data_as(P(C.c_int32)),
+                                         minov, s5, s3, out_dir.encode(), _i64(counts), _i64(rpc), cap,
+                                         det.ctypes.data_as(P(C.c_uint8)), miss, 4096)
+        if rc == -74 and miss.value:
+            raise KeyError(miss.value.decode())
+        self._check(rc, "region_split")
+        return counts, rpc[:cap], det[:R]
 
     def align_pairs(self, p: Params, queries, targets, with_ops: bool = False) -> dict:
         qb, qo = _pack(queries)

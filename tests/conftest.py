@@ -15,6 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ont-tcrconsensus_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))  # fixture writers (data only)
 
 
 def pytest_configure(config):

@@ -45,6 +45,12 @@ CASES = {
 }
 
 
+def _max_cluster(cluster) -> int:
+    cl = np.asarray(cluster)
+    cl = cl[cl >= 0]  # length-filtered records are -1
+    return int(np.bincount(cl).max()) if len(cl) else 0
+
+
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -115,7 +121,7 @@ def main(configs):
         d = digest(r)
         d.update(config=cfg, scale=scale, preset=preset, identity=idn, minlen=lo, maxlen=hi, n_reads=len(seqs),
                  alignments=r["stats"]["alignments"], cells=r["stats"]["cells"],
-                 max_cluster=int(np.bincount(np.asarray(r["cluster"])).max()) if len(seqs) else 0,
+                 max_cluster=_max_cluster(r["cluster"]),
                  oracle_seconds=round(dt, 2), oracle_threads=1, host_cpu=_cpu_model())
         out.setdefault(cfg, {})[name] = d
         print(name, d, flush=True)

@@ -15,6 +15,8 @@ for st in "$@"; do
     tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
              > "$out/tests.log" 2>&1; rc=$?; tail -3 "$out/tests.log" ;;
     c2) timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$out/c2.json" 2> "$out/c2.err"; rc=$? ;;
+    c3cpu) timeout -k 10 500 python3 -u bench.py --config 3 --steps 1 --warmup 1 > "$out/c3cpu.json" 2> "$out/c3cpu.err"; rc=$? ;;
+    c2cpu) timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 > "$out/c2cpu.json" 2> "$out/c2cpu.err"; rc=$? ;;
     c3) timeout -k 10 400 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
     c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
     c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
