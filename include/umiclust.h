@@ -94,6 +94,7 @@ typedef struct umiclust_stats {
   double t_run_s;         /* file path: the whole call, read to files written */
   int64_t n_reruns;       /* block pieces re-run alone after an in-window peer list overflowed */
   int64_t n_overlap_passes; /* overlap hash-table passes (1 + re-seeds after 64-bit hash collisions) */
+  int64_t n_lazy_passes;  /* passes whose in-window peers were aligned on demand (round B) only */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

@@ -255,7 +255,9 @@ struct umiclust_ctx {
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
-  int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -       // skip peers predicted to be members (UMICLUST_PEER_PREDICT=0: align all)
+  int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
+  int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
+  int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   DevBuf<uint8_t> t_ops, t_mstrand;
@@ -478,7 +480,8 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // threshold, and one download of the walk states, top lists, walked results and peer results.
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
-void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own, int32_t region) {
+void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own, int32_t region,
+                  bool lazy_peers = false) {
   const int32_t w0 = prev ? prev->base : q0;
   const int both = c->both;
   const int32_t nqs = nq * both;
@@ -582,7 +585,8 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
          "walk 0");
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
                            P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2, P.d_counters.p + 10, P.d_counters.p + 8,
-                           peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, st),
+                           peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, lazy_peers ? 0 : 1,
+                           st),
          "peer pairs");
   c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * (kWalk + kPeerCap), P.d_counters.p + 2,
                       P.d_outidx.p, c->sc, P.d_res.p, st),
@@ -847,7 +851,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
           bidx.push_back((uint32_t)(qs * kSlots + x));
         }
         for (int y = 0; y < R.np; y++)
-          if (!((R.peer[y] >> 25) & 1u)) {
+          // a peer that is a member never enters the merged walk (only centroids are candidates)
+          if (!((R.peer[y] >> 25) & 1u) && state[(uint32_t)w0 + (R.peer[y] & 0xffffu)] != ST_MEMBER) {
             bpq.push_back(qv);
             bpt.push_back((uint32_t)w0 + (R.peer[y] & 0xffffu));
             bidx.push_back((uint32_t)(qs * kSlots + kWalk + y));
@@ -1006,13 +1011,19 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     c->hip(c->arena.ensure((size_t)off + 64), "alloc arena");
   }
   std::vector<std::pair<int32_t, int32_t>> blocks;
-  for (int32_t q0 = s0; q0 < s1;) {
-    int32_t same = 1;
-    while (q0 + same < s1 && same < B && c->hlen[q0 + same] == c->hlen[q0]) same++;
-    blocks.push_back({q0, same});
-    q0 += same;
-  }
-  const int32_t nb = (int32_t)blocks.size();
+  // the blocks from query `from` on, at most `bmax` queries of one length each
+  auto split_blocks = [&](int32_t from, int32_t bmax) {
+    for (int32_t q0 = from; q0 < s1;) {
+      int32_t same = 1;
+      while (q0 + same < s1 && same < bmax && c->hlen[q0 + same] == c->hlen[q0]) same++;
+      blocks.push_back({q0, same});
+      q0 += same;
+    }
+  };
+  // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
+  int32_t b_eff = std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
+  split_blocks(s0, b_eff);
+  int32_t nb = (int32_t)blocks.size();
   std::vector<int32_t> new_cents;
   // A block whose peer list overflowed: re-run it alone (window = itself, index complete up to it)
   // in halving pieces, synchronously.
@@ -1039,9 +1050,13 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   // exact.  Invariant at the top of iteration k: pass k and (if any) pass k+1 are queued, the
   // index holds blocks < k.  Block k's peer tile lives in blk_tile[k % 3] (used by passes k, k+1).
   auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % 3]; };
+  // Lazy peers: once new centroids have become rare (the last resolved block created fewer than
+  // lazy_permille per mille), in-window peers are not aligned speculatively; a query whose relevant peer
+  // turns out to be a centroid is deferred and round B aligns what it needs (deep clusters: config 5)
+  bool lazy = false;
   auto enqueue = [&](int32_t k, bool with_prev) {
     enqueue_pass(c, c->pass[k & 1], blocks[k].first, blocks[k].second, with_prev ? &tile_of(k - 1) : nullptr,
-                 tile_of(k), k & 1);
+                 tile_of(k), k & 1, lazy);
   };
   if (nb > 0) enqueue(0, false);
   if (nb > 1) enqueue(1, true);
@@ -1055,14 +1070,26 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
         Q.live = false;
       }
       run_alone(blocks[k].first, blocks[k].second);
+      // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
+      // same-molecule peers), so the overflow re-runs do not repeat block after block
+      if (b_eff > 256 && k + 1 < nb) {
+        b_eff /= 2;
+        const int32_t from = blocks[k].first + blocks[k].second;
+        blocks.resize((size_t)k + 1);
+        split_blocks(from, b_eff);
+        nb = (int32_t)blocks.size();
+      }
       if (k + 1 < nb) enqueue(k + 1, false);
       if (k + 2 < nb) enqueue(k + 2, true);
       continue;
     }
     append_centroids(c, new_cents);
     c->stats.n_blocks++;
+    lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
+    c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
     if (k + 2 < nb) enqueue(k + 2, true);
   }
+  c->b_hint = b_eff;
   c->hip(hipStreamSynchronize(c->st_al), "sync");
   c->hip(hipStreamSynchronize(c->st), "sync");
   for (size_t i = 0; i < c->nix; i++) {
@@ -1949,6 +1976,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
+  if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
     if (c->pf_prof.ensure(9) != hipSuccess || hipMemset(c->pf_prof.p, 0, 9 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;

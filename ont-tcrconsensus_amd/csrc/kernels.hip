@@ -1191,14 +1191,14 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
                              uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum,
                              uint32_t* __restrict__ nstat, uint32_t out0, const uint8_t* __restrict__ strong,
-                             unsigned long long* __restrict__ aligned) {
+                             unsigned long long* __restrict__ aligned, int32_t emit) {
   // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
   // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   if (qs >= nqs) return;
   const int np = npeer[qs];
   aligned[qs] = 0ull;
-  if (np == 255 || np == 0) return;
+  if (np == 255 || np == 0 || !emit) return;
   const WalkState w = ws[qs];
   unsigned long long rel = 0;
   for (int x = 0; x < np; x++) {
@@ -1230,10 +1230,10 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
                              uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
-                             unsigned long long* aligned, hipStream_t st) {
+                             unsigned long long* aligned, int32_t emit, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0, strong, aligned);
+                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0, strong, aligned, emit);
   return hipGetLastError();
 }
 

@@ -166,7 +166,7 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
                              uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
-                             unsigned long long* aligned, hipStream_t st);
+                             unsigned long long* aligned, int32_t emit, hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
 constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {

@@ -78,6 +78,7 @@ class Stats(C.Structure):
         ("t_run_s", C.c_double),
         ("n_reruns", C.c_int64),
         ("n_overlap_passes", C.c_int64),
+        ("n_lazy_passes", C.c_int64),
     ]
 
     def as_dict(self) -> dict:
