@@ -252,6 +252,9 @@ struct umiclust_ctx {
   std::vector<BinOut> bout;
   umiclust_stats stats{};
   int32_t block_size = 8192;
+  // UMICLUST_BLOCK unset: a bin of n queries uses blocks of about n / block_div (>= 2048): a small bin's
+  // window then holds fewer same-molecule peers (fewer speculative peer alignments and overflows)
+  int32_t block_div = 16;
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
@@ -989,7 +992,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   double t_pf = 0, t_al = 0, t_host = 0;
   // blocks of at most B queries of one length (the aligner is compiled per query length); a block's
   // peer tile fills one kPeerRegion of the prefilter counters, so B <= kMaxBlock
-  const int32_t B = std::max(1, std::min<int32_t>(c->block_size, kMaxBlock));
+  int32_t B = std::max(1, std::min<int32_t>(c->block_size, kMaxBlock));
+  if (c->block_div > 0) B = std::min<int32_t>(B, std::max<int32_t>(2048, ((s1 - s0) / c->block_div + 255) & ~255));
   c->pass_B = B;
   for (Pass& P : c->pass) ensure_pass_buffers(c, P, B);
   // postings arena: the base, delta, peer-ring and solo slots, then the sealed tile slots in creation
@@ -1972,7 +1976,11 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     if (err) *err = UMICLUST_EDEVICE;
     return nullptr;
   }
-  if (const char* b = getenv("UMICLUST_BLOCK")) c->block_size = std::max(1, std::min(kTile, atoi(b)));
+  if (const char* b = getenv("UMICLUST_BLOCK")) {
+    c->block_size = std::max(1, std::min(kTile, atoi(b)));
+    c->block_div = 0;
+  }
+  if (const char* b = getenv("UMICLUST_BLOCK_DIV")) c->block_div = std::max(0, atoi(b));
   if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
