@@ -34,3 +34,25 @@ def test_fixtures_cover_the_branches():
     assert cs["append_existing"]["out_files"][next(iter(cs["append_existing"]["pre_existing"]))].startswith(">old")
     flags = {r["flag"] & 0x914 for c in cs.values() for r in c["records"]}
     assert {0, 4, 16, 256, 2048} <= flags | {x & ~16 for x in flags}
+
+
+@pytest.mark.parametrize("case", cases(), ids=[c["name"] for c in cases()])
+def test_oracle_restatement_vs_reference_fixtures(case):
+    """oracle/region_split.py (the f4 checker and CPU baseline) reproduces the reference's files and counts."""
+    import region_split as ors
+    recs = [bam.AlignedSegment([tuple(r) for r in case["refs"]], r["ref"], r["pos"], r["flag"], r["name"],
+                               [("MIDNSHP=X".index(op), ln) for op, ln in r["cigar"]], r["seq"] or None)
+            for r in case["records"]]
+    lengths = {nm: ln for nm, ln in case["regions"]}
+    kw = dict(minimal_region_overlap=case["minimal_region_overlap"], max_softclip_5_end=case["max_softclip_5_end"],
+              max_softclip_3_end=case["max_softclip_3_end"])
+    if case["error"]:
+        with pytest.raises(KeyError) as e:
+            ors.split_records(recs, lengths, case["clusters"], **kw)
+        assert f"KeyError: {e.value}" == case["error"]
+        return
+    counts, per_cluster, texts, _ = ors.split_records(recs, lengths, case["clusters"], **kw)
+    want = {fn: t[len(case["pre_existing"].get(fn, "")):] for fn, t in case["out_files"].items()}
+    assert {f"region_cluster{k}.fasta": t for k, t in texts.items()} == want
+    log = next(iter(case["log_files"].values()))
+    assert f"Total # primary alignments in bam file: {counts['primary']}\n" in log

@@ -23,8 +23,9 @@ for st in "$@"; do
     e2e) timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --e2e > "$out/e2e.json" 2> "$out/e2e.err"; rc=$? ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$out/trace.log" 2>&1; rc=$? ;;
-    pmc_fetch|pmc_write|pmc_sq|pmc_valu|pmc_l2)
+    pmc_fetch|pmc_write|pmc_sq|pmc_valu|pmc_l2|pmc_inst)
        case $st in
+         pmc_inst) ctr="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR" ;;
          pmc_l2) ctr="TCC_REQ_sum TCC_HIT_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" ;;
          pmc_fetch) ctr="FETCH_SIZE" ;;
          pmc_write) ctr="WRITE_SIZE" ;;
