@@ -177,6 +177,13 @@ struct umiclust_ctx {
   bool loaded = false;
   bool clustered = false;
   DevBuf<unsigned long long> pf_prof;  // prefilter phase clocks (UMICLUST_PFPROF)
+  // UMI extraction (f1): gathered adapter windows, kept across calls
+  PinBuf<char> ex_win;
+  PinBuf<uint8_t> ex_len;
+  DevBuf<char> ex_dwin;
+  DevBuf<uint8_t> ex_dlen;
+  DevBuf<int32_t> ex_dout;
+  DevBuf<ExtractPatterns> ex_dpat;
 
   // input (host copies kept only for the file path outputs).  A load holds one or more independent
   // region bins (umiclust_load_bins): bin b is input records [bin_in[b], bin_in[b+1]) and sorted
@@ -2426,6 +2433,45 @@ void extract_device(umiclust_ctx* c, const char* seqs, const int64_t* offs, int6
   ExtractPatterns P;
   build_patterns(c, fwd, rev, P);
   if (n == 0) return;
+  // Only the adapter windows are read: with short windows the host gathers them (its threads, into pinned
+  // memory) and the device gets ~141 B per read instead of the whole read
+  const int32_t S = (a5 + a3 + 3) & ~3;
+  if (a3 > 0 && a5 + a3 > 0 && S <= kExMaxSlot && a5 <= 255 && a3 <= 255) {
+    PinBuf<char>& hw = c->ex_win;
+    PinBuf<uint8_t>& hl = c->ex_len;
+    c->hip(hw.ensure((size_t)n * S + 16), "alloc pinned");
+    c->hip(hl.ensure((size_t)n * 2), "alloc pinned");
+    const int T = n < 65536 ? 1 : io_threads();
+    parallel_for(T, [&](int t) {
+      const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+      for (int64_t i = lo; i < hi; i++) {
+        const char* b = seqs + offs[i];
+        const int64_t len = offs[i + 1] - offs[i];
+        // Python slicing: seq[:a5] and seq[-a3:]
+        const int64_t l5 = a5 < len ? a5 : len, l3 = a3 < len ? a3 : len;
+        char* d = hw.p + i * S;
+        memcpy(d, b, (size_t)l5);
+        memcpy(d + a5, b + len - l3, (size_t)l3);
+        hl.p[2 * i] = (uint8_t)l5;
+        hl.p[2 * i + 1] = (uint8_t)l3;
+      }
+    });
+    DevBuf<char>& d_w = c->ex_dwin;
+    DevBuf<uint8_t>& d_l = c->ex_dlen;
+    DevBuf<int32_t>& d_out = c->ex_dout;
+    DevBuf<ExtractPatterns>& d_p = c->ex_dpat;
+    c->hip(d_w.ensure((size_t)n * S + 16), "alloc");
+    c->hip(d_l.ensure((size_t)n * 2), "alloc");
+    c->hip(d_out.ensure((size_t)n * 6), "alloc");
+    c->hip(d_p.ensure(1), "alloc");
+    c->hip(hipMemcpyAsync(d_w.p, hw.p, (size_t)n * S, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(d_l.p, hl.p, (size_t)n * 2, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(d_p.p, &P, sizeof(P), hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(launch_extract_win(d_w.p, d_l.p, n, S, a5, k, d_p.p, d_out.p, c->st), "extract");
+    c->hip(hipMemcpyAsync(out, d_out.p, (size_t)n * 6 * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync");
+    return;
+  }
   const int64_t bytes = offs[n] - offs[0];
   std::vector<int64_t> rel((size_t)n + 1);
   for (int64_t i = 0; i <= n; i++) rel[i] = offs[i] - offs[0];

@@ -83,6 +83,72 @@ __global__ void k_extract(const char* __restrict__ seqs, const int64_t* __restri
   o[2] = end;
 }
 
+// Compact-window form: the host gathered every read's two windows into win[i * S, i * S + S) (5' window at
+// offset 0, 3' window at a5; S = a5 + a3 rounded to 4), their lengths in wlen[2 i + w].  A workgroup of
+// 256 threads takes 128 reads: their S-byte slots are copied into LDS with coalesced 16-byte loads, then each
+// thread runs the same two Myers passes on its window from LDS (the byte-per-lane gathers of k_extract touch
+// one cache line per lane per step).
+constexpr int kExReads = 128;
+__global__ __launch_bounds__(256) void k_extract_win(const char* __restrict__ win, const uint8_t* __restrict__ wlen,
+                                                     int64_t n, int32_t S, int32_t a5, int32_t k,
+                                                     const ExtractPatterns* __restrict__ P, int32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char ex_smem[];
+  const int64_t i0 = (int64_t)blockIdx.x * kExReads;
+  const int nr = (int)(n - i0 < kExReads ? n - i0 : kExReads);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(win + i0 * S);
+    uint4* dst = reinterpret_cast<uint4*>(ex_smem);
+    const int nv = (nr * S + 15) >> 4;
+    for (int x = threadIdx.x; x < nv; x += blockDim.x) dst[x] = src[x];
+  }
+  __syncthreads();
+  const int r = threadIdx.x >> 1, w = threadIdx.x & 1;
+  if (r >= nr) return;
+  const int64_t t = (i0 + r) * 2 + w;
+  const char* wp = ex_smem + r * S + (w ? a5 : 0);
+  const int wl = wlen[t];
+  const int m = P->m[w];
+  const uint64_t* peq = P->peq[w];
+  const uint64_t* peqr = P->peqr[w];
+  const uint64_t mask = m == 64 ? ~0ull : ((1ull << m) - 1ull), hb = 1ull << (m - 1);
+  uint64_t Pv = mask, Mv = 0;
+  int score = m, best = 1 << 30, end = -1;
+  for (int j = 0; j < wl; j++) {
+    myers_step(peq[(uint8_t)wp[j]], mask, hb, 0ull, Pv, Mv, score);
+    if (score < best) {
+      best = score;
+      end = j;
+    }
+  }
+  int32_t* o = out + t * 3;
+  if (end < 0 || best > k) {
+    o[0] = -1;
+    o[1] = -1;
+    o[2] = -1;
+    return;
+  }
+  Pv = mask;
+  Mv = 0;
+  score = m;
+  int last = -1;
+  for (int q = 0; q <= end; q++) {
+    myers_step(peqr[(uint8_t)wp[end - q]], mask, hb, 1ull, Pv, Mv, score);
+    if (score == best) last = q;
+  }
+  o[0] = best;
+  o[1] = end - last;
+  o[2] = end;
+}
+
+hipError_t launch_extract_win(const char* win, const uint8_t* wlen, int64_t n, int32_t S, int32_t a5, int32_t k,
+                              const ExtractPatterns* P, int32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const size_t smem = (size_t)kExReads * S + 16;
+  hipLaunchKernelGGL(k_extract_win, dim3((unsigned)((n + kExReads - 1) / kExReads)), dim3(2 * kExReads), smem, st, win,
+                     wlen, n, S, a5, k, P, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_extract(const char* seqs, const int64_t* offs, int64_t n, int32_t a5, int32_t a3, int32_t k,
                           const ExtractPatterns* P, int32_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;

@@ -238,6 +238,10 @@ struct ExtractPatterns {
 // out[(i * 2 + w) * 3 ...] = (edit distance or -1, start, end) of edlib HW locations[0] in window w of read i
 hipError_t launch_extract(const char* seqs, const int64_t* offs, int64_t n, int32_t a5, int32_t a3, int32_t k,
                           const ExtractPatterns* P, int32_t* out, hipStream_t st);
+// the same on host-gathered windows (read i's at win[i * S ...], 5' window first, 3' at a5; lengths wlen[2i + w])
+constexpr int kExMaxSlot = 252;  // S <= this: 128 slots fit the LDS staging of k_extract_win
+hipError_t launch_extract_win(const char* win, const uint8_t* wlen, int64_t n, int32_t S, int32_t a5, int32_t k,
+                              const ExtractPatterns* P, int32_t* out, hipStream_t st);
 
 // ---- region binning of BAM records (regionsplit.hip) ----
 enum : int8_t { kBamUnmapped = 0, kBamSecondary = 1, kBamShort = 2, kBamLong = 3, kBamKept = 4, kBamNoRegion = 5,

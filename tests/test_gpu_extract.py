@@ -69,6 +69,19 @@ def test_windows_vs_oracle(gpu_ctx, seed, k):
             assert g == (want if want else (-1, -1, -1)), (i, w, win)
 
 
+@pytest.mark.parametrize("a5,a3", [(73, 68), (81, 76), (0, 40), (250, 0), (400, 300), (5, 255)])
+def test_window_sizes_vs_oracle(gpu_ctx, a5, a3):
+    """Both device paths: host-gathered windows (short windows) and whole reads (a3 == 0: the whole read as
+    Python's seq[-0:] gives; windows past the gather limit), against Python slicing semantics."""
+    seqs = [s for _, s in _reads(8, 250)]
+    got = gpu_ctx.extract_umis(seqs, a5, a3, 3, FWD, REV)
+    for i, s in enumerate(seqs):
+        for w, (pat, win) in enumerate(((FWD, s[:a5]), (REV, s[-a3:]))):
+            want = ox.hw_locate(pat, win, 3)
+            g = tuple(int(x) for x in got[i, 3 * w:3 * w + 3])
+            assert g == (want if want else (-1, -1, -1)), (i, w, a5, a3)
+
+
 def test_single_window_helper(gpu_ctx):
     for name, s in _reads(4, 50):
         assert ge.extract_umi(s[:73], FWD, 3) == ox.extract_umi(s[:73], FWD, 3)
