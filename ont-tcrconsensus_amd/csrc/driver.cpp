@@ -151,9 +151,12 @@ struct Pass {
   DevBuf<HostQs> d_hq;              // k_pack's per query-strand outcomes, copied to h_hq by DMA
   DevBuf<unsigned long long> d_paligned;  // per query-strand: the peers k_peer_pairs aligned
   DevBuf<uint32_t> d_reccount;
-  // written by k_pack into host memory: per query-strand outcomes, records, counters
+  DevBuf<uint32_t> d_rec;           // k_pack's records, copied to h_rec by DMA (a prefix of rec_est words;
+                                    // the host fetches the rest in the rare pass that used more)
+  uint32_t rec_est = 1u << 16;
+  // host side: per query-strand outcomes and records (DMA), counters (written by k_pack), record words used
   PinBuf<HostQs> h_hq;
-  PinBuf<uint32_t> h_rec, h_counters;
+  PinBuf<uint32_t> h_rec, h_counters, h_reccount;
   std::vector<HostQs> hq_copy;
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   ~Pass() {
@@ -477,7 +480,9 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_reccount.ensure(1), "alloc");
   c->hip(P.h_hq.ensure(nqs), "pin");
   c->hip(P.h_rec.ensure(nqs * kRecWords), "pin");
+  c->hip(P.d_rec.ensure(nqs * kRecWords), "alloc");
   c->hip(P.h_counters.ensure(16), "pin");
+  c->hip(P.h_reccount.ensure(1), "pin");
   // fixed capacities, so a pass never frees memory a queued pass still reads
   c->hip(P.h_tiles.ensure(64), "pin");
   c->hip(P.d_tiles.ensure(64), "alloc");
@@ -612,9 +617,12 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
                      P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_paligned.p, P.d_reccount.p,
                      P.d_hq.p,
-                     P.h_rec.p, P.d_counters.p, P.h_counters.p, st),
+                     P.d_rec.p, P.d_counters.p, P.h_counters.p, st),
          "pack");
   c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
+  c->hip(hipMemcpyAsync(P.h_reccount.p, P.d_reccount.p, 4, hipMemcpyDeviceToHost, st), "d2h record count");
+  const size_t est = std::min<size_t>(P.rec_est, P.d_rec.n);
+  c->hip(hipMemcpyAsync(P.h_rec.p, P.d_rec.p, est * 4, hipMemcpyDeviceToHost, st), "d2h records");
   c->hip(hipEventRecord(P.ev[4], st), "event");
 }
 
@@ -642,6 +650,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   t_pf += ms * 1e-3;
   c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;
+  {
+    // records past the DMA'd prefix (a pass that used more than the estimate): fetch the rest now
+    const size_t used = *P.h_reccount.p, est = std::min<size_t>(P.rec_est, P.d_rec.n);
+    if (used > est) {
+      c->hip(hipMemcpyAsync(P.h_rec.p + est, P.d_rec.p + est, (used - est) * 4, hipMemcpyDeviceToHost, c->st_copy),
+             "d2h records");
+      c->hip(hipStreamSynchronize(c->st_copy), "sync");
+    }
+    P.rec_est = (uint32_t)std::max<size_t>(1u << 16, used + used / 2 + 4096);
+  }
   c->stats.kmer_postings += P.h_counters.p[0];
   c->stats.pairs_peer += P.h_counters.p[8];
   // every alignment the device computed for this pass (walk rounds + speculative peers)

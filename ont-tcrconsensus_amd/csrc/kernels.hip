@@ -1237,7 +1237,7 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
   return hipGetLastError();
 }
 
-// What the host needs of a pass, written straight into pinned host memory (no copies): per
+// What the host needs of a pass, written to device buffers the host receives by DMA: per
 // query-strand the device walk's outcome (HostQs), and -- only for query-strands with a relevant
 // peer, whose outcome depends on which peers turn out to be centroids -- a record with the walk's
 // candidate list (seqno, k-mer count, result of the walked ones) and every peer (window id, count,
