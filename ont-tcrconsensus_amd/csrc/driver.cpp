@@ -159,6 +159,7 @@ struct Pass {
   PinBuf<HostQs> h_hq;
   PinBuf<uint32_t> h_rec, h_counters, h_reccount;
   std::vector<HostQs> hq_copy;
+  std::vector<uint32_t> rec_copy;
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   ~Pass() {
     for (hipEvent_t e : ev)
@@ -275,6 +276,9 @@ struct umiclust_ctx {
   int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
+  bool debug = getenv("UMICLUST_DEBUG") != nullptr;
+  int64_t dbg_q[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: queries without records / records with only earlier-block
+                                    // relevant peers / with an in-block relevant peer / host ns in pass 1
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   DevBuf<uint8_t> t_ops, t_mstrand;
@@ -692,8 +696,18 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     const uint32_t *seq, *res, *cw, *peer, *pres;
     uint32_t count(int x) const { return (cw[x >> 2] >> ((x & 3) * 8)) & 0xffu; }
   };
+  // the records are copied into pageable memory first (one streaming read; scattered reads of the DMA'd
+  // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
+  const uint32_t* recs = P.h_rec.p;
+  static const bool rec_copy = !(getenv("UMICLUST_RECCOPY") && atoi(getenv("UMICLUST_RECCOPY")) == 0);
+  if (rec_copy) {
+    const double tc1 = now_s();
+    P.rec_copy.assign(P.h_rec.p, P.h_rec.p + *P.h_reccount.p);
+    recs = P.rec_copy.data();
+    c->stats.t_sync_s += now_s() - tc1;
+  }
   auto rec_of = [&](const HostQs& h) {
-    const uint32_t* r = P.h_rec.p + h.rec;
+    const uint32_t* r = recs + h.rec;
     Rec R;
     R.nt = (int)(r[0] & 0xffu);
     R.np = (int)((r[0] >> 8) & 0xffu);
@@ -862,8 +876,25 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
     return true;
   };
+  if (c->debug) {
+    const uint32_t inb = (uint32_t)(q0 - w0);
+    for (int32_t ql = 0; ql < nq; ql++) {
+      int cls = 0;
+      for (int s = 0; s < both; s++) {
+        const HostQs& h = hq[ql * both + s];
+        if (h.rec == 0xffffffffu) continue;
+        cls = std::max(cls, 1);
+        const Rec R = rec_of(h);
+        for (int y = 0; y < R.np; y++)
+          if (((R.peer[y] >> 24) & 1u) && (R.peer[y] & 0xffffu) >= inb) cls = 2;
+      }
+      c->dbg_q[cls]++;
+    }
+  }
+  const double tp0 = now_s();
   for (int32_t ql = 0; ql < nq; ql++)
     if (!resolve(ql, false)) deferred.push_back(ql);
+  c->dbg_q[3] += (int64_t)((now_s() - tp0) * 1e9);
   t_host += now_s() - th0;
   c->stats.t_host_pass1_s += now_s() - th0;
   c->stats.n_deferred += (int64_t)deferred.size();
@@ -1270,6 +1301,10 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: n %d mispredicted %lld saved(seen) %lld blocked %lld deferred %lld\n", bin, n,
             (long long)c->dbg[0], (long long)c->dbg[1], (long long)c->dbg[2], (long long)c->stats.n_deferred);
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: queries no-record %lld earlier-block-only %lld in-block %lld; pass-1 host %.3f s\n", bin,
+            (long long)c->dbg_q[0], (long long)c->dbg_q[1], (long long)c->dbg_q[2], c->dbg_q[3] * 1e-9);
+  c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
   c->dbg[0] = c->dbg[1] = c->dbg[2] = 0;
 }
 
