@@ -36,6 +36,10 @@
 #include <string>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
@@ -160,11 +164,77 @@ struct Pass {
   PinBuf<uint32_t> h_rec, h_counters, h_reccount;
   std::vector<HostQs> hq_copy;
   std::vector<uint32_t> rec_copy;
+  // parallel classification of the pass's query-strands (resolve_pass): 0 the device outcome is final,
+  // 1 final unless one of its in-block relevant peers (deps) turns out a centroid or is undetermined,
+  // 2 resolved sequentially in full
+  std::vector<uint8_t> kind, ndeps;
+  std::vector<uint16_t> deps;
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   ~Pass() {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
   }
+};
+
+// A small persistent worker pool: run(T, f) calls f(t) for t in [0, T) on the workers and the caller (t = 0).
+class WorkPool {
+ public:
+  explicit WorkPool(int n) {
+    for (int i = 1; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~WorkPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  void run(const std::function<void(int)>& f) {
+    if (th_.empty()) {
+      f(0);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      pending_ = (int)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(i);
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (--pending_ == 0) done_.notify_one();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
 };
 
 }  // namespace
@@ -229,8 +299,13 @@ struct umiclust_ctx {
   std::vector<uint8_t> cent_len;
   int32_t cnt_ge[kMaxLen + 1] = {};  // centroids of length >= L
   // two passes in flight (software pipeline over blocks) + round B on a side stream
-  Pass pass[2];
-  Tile blk_tile[3], solo_tile;    // per-block peer tiles (ring), overflow re-runs
+  Pass pass[kPeerTiles];          // passes in flight (the pipeline depth: UMICLUST_DEPTH, <= kPeerTiles)
+  Tile blk_tile[kPeerTiles + 1], solo_tile;  // per-block peer tiles (ring of depth + 1), overflow re-runs
+  // passes in flight: 2 by default; 3 (window of three blocks) hides more host time but its extra peers cost
+  // more than that on configs 2/3/5 (profiles/r02/pipeline_depth_sweep.json)
+  int32_t depth = 2;
+  std::unique_ptr<WorkPool> pool;  // host threads of resolve_pass (UMICLUST_RESOLVE_THREADS)
+  int32_t resolve_threads = 4;
   DevBuf<uint16_t> arena;         // postings of every tile (one buffer, one descriptor per pass)
   uint64_t sealed_slot0 = 0;      // arena index of sealed tile 0's slot
   int32_t index_end = 0;          // centroid ordinals [0, index_end) are indexed
@@ -277,7 +352,9 @@ struct umiclust_ctx {
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
-  int64_t dbg_q[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: queries without records / records with only earlier-block
+  int64_t dbg_q[4] = {0, 0, 0, 0};
+  int64_t dbg_p[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: strands on the inline path / with > kInlineRel relevant
+                                    // peers / reading their record / peers scanned there  // UMICLUST_DEBUG: queries without records / records with only earlier-block
                                     // relevant peers / with an in-block relevant peer / host ns in pass 1
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
@@ -503,9 +580,9 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // threshold, and one download of the walk states, top lists, walked results and peer results.
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
-void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* prev, Tile& own, int32_t region,
-                  bool lazy_peers = false) {
-  const int32_t w0 = prev ? prev->base : q0;
+void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* const* prevs, int nprev, Tile& own,
+                  int32_t region, bool lazy_peers = false) {
+  const int32_t w0 = nprev > 0 ? prevs[0]->base : q0;
   const int both = c->both;
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
@@ -550,7 +627,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   }
   {
     uint64_t peer_lo = own.post_base;
-    if (prev) peer_lo = std::min(peer_lo, prev->post_base);
+    for (int i = 0; i < nprev; i++) peer_lo = std::min(peer_lo, prevs[i]->post_base);
     for (int s = 0; s < std::max(a.nseg, 1); s++) {
       uint64_t lo = (s == std::max(a.nseg, 1) - 1) ? peer_lo : UINT64_MAX;
       if (a.nseg > 0)
@@ -564,8 +641,12 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.nq = nq;
   a.both = both;
   a.minwordmatches = c->p.minwordmatches;
-  a.peer[0] = prev ? view_of(*prev) : TileView{};
-  a.peer[1] = view_of(own);
+  // peer slots oldest first, the own tile last; missing earlier blocks leave n = 0 slots in front
+  for (int i = 0; i < kPeerTiles - 1; i++) {
+    const int j = i - (kPeerTiles - 1 - nprev);
+    a.peer[i] = j >= 0 ? view_of(*prevs[j]) : TileView{};
+  }
+  a.peer[kPeerTiles - 1] = view_of(own);
   a.peer_base = w0;
   a.ptop = P.d_ptop.p;
   a.pntop = P.d_pntop.p;
@@ -738,6 +819,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       device_outcome(h, o);
       return 0;
     }
+    if (c->debug) c->dbg_p[h.nrel <= (uint32_t)kInlineRel ? 0 : 1]++;
     if (h.nrel <= (uint32_t)kInlineRel) {
       bool cent = false;
       for (uint32_t i = 0; i < h.nrel; i++) {
@@ -753,7 +835,9 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
         return 0;
       }
     }
+    if (c->debug) c->dbg_p[2]++;
     const Rec R = rec_of(h);
+    if (c->debug) c->dbg_p[3] += R.np;
     bool affects = false, undet = false;
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
@@ -839,14 +923,14 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       }
     return 2;
   };
-  auto resolve = [&](int32_t ql, bool allow_extra) -> bool {
+  auto resolve = [&](int32_t ql, bool allow_extra, auto&& strand_fn) -> bool {
     const int32_t q = q0 + ql;
     Outcome best, os[2];
     int bs = 0;
     bool open = false, member = false;
     for (int s = 0; s < both; s++) {
       bool cert = false;
-      if (strand_outcome(ql * both + s, q, allow_extra, os[s], cert) != 0) {
+      if (strand_fn(ql * both + s, q, allow_extra, os[s], cert) != 0) {
         open = true;
         member |= cert;
       } else {
@@ -876,7 +960,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
     return true;
   };
-  if (c->debug) {
+  if (c->debug && getenv("UMICLUST_DEBUG_CLASSES")) {
     const uint32_t inb = (uint32_t)(q0 - w0);
     for (int32_t ql = 0; ql < nq; ql++) {
       int cls = 0;
@@ -892,8 +976,81 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
   }
   const double tp0 = now_s();
+  // Phase 1 (host threads): classify every query-strand.  Peers in earlier blocks are final, so a strand
+  // whose relevant peers there include a centroid needs the full (sequential) resolution, and one whose
+  // relevant peers are all earlier-block members and in-block peers keeps its device outcome unless one of
+  // those in-block peers becomes a centroid or is deferred -- checked in order in phase 2.
+  constexpr int kDeps = 8;
+  const uint32_t inb = (uint32_t)(q0 - w0);
+  P.kind.resize((size_t)nqs);
+  P.ndeps.resize((size_t)nqs);
+  P.deps.resize((size_t)nqs * kDeps);
+  auto classify = [&](int32_t qs) {
+    const HostQs& h = hq[qs];
+    uint8_t& kd = P.kind[qs];
+    if (h.rec == 0xffffffffu) {
+      kd = 0;
+      return;
+    }
+    int nd = 0;
+    uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
+    auto rel_peer = [&](uint32_t id) -> bool {  // false: needs the full resolution
+      if (id >= inb) {
+        if (nd == kDeps) return false;
+        d[nd++] = (uint16_t)id;
+        return true;
+      }
+      return state[(uint32_t)w0 + id] != ST_CENT;
+    };
+    bool ok = true;
+    if (h.nrel <= (uint32_t)kInlineRel) {
+      for (uint32_t i = 0; i < h.nrel && ok; i++) ok = rel_peer(h.rel[i]);
+    } else {
+      const Rec R = rec_of(h);
+      for (int y = 0; y < R.np && ok; y++)
+        if ((R.peer[y] >> 24) & 1u) ok = rel_peer(R.peer[y] & 0xffffu);
+    }
+    kd = !ok ? 2 : nd ? 1 : 0;
+    P.ndeps[qs] = (uint8_t)nd;
+  };
+  if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
+  const int T = nqs < 2048 ? 1 : c->pool->size();
+  if (T == 1) {
+    for (int32_t qs = 0; qs < nqs; qs++) classify(qs);
+  } else {
+    c->pool->run([&](int t) {
+      const int32_t lo = (int32_t)((int64_t)nqs * t / T), hi = (int32_t)((int64_t)nqs * (t + 1) / T);
+      for (int32_t qs = lo; qs < hi; qs++) classify(qs);
+    });
+  }
+  // Phase 2 (sequential, sorted order): confirm the device outcomes against the in-block peers' states
+  auto strand_fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
+    const HostQs& h = hq[qs];
+    cert = false;
+    if (P.kind[qs] == 0) {
+      device_outcome(h, o);
+      return 0;
+    }
+    if (P.kind[qs] == 1) {
+      const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
+      bool cent = false;
+      for (int i = 0; i < P.ndeps[qs]; i++) {
+        const uint8_t st = state[(uint32_t)w0 + d[i]];
+        if (st == ST_UNDET) {
+          cert = cert_device(h);
+          return 1;
+        }
+        cent |= st == ST_CENT;
+      }
+      if (!cent) {
+        device_outcome(h, o);
+        return 0;
+      }
+    }
+    return strand_outcome(qs, q, false, o, cert);
+  };
   for (int32_t ql = 0; ql < nq; ql++)
-    if (!resolve(ql, false)) deferred.push_back(ql);
+    if (!resolve(ql, false, strand_fast)) deferred.push_back(ql);
   c->dbg_q[3] += (int64_t)((now_s() - tp0) * 1e9);
   t_host += now_s() - th0;
   c->stats.t_host_pass1_s += now_s() - th0;
@@ -957,7 +1114,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       extra_have[(size_t)extra_row[qs] * kSlots + e] = 1;
     }
     for (int32_t ql : deferred)
-      if (!resolve(ql, true))
+      if (!resolve(ql, true, strand_outcome))
         c->fail(UMICLUST_EDEVICE, "internal: deferred query %d still unresolved", q0 + ql);
     t_host += now_s() - th2;
     std::sort(new_cents.begin(), new_cents.end());
@@ -1062,7 +1219,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   for (Pass& P : c->pass) ensure_pass_buffers(c, P, B);
   // postings arena: the base, delta, peer-ring and solo slots, then the sealed tile slots in creation
   // order (n / kTile of them at most); a prefilter pass reads the slots of one counter segment (plus
-  // the first four in its last pass), which keeps its 32-bit buffer offsets in range
+  // the unsealed ones in its last pass), which keeps its 32-bit buffer offsets in range
   {
     uint64_t off = 0;
     auto slot = [&](Tile& t, int64_t nseq) {
@@ -1100,7 +1257,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     int32_t piece = nq;
     for (int32_t q = q0; q < q0 + nq;) {
       const int32_t m = std::min(piece, q0 + nq - q);
-      enqueue_pass(c, P, q, m, nullptr, c->solo_tile, 0);
+      enqueue_pass(c, P, q, m, nullptr, 0, c->solo_tile, 0);
       c->stats.n_reruns++;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
@@ -1112,40 +1269,45 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
       q += m;
     }
   };
-  // Software pipeline over blocks: pass k+1 is queued before the host resolves block k.  Pass j
-  // runs against the index of the blocks before its peer window, and the window covers every
-  // later query before block j's, so C_old u window = all queries before j: the merged walk is
-  // exact.  Invariant at the top of iteration k: pass k and (if any) pass k+1 are queued, the
-  // index holds blocks < k.  Block k's peer tile lives in blk_tile[k % 3] (used by passes k, k+1).
-  auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % 3]; };
+  // Software pipeline over blocks, D = c->depth passes in flight: passes k+1 .. k+D-1 are queued before
+  // the host resolves block k.  Pass j runs against the index of the blocks before its peer window (blocks
+  // j-D+1 .. j), and the window covers every later query before block j's, so C_old u window = all queries
+  // before j: the merged walk is exact.  Invariant at the top of iteration k: passes k .. k+D-1 (those that
+  // exist) are queued, the index holds blocks < k.  Block k's peer tile lives in blk_tile[k % (D + 1)]
+  // (read by passes k .. k+D-1) and counts into peer region k % D of the prefilter counters.
+  const int D = c->depth;
+  auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % (D + 1)]; };
   // Lazy peers: once new centroids have become rare (the last resolved block created fewer than
   // lazy_permille per mille), in-window peers are not aligned speculatively; a query whose relevant peer
   // turns out to be a centroid is deferred and round B aligns what it needs (deep clusters: config 5)
   bool lazy = false;
-  auto enqueue = [&](int32_t k, bool with_prev) {
-    enqueue_pass(c, c->pass[k & 1], blocks[k].first, blocks[k].second, with_prev ? &tile_of(k - 1) : nullptr,
-                 tile_of(k), k & 1, lazy);
+  // enqueue block k's pass with the nprev blocks before it in its peer window
+  auto enqueue = [&](int32_t k, int nprev) {
+    const Tile* prevs[kPeerTiles];
+    for (int i = 0; i < nprev; i++) prevs[i] = &tile_of(k - nprev + i);
+    enqueue_pass(c, c->pass[k % D], blocks[k].first, blocks[k].second, prevs, nprev, tile_of(k), k % D, lazy);
   };
-  if (nb > 0) enqueue(0, false);
-  if (nb > 1) enqueue(1, true);
+  for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
   for (int32_t k = 0; k < nb; k++) {
-    Pass& P = c->pass[k & 1];
-    Pass& Q = c->pass[(k + 1) & 1];
-    if (k + 2 < nb) {
-      // block k+2's peer tile depends on its queries only: build it now, behind pass k+1's prefilter on
-      // the main stream, while the host resolves block k (its ring slot was last read by pass k's prefilter)
-      Tile& t = tile_of(k + 2);
-      build_tile(c, t, c->d_iota.p, blocks[k + 2].first, blocks[k + 2].second, 0, ((k + 2) & 1) * kPeerRegion,
+    Pass& P = c->pass[k % D];
+    if (k + D < nb) {
+      // block k+D's peer tile depends on its queries only: build it now, behind the queued prefilters on the
+      // main stream, while the host resolves block k (its ring slot was last read by pass k+D-2's prefilter)
+      Tile& t = tile_of(k + D);
+      build_tile(c, t, c->d_iota.p, blocks[k + D].first, blocks[k + D].second, 0, ((k + D) % D) * kPeerRegion,
                  1 << 30);
-      t.base = blocks[k + 2].first;
-      t.seg = (k + 2) & 1;
+      t.base = blocks[k + D].first;
+      t.seg = (k + D) % D;
       t.prebuilt = true;
     }
     if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
-      // drain the queued pass k+1 (its window included block k) and restart the pipeline
-      if (Q.live) {
-        c->hip(hipEventSynchronize(Q.ev[4]), "sync");
-        Q.live = false;
+      // drain the queued passes k+1 .. k+D-1 (their windows include block k) and restart the pipeline
+      for (int i = 1; i < D; i++) {
+        Pass& Q = c->pass[(k + i) % D];
+        if (Q.live) {
+          c->hip(hipEventSynchronize(Q.ev[4]), "sync");
+          Q.live = false;
+        }
       }
       run_alone(blocks[k].first, blocks[k].second);
       // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
@@ -1157,15 +1319,15 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
         split_blocks(from, b_eff);
         nb = (int32_t)blocks.size();
       }
-      if (k + 1 < nb) enqueue(k + 1, false);
-      if (k + 2 < nb) enqueue(k + 2, true);
+      for (int i = 1; i <= D; i++)
+        if (k + i < nb) enqueue(k + i, i - 1);
       continue;
     }
     append_centroids(c, new_cents);
     c->stats.n_blocks++;
     lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
-    c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
-    if (k + 2 < nb) enqueue(k + 2, true);
+    c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
+    if (k + D < nb) enqueue(k + D, D - 1);
   }
   c->b_hint = b_eff;
   c->hip(hipStreamSynchronize(c->st_al), "sync");
@@ -1304,7 +1466,11 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: queries no-record %lld earlier-block-only %lld in-block %lld; pass-1 host %.3f s\n", bin,
             (long long)c->dbg_q[0], (long long)c->dbg_q[1], (long long)c->dbg_q[2], c->dbg_q[3] * 1e-9);
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: strands inline %lld many-relevant %lld record-read %lld peers-scanned %lld\n", bin,
+            (long long)c->dbg_p[0], (long long)c->dbg_p[1], (long long)c->dbg_p[2], (long long)c->dbg_p[3]);
   c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
+  c->dbg_p[0] = c->dbg_p[1] = c->dbg_p[2] = c->dbg_p[3] = 0;
   c->dbg[0] = c->dbg[1] = c->dbg[2] = 0;
 }
 
@@ -2059,16 +2225,18 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
            ? hipStreamCreateWithFlags(&c->st_al, hipStreamNonBlocking)
            : hipStreamCreateWithPriority(&c->st_al, hipStreamNonBlocking, al_priority())) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess ||
-      hipEventCreate(&c->pass[0].ev[0]) != hipSuccess || hipEventCreate(&c->pass[0].ev[1]) != hipSuccess ||
-      hipEventCreate(&c->pass[0].ev[2]) != hipSuccess || hipEventCreate(&c->pass[0].ev[3]) != hipSuccess ||
-      hipEventCreate(&c->pass[0].ev[4]) != hipSuccess || hipEventCreate(&c->pass[1].ev[0]) != hipSuccess ||
-      hipEventCreate(&c->pass[1].ev[1]) != hipSuccess || hipEventCreate(&c->pass[1].ev[2]) != hipSuccess ||
-      hipEventCreate(&c->pass[1].ev[3]) != hipSuccess || hipEventCreate(&c->pass[1].ev[4]) != hipSuccess) {
+      hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess || [&] {
+        for (Pass& P : c->pass)
+          for (hipEvent_t& e : P.ev)
+            if (hipEventCreate(&e) != hipSuccess) return true;
+        return false;
+      }()) {
     delete c;
     if (err) *err = UMICLUST_EDEVICE;
     return nullptr;
   }
+  if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
+  if (const char* e = getenv("UMICLUST_RESOLVE_THREADS")) c->resolve_threads = std::max(1, std::min(16, atoi(e)));
   if (const char* b = getenv("UMICLUST_BLOCK")) {
     c->block_size = std::max(1, std::min(kTile, atoi(b)));
     c->block_div = 0;

@@ -387,7 +387,8 @@ constexpr int kPfThreads = 256;
 constexpr int kPfWaves = kPfThreads / 64;
 constexpr int kPfCand = 1024;   // LDS candidate buffer (centroids)
 constexpr int kRankSel = 512;   // candidate counts up to this are selected by rank
-constexpr int kPfTiles = 12;    // tiles per counter segment: 7 sealed + base + delta + 2 peer (+1)
+constexpr int kPfTiles = 12;    // tiles per counter segment: 7 sealed + base + delta + kPeerTiles peer
+static_assert(7 + 2 + kPeerTiles <= kPfTiles, "list table too small for the peer window");
 constexpr int kPfLists = kMaxKmers * kPfTiles;
 // the list-table scan packs (chunks << kListBits | lists) into 32 bits; a list holds <= kTile / kParts
 // postings (<= 1024 chunks + padding), so the chunk total stays below 2^(32 - kListBits)
@@ -398,8 +399,8 @@ static_assert(kPfLists < (1 << kListBits) && (uint64_t)kPfLists * (kTile / kPart
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
-constexpr int kPfWinBase = 1024;
-constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors  // windows whose base list is tabulated (the rest: binary search)
+constexpr int kPfWinBase = 256;   // windows whose base list is tabulated (the rest: binary search)
+constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors
 struct PfShared {
   union {
     struct {                        // list table (count phase)
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     const bool last = sg == npass - 1;
     const int t0 = a.nseg > 0 ? a.seg_tile[sg] : 0;
     const int nct = a.nseg > 0 ? a.seg_tile[sg + 1] - t0 : 0;  // centroid tiles of this segment
-    const int ntl = nct + (last ? 2 : 0);                       // + the peer tiles in the last pass
+    const int ntl = nct + (last ? kPeerTiles : 0);              // + the peer tiles in the last pass
     const int seg0 = sg * kSegCentroids;
     const int segn = min(a.ncent - seg0, kSegCentroids);
     const int nsubC = segn > part ? (segn - part + kParts - 1) >> kPartShift : 0;
@@ -625,7 +626,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     for (int it = 0; it < kPfTilesPerWave; it++) {
       const int ti = wv + it * kPfWaves;
       if (ti < nct) tvs[it] = load_view(a.tiles + t0 + ti);
-      else if (ti < ntl) tvs[it] = ti == nct ? a.peer[0] : a.peer[1];
+      else if (ti < ntl) tvs[it] = a.peer[ti - nct];
       else tvs[it].n = 0;
     }
     PF_MARK(6)
@@ -642,7 +643,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
 #pragma unroll
     for (int it = 0; it < kPfTilesPerWave; it++) {
       const bool live = thr > 0 && tvs[it].n > 0;
-      const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[1].off) + ((uint32_t)part << 16));
+      const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
       o0[it] = ld_off2(op, km0);
       o1[it] = ld_off2(op, km1);
     }
@@ -778,8 +779,8 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     if (last) {
       // peers: the window queries before q, every count >= thr (all of them when thr == 0)
 #pragma unroll
-      for (int v = 0; v < 2; v++) {
-        const TileView pv = v == 0 ? a.peer[0] : a.peer[1];
+      for (int v = 0; v < kPeerTiles; v++) {
+        const TileView pv = a.peer[v];
         if (pv.n <= 0) continue;
         const int lim = min(pv.n, q - pv.base);
         const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;

@@ -23,8 +23,8 @@ constexpr int kTile = 65536;        // centroids per sealed index tile
 // part-major (bin = part << 16 | k-mer) and every list is padded to a multiple of 8 postings
 // (16-byte chunks; padding postings hit spare counters), so the counting loop needs no bounds.
 // A posting IS its LDS counter index:
-//   [0, kPeerRegion)              peer tiles of even blocks   (x - base) / kParts
-//   [kPeerRegion, 2*kPeerRegion)  peer tiles of odd blocks
+//   [r*kPeerRegion, (r+1)*kPeerRegion)  peer tile of a block in region r = block % depth (r < kPeerTiles)
+//                                       (x - base) / kParts
 //   [kDummy, kDummy + 64)         padding postings
 //   [kTrash, kTrash + 256)        lanes past the end of the posting stream, one word per lane (never read)
 //   [kCentBase, ...)              centroids: kCentBase + (ordinal % kSegCentroids) / kParts
@@ -34,7 +34,8 @@ constexpr int kPartShift = 3;
 constexpr int kBins = kParts << 16;
 constexpr int kMaxBlock = 8192;                     // queries per greedy block
 constexpr int kPeerRegion = kMaxBlock / kParts;     // counter slots per part of a peer tile
-constexpr int kDummy = 2 * kPeerRegion;
+constexpr int kPeerTiles = 3;                       // blocks in a prefilter's peer window, at most
+constexpr int kDummy = kPeerTiles * kPeerRegion;
 constexpr int kTrash = kDummy + 64;
 constexpr int kCentBase = kTrash + 256;
 constexpr int kSegCentroids = 7 * kTile;            // counter indexes stay below 65536
@@ -108,7 +109,7 @@ struct PrefilterArgs {
   // peer tiles: mini indexes over the + strand k-mers of the previous block and of this block
   // (base = first seqno, n = 0 if absent); together they cover the peer window [peer_base, q0+nq),
   // and a query sees the window entries before it
-  TileView peer[2];
+  TileView peer[kPeerTiles];  // oldest first, the block's own tile last (absent ones: n = 0)
   int32_t peer_base;
   // per-(query-strand, part) outputs, merged by launch_prefilter's second kernel
   unsigned long long* ptop;  // [nqs*kParts*kTopHits] keys (127-count)<<56 | len<<48 | ordinal, sorted
