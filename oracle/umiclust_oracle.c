@@ -108,11 +108,10 @@ static int dust_wo(int len, const char *s, int *beg, int *end) {
   int bestv = 0, besti = 0, bestj = 0;
   int counts[64];
   int words[64];
-  int w = 0;
+  unsigned w = 0;  /* only the last triplet (6 bits) is used; unsigned: no overflow on long windows */
   for (int j = 0; j < len; j++) {
-    w <<= 2;
-    w |= map2[(unsigned char)s[j]];
-    words[j] = w & 63;
+    w = (w << 2) | (unsigned)map2[(unsigned char)s[j]];
+    words[j] = (int)(w & 63u);
   }
   for (int i = 0; i < l1; i++) {
     memset(counts, 0, sizeof(counts));
