@@ -146,6 +146,7 @@ struct Pass {
   DevBuf<uint8_t> d_top_count, d_ntop;
   DevBuf<unsigned long long> d_ptop;  // per-(query-strand, part) prefilter lists
   DevBuf<uint8_t> d_pntop, d_ppeer_count, d_pnpeer;
+  DevBuf<uint32_t> d_ppost;  // postings touched per (query-strand, part), summed by k_pf_merge
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
@@ -549,10 +550,11 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_ppeer_id.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_ppeer_count.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_pnpeer.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_ppost.ensure(nqs * kParts), "alloc");
   c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
-  c->hip(P.d_counters.ensure(16), "alloc");
+  c->hip(P.d_counters.ensure(16 + kPostSpread * 32), "alloc");
   // pair lists: a launch aligns up to kWalk walk pairs plus kPeerCap peer pairs per query-strand; results
   // land in d_res: walk candidate x of qs at [qs * kWalk + x], peer y at [nqs * kWalk + qs * kPeerCap + y]
   c->hip(P.d_pq.ensure(nqs * (kWalk + kPeerCap)), "alloc");
@@ -610,7 +612,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   if (nv > 0)
     c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
-  c->hip(hipMemsetAsync(P.d_counters.p, 0, 16 * 4, st), "memset");
+  c->hip(hipMemsetAsync(P.d_counters.p, 0, (16 + kPostSpread * 32) * 4, st), "memset");
   PrefilterArgs a{};
   a.seqs = dev_seqs(c);
   a.arena = c->arena.p;
@@ -653,6 +655,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;
+  a.ppost = P.d_ppost.p;
   a.top_seqno = P.d_top_seqno.p;
   a.top_count = P.d_top_count.p;
   a.ntop = P.d_ntop.p;

@@ -399,7 +399,7 @@ static_assert(kPfLists < (1 << kListBits) && (uint64_t)kPfLists * (kTile / kPart
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
-constexpr int kPfWinBase = 256;   // windows whose base list is tabulated (the rest: binary search)
+constexpr int kPfWinBase = 128;   // windows whose base list and start mask are tabulated (the rest: search)
 constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors
 struct PfShared {
   union {
@@ -407,6 +407,8 @@ struct PfShared {
       uint32_t lstart[kPfLists + 66];  // first chunk of each non-empty list, then the chunk total
       uint32_t lbias[kPfLists];        // posting index of chunk g of list L: lbias[L] + 8 g
       uint16_t wbase[kPfWinBase];      // the list holding chunk 64 w
+      uint32_t wlo[kPfWinBase];        // bit b (b > 0): a list starts at chunk 64 w + b (b < 32) ...
+      uint32_t whi[kPfWinBase];        // ... (b >= 32)
     };
     uint32_t cand[kPfCand];         // candidate sub-ids, then 30-bit keys (scan / select phases)
   };
@@ -489,13 +491,31 @@ __device__ __forceinline__ TileView load_view(const TileView* p) {
   return __builtin_bit_cast(TileView, r);
 }
 
-// the 8 postings of a chunk: one counter increment each
-__device__ __forceinline__ void pf_chunk(uint32_t* cnt, const uint4& v) {
+// The u8 counters live at LDS byte kPfSharedBytes: k_prefilter has no static LDS, so its dynamic LDS
+// starts at address 0 and the counter base folds into the ds_add offset field.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void lds_add(uint32_t byte_addr, uint32_t v) {
+  // result unused -> ds_add_u32 (no return)
+  __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(kPfSharedBytes + byte_addr), v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// the 8 postings of a chunk: one counter increment each (`one` = 0 adds nothing: lanes past the stream).
+// Posting c is the counter byte: dword c & ~3, byte c & 3, i.e. add one << 8 (c & 3).  Per posting pair
+// (a u32 of the chunk): one packed shift puts (c & 3) << 3 into the low 5 bits of both halves (the
+// shifter reads only those), the high half's shift selects word 1 by SDWA: 5 VALU per pair.
+__device__ __forceinline__ void pf_chunk(const uint4& v, uint32_t one) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const uint32_t c = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
-    atomicAdd(&cnt[c >> 2], 1u << ((c & 3) * 8));  // result unused -> ds_add_u32 (no return)
+  for (int e = 0; e < 4; e++) {
+    const uint32_t x = w[e];
+    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) << (u16x2){3, 3});
+    uint32_t vhi;
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : "=v"(vhi)
+        : "v"(t), "v"(one));
+    lds_add(x & 0xfffcu, one << (t & 31u));
+    lds_add((x >> 16) & 0xfffcu, vhi);
   }
 }
 
@@ -569,6 +589,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return base + inc - v;
 }
 
+// kStop > 0 (phase probes, UMICLUST_PFPROBE): return after phase kStop (1 table, 2 count, 3 scan) and write
+// nothing, so per-kernel counters of the probe launches attribute the instructions to the phases
+template <int kStop>
 __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
@@ -662,8 +685,10 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
       sum_ch += nch[j];
       sum_ne += nch[j] ? 1u : 0u;
     }
+    // window start masks (set below, after block_excl_scan's barriers)
+    if (tid < kPfWinBase) S.wlo[tid] = 0u;
+    else if (tid < 2 * kPfWinBase) S.whi[tid - kPfWinBase] = 0u;
     // packed scan: chunks << kListBits | lists (see kListBits)
-    // list, so the chunk total stays below 2^22)
     uint32_t tot;
     const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, S.wsum, tot);
     const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
@@ -674,6 +699,8 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
         if (nch[j]) {
           S.lstart[li] = ci;
           S.lbias[li] = bse[j] - 8u * ci;
+          if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase)
+            atomicOr(((ci & 32u) ? S.whi : S.wlo) + (ci >> 6), 1u << (ci & 31u));
           // windows whose first chunk lies in this list
           for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch[j] && w < (uint32_t)kPfWinBase; w++)
             S.wbase[w] = (uint16_t)li;
@@ -684,6 +711,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     }
     __syncthreads();
     PF_MARK(0)
+    if (kStop == 1) return;
     // count
     if (T > 0) {
       const uint32_t nwin = (T + 63u) >> 6;
@@ -693,12 +721,18 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
       // the window (lstart[m + 1 + l] - 64 w < 64) set one bit each of a wave-uniform mask, and the
       // lane's list is m + the starts at or before it.  Windows are independent, so the address
       // chains of a batch overlap.
+      const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
+      const uint32_t below_hi = lane < 32 ? 0u : (lane == 63 ? 0xffffffffu : (2u << (lane - 32)) - 1u);
       auto window = [&](uint32_t w) -> uint32_t {
         if (w >= nwin) return 0xffffffffu;
         const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
         uint32_t m;
         if (w < (uint32_t)kPfWinBase) {
+          // tabulated: the base list and the lists starting inside the window (one bit each)
           m = S.wbase[w];
+          const uint32_t L0 = m + (uint32_t)__builtin_popcount(S.wlo[w] & below_lo) +
+                              (uint32_t)__builtin_popcount(S.whi[w] & below_hi);
+          return g < T ? S.lbias[L0] + 8u * g : 0xffffffffu;
         } else {
           int lo = 0, hi = (int)nlc - 1;
           while (lo < hi) {
@@ -720,29 +754,30 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
       // them would wait for the loads in flight) and the loop body has no exit between the halves:
       // every load and counter update is unconditional, so the compiler neither sinks a prefetch
       // below the other batch's updates nor waits for more than the oldest loads.  A lane past the
-      // end of the stream reads chunk 0 and counts into its own trash counter word.
-      const uint32_t tw = (uint32_t)(kTrash + 4 * lane), tr = tw | (tw << 16);
-      const uint4 trash = make_uint4(tr, tr, tr, tr);
+      // end of the stream reads chunk 0 and adds 0.
       auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
+      // a lane past the stream's end reads chunk 0 and adds 0; a window past the end is skipped
+      auto one = [](uint32_t i) { return i != 0xffffffffu ? 1u : 0u; };
       constexpr uint32_t S1 = kPfWaves;
-      uint32_t w = (uint32_t)wave;
+      uint32_t w = (uint32_t)wv;  // wave-uniform (SGPR): the window bounds are scalar branches
       uint32_t a0 = window(w), a1 = window(w + S1);
       uint4 v0 = ldv(a0), v1 = ldv(a1);
       for (; w < nwin; w += 4 * S1) {
         const uint32_t b0 = window(w + 2 * S1), b1 = window(w + 3 * S1);
         const uint4 u0 = ldv(b0), u1 = ldv(b1);
-        pf_chunk(cnt, a0 != 0xffffffffu ? v0 : trash);
-        pf_chunk(cnt, a1 != 0xffffffffu ? v1 : trash);
+        pf_chunk(v0, one(a0));
+        if (w + S1 < nwin) pf_chunk(v1, one(a1));
         a0 = window(w + 4 * S1);
         a1 = window(w + 5 * S1);
         v0 = ldv(a0);
         v1 = ldv(a1);
-        pf_chunk(cnt, b0 != 0xffffffffu ? u0 : trash);
-        pf_chunk(cnt, b1 != 0xffffffffu ? u1 : trash);
+        if (w + 2 * S1 < nwin) pf_chunk(u0, one(b0));
+        if (w + 3 * S1 < nwin) pf_chunk(u1, one(b1));
       }
     }
     __syncthreads();
     PF_MARK(1)
+    if (kStop == 2) return;
     if (wave == 0) {
       // postings touched (stats): every chunk posting minus the padding ones, counted by the spare
       // counters (<= 7 pads per list spread over 64 counters: no u8 overflow in practice)
@@ -756,9 +791,12 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     if (thr > 0) {
       const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
       const uint4* c4 = cnt4 + kCentBase / 16;
-      for (int x0 = wave * 64; x0 < lim4; x0 += kPfThreads) {
+      for (int x0 = wv * 64; x0 < lim4; x0 += kPfThreads) {
         const int x = x0 + lane;
         const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+        // most sweeps hold no candidate: one OR over the four words decides (no carries cross bytes)
+        if (__ballot((((v.x + add) | (v.y + add) | (v.z + add) | (v.w + add)) & 0x80808080u) != 0u) == 0ull)
+          continue;
         uint32_t mk[4] = {(v.x + add) & 0x80808080u, (v.y + add) & 0x80808080u, (v.z + add) & 0x80808080u,
                           (v.w + add) & 0x80808080u};
         const uint32_t n = (uint32_t)(__builtin_popcount(mk[0]) + __builtin_popcount(mk[1]) +
@@ -786,11 +824,12 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
         const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
         const int nwords = (nsubP + 3) >> 2;
         const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
-        for (int x0 = wave * 64; x0 < nwords; x0 += kPfThreads) {
+        for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
           const int x = x0 + lane;
           const uint32_t w = x < nwords ? pw[x] : 0u;
           const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
           uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
+          if (__ballot(mk != 0u) == 0ull) continue;
           uint32_t slot = wave_alloc((uint32_t)__builtin_popcount(mk), &S.npc);
           while (mk) {
             const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
@@ -806,6 +845,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     }
     __syncthreads();
     PF_MARK(2)
+    if (kStop == 3) return;
     const bool scan_mode = (thr == 0) || S.overflow;
     const int nchunks = scan_mode ? (nsubC + kPfCand - 1) / kPfCand : 1;
     for (int ch = 0; ch < nchunks; ch++) {
@@ -927,7 +967,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
   if (tid == 0) {
     a.pntop[pq_] = (uint8_t)(ntop < 0 ? -1 - ntop : ntop);
     a.pnpeer[pq_] = (uint8_t)(np > kPeerCap ? 255 : np);
-    if (a.postings_touched && S.post_local) atomicAdd(a.postings_touched, S.post_local);
+    if (kStop == 0) a.ppost[pq_] = S.post_local;  // a per-workgroup atomic on one address serialises
   }
   PF_MARK(4)
   if (prof) {
@@ -993,6 +1033,21 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
     }
   }
+  // postings touched (stats): the parts' counts, one atomic per workgroup
+  {
+    __shared__ uint32_t wpost[kMergeWaves];
+    uint32_t pp = (live && lane < kParts) ? a.ppost[p0 + lane] : 0u;
+#pragma unroll
+    for (int d = 1; d < kParts; d <<= 1) pp += __shfl_xor(pp, d, 64);
+    if (lane == 0) wpost[wave] = pp;
+    __syncthreads();
+    if (threadIdx.x == 0 && a.postings_touched) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kMergeWaves; w++) t += wpost[w];
+      if (t) atomicAdd(a.postings_touched + 16 + 32 * (blockIdx.x % kPostSpread), t);
+    }
+  }
   // peers
   int np_l = (live && lane < kParts) ? (int)a.pnpeer[p0 + lane] : 0;
   const bool over = __any(np_l == 255);
@@ -1036,14 +1091,23 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   if (!attr_set_on_device(k_attr_prefilter)) {
     const int most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
-    hipError_t e = hipFuncSetAttribute((const void*)k_prefilter, hipFuncAttributeMaxDynamicSharedMemorySize, most);
-    if (e != hipSuccess) return e;
+    for (const void* f : {(const void*)k_prefilter<0>, (const void*)k_prefilter<1>, (const void*)k_prefilter<2>,
+                          (const void*)k_prefilter<3>}) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, most);
+      if (e != hipSuccess) return e;
+    }
     mark_attr_set(k_attr_prefilter);
   }
   // LDS: the fixed part + counters for the peer regions, the spares and one segment's centroids
   const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
   const size_t smem = (size_t)kPfSharedBytes + kCentBase + ((((segn + kParts - 1) >> kPartShift) + 15) & ~15);
-  hipLaunchKernelGGL(k_prefilter, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+  hipLaunchKernelGGL(k_prefilter<0>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+  static const bool probe = getenv("UMICLUST_PFPROBE") != nullptr;
+  if (probe) {
+    hipLaunchKernelGGL(k_prefilter<1>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+    hipLaunchKernelGGL(k_prefilter<2>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+    hipLaunchKernelGGL(k_prefilter<3>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+  }
   hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st,
                      a, nqs);
   return hipGetLastError();
@@ -1258,7 +1322,13 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
                                               const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
   const int lane = threadIdx.x & 63;
   const int qs = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x < 16) hcounters[threadIdx.x] = counters[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // counters[0] = the postings partial sums (k_pf_merge spreads its atomics over kPostSpread lines)
+    uint32_t v = threadIdx.x < kPostSpread ? counters[16 + 32 * threadIdx.x] : 0u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
+    if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : counters[threadIdx.x];
+  }
   if (qs >= nqs) return;
   const WalkState w = ws[qs];
   const int np = npeer[qs];

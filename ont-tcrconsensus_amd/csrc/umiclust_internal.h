@@ -89,6 +89,8 @@ hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int
                              int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod, uint32_t* cursor,
                              uint16_t* post, hipStream_t st);
 // prefilter: for query-strands qs in [0, nqs): query seqno = q0 + qs/2 (or qs if !both), strand.
+// postings-touched partial sums: slots counters[16 + 32 s], s < kPostSpread (separate L2 lines)
+constexpr int kPostSpread = 32;
 struct PrefilterArgs {
   DevSeqs seqs;
   const uint16_t* arena;   // postings of every tile
@@ -117,6 +119,7 @@ struct PrefilterArgs {
   uint16_t* ppeer_id;        // [nqs*kParts*kPeerCap]
   uint8_t* ppeer_count;      // [nqs*kParts*kPeerCap]
   uint8_t* pnpeer;           // [nqs*kParts] (255 = overflow)
+  uint32_t* ppost;           // [nqs*kParts] postings touched (stats; one atomic per merge workgroup)
   // outputs
   uint32_t* top_seqno;     // [nqs*kTopHits]
   uint8_t* top_count;      // [nqs*kTopHits]
@@ -126,7 +129,8 @@ struct PrefilterArgs {
   uint8_t* npeer;          // [nqs] (255 = overflow)
   uint8_t* strong;         // [seqno * 2 + strand] the query has a near-identical earlier window query
   int32_t strong_eighths;  // ... sharing >= strong_eighths / 8 of its k-mers
-  uint32_t* postings_touched;  // [1] atomic counter (stats)
+  uint32_t* postings_touched;  // counters[0]; the merge adds into kPostSpread slots 128 B apart after
+                               // counters[16], which k_pack sums into the host copy of counters[0]
   unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
 };
 // two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
