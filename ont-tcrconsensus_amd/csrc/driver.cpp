@@ -144,8 +144,8 @@ struct Pass {
   DevBuf<TileView> d_tiles;
   DevBuf<uint32_t> d_top_seqno;
   DevBuf<uint8_t> d_top_count, d_ntop;
-  DevBuf<unsigned long long> d_ptop;  // per-(query-strand, part) prefilter lists
-  DevBuf<uint8_t> d_pntop, d_ppeer_count, d_pnpeer;
+  DevBuf<uint32_t> d_pcand, d_units;  // per-(query-strand, part) prefilter candidates, overflowed units
+  DevBuf<uint8_t> d_pncand, d_ppeer_count, d_pnpeer;
   DevBuf<uint32_t> d_ppost;  // postings touched per (query-strand, part), summed by k_pf_merge
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
@@ -545,8 +545,9 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_top_seqno.ensure(nqs * kTopHits), "alloc");
   c->hip(P.d_top_count.ensure(nqs * kTopHits), "alloc");
   c->hip(P.d_ntop.ensure(nqs), "alloc");
-  c->hip(P.d_ptop.ensure(nqs * kParts * kTopHits), "alloc");
-  c->hip(P.d_pntop.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_pcand.ensure(nqs * kParts * kPartCand), "alloc");
+  c->hip(P.d_pncand.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_units.ensure(nqs * kParts), "alloc");
   c->hip(P.d_ppeer_id.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_ppeer_count.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_pnpeer.ensure(nqs * kParts), "alloc");
@@ -554,7 +555,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
-  c->hip(P.d_counters.ensure(16 + kPostSpread * 32), "alloc");
+  c->hip(P.d_counters.ensure(kCountersLen), "alloc");
   // pair lists: a launch aligns up to kWalk walk pairs plus kPeerCap peer pairs per query-strand; results
   // land in d_res: walk candidate x of qs at [qs * kWalk + x], peer y at [nqs * kWalk + qs * kPeerCap + y]
   c->hip(P.d_pq.ensure(nqs * (kWalk + kPeerCap)), "alloc");
@@ -612,7 +613,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   if (nv > 0)
     c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
-  c->hip(hipMemsetAsync(P.d_counters.p, 0, (16 + kPostSpread * 32) * 4, st), "memset");
+  c->hip(hipMemsetAsync(P.d_counters.p, 0, kCountersLen * 4, st), "memset");
   PrefilterArgs a{};
   a.seqs = dev_seqs(c);
   a.arena = c->arena.p;
@@ -650,8 +651,13 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   }
   a.peer[kPeerTiles - 1] = view_of(own);
   a.peer_base = w0;
-  a.ptop = P.d_ptop.p;
-  a.pntop = P.d_pntop.p;
+  a.pcand = P.d_pcand.p;
+  a.pncand = P.d_pncand.p;
+  a.units = P.d_units.p;
+  a.nunits = P.d_counters.p + kUnitsSlot;
+  // list table of the lean kernel: every k-mer of the block's length in every tile it reads
+  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, c->hlen[q0] - 7) *
+                                              ((a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0) + kPeerTiles));
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;

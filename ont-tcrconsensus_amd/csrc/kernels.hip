@@ -491,12 +491,13 @@ __device__ __forceinline__ TileView load_view(const TileView* p) {
   return __builtin_bit_cast(TileView, r);
 }
 
-// The u8 counters live at LDS byte kPfSharedBytes: k_prefilter has no static LDS, so its dynamic LDS
-// starts at address 0 and the counter base folds into the ds_add offset field.
+// The u8 counters live at LDS byte kBase (k_pf_count: 0, k_pf_full: kPfSharedBytes).  Neither kernel has
+// static LDS, so the dynamic LDS starts at address 0 and the base folds into the ds_add offset field.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+template <uint32_t kBase>
 __device__ __forceinline__ void lds_add(uint32_t byte_addr, uint32_t v) {
   // result unused -> ds_add_u32 (no return)
-  __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(kPfSharedBytes + byte_addr), v, __ATOMIC_RELAXED,
+  __hip_atomic_fetch_add((lds_u32*)(uintptr_t)(kBase + byte_addr), v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -504,6 +505,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // Posting c is the counter byte: dword c & ~3, byte c & 3, i.e. add one << 8 (c & 3).  Per posting pair
 // (a u32 of the chunk): one packed shift puts (c & 3) << 3 into the low 5 bits of both halves (the
 // shifter reads only those), the high half's shift selects word 1 by SDWA: 5 VALU per pair.
+template <uint32_t kBase>
 __device__ __forceinline__ void pf_chunk(const uint4& v, uint32_t one) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -514,8 +516,8 @@ __device__ __forceinline__ void pf_chunk(const uint4& v, uint32_t one) {
     asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
         : "=v"(vhi)
         : "v"(t), "v"(one));
-    lds_add(x & 0xfffcu, one << (t & 31u));
-    lds_add((x >> 16) & 0xfffcu, vhi);
+    lds_add<kBase>(x & 0xfffcu, one << (t & 31u));
+    lds_add<kBase>((x >> 16) & 0xfffcu, vhi);
   }
 }
 
@@ -589,16 +591,154 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return base + inc - v;
 }
 
-// kStop > 0 (phase probes, UMICLUST_PFPROBE): return after phase kStop (1 table, 2 count, 3 scan) and write
-// nothing, so per-kernel counters of the probe launches attribute the instructions to the phases
-template <int kStop>
-__global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
+// The list table of one counting pass.  Wave w takes tiles w, w + kPfWaves, ... (the tile view is
+// wave-uniform: scalar loads, issued before anything waits) and lane l the query's k-mers l and l + 64;
+// every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's offsets, a
+// k-mer slot past nk reads list 0) and masked afterwards.  A packed block scan lays the non-empty lists
+// end to end as one stream of T 16-byte chunks: lstart[L] = first chunk of list L (then T), lbias[L] =
+// posting index of chunk g of list L minus 8 g; per 64-chunk window w < kPfWinBase, wbase[w] = the list
+// holding chunk 64 w and wlo/whi[w] bit b = a list starts at chunk 64 w + b (b > 0).  Ends with a barrier.
+// a part candidate for the merge: count << 24 | ordinal (ordinals stay below kMaxSegs * kSegCentroids < 2^23)
+static_assert(kMaxSegs * kSegCentroids < (1 << 24), "ordinal field");
+__device__ __forceinline__ uint32_t cand_entry(unsigned long long key64) {
+  return ((127u - (uint32_t)(key64 >> 56)) << 24) | (uint32_t)(key64 & 0xffffffu);
+}
+struct PfTable {
+  uint32_t* lstart;
+  uint32_t* lbias;
+  uint16_t* wbase;
+  uint32_t* wlo;
+  uint32_t* whi;
+  uint32_t* wsum;
+};
+__device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, int t0, int nct, int ntl,
+                                              uint64_t pbase, int part, int thr, int nk, uint32_t km0, uint32_t km1,
+                                              int wv, int lane, int tid, uint32_t& T, uint32_t& nlc) {
+  TileView tvs[kPfTilesPerWave];
+#pragma unroll
+  for (int it = 0; it < kPfTilesPerWave; it++) {
+    const int ti = wv + it * kPfWaves;
+    if (ti < nct) tvs[it] = load_view(a.tiles + t0 + ti);
+    else if (ti < ntl) tvs[it] = a.peer[ti - nct];
+    else tvs[it].n = 0;
+  }
+  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
+  u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
+#pragma unroll
+  for (int it = 0; it < kPfTilesPerWave; it++) {
+    const bool live = thr > 0 && tvs[it].n > 0;
+    const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
+    o0[it] = ld_off2(op, km0);
+    o1[it] = ld_off2(op, km1);
+  }
+#pragma unroll
+  for (int it = 0; it < kPfTilesPerWave; it++) {
+    const bool live = thr > 0 && tvs[it].n > 0;
+    const uint32_t tbase = (uint32_t)(tvs[it].post_base - pbase);
+    nch[2 * it] = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
+    bse[2 * it] = tbase + o0[it].x;
+    nch[2 * it + 1] = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
+    bse[2 * it + 1] = tbase + o1[it].x;
+  }
+#pragma unroll
+  for (int j = 0; j < kPfSlots; j++) {
+    sum_ch += nch[j];
+    sum_ne += nch[j] ? 1u : 0u;
+  }
+  // window start masks (set below, after block_excl_scan's barriers)
+  if (tid < kPfWinBase) tb.wlo[tid] = 0u;
+  else if (tid < 2 * kPfWinBase) tb.whi[tid - kPfWinBase] = 0u;
+  // packed scan: chunks << kListBits | lists (see kListBits)
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
+  T = tot >> kListBits;
+  nlc = tot & kListMask;
+  uint32_t li = ex & kListMask, ci = ex >> kListBits;
+#pragma unroll
+  for (int j = 0; j < kPfSlots; j++)
+    if (nch[j]) {
+      tb.lstart[li] = ci;
+      tb.lbias[li] = bse[j] - 8u * ci;
+      if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase)
+        atomicOr(((ci & 32u) ? tb.whi : tb.wlo) + (ci >> 6), 1u << (ci & 31u));
+      // windows whose first chunk lies in this list
+      for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch[j] && w < (uint32_t)kPfWinBase; w++)
+        tb.wbase[w] = (uint16_t)li;
+      li++;
+      ci += nch[j];
+    }
+  if (tid < 66) tb.lstart[nlc + tid] = T;
+  __syncthreads();
+}
+
+// Count the stream of T chunks into the u8 counters at LDS byte kBase (every wave; no barrier).
+// Arena index of a lane's chunk of window w (~0u past the stream's end): the window's base list m (the one
+// holding chunk 64 w) and the lists starting inside it come from the table (windows past kPfWinBase: a
+// binary search over lstart and a DPP OR-scan of the starts), and the lane's list is m + the starts at or
+// before it.  Wave v counts windows v, v + 4, v + 8, ... in batches of two, one batch of loads in flight
+// ahead of the batch being counted; two register sets are used alternately (a copy between them would wait
+// for the loads in flight).  A lane past the end of the stream reads chunk 0 and adds 0; a window past the
+// end is skipped (wave-uniform branch).
+template <uint32_t kBase>
+__device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
+                                                const uint32_t* lstart, const uint32_t* lbias,
+                                                const uint16_t* wbase, const uint32_t* wlo, const uint32_t* whi,
+                                                int lane, int wv) {
+  const uint32_t nwin = (T + 63u) >> 6;
+  const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
+  const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
+  const uint32_t below_hi = lane < 32 ? 0u : (2u << (lane - 32)) - 1u;
+  auto window = [&](uint32_t w) -> uint32_t {
+    if (w >= nwin) return 0xffffffffu;
+    const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
+    if (w < (uint32_t)kPfWinBase) {
+      const uint32_t L0 = wbase[w] + (uint32_t)__builtin_popcount(wlo[w] & below_lo) +
+                          (uint32_t)__builtin_popcount(whi[w] & below_hi);
+      return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
+    }
+    int lo = 0, hi = (int)nlc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (lstart[mid] <= g0) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t m = (uint32_t)lo;
+    const uint32_t bit = lstart[m + 1 + lane] - g0;
+    uint32_t lo32 = bit < 32u ? 1u << bit : 0u, hi32 = bit - 32u < 32u ? 1u << (bit - 32u) : 0u;
+    wave_or2_dpp(lo32, hi32);
+    const unsigned long long sm = ((unsigned long long)lane63(hi32) << 32) | lane63(lo32);
+    const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
+    return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
+  };
+  auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
+  auto one = [](uint32_t i) { return i != 0xffffffffu ? 1u : 0u; };
+  constexpr uint32_t S1 = kPfWaves;
+  uint32_t w = (uint32_t)wv;  // wave-uniform (SGPR): the window bounds are scalar branches
+  uint32_t a0 = window(w), a1 = window(w + S1);
+  uint4 v0 = ldv(a0), v1 = ldv(a1);
+  for (; w < nwin; w += 4 * S1) {
+    const uint32_t b0 = window(w + 2 * S1), b1 = window(w + 3 * S1);
+    const uint4 u0 = ldv(b0), u1 = ldv(b1);
+    pf_chunk<kBase>(v0, one(a0));
+    if (w + S1 < nwin) pf_chunk<kBase>(v1, one(a1));
+    a0 = window(w + 4 * S1);
+    a1 = window(w + 5 * S1);
+    v0 = ldv(a0);
+    v1 = ldv(a1);
+    if (w + 2 * S1 < nwin) pf_chunk<kBase>(u0, one(b0));
+    if (w + 3 * S1 < nwin) pf_chunk<kBase>(u1, one(b1));
+  }
+}
+
+// The full counting kernel: every counter segment (bins beyond kSegCentroids centroids) and the exact
+// selection of a part's top-41 for any candidate count (it also re-runs the units the lean kernel could
+// not finish: more than kPartCand candidates, or a threshold of 0).  One (query-strand, part) unit.
+__device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t unit, unsigned char* pf_smem) {
   PfShared& S = *reinterpret_cast<PfShared*>(pf_smem);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem + kPfSharedBytes);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // optional phase timing (a.prof != nullptr): thread 0's shader-clock deltas between barriers
-  const bool prof = a.prof != nullptr && tid == 0 && blockIdx.x % 61u == 0;  // sampled workgroups
+  const bool prof = a.prof != nullptr && tid == 0 && unit % 61u == 0;  // sampled units
   unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PF_MARK(i)                                              \
   if (prof) {                                                   \
@@ -607,8 +747,8 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     tacc[i] += t_ - tprev;                                      \
     tprev = t_;                                                 \
   }
-  const int part = (int)(blockIdx.x & (kParts - 1));
-  const int qs = (int)(blockIdx.x >> kPartShift);
+  const int part = (int)(unit & (kParts - 1));
+  const int qs = (int)(unit >> kPartShift);
   const int qlocal = qs / a.both;
   const int strand = qs % a.both;
   const int32_t q = a.q0 + qlocal;
@@ -641,143 +781,19 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     // the pass's postings are addressed from its lowest arena slot (32-bit buffer offsets)
     const uint64_t pbase = a.seg_base[sg];
     const __amdgpu_buffer_rsrc_t arena = arena_rsrc(uniform_ptr(a.arena + pbase));
-    // list table: wave w takes tiles w, w + kPfWaves, ... (the tile view is wave-uniform: scalar
-    // loads, issued before anything waits) and lane l the query's k-mers l and l + 64; compacted to
-    // the non-empty lists below
-    TileView tvs[kPfTilesPerWave];
-#pragma unroll
-    for (int it = 0; it < kPfTilesPerWave; it++) {
-      const int ti = wv + it * kPfWaves;
-      if (ti < nct) tvs[it] = load_view(a.tiles + t0 + ti);
-      else if (ti < ntl) tvs[it] = a.peer[ti - nct];
-      else tvs[it].n = 0;
-    }
-    PF_MARK(6)
     for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
     if (tid == 0) {
       S.ncand = 0;
       S.npc = 0;
       S.overflow = 0;
     }
-    // every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's
-    // offsets, a k-mer slot past nk reads list 0) and masked afterwards
-    uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
-    u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
-#pragma unroll
-    for (int it = 0; it < kPfTilesPerWave; it++) {
-      const bool live = thr > 0 && tvs[it].n > 0;
-      const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
-      o0[it] = ld_off2(op, km0);
-      o1[it] = ld_off2(op, km1);
-    }
-#pragma unroll
-    for (int it = 0; it < kPfTilesPerWave; it++) {
-      const bool live = thr > 0 && tvs[it].n > 0;
-      const uint32_t tb = (uint32_t)(tvs[it].post_base - pbase);
-      nch[2 * it] = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
-      bse[2 * it] = tb + o0[it].x;
-      nch[2 * it + 1] = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
-      bse[2 * it + 1] = tb + o1[it].x;
-    }
-    PF_MARK(7)
-#pragma unroll
-    for (int j = 0; j < kPfSlots; j++) {
-      sum_ch += nch[j];
-      sum_ne += nch[j] ? 1u : 0u;
-    }
-    // window start masks (set below, after block_excl_scan's barriers)
-    if (tid < kPfWinBase) S.wlo[tid] = 0u;
-    else if (tid < 2 * kPfWinBase) S.whi[tid - kPfWinBase] = 0u;
-    // packed scan: chunks << kListBits | lists (see kListBits)
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, S.wsum, tot);
-    const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
-    {
-      uint32_t li = ex & kListMask, ci = ex >> kListBits;
-#pragma unroll
-      for (int j = 0; j < kPfSlots; j++)
-        if (nch[j]) {
-          S.lstart[li] = ci;
-          S.lbias[li] = bse[j] - 8u * ci;
-          if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase)
-            atomicOr(((ci & 32u) ? S.whi : S.wlo) + (ci >> 6), 1u << (ci & 31u));
-          // windows whose first chunk lies in this list
-          for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch[j] && w < (uint32_t)kPfWinBase; w++)
-            S.wbase[w] = (uint16_t)li;
-          li++;
-          ci += nch[j];
-        }
-      if (tid < 66) S.lstart[nlc + tid] = T;
-    }
-    __syncthreads();
+    uint32_t T, nlc;
+    pf_list_table(a, PfTable{S.lstart, S.lbias, S.wbase, S.wlo, S.whi, S.wsum}, t0, nct, ntl, pbase, part, thr, nk,
+                  km0, km1, wv, lane, tid, T, nlc);
     PF_MARK(0)
-    if (kStop == 1) return;
-    // count
-    if (T > 0) {
-      const uint32_t nwin = (T + 63u) >> 6;
-      const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
-      // arena index of this lane's chunk of window w (~0u past the stream's end).  The window's
-      // base list m (the one holding chunk 64 w) comes from the table; the lists that start inside
-      // the window (lstart[m + 1 + l] - 64 w < 64) set one bit each of a wave-uniform mask, and the
-      // lane's list is m + the starts at or before it.  Windows are independent, so the address
-      // chains of a batch overlap.
-      const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
-      const uint32_t below_hi = lane < 32 ? 0u : (lane == 63 ? 0xffffffffu : (2u << (lane - 32)) - 1u);
-      auto window = [&](uint32_t w) -> uint32_t {
-        if (w >= nwin) return 0xffffffffu;
-        const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
-        uint32_t m;
-        if (w < (uint32_t)kPfWinBase) {
-          // tabulated: the base list and the lists starting inside the window (one bit each)
-          m = S.wbase[w];
-          const uint32_t L0 = m + (uint32_t)__builtin_popcount(S.wlo[w] & below_lo) +
-                              (uint32_t)__builtin_popcount(S.whi[w] & below_hi);
-          return g < T ? S.lbias[L0] + 8u * g : 0xffffffffu;
-        } else {
-          int lo = 0, hi = (int)nlc - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (S.lstart[mid] <= g0) lo = mid;
-            else hi = mid - 1;
-          }
-          m = (uint32_t)lo;
-        }
-        const uint32_t bit = S.lstart[m + 1 + lane] - g0;
-        uint32_t lo32 = bit < 32u ? 1u << bit : 0u, hi32 = bit - 32u < 32u ? 1u << (bit - 32u) : 0u;
-        wave_or2_dpp(lo32, hi32);
-        const unsigned long long sm = ((unsigned long long)lane63(hi32) << 32) | lane63(lo32);
-        const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
-        return g < T ? S.lbias[L0] + 8u * g : 0xffffffffu;
-      };
-      // wave v counts windows v, v + 4, v + 8, ... in batches of two, one batch of loads in flight
-      // ahead of the batch being counted.  Two register sets are used alternately (a copy between
-      // them would wait for the loads in flight) and the loop body has no exit between the halves:
-      // every load and counter update is unconditional, so the compiler neither sinks a prefetch
-      // below the other batch's updates nor waits for more than the oldest loads.  A lane past the
-      // end of the stream reads chunk 0 and adds 0.
-      auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
-      // a lane past the stream's end reads chunk 0 and adds 0; a window past the end is skipped
-      auto one = [](uint32_t i) { return i != 0xffffffffu ? 1u : 0u; };
-      constexpr uint32_t S1 = kPfWaves;
-      uint32_t w = (uint32_t)wv;  // wave-uniform (SGPR): the window bounds are scalar branches
-      uint32_t a0 = window(w), a1 = window(w + S1);
-      uint4 v0 = ldv(a0), v1 = ldv(a1);
-      for (; w < nwin; w += 4 * S1) {
-        const uint32_t b0 = window(w + 2 * S1), b1 = window(w + 3 * S1);
-        const uint4 u0 = ldv(b0), u1 = ldv(b1);
-        pf_chunk(v0, one(a0));
-        if (w + S1 < nwin) pf_chunk(v1, one(a1));
-        a0 = window(w + 4 * S1);
-        a1 = window(w + 5 * S1);
-        v0 = ldv(a0);
-        v1 = ldv(a1);
-        if (w + 2 * S1 < nwin) pf_chunk(u0, one(b0));
-        if (w + 3 * S1 < nwin) pf_chunk(u1, one(b1));
-      }
-    }
+    if (T > 0) pf_count_stream<kPfSharedBytes>(arena, T, nlc, S.lstart, S.lbias, S.wbase, S.wlo, S.whi, lane, wv);
     __syncthreads();
     PF_MARK(1)
-    if (kStop == 2) return;
     if (wave == 0) {
       // postings touched (stats): every chunk posting minus the padding ones, counted by the spare
       // counters (<= 7 pads per list spread over 64 counters: no u8 overflow in practice)
@@ -845,7 +861,6 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
     }
     __syncthreads();
     PF_MARK(2)
-    if (kStop == 3) return;
     const bool scan_mode = (thr == 0) || S.overflow;
     const int nchunks = scan_mode ? (nsubC + kPfCand - 1) / kPfCand : 1;
     for (int ch = 0; ch < nchunks; ch++) {
@@ -896,7 +911,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
           int r = 0;
           for (int y = 0; y < nc; y++) r += S.cand[y] < kx;
           if (r < kTopHits) {
-            if (direct) a.ptop[pq_ * kTopHits + r] = key64(kx);
+            if (direct) a.pcand[pq_ * kPartCand + r] = cand_entry(key64(kx));
             else S.best[r] = kx;
           }
         }
@@ -907,7 +922,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
         __syncthreads();
         bitonic_u32(S.cand, np2);
         for (int x = tid; x < nbest; x += kPfThreads) {
-          if (direct) a.ptop[pq_ * kTopHits + x] = key64(S.cand[x]);
+          if (direct) a.pcand[pq_ * kPartCand + x] = cand_entry(key64(S.cand[x]));
           else S.best[x] = S.cand[x];
         }
       }
@@ -963,11 +978,11 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
   }
   __syncthreads();
   const int ntop = S.ntop;  // < 0: -1 - (entries written directly)
-  if (tid < ntop) a.ptop[pq_ * kTopHits + tid] = S.top[tid];
+  if (tid < ntop) a.pcand[pq_ * kPartCand + tid] = cand_entry(S.top[tid]);
   if (tid == 0) {
-    a.pntop[pq_] = (uint8_t)(ntop < 0 ? -1 - ntop : ntop);
+    a.pncand[pq_] = (uint8_t)(ntop < 0 ? -1 - ntop : ntop);
     a.pnpeer[pq_] = (uint8_t)(np > kPeerCap ? 255 : np);
-    if (kStop == 0) a.ppost[pq_] = S.post_local;  // a per-workgroup atomic on one address serialises
+    a.ppost[pq_] = S.post_local;  // summed by the merge: a per-workgroup atomic on one address serialises
   }
   PF_MARK(4)
   if (prof) {
@@ -978,64 +993,160 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_prefilter(PrefilterArgs a) {
 #undef PF_MARK
 }
 
-// One wave per query-strand: the kParts sorted part lists (distinct seqnos, so distinct keys) are
-// staged in LDS and every key finds its rank in the union by binary search in the other lists;
-// ranks < 41 are the exact top-41.  Peer lists are concatenated in part order.
+__global__ __launch_bounds__(kPfThreads, 5) void k_pf_full(PrefilterArgs a, int unit_mode) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
+  if (!unit_mode) {
+    pf_full_unit(a, blockIdx.x, pf_smem);
+    return;
+  }
+  // the overflowed units of the lean kernel (usually none)
+  const uint32_t nu = *a.nunits;
+  for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+    pf_full_unit(a, a.units[u], pf_smem);
+    __syncthreads();
+  }
+}
+
+// The lean counting kernel (one counter segment): list table, count, then every centroid counter >= the
+// threshold becomes a part candidate (count << 24 | ordinal, unsorted, at most kPartCand) and every earlier
+// window query over it a peer (unsorted); lengths, keys and the top-41 are the merge's.  Only what counting
+// needs lives in LDS -- the u8 counters from address 0, then the list table sized by a.nlist_cap -- and
+// the kernel keeps few registers, so up to 8 workgroups share a CU.
+struct PfCountHdr {
+  uint32_t wsum[kPfWaves];
+  uint32_t ncand, npc, pad0, pad1;
+};
+__host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
+  return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 2 + 2 * kPfWinBase * 4 + (2 * nlist_cap + 66) * 4);
+}
+__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
+  PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
+  uint16_t* wbase = reinterpret_cast<uint16_t*>(pf_smem + tab_off + sizeof(PfCountHdr));
+  uint32_t* wlo = reinterpret_cast<uint32_t*>(wbase + kPfWinBase);
+  uint32_t* whi = wlo + kPfWinBase;
+  uint32_t* lstart = whi + kPfWinBase;
+  uint32_t* lbias = lstart + a.nlist_cap + 66;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int part = (int)(blockIdx.x & (kParts - 1));
+  const int qs = (int)(blockIdx.x >> kPartShift);
+  const int strand = qs % a.both;
+  const int32_t q = a.q0 + qs / a.both;
+  const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
+  const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
+  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane < kKmerStride - 64 ? lane : 0)];
+  const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
+  const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
+  const int64_t pq_ = (int64_t)qs * kParts + part;
+  const int nct = a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0;
+  const int nsubC = a.ncent > part ? (a.ncent - part + kParts - 1) >> kPartShift : 0;
+  const int ncnt = kCentBase + ((nsubC + 15) & ~15);
+  const uint64_t pbase = a.seg_base[0];
+  const __amdgpu_buffer_rsrc_t arena = arena_rsrc(uniform_ptr(a.arena + pbase));
+  uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
+  for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid == 0) {
+    H.ncand = 0;
+    H.npc = 0;
+  }
+  uint32_t T, nlc;
+  pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
+                km0, km1, wv, lane, tid, T, nlc);
+  if (T > 0) pf_count_stream<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
+  __syncthreads();
+  if (wv == 0) {
+    // postings touched (stats): every chunk posting minus the padding ones (the spare counters)
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
+    const uint32_t pads = lane63(wave_scan_dpp((uint32_t)cb[kDummy + lane], OpAdd()));
+    if (lane == 0) a.ppost[pq_] = 8u * T - pads;
+  }
+  // centroid counters >= thr (SWAR: bytes <= 112, so byte + 128 - thr sets bit 7 iff >= thr); a sweep
+  // of 64 counter vectors with no candidate costs one OR and a ballot
+  const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
+  if (thr > 0) {
+    const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
+    const uint4* c4 = cnt4 + kCentBase / 16;
+    for (int x0 = wv * 64; x0 < lim4; x0 += kPfThreads) {
+      const int x = x0 + lane;
+      const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+      if (__ballot((((v.x + add) | (v.y + add) | (v.z + add) | (v.w + add)) & 0x80808080u) != 0u) == 0ull) continue;
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+      uint32_t mk[4] = {(v.x + add) & 0x80808080u, (v.y + add) & 0x80808080u, (v.z + add) & 0x80808080u,
+                        (v.w + add) & 0x80808080u};
+      const uint32_t n = (uint32_t)(__builtin_popcount(mk[0]) + __builtin_popcount(mk[1]) +
+                                    __builtin_popcount(mk[2]) + __builtin_popcount(mk[3]));
+      uint32_t slot = wave_alloc(n, &H.ncand);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        while (mk[j]) {
+          const uint32_t byte = (uint32_t)__builtin_ctz(mk[j]) >> 3;
+          mk[j] &= mk[j] - 1u;
+          const uint32_t c = (uint32_t)x * 16u + (uint32_t)j * 4u + byte;
+          const uint32_t cv = (wd[j] >> (8 * byte)) & 0xffu;
+          if (slot < (uint32_t)kPartCand) a.pcand[pq_ * kPartCand + slot] = (cv << 24) | ((c << kPartShift) + part);
+          slot++;
+        }
+      }
+    }
+  }
+  // peers: the window queries before q, every count >= thr (all of them when thr == 0)
+#pragma unroll
+  for (int v = 0; v < kPeerTiles; v++) {
+    const TileView pv = a.peer[v];
+    if (pv.n <= 0) continue;
+    const int lim = min(pv.n, q - pv.base);
+    const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
+    const int nwords = (nsubP + 3) >> 2;
+    const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
+    for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
+      const int x = x0 + lane;
+      const uint32_t w = x < nwords ? pw[x] : 0u;
+      const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
+      uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
+      if (__ballot(mk != 0u) == 0ull) continue;
+      uint32_t slot = wave_alloc((uint32_t)__builtin_popcount(mk), &H.npc);
+      while (mk) {
+        const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
+        mk &= mk - 1u;
+        if (slot < (uint32_t)kPeerCap) {
+          const int32_t sq = pv.base + ((4 * x + (int)byte) << kPartShift) + part;
+          a.ppeer_id[pq_ * kPeerCap + slot] = (uint16_t)(sq - a.peer_base);
+          a.ppeer_count[pq_ * kPeerCap + slot] = (uint8_t)((w >> (8 * byte)) & 0xffu);
+        }
+        slot++;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t nc = H.ncand, np = H.npc;
+    const bool ovf = thr == 0 || nc > (uint32_t)kPartCand;
+    a.pncand[pq_] = (uint8_t)(ovf ? 255u : nc);
+    a.pnpeer[pq_] = (uint8_t)(np > (uint32_t)kPeerCap ? 255u : np);
+    if (ovf) a.units[atomicAdd(a.nunits, 1u)] = (uint32_t)pq_;
+  }
+}
+
+// One wave per query-strand.  Candidates: the parts' lists (distinct ordinals) get their u64 keys
+// (127-count) << 56 | length << 48 | ordinal -- vsearch's order: count desc, length asc, seqno asc (ordinal
+// order is seqno order) -- and every key its rank in the union by counting smaller keys; ranks < 41 are
+// the exact top-41 (a part's list holds every candidate over the threshold, or the full kernel's exact
+// part top-41: top-41 of a union = top-41 of the parts' top-41s).  Peers: sorted within each part by
+// (count desc, length asc, window id asc) and concatenated in part order.
 constexpr int kMergeWaves = 4;
 __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs) {
-  __shared__ unsigned long long keys[kMergeWaves][kParts * kTopHits];
+  __shared__ unsigned long long keys[kMergeWaves][kParts * kPartCand];
+  __shared__ uint32_t pkeys[kMergeWaves][kPeerCap];
+  __shared__ uint32_t wpost[kMergeWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qs = (int)blockIdx.x * kMergeWaves + wave;
   const bool live = qs < nqs;
   unsigned long long* K = keys[wave];
   const int64_t p0 = (int64_t)qs * kParts;
-  // list sizes and offsets (lanes 0..kParts-1)
-  int n_l = (live && lane < kParts) ? (int)a.pntop[p0 + lane] : 0;
-  int inc = n_l;
-#pragma unroll
-  for (int d = 1; d < kParts; d <<= 1) {
-    const int u = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += u;
-  }
-  const int o_l = inc - n_l;
-  const int total = __shfl(inc, kParts - 1, 64);
-  // list sizes / offsets as wave-uniform values (shuffles only with every lane active)
-  int ln[kParts], lo[kParts];
-#pragma unroll
-  for (int l = 0; l < kParts; l++) {
-    ln[l] = __shfl(n_l, l, 64);
-    lo[l] = __shfl(o_l, l, 64);
-  }
-#pragma unroll
-  for (int l = 0; l < kParts; l++)
-    for (int x = lane; x < ln[l]; x += 64) K[lo[l] + x] = a.ptop[(p0 + l) * kTopHits + x];
-  __syncthreads();
-  for (int e = lane; e < total; e += 64) {
-    const unsigned long long key = K[e];
-    int rank = 0;
-#pragma unroll
-    for (int l = 0; l < kParts; l++) {
-      const int n = ln[l], o = lo[l];
-      if (e >= o && e < o + n) {
-        rank += e - o;  // own list: its position
-        continue;
-      }
-      int b0 = 0, b1 = n;
-      while (b0 < b1) {
-        const int mid = (b0 + b1) >> 1;
-        if (K[o + mid] < key) b0 = mid + 1;
-        else b1 = mid;
-      }
-      rank += b0;
-    }
-    if (rank < kTopHits) {
-      a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)a.cent_seqno[(uint32_t)(key & 0xffffffffull)];
-      a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
-    }
-  }
-  // postings touched (stats): the parts' counts, one atomic per workgroup
+  // postings touched (stats): the parts' counts, one atomic per workgroup into one of kPostSpread lines
   {
-    __shared__ uint32_t wpost[kMergeWaves];
     uint32_t pp = (live && lane < kParts) ? a.ppost[p0 + lane] : 0u;
 #pragma unroll
     for (int d = 1; d < kParts; d <<= 1) pp += __shfl_xor(pp, d, 64);
@@ -1048,8 +1159,41 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       if (t) atomicAdd(a.postings_touched + 16 + 32 * (blockIdx.x % kPostSpread), t);
     }
   }
+  if (!live) return;
+  // list sizes and offsets (lanes 0..kParts-1)
+  const int n_l = lane < kParts ? min((int)a.pncand[p0 + lane], kPartCand) : 0;
+  int inc = n_l;
+#pragma unroll
+  for (int d = 1; d < kParts; d <<= 1) {
+    const int u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  const int o_l = inc - n_l;
+  const int total = __shfl(inc, kParts - 1, 64);
+#pragma unroll
+  for (int l = 0; l < kParts; l++) {
+    const int n = __shfl(n_l, l, 64), o = __shfl(o_l, l, 64);
+    for (int x = lane; x < n; x += 64) {
+      const uint32_t e = a.pcand[(p0 + l) * kPartCand + x];
+      const uint32_t ord = e & 0xffffffu;
+      const uint32_t len = a.seqs.lens[a.cent_seqno[ord]];
+      K[o + x] = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)len << 48) | ord;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int e = lane; e < total; e += 64) {
+    const unsigned long long key = K[e];
+    int rank = 0;
+    for (int y = 0; y < total; y++) rank += K[y] < key;
+    if (rank < kTopHits) {
+      a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)a.cent_seqno[(uint32_t)(key & 0xffffffu)];
+      a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
+    }
+  }
   // peers
-  int np_l = (live && lane < kParts) ? (int)a.pnpeer[p0 + lane] : 0;
+  const int np_l = lane < kParts ? (int)a.pnpeer[p0 + lane] : 0;
   const bool over = __any(np_l == 255);
   int pinc = np_l;
 #pragma unroll
@@ -1059,7 +1203,6 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
   const int ptotal = __shfl(pinc, kParts - 1, 64);
   const int po_l = pinc - np_l;
-  if (!live) return;
   const bool povf = over || ptotal > kPeerCap;
   // strong[seqno * 2 + strand]: the query has an earlier window query sharing >= 5/8 of its k-mers (it is
   // then all but surely a member, not a centroid: later queries need not align against it speculatively)
@@ -1077,36 +1220,59 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
         (uint8_t)(!povf && pmax * 8 >= nkq * a.strong_eighths && pmax > a.minwordmatches);
   }
   if (povf) return;
+  uint32_t* P = pkeys[wave];
   for (int l = 0; l < kParts; l++) {
     const int n = __shfl(np_l, l, 64), o = __shfl(po_l, l, 64);
+    if (n == 0) continue;
+    uint32_t key = 0xffffffffu;
     if (lane < n) {
-      a.peer_id[(int64_t)qs * kPeerCap + o + lane] = a.ppeer_id[(p0 + l) * kPeerCap + lane];
-      a.peer_count[(int64_t)qs * kPeerCap + o + lane] = a.ppeer_count[(p0 + l) * kPeerCap + lane];
+      const uint32_t id = a.ppeer_id[(p0 + l) * kPeerCap + lane];
+      const uint32_t cv = a.ppeer_count[(p0 + l) * kPeerCap + lane];
+      key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[a.peer_base + (int32_t)id] << 16) | id;
+      P[lane] = key;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < n) {
+      int r = 0;
+      for (int y = 0; y < n; y++) r += P[y] < key;
+      a.peer_id[(int64_t)qs * kPeerCap + o + r] = (uint16_t)(key & 0xffffu);
+      a.peer_count[(int64_t)qs * kPeerCap + o + r] = (uint8_t)(127u - (key >> 23));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
+  const int full_most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
+  const int count_most = kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists);
   if (!attr_set_on_device(k_attr_prefilter)) {
-    const int most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
-    for (const void* f : {(const void*)k_prefilter<0>, (const void*)k_prefilter<1>, (const void*)k_prefilter<2>,
-                          (const void*)k_prefilter<3>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, most);
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_pf_count, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+    if (e != hipSuccess) return e;
     mark_attr_set(k_attr_prefilter);
   }
-  // LDS: the fixed part + counters for the peer regions, the spares and one segment's centroids
+  // LDS of the full kernel: the fixed part + counters for the peer regions, the spares and one
+  // segment's centroids
   const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
-  const size_t smem = (size_t)kPfSharedBytes + kCentBase + ((((segn + kParts - 1) >> kPartShift) + 15) & ~15);
-  hipLaunchKernelGGL(k_prefilter<0>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
-  static const bool probe = getenv("UMICLUST_PFPROBE") != nullptr;
-  if (probe) {
-    hipLaunchKernelGGL(k_prefilter<1>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
-    hipLaunchKernelGGL(k_prefilter<2>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
-    hipLaunchKernelGGL(k_prefilter<3>, dim3(nqs * kParts), dim3(kPfThreads), smem, st, a);
+  const size_t sub = (size_t)(((segn + kParts - 1) >> kPartShift) + 15) & ~(size_t)15;
+  const size_t smem_full = (size_t)kPfSharedBytes + kCentBase + sub;
+  if (a.nseg <= 1) {
+    // lean counting, then the full kernel over the units it could not finish (the grid exits at once
+    // when there are none), then the merge
+    if (a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
+    const uint32_t tab_off = (uint32_t)(kCentBase + sub);
+    hipLaunchKernelGGL(k_pf_count, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
+                       st, a, tab_off);
+    hipLaunchKernelGGL(k_pf_full, dim3(256), dim3(kPfThreads), smem_full, st, a, 1);
+  } else {
+    hipLaunchKernelGGL(k_pf_full, dim3(nqs * kParts), dim3(kPfThreads), smem_full, st, a, 0);
   }
   hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st,
                      a, nqs);

@@ -91,6 +91,10 @@ hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int
 // prefilter: for query-strands qs in [0, nqs): query seqno = q0 + qs/2 (or qs if !both), strand.
 // postings-touched partial sums: slots counters[16 + 32 s], s < kPostSpread (separate L2 lines)
 constexpr int kPostSpread = 32;
+constexpr int kPartCand = 64;  // candidates a (query-strand, part) passes to the merge
+// pass counters: [0..15] stats and pair counts, the postings partial sums, the overflowed-unit count
+constexpr int kUnitsSlot = 16 + kPostSpread * 32;
+constexpr int kCountersLen = kUnitsSlot + 32;
 struct PrefilterArgs {
   DevSeqs seqs;
   const uint16_t* arena;   // postings of every tile
@@ -113,9 +117,14 @@ struct PrefilterArgs {
   // and a query sees the window entries before it
   TileView peer[kPeerTiles];  // oldest first, the block's own tile last (absent ones: n = 0)
   int32_t peer_base;
-  // per-(query-strand, part) outputs, merged by launch_prefilter's second kernel
-  unsigned long long* ptop;  // [nqs*kParts*kTopHits] keys (127-count)<<56 | len<<48 | ordinal, sorted
-  uint8_t* pntop;            // [nqs*kParts]
+  int32_t nlist_cap;       // list-table capacity of the lean counting kernel (>= k-mers x tiles)
+  // per-(query-strand, part) outputs, merged by launch_prefilter's last kernel: candidates (count >= the
+  // threshold) as count << 24 | ordinal, unsorted, at most kPartCand (255 in pncand: overflow, re-run by
+  // the full kernel, which writes its exact part top-41 in the same form)
+  uint32_t* pcand;           // [nqs*kParts*kPartCand]
+  uint8_t* pncand;           // [nqs*kParts]
+  uint32_t* units;           // [nqs*kParts] overflowed (query-strand, part) units, *nunits of them
+  uint32_t* nunits;
   uint16_t* ppeer_id;        // [nqs*kParts*kPeerCap]
   uint8_t* ppeer_count;      // [nqs*kParts*kPeerCap]
   uint8_t* pnpeer;           // [nqs*kParts] (255 = overflow)
