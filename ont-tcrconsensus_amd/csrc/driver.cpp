@@ -171,9 +171,17 @@ struct Pass {
   std::vector<uint8_t> kind, ndeps;
   std::vector<uint16_t> deps;
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
+  // split passes: the counting half (enqueue_count) of the block this buffer set serves next
+  PinBuf<TileView> h_tiles_a;
+  DevBuf<TileView> d_tiles_a;
+  DevBuf<uint32_t> d_anunits;  // overflowed units of the lean kernel (the merge resets it)
+  hipEvent_t ev_a = nullptr;   // after the counting half's view upload (h_tiles_a may be rewritten)
+  bool a_live = false, a_timed = false;
+  int32_t a_q0 = -1, a_base = 0, a_slot = 0, t_slot = 0;
   ~Pass() {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (ev_a) (void)hipEventDestroy(ev_a);
   }
 };
 
@@ -293,7 +301,8 @@ struct umiclust_ctx {
   // every kDelta new centroids) + a delta tile (rebuilt every block): an LSM layout, so a block
   // only rebuilds postings of at most kDelta centroids
   std::vector<Tile*> tiles;       // sealed
-  Tile base_tile, delta_tile;
+  Tile base_tile, delta_tile[2];  // the delta alternates: a counting half may still read the previous one
+  int32_t delta_cur = 0;
   int32_t sealed_end = 0, base_end = 0;
   DevBuf<int32_t> d_cent;         // ordinal -> seqno
   DevBuf<uint8_t> d_cent_len;     // ordinal -> length
@@ -305,6 +314,15 @@ struct umiclust_ctx {
   // passes in flight: 2 by default; 3 (window of three blocks) hides more host time but its extra peers cost
   // more than that on configs 2/3/5 (profiles/r02/pipeline_depth_sweep.json)
   int32_t depth = 2;
+  // split passes (depth 2, UMICLUST_SPLIT=0 turns them off): a block's counting runs against the index
+  // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
+  // wait for its resolution, so the counting leaves the host <-> device critical cycle
+  int32_t split_env = -1;         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
+  bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
+                                  // concurrent counting slows the pass chain the host waits for)
+  DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
+  PinBuf<int32_t> h_seq2ord;
+  hipEvent_t a_ev[4][3] = {};     // counting halves, ring by block: begin / end (st_pf), gate (main stream)
   std::unique_ptr<WorkPool> pool;  // host threads of resolve_pass (UMICLUST_RESOLVE_THREADS)
   int32_t resolve_threads = 4;
   DevBuf<uint16_t> arena;         // postings of every tile (one buffer, one descriptor per pass)
@@ -313,6 +331,8 @@ struct umiclust_ctx {
   int32_t pass_B = 0;
   hipStream_t st_b = nullptr, st_copy = nullptr;
   hipStream_t st_al = nullptr;    // walk / alignment rounds / packing of the passes
+  hipStream_t st_pf = nullptr;    // counting halves of split passes (the main stream does not queue behind them)
+  int32_t last_a_slot = -1;       // a_ev slot of the latest counting half
   hipEvent_t evb[2] = {nullptr, nullptr};
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ix_events;  // index rebuild timing
@@ -574,6 +594,13 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   // fixed capacities, so a pass never frees memory a queued pass still reads
   c->hip(P.h_tiles.ensure(64), "pin");
   c->hip(P.d_tiles.ensure(64), "alloc");
+  c->hip(P.h_tiles_a.ensure(64), "pin");
+  c->hip(P.d_tiles_a.ensure(64), "alloc");
+  if (!P.d_anunits.p) {
+    c->hip(P.d_anunits.ensure(1), "alloc");
+    c->hip(hipMemsetAsync(P.d_anunits.p, 0, 4, c->st), "memset");
+  }
+  if (!P.ev_a) c->hip(hipEventCreate(&P.ev_a), "event");
 }
 
 // Enqueue the device pass of block [q0, q0+nq) against the index as it stands (centroids of the
@@ -584,7 +611,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
 void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* const* prevs, int nprev, Tile& own,
-                  int32_t region, bool lazy_peers = false) {
+                  int32_t region, bool lazy_peers = false, bool after_count = false) {
   const int32_t w0 = nprev > 0 ? prevs[0]->base : q0;
   const int both = c->both;
   const int32_t nqs = nq * both;
@@ -609,7 +636,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   for (Tile* t : c->tiles)
     if (t->n > 0) P.h_tiles.p[nv++] = view_of(*t);
   if (c->base_tile.n > 0) P.h_tiles.p[nv++] = view_of(c->base_tile);
-  if (c->delta_tile.n > 0) P.h_tiles.p[nv++] = view_of(c->delta_tile);
+  if (c->delta_tile[c->delta_cur].n > 0) P.h_tiles.p[nv++] = view_of(c->delta_tile[c->delta_cur]);
   if (nv > 0)
     c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
@@ -654,7 +681,20 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.pcand = P.d_pcand.p;
   a.pncand = P.d_pncand.p;
   a.units = P.d_units.p;
-  a.nunits = P.d_counters.p + kUnitsSlot;
+  a.nunits = P.d_anunits.p;
+  a.flag_tile = -1;
+  a.cand_base = w0;
+  a.peer_shift = 0;
+  a.peer_id_add = 0;
+  a.seq2ord = c->d_seq2ord.p - c->bin_s[c->cur_bin];
+  const bool second_half = after_count && P.a_live && P.a_q0 == q0;
+  if (second_half) {
+    // the counting half ran with the window one block wider (oldest first): its peer ids are relative to
+    // that window's start
+    a.cand_base = P.a_base;
+    a.peer_shift = w0 - P.a_base;
+    a.peer_id_add = a.peer_shift;
+  }
   // list table of the lean kernel: every k-mer of the block's length in every tile it reads
   a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, c->hlen[q0] - 7) *
                                               ((a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0) + kPeerTiles));
@@ -672,9 +712,13 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.strong_eighths = c->strong_eighths;
   a.postings_touched = P.d_counters.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
+  if (second_half) c->hip(hipStreamWaitEvent(st, c->a_ev[P.a_slot][1], 0), "wait");
   c->hip(hipEventRecord(P.ev[0], st), "event");
-  c->hip(launch_prefilter(a, st), "prefilter");
+  c->hip(launch_prefilter(a, st, second_half ? 2 : 0), "prefilter");
   c->hip(hipEventRecord(P.ev[1], st), "event");
+  P.a_timed = second_half;
+  P.t_slot = P.a_slot;
+  P.a_live = false;
   // The walk, its alignment rounds and the packing run on the align stream: they read only this
   // pass's buffers and the sequences, so the main stream goes on with the index append of the block
   // being resolved and the next pass's prefilter while these small launches run.
@@ -726,6 +770,90 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipEventRecord(P.ev[4], st), "event");
 }
 
+// The counting half of a split pass (block [q0, q0+nq), launch_prefilter mode 1): the lean kernel against
+// the index as it stands and the window's peer tiles `wins` (oldest first, the block's own -- built -- last);
+// the hits of wins[flag] (a block not yet resolved) become flagged candidates.  The second half is
+// enqueue_pass(..., after_count = true) once that block is resolved and appended.  Bins past one counter
+// segment are not split (a_live stays false and the second half runs the whole prefilter).
+void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* const* wins, int nwin, int flag,
+                   int32_t slot) {
+  P.a_live = false;
+  const int32_t nseg = (c->index_end + kSegCentroids - 1) / kSegCentroids;
+  if (nseg > 1) return;
+  for (auto& e : c->a_ev[slot])
+    if (!e) c->hip(hipEventCreate(&e), "event");
+  // on its own stream, gated by the main stream's work so far (index append, peer tiles, this buffer set's
+  // last merge): the main stream's next append and second half do not queue behind it
+  hipStream_t st = c->st;
+  if (c->split_stream) {
+    // created on first use, after the others: HIP hands streams hardware queues in creation order, and an
+    // extra stream created earlier would push the alignment stream onto the main stream's queue
+    if (!c->st_pf) c->hip(hipStreamCreateWithFlags(&c->st_pf, hipStreamNonBlocking), "stream");
+    c->hip(hipEventRecord(c->a_ev[slot][2], c->st), "event");
+    st = c->st_pf;
+    c->hip(hipStreamWaitEvent(st, c->a_ev[slot][2], 0), "wait");
+  }
+  c->hip(hipEventSynchronize(P.ev_a), "sync");  // the last upload from h_tiles_a is done
+  int32_t nv = 0;
+  const size_t need = c->tiles.size() + 2;
+  if (need > P.h_tiles_a.n) {
+    c->hip(hipStreamSynchronize(st), "sync");  // rare: the views array grows
+    c->hip(P.h_tiles_a.ensure(need * 2), "pin");
+    c->hip(P.d_tiles_a.ensure(need * 2), "alloc");
+  }
+  for (Tile* t : c->tiles)
+    if (t->n > 0) P.h_tiles_a.p[nv++] = view_of(*t);
+  if (c->base_tile.n > 0) P.h_tiles_a.p[nv++] = view_of(c->base_tile);
+  if (c->delta_tile[c->delta_cur].n > 0) P.h_tiles_a.p[nv++] = view_of(c->delta_tile[c->delta_cur]);
+  if (nv > 0)
+    c->hip(hipMemcpyAsync(P.d_tiles_a.p, P.h_tiles_a.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
+           "tiles");
+  c->hip(hipEventRecord(P.ev_a, st), "event");
+  PrefilterArgs a{};
+  a.seqs = dev_seqs(c);
+  a.arena = c->arena.p;
+  a.tiles = P.d_tiles_a.p;
+  a.ntiles = nv;
+  a.ncent = c->index_end;
+  a.nseg = nseg;
+  a.seg_tile[0] = 0;
+  a.seg_tile[1] = nv;
+  uint64_t lo = UINT64_MAX;
+  for (int i = 0; i < nwin; i++) lo = std::min(lo, wins[i]->post_base);
+  for (int v = 0; v < nv; v++) lo = std::min(lo, P.h_tiles_a.p[v].post_base);
+  a.seg_base[0] = lo;
+  a.cent_seqno = c->d_cent.p;
+  for (int L = 0; L <= kMaxLen; L++) a.cnt_ge[L] = c->cnt_ge[L];
+  a.q0 = q0;
+  a.nq = nq;
+  a.both = c->both;
+  a.minwordmatches = c->p.minwordmatches;
+  for (int i = 0; i < kPeerTiles; i++) {
+    const int j = i - (kPeerTiles - nwin);
+    a.peer[i] = j >= 0 ? view_of(*wins[j]) : TileView{};
+  }
+  a.flag_tile = flag >= 0 ? (kPeerTiles - nwin) + flag : -1;
+  a.peer_base = a.cand_base = wins[0]->base;
+  a.seq2ord = c->d_seq2ord.p - c->bin_s[c->cur_bin];
+  a.pcand = P.d_pcand.p;
+  a.pncand = P.d_pncand.p;
+  a.units = P.d_units.p;
+  a.nunits = P.d_anunits.p;
+  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, c->hlen[q0] - 7) * (nv + kPeerTiles));
+  a.ppeer_id = P.d_ppeer_id.p;
+  a.ppeer_count = P.d_ppeer_count.p;
+  a.pnpeer = P.d_pnpeer.p;
+  a.ppost = P.d_ppost.p;
+  c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
+  c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
+  c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
+  c->last_a_slot = slot;
+  P.a_live = true;
+  P.a_q0 = q0;
+  P.a_base = wins[0]->base;
+  P.a_slot = slot;
+}
+
 // Wait for a pass and resolve its block on the host in sorted order.  Returns false if a peer
 // list overflowed (the caller re-runs the block in smaller pieces).  Every query of the peer
 // window before the block is already resolved, so peers are final or earlier in this block.
@@ -748,6 +876,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   float ms = 0;
   c->hip(hipEventElapsedTime(&ms, P.ev[0], P.ev[1]), "elapsed");
   t_pf += ms * 1e-3;
+  if (P.a_timed) {
+    c->hip(hipEventElapsedTime(&ms, c->a_ev[P.t_slot][0], c->a_ev[P.t_slot][1]), "elapsed");
+    t_pf += ms * 1e-3;
+  }
   c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;
   {
@@ -1142,6 +1274,16 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     c->cent_len.push_back(c->hlen[q]);
     for (int L = 0; L <= c->hlen[q]; L++) c->cnt_ge[L]++;
   }
+  {
+    // seqno -> ordinal for the merge's flagged hits (the new centroids are in sorted order)
+    const int32_t s0 = c->bin_s[c->cur_bin];
+    for (size_t i = 0; i < new_cents.size(); i++) c->h_seq2ord.p[new_cents[i] - s0] = ord0 + (int32_t)i;
+    const int32_t lo = new_cents.front() - s0, hi = new_cents.back() - s0;
+    if (hi >= lo)
+      c->hip(hipMemcpyAsync(c->d_seq2ord.p + lo, c->h_seq2ord.p + lo, (size_t)(hi - lo + 1) * 4, hipMemcpyHostToDevice,
+                            st),
+             "h2d seq2ord");
+  }
   memcpy(c->h_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4);
   memcpy(c->h_cent_len.p + ord0, c->cent_len.data() + ord0, new_cents.size());
   c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->h_cent.p + ord0, new_cents.size() * 4, hipMemcpyHostToDevice, st),
@@ -1170,24 +1312,29 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     c->base_tile.n = 0;
   }
   if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
+    // the base is rebuilt in place: the latest counting half (on st_pf) may still read it
+    if (c->last_a_slot >= 0) c->hip(hipStreamWaitEvent(st, c->a_ev[c->last_a_slot][1], 0), "wait");
     c->base_tile.base = c->sealed_end;
     c->base_tile.seg = c->sealed_end / kSegCentroids;
     build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, c->sealed_end, kCentBase,
                kSegCentroids);
     c->base_end = ordend;
   }
-  c->delta_tile.base = c->base_end;
-  c->delta_tile.seg = c->base_end / kSegCentroids;
+  // the other delta slot was last read by a counting half the main stream has already waited for (the
+  // second half of its pass precedes this append)
+  c->delta_cur ^= 1;
+  Tile& dt = c->delta_tile[c->delta_cur];
+  dt.base = c->base_end;
+  dt.seg = c->base_end / kSegCentroids;
   if (ordend > c->base_end)
-    build_tile(c, c->delta_tile, c->d_cent.p, c->base_end, ordend - c->base_end, c->base_end, kCentBase,
-               kSegCentroids);
+    build_tile(c, dt, c->d_cent.p, c->base_end, ordend - c->base_end, c->base_end, kCentBase, kSegCentroids);
   else
-    c->delta_tile.n = 0;
+    dt.n = 0;
   c->index_end = ordend;
   c->hip(hipEventRecord(ev.second, st), "event");
 }
 
-void cluster_all(umiclust_ctx* c, int32_t bin) {
+void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   const double t0 = now_s();
   if (bin < 0 || bin + 1 >= (int32_t)c->bin_s.size()) c->fail(UMICLUST_EINVAL, "bin %d out of range", bin);
   // one bin = the sorted seqnos [s0, s1); seqnos stay absolute everywhere
@@ -1206,7 +1353,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   c->hip(hipStreamSynchronize(c->st), "sync");  // no queued work may still read the old tiles
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();
-  c->base_tile.n = c->delta_tile.n = 0;
+  if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
+  c->base_tile.n = c->delta_tile[0].n = c->delta_tile[1].n = 0;
+  c->last_a_slot = -1;
   c->sealed_end = c->base_end = 0;
   c->index_end = 0;
   c->nix = 0;
@@ -1217,6 +1366,10 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
   c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->h_cent.ensure((size_t)n + 1), "pin cent");
   c->hip(c->h_cent_len.ensure((size_t)n + 1), "pin cent");
+  c->hip(c->d_seq2ord.ensure((size_t)n + 1), "alloc seq2ord");
+  c->hip(c->h_seq2ord.ensure((size_t)n + 1), "pin seq2ord");
+  std::fill(c->h_seq2ord.p, c->h_seq2ord.p + n, -1);
+  c->hip(hipMemsetAsync(c->d_seq2ord.p, 0xff, (size_t)n * 4, c->st), "memset");
   std::vector<uint8_t> state_buf((size_t)n, ST_UNDET);
   StateView state{state_buf.data(), s0};
   double t_pf = 0, t_al = 0, t_host = 0;
@@ -1237,7 +1390,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
       off += t.post_cap;
     };
     slot(c->base_tile, kTile);
-    slot(c->delta_tile, kDelta);
+    slot(c->delta_tile[0], kDelta);
+    slot(c->delta_tile[1], kDelta);
     for (Tile& t : c->blk_tile) slot(t, kMaxBlock);
     slot(c->solo_tile, kMaxBlock);
     c->sealed_slot0 = off;
@@ -1296,6 +1450,83 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     for (int i = 0; i < nprev; i++) prevs[i] = &tile_of(k - nprev + i);
     enqueue_pass(c, c->pass[k % D], blocks[k].first, blocks[k].second, prevs, nprev, tile_of(k), k % D, lazy);
   };
+  // split passes shorten the host <-> device cycle of one bin at the price of a wider counting window;
+  // multi-bin sets run several lanes on one GPU, which is throughput-bound: there the whole passes win
+  // (configs 2 / 5: +12 % / +2 %, config 3: -6 %; profiles/r02/split_ab.json)
+  const bool split = c->split_env >= 0 ? c->split_env != 0 : !multi_bin;
+  if (split && D == 2) {
+    // Split passes.  Pass j = counting half A(j) (index of blocks <= j-3, window j-2 .. j with block j-2
+    // flagged) enqueued after block j-3 is resolved, and second half R(j) (the full kernel over A's
+    // overflowed units against index <= j-2 / window j-1 .. j, the merge keeping the flagged hits that are
+    // centroids, then walk / align / pack) after block j-2 is.  Block j's peer tile: blk_tile[j % 4],
+    // counter region j % 3 (three consecutive blocks share a counting window).
+    auto stile = [&](int32_t j) -> Tile& { return c->blk_tile[j % (kPeerTiles + 1)]; };
+    auto build_peer = [&](int32_t j) {
+      Tile& t = stile(j);
+      const int32_t region = j % kPeerTiles;
+      if (!(t.prebuilt && t.base == blocks[j].first && t.n == blocks[j].second && t.seg == region))
+        build_tile(c, t, c->d_iota.p, blocks[j].first, blocks[j].second, 0, region * kPeerRegion, 1 << 30);
+      t.base = blocks[j].first;
+      t.seg = region;
+      t.len = c->hlen[blocks[j].first];
+      t.prebuilt = true;
+    };
+    // R(j) with the window's blocks from `first` (first = j - 1 in the steady state)
+    auto second_half = [&](int32_t j, int32_t first, bool after_count) {
+      const Tile* prevs[kPeerTiles];
+      int np = 0;
+      for (int32_t i = first; i < j; i++) prevs[np++] = &stile(i);
+      enqueue_pass(c, c->pass[j % 2], blocks[j].first, blocks[j].second, prevs, np, stile(j), j % kPeerTiles, lazy,
+                   after_count);
+    };
+    auto count_half = [&](int32_t j, int32_t first, int flag) {
+      const Tile* wins[kPeerTiles];
+      int nw = 0;
+      for (int32_t i = first; i <= j; i++) wins[nw++] = &stile(i);
+      enqueue_count(c, c->pass[j % 2], blocks[j].first, blocks[j].second, wins, nw, flag, j % 4);
+    };
+    // the index holds the blocks before r and nothing is queued: classic passes r (window r) and r+1 (window
+    // r, r+1), then A(r+2) with block r flagged
+    auto prime = [&](int32_t r) {
+      for (int32_t j = r; j < r + 3 && j < nb; j++) build_peer(j);
+      if (r < nb) second_half(r, r, false);
+      if (r + 1 < nb) second_half(r + 1, r, false);
+      if (r + 2 < nb) count_half(r + 2, r, 0);
+    };
+    prime(0);
+    for (int32_t k = 0; k < nb; k++) {
+      Pass& P = c->pass[k % 2];
+      if (k + 3 < nb) build_peer(k + 3);  // queries only: built while the host resolves block k
+      if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+        // drain everything queued (its windows include block k) and restart the pipeline after block k
+        c->hip(hipStreamSynchronize(c->st_al), "sync");
+        if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
+        c->hip(hipStreamSynchronize(c->st), "sync");
+        for (Pass& Q : c->pass) {
+          Q.live = false;
+          Q.a_live = false;
+          c->hip(hipMemsetAsync(Q.d_anunits.p, 0, 4, c->st), "memset");
+        }
+        run_alone(blocks[k].first, blocks[k].second);
+        if (b_eff > 256 && k + 1 < nb) {
+          b_eff /= 2;
+          const int32_t from = blocks[k].first + blocks[k].second;
+          blocks.resize((size_t)k + 1);
+          split_blocks(from, b_eff);
+          nb = (int32_t)blocks.size();
+        }
+        for (Tile& t : c->blk_tile) t.prebuilt = false;
+        prime(k + 1);
+        continue;
+      }
+      append_centroids(c, new_cents);
+      c->stats.n_blocks++;
+      lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
+      c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
+      if (k + 2 < nb) second_half(k + 2, k + 1, true);
+      if (k + 3 < nb) count_half(k + 3, k + 1, 0);
+    }
+  } else {
   for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k % D];
@@ -1338,7 +1569,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin) {
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
     if (k + D < nb) enqueue(k + D, D - 1);
   }
+  }
   c->b_hint = b_eff;
+  if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
   c->hip(hipStreamSynchronize(c->st_al), "sync");
   c->hip(hipStreamSynchronize(c->st), "sync");
   for (size_t i = 0; i < c->nix; i++) {
@@ -2245,6 +2478,10 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     return nullptr;
   }
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
+  if (const char* e = getenv("UMICLUST_SPLIT")) {
+    c->split_env = atoi(e) != 0 ? 1 : 0;
+    c->split_stream = atoi(e) == 2;
+  }
   if (const char* e = getenv("UMICLUST_RESOLVE_THREADS")) c->resolve_threads = std::max(1, std::min(16, atoi(e)));
   if (const char* b = getenv("UMICLUST_BLOCK")) {
     c->block_size = std::max(1, std::min(kTile, atoi(b)));
@@ -2282,6 +2519,7 @@ void umiclust_destroy(umiclust_ctx* c) {
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st_al) (void)hipStreamDestroy(c->st_al);
+  if (c->st_pf) (void)hipStreamDestroy(c->st_pf);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -2411,7 +2649,7 @@ int32_t umiclust_load_bins(umiclust_ctx* c, const umiclust_params* p, const char
 int64_t umiclust_cluster_bin(umiclust_ctx* c, int32_t bin, umiclust_stats* stats) {
   UC_GUARD(c, {
     if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster_bin before umiclust_load_bins");
-    cluster_all(c, bin);
+    cluster_all(c, bin, true);
     if (stats) *stats = c->stats;
     return c->nclusters;
   });

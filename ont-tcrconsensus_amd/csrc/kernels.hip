@@ -972,7 +972,7 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
       const uint32_t kx = S.pcand[x];
       int r = 0;
       for (int y = 0; y < np; y++) r += S.pcand[y] < kx;
-      a.ppeer_id[pq_ * kPeerCap + r] = (uint16_t)(kx & 0xffffu);
+      a.ppeer_id[pq_ * kPeerCap + r] = (uint16_t)((kx & 0xffffu) + (uint32_t)a.peer_id_add);
       a.ppeer_count[pq_ * kPeerCap + r] = (uint8_t)(127u - (kx >> 23));
     }
   }
@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
 #pragma unroll
   for (int v = 0; v < kPeerTiles; v++) {
     const TileView pv = a.peer[v];
-    if (pv.n <= 0) continue;
+    if (pv.n <= 0 || v == a.flag_tile) continue;
     const int lim = min(pv.n, q - pv.base);
     const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
     const int nwords = (nsubP + 3) >> 2;
@@ -1112,9 +1112,32 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
         mk &= mk - 1u;
         if (slot < (uint32_t)kPeerCap) {
           const int32_t sq = pv.base + ((4 * x + (int)byte) << kPartShift) + part;
-          a.ppeer_id[pq_ * kPeerCap + slot] = (uint16_t)(sq - a.peer_base);
+          a.ppeer_id[pq_ * kPeerCap + slot] = (uint16_t)(sq - a.cand_base);
           a.ppeer_count[pq_ * kPeerCap + slot] = (uint8_t)((w >> (8 * byte)) & 0xffu);
         }
+        slot++;
+      }
+    }
+  }
+  // the flagged tile (a split pass's unresolved oldest block): its hits are candidates for the merge
+  if (a.flag_tile >= 0) {
+    const TileView pv = a.peer[a.flag_tile];
+    const int nsubP = pv.n > part ? (pv.n - part + kParts - 1) >> kPartShift : 0;
+    const int nwords = (nsubP + 3) >> 2;
+    const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
+    for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
+      const int x = x0 + lane;
+      const uint32_t w = x < nwords ? pw[x] : 0u;
+      const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;
+      uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
+      if (__ballot(mk != 0u) == 0ull) continue;
+      uint32_t slot = wave_alloc((uint32_t)__builtin_popcount(mk), &H.ncand);
+      while (mk) {
+        const uint32_t byte = (uint32_t)__builtin_ctz(mk) >> 3;
+        mk &= mk - 1u;
+        const int32_t sq = pv.base + ((4 * x + (int)byte) << kPartShift) + part;
+        if (slot < (uint32_t)kPartCand)
+          a.pcand[pq_ * kPartCand + slot] = (((w >> (8 * byte)) & 0xffu) << 24) | 0x800000u | (uint32_t)(sq - a.cand_base);
         slot++;
       }
     }
@@ -1159,6 +1182,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       if (t) atomicAdd(a.postings_touched + 16 + 32 * (blockIdx.x % kPostSpread), t);
     }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nunits = 0;  // the full kernel has read it (stream order)
   if (!live) return;
   // list sizes and offsets (lanes 0..kParts-1)
   const int n_l = lane < kParts ? min((int)a.pncand[p0 + lane], kPartCand) : 0;
@@ -1175,11 +1199,25 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
     const int n = __shfl(n_l, l, 64), o = __shfl(o_l, l, 64);
     for (int x = lane; x < n; x += 64) {
       const uint32_t e = a.pcand[(p0 + l) * kPartCand + x];
-      const uint32_t ord = e & 0xffffffu;
-      const uint32_t len = a.seqs.lens[a.cent_seqno[ord]];
-      K[o + x] = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)len << 48) | ord;
+      unsigned long long key = ~0ull;  // a flagged hit that turned out a member: no candidate
+      if (e & 0x800000u) {
+        const int32_t sq = a.cand_base + (int32_t)(e & 0x7fffffu);
+        const int32_t ord = a.seq2ord[sq];
+        if (ord >= 0)
+          key = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)a.seqs.lens[sq] << 48) |
+                (uint32_t)ord;
+      } else {
+        const uint32_t ord = e & 0xffffffu;
+        const uint32_t len = a.seqs.lens[a.cent_seqno[ord]];
+        key = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)len << 48) | ord;
+      }
+      K[o + x] = key;
     }
   }
+  int nvalid = 0;
+  for (int e = lane; e < total; e += 64) nvalid += K[e] != ~0ull;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) nvalid += __shfl_xor(nvalid, d, 64);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1187,7 +1225,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
     const unsigned long long key = K[e];
     int rank = 0;
     for (int y = 0; y < total; y++) rank += K[y] < key;
-    if (rank < kTopHits) {
+    if (rank < kTopHits && key != ~0ull) {
       a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)a.cent_seqno[(uint32_t)(key & 0xffffffu)];
       a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
     }
@@ -1212,7 +1250,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
 #pragma unroll
   for (int d = 1; d < kParts; d <<= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
   if (lane == 0) {
-    a.ntop[qs] = (uint8_t)min(total, kTopHits);
+    a.ntop[qs] = (uint8_t)min(nvalid, kTopHits);
     a.npeer[qs] = (uint8_t)(povf ? 255 : ptotal);
     const int32_t q = a.q0 + qs / a.both;
     const int nkq = a.seqs.nk[(int64_t)q * 2 + qs % a.both];
@@ -1226,7 +1264,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
     if (n == 0) continue;
     uint32_t key = 0xffffffffu;
     if (lane < n) {
-      const uint32_t id = a.ppeer_id[(p0 + l) * kPeerCap + lane];
+      const uint32_t id = a.ppeer_id[(p0 + l) * kPeerCap + lane] - (uint32_t)a.peer_shift;  // peer_base-relative
       const uint32_t cv = a.ppeer_count[(p0 + l) * kPeerCap + lane];
       key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[a.peer_base + (int32_t)id] << 16) | id;
       P[lane] = key;
@@ -1246,7 +1284,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
 }
 
-hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
+hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
   const int full_most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
@@ -1263,13 +1301,16 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st) {
   const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
   const size_t sub = (size_t)(((segn + kParts - 1) >> kPartShift) + 15) & ~(size_t)15;
   const size_t smem_full = (size_t)kPfSharedBytes + kCentBase + sub;
-  if (a.nseg <= 1) {
-    // lean counting, then the full kernel over the units it could not finish (the grid exits at once
-    // when there are none), then the merge
-    if (a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
+  if (mode == 1 || (mode == 0 && a.nseg <= 1)) {
+    // lean counting (one counter segment)
+    if (a.nseg > 1 || a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
     const uint32_t tab_off = (uint32_t)(kCentBase + sub);
     hipLaunchKernelGGL(k_pf_count, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
                        st, a, tab_off);
+    if (mode == 1) return hipGetLastError();
+  }
+  if (mode == 2 || a.nseg <= 1) {
+    // the full kernel over the units the lean kernel could not finish (exits at once when there are none)
     hipLaunchKernelGGL(k_pf_full, dim3(256), dim3(kPfThreads), smem_full, st, a, 1);
   } else {
     hipLaunchKernelGGL(k_pf_full, dim3(nqs * kParts), dim3(kPfThreads), smem_full, st, a, 0);

@@ -124,7 +124,17 @@ struct PrefilterArgs {
   uint32_t* pcand;           // [nqs*kParts*kPartCand]
   uint8_t* pncand;           // [nqs*kParts]
   uint32_t* units;           // [nqs*kParts] overflowed (query-strand, part) units, *nunits of them
-  uint32_t* nunits;
+  uint32_t* nunits;  // (the merge resets *nunits to 0)
+  // split passes (the counting of a block runs before the block two ahead of it is resolved): peer tile
+  // flag_tile (>= 0) is that unresolved block; its hits become flagged candidates count << 24 | 1 << 23 |
+  // (seqno - cand_base), kept by the merge if seq2ord[seqno] >= 0 (a centroid by then).  Stored peer ids
+  // are relative to cand_base; the merge writes them relative to peer_base (id - peer_shift), and the full
+  // kernel stores its own (peer_base-relative) ids + peer_id_add.
+  int32_t flag_tile;
+  int32_t cand_base;
+  int32_t peer_shift;
+  int32_t peer_id_add;
+  const int32_t* seq2ord;  // [seqno] centroid ordinal or -1 (absolute seqnos)
   uint16_t* ppeer_id;        // [nqs*kParts*kPeerCap]
   uint8_t* ppeer_count;      // [nqs*kParts*kPeerCap]
   uint8_t* pnpeer;           // [nqs*kParts] (255 = overflow)
@@ -143,7 +153,10 @@ struct PrefilterArgs {
   unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
 };
 // two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
-hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st);
+// mode 0: the whole prefilter (lean counting + the full kernel over its overflowed units, or the full
+// kernel alone for multi-segment bins, then the merge); mode 1: only the lean counting (a split pass's
+// first half); mode 2: the full kernel over the units mode 1 left + the merge (its second half)
+hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode = 0);
 
 // alignment of pairs whose queries all have length qlen; pq = (query seqno << 1) | strand, pt = target seqno (plus strand)
 // out[outidx ? outidx[k] : k] = matches | internal << 8 | (score & 0xffff) << 16.

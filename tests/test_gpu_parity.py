@@ -178,6 +178,46 @@ def test_block_size_invariance(block, monkeypatch):
     _cmp_cluster(g, orc.cluster(orc.params(1, 0.93, 58, 68), seqs))
 
 
+@pytest.mark.parametrize("split", ["0", "1", "2"])
+@pytest.mark.parametrize("block", [7, 64, 1000])
+def test_pipeline_modes(split, block, monkeypatch):
+    """Whole passes (UMICLUST_SPLIT=0) and split passes -- the counting half against the index before the
+    block two ahead is resolved, that block's hits flagged and kept by the merge only if they turn out
+    centroids -- on the main stream (1) or on their own stream (2): membership, strands, centroids,
+    consensus, alignment count and cells equal the oracle's for any block size."""
+    u = synth.make_umis(200, seed=23, max_reads=2500, orient_mix=0.2)
+    seqs = u.as_list()
+    monkeypatch.setenv("UMICLUST_BLOCK", str(block))
+    monkeypatch.setenv("UMICLUST_SPLIT", split)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.93, 58, 68), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(1, 0.93, 58, 68), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+
+
+@pytest.mark.parametrize("split", ["0", "1", "2"])
+def test_pipeline_modes_deep_clusters(split, monkeypatch):
+    """Config-5 style deep clusters (long UMIs, 15 % indels) with small blocks: peer lists overflow, blocks
+    re-run alone and the pipeline restarts mid-bin, in every pipeline mode."""
+    u = synth.make_umis(8, seed=31, max_reads=2500, orient_mix=0.3, mean_reads=1500.0, error_rate=0.15,
+                        split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                        pattern_rev=synth.UMI_REV_LONG)
+    seqs = u.as_list()
+    monkeypatch.setenv("UMICLUST_BLOCK", "256")
+    monkeypatch.setenv("UMICLUST_SPLIT", split)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.75, 80, 110), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(1, 0.75, 80, 110), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+    assert st["n_reruns"] > 0  # the overflow re-run and the pipeline restart were exercised
+
+
 def test_edge_inputs(gpu_ctx):
     p = _lib.params(1, 0.93, 58, 68)
     op = orc.params(1, 0.93, 58, 68)
@@ -374,11 +414,14 @@ def _multibin_cases():
 
 
 @pytest.mark.parametrize("name,gold", _multibin_cases(), ids=[n for n, _ in _multibin_cases()])
-def test_multibin_vs_oracle_golden(name, gold):
+@pytest.mark.parametrize("split", ["default", "1"])
+def test_multibin_vs_oracle_golden(name, gold, split, monkeypatch):
     """BASELINE configs 3 (24 barcodes x 40 Zipf bins) and 4 (both rounds, round 2 on the round-1 consensus
     UMIs) at reduced scale: every bin resident in one load, clustered bin by bin; the checksum of the per-bin
     digests (membership, strands, centroids, consensus) and every bin's cluster count equal the oracle's."""
     from umiclust import binset, synth
+    if split != "default":  # multi-bin sets run whole passes unless UMICLUST_SPLIT says otherwise
+        monkeypatch.setenv("UMICLUST_SPLIT", split)
     bs = synth.concat_bins(synth.config_bins(gold["config"], gold["scale"], workers=4))
     assert len(bs.bins) == gold["n_bins"] and bs.n == gold["n_reads"]
     rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if "round2" in gold else [])
