@@ -106,30 +106,37 @@ def full_bin_cpu_reference(config: int) -> dict | None:
 
 
 def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
-    """k_prefilter against the L2-served gather rate (its postings stay L2-resident: parts = XCDs), with
-    the HBM fraction as a side figure; k_align against the integer VALU issue ceiling."""
+    """The prefilter's counting kernel k_pf_count against the L2-served gather rate (its postings stay
+    L2-resident: parts = XCDs), with the HBM fraction as a side figure; k_align against the integer VALU
+    issue ceiling.  The kernel's launch time is its own HIP-event bracket on the stream it runs on
+    (umiclust_stats.t_count_s / n_count_launches); the postings are every posting the prefilter streamed."""
+    t_cnt = sum(s.get("t_count_s", 0.0) for s in stats)
+    n_cnt = sum(s.get("n_count_launches", 0) for s in stats)
     t_pf = sum(s["t_prefilter_s"] for s in stats)
     t_al = sum(s["t_align_s"] for s in stats)
-    n_launch = sum(s["n_blocks"] for s in stats)
+    n_blocks = sum(s["n_blocks"] for s in stats)
+    if n_cnt == 0:  # multi-segment bins only: the full kernel counts
+        t_cnt, n_cnt = t_pf, n_blocks
     pf_bytes = sum(s["kmer_postings"] for s in stats) * 2
     traffic = None
     if os.path.exists(traffic_json):
         try:
             tj = json.load(open(traffic_json))
-            if tj.get("config", 2) == config:  # PMC traffic is per workload
+            if tj.get("config", 2) == config and tj.get("kernel") == "k_pf_count":  # PMC traffic is per workload
                 traffic = tj.get("prefilter_hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    achieved = pf_bytes / t_pf / 1e9 if t_pf > 0 else 0.0
-    roof = dict(kernel="k_prefilter", bound="l2", achieved=achieved, peak=L2_GATHER_GBS, unit="GB/s",
+    achieved = pf_bytes / t_cnt / 1e9 if t_cnt > 0 else 0.0
+    roof = dict(kernel="k_pf_count", bound="l2", achieved=achieved, peak=L2_GATHER_GBS, unit="GB/s",
                 frac=achieved / L2_GATHER_GBS, traffic=traffic,
                 hbm_frac=achieved / HBM_PEAK_GBS, hbm_peak=HBM_PEAK_GBS,
-                bytes_per_launch=pf_bytes / max(1, n_launch), launches=n_launch,
-                avg_launch_ms=1e3 * t_pf / max(1, n_launch),
+                bytes_per_launch=pf_bytes / max(1, n_cnt), launches=n_cnt,
+                avg_launch_ms=1e3 * t_cnt / max(1, n_cnt),
+                prefilter_ms_per_block=1e3 * t_pf / max(1, n_blocks),
                 note="2 B per u16 posting streamed (postings served from the XCD-partitioned L2; measured HBM "
-                     "traffic is `traffic`); peak = L2-served gather rate, MI355X_MICROARCH.md (1,152-B rows); "
-                     "the 16-B-per-lane chunk gathers keep the texture data path (TD) 77 % busy and TA 42 % "
-                     "(profiles/r02/pmc_ta_td_c2.json): the kernel is bound by that path, not by L2 or HBM")
+                     "traffic is `traffic`); peak = L2-served gather rate, MI355X_MICROARCH.md (1,152-B rows). "
+                     "What binds it is instruction issue, not bytes: VALU and LDS-atomic issue per posting "
+                     "(profiles/r02/pmc_pf_count_c2.json)")
     cells = sum(s["cells"] for s in stats)
     cells_c = sum(s["cells_computed"] for s in stats)
     g_alg = cells / t_al / 1e9 if t_al else 0.0

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 2
+#define UMICLUST_ABI_VERSION 3
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -95,6 +95,8 @@ typedef struct umiclust_stats {
   int64_t n_reruns;       /* block pieces re-run alone after an in-window peer list overflowed */
   int64_t n_overlap_passes; /* overlap hash-table passes (1 + re-seeds after 64-bit hash collisions) */
   int64_t n_lazy_passes;  /* passes whose in-window peers were aligned on demand (round B) only */
+  double t_count_s;       /* kernel time, the prefilter's counting kernel alone (k_pf_count, HIP events) */
+  int64_t n_count_launches; /* its launches (one per pass over one counter segment) */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

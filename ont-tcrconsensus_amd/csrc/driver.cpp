@@ -176,12 +176,16 @@ struct Pass {
   DevBuf<TileView> d_tiles_a;
   DevBuf<uint32_t> d_anunits;  // overflowed units of the lean kernel (the merge resets it)
   hipEvent_t ev_a = nullptr;   // after the counting half's view upload (h_tiles_a may be rewritten)
+  hipEvent_t ev_c[2] = {};     // whole passes: the counting kernel alone
+  bool c_timed = false;
   bool a_live = false, a_timed = false;
   int32_t a_q0 = -1, a_base = 0, a_slot = 0, t_slot = 0;
   ~Pass() {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
     if (ev_a) (void)hipEventDestroy(ev_a);
+    for (hipEvent_t e : ev_c)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -714,7 +718,21 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
   if (second_half) c->hip(hipStreamWaitEvent(st, c->a_ev[P.a_slot][1], 0), "wait");
   c->hip(hipEventRecord(P.ev[0], st), "event");
-  c->hip(launch_prefilter(a, st, second_half ? 2 : 0), "prefilter");
+  P.c_timed = false;
+  if (second_half) {
+    c->hip(launch_prefilter(a, st, 2), "prefilter");
+  } else if (a.nseg <= 1) {
+    // whole pass: the lean counting (timed alone), then the full kernel over its overflowed units + merge
+    for (auto& e : P.ev_c)
+      if (!e) c->hip(hipEventCreate(&e), "event");
+    c->hip(hipEventRecord(P.ev_c[0], st), "event");
+    c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
+    c->hip(hipEventRecord(P.ev_c[1], st), "event");
+    c->hip(launch_prefilter(a, st, 2), "prefilter");
+    P.c_timed = true;
+  } else {
+    c->hip(launch_prefilter(a, st, 0), "prefilter");
+  }
   c->hip(hipEventRecord(P.ev[1], st), "event");
   P.a_timed = second_half;
   P.t_slot = P.a_slot;
@@ -879,6 +897,12 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   if (P.a_timed) {
     c->hip(hipEventElapsedTime(&ms, c->a_ev[P.t_slot][0], c->a_ev[P.t_slot][1]), "elapsed");
     t_pf += ms * 1e-3;
+    c->stats.t_count_s += ms * 1e-3;
+    c->stats.n_count_launches++;
+  } else if (P.c_timed) {
+    c->hip(hipEventElapsedTime(&ms, P.ev_c[0], P.ev_c[1]), "elapsed");
+    c->stats.t_count_s += ms * 1e-3;
+    c->stats.n_count_launches++;
   }
   c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;

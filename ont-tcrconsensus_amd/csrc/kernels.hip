@@ -1515,8 +1515,11 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
 // candidate list (seqno, k-mer count, result of the walked ones) and every peer (window id, count,
 // relevant flag, result of the aligned ones).  One wave per query-strand, lanes writing consecutive
 // words.  Record layout (u32 words): nt | np << 8, seqno[nt], res[nt], counts[(nt+3)/4] (u8 x4),
-// peer[np] (id | count << 16 | relevant << 24 | aligned << 25), peer_res[np] (valid if aligned).
-__global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uint8_t* __restrict__ lens,
+// peer[np] (id | count << 16 | relevant << 24 | aligned << 25), peer_res[np] (valid if aligned).  Record
+// space is taken with one atomic per workgroup of kPackWaves query-strands (a same-address atomic per
+// query-strand serialises in the L2).
+constexpr int kPackWaves = 4;
+__global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w0, const uint8_t* __restrict__ lens,
                                               const WalkState* __restrict__ ws, const uint8_t* __restrict__ ntop,
                                               const uint32_t* __restrict__ top_seqno,
                                               const uint8_t* __restrict__ top_count, const uint32_t* __restrict__ res,
@@ -1527,8 +1530,9 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
                                               uint32_t* __restrict__ reccount,
                                               HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
                                               const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
-  const int lane = threadIdx.x & 63;
-  const int qs = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  __shared__ uint32_t wsize[kPackWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qs = (int)blockIdx.x * kPackWaves + wave;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // counters[0] = the postings partial sums (k_pf_merge spreads its atomics over kPostSpread lines)
     uint32_t v = threadIdx.x < kPostSpread ? counters[16 + 32 * threadIdx.x] : 0u;
@@ -1536,12 +1540,12 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
     if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : counters[threadIdx.x];
   }
-  if (qs >= nqs) return;
-  const WalkState w = ws[qs];
-  const int np = npeer[qs];
+  const bool live = qs < nqs;
+  const WalkState w = ws[live ? qs : 0];
+  const int np = live ? npeer[qs] : 0;
   bool rel = false, al = false;
   uint32_t pw = 0;
-  if (np != 255 && lane < np) {
+  if (live && np != 255 && lane < np) {
     const uint32_t id = peer_id[(int64_t)qs * kPeerCap + lane];
     const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + lane];
     const uint32_t ps = (uint32_t)w0 + id;
@@ -1550,12 +1554,26 @@ __global__ __launch_bounds__(256) void k_pack(int32_t nqs, int32_t w0, const uin
     pw = id | (cnt << 16) | (rel ? 1u << 24 : 0u) | (al ? 1u << 25 : 0u);
   }
   uint32_t base = 0xffffffffu;
-  if (__any(rel)) {
-    const int nt = min((int)ntop[qs], kWalk);
-    const int ncw = (nt + 3) >> 2;
-    uint32_t b = 0;
-    if (lane == 0) b = atomicAdd(reccount, (uint32_t)(1 + 2 * nt + ncw + 2 * np));
-    base = (uint32_t)__shfl((int)b, 0, 64);
+  const bool has_rec = __any(rel);
+  const int nt = live ? min((int)ntop[qs], kWalk) : 0;
+  const int ncw = (nt + 3) >> 2;
+  // record space: the workgroup's sizes scanned in LDS, one atomic
+  if (lane == 0) wsize[wave] = has_rec ? (uint32_t)(1 + 2 * nt + ncw + 2 * np) : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int i = 0; i < kPackWaves; i++) {
+      const uint32_t x = wsize[i];
+      wsize[i] = tot;
+      tot += x;
+    }
+    const uint32_t b0 = tot ? atomicAdd(reccount, tot) : 0u;
+    for (int i = 0; i < kPackWaves; i++) wsize[i] += b0;
+  }
+  __syncthreads();
+  if (!live) return;
+  if (has_rec) {
+    base = wsize[wave];
     uint32_t* r = rec + base;
     if (lane == 0) r[0] = (uint32_t)nt | ((uint32_t)np << 8);
     if (lane < nt) {
@@ -1611,7 +1629,8 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
                        uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pack, dim3((nqs + 3) / 4), dim3(256), 0, st, nqs, w0, lens, ws, ntop, top_seqno, top_count,
+  hipLaunchKernelGGL(k_pack, dim3((nqs + kPackWaves - 1) / kPackWaves), dim3(64 * kPackWaves), 0, st, nqs, w0, lens,
+                     ws, ntop, top_seqno, top_count,
                      res, npeer, peer_id, peer_count, peer_res, aligned, reccount, hq, rec, counters, hcounters);
   return hipGetLastError();
 }

@@ -79,6 +79,8 @@ class Stats(C.Structure):
         ("n_reruns", C.c_int64),
         ("n_overlap_passes", C.c_int64),
         ("n_lazy_passes", C.c_int64),
+        ("t_count_s", C.c_double),
+        ("n_count_launches", C.c_int64),
     ]
 
     def as_dict(self) -> dict:
