@@ -321,12 +321,18 @@ struct umiclust_ctx {
   // split passes (depth 2, UMICLUST_SPLIT=0 turns them off): a block's counting runs against the index
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
-  int32_t split_env = -1;         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
+  int32_t split_env = -1;
+  bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
   DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
   PinBuf<int32_t> h_seq2ord;
   hipEvent_t a_ev[4][3] = {};     // counting halves, ring by block: begin / end (st_pf), gate (main stream)
+  // split passes: index appends and peer-tile builds run on st_b beside the counting on the main stream;
+  // they start after the latest second half (every earlier reader of the slots they rebuild precedes it)
+  // and the main stream's next pass waits for ix_done
+  hipStream_t ix_st = nullptr;     // null: the main stream
+  hipEvent_t ix_done = nullptr, last_r_ev = nullptr;
   std::unique_ptr<WorkPool> pool;  // host threads of resolve_pass (UMICLUST_RESOLVE_THREADS)
   int32_t resolve_threads = 4;
   DevBuf<uint16_t> arena;         // postings of every tile (one buffer, one descriptor per pass)
@@ -470,19 +476,20 @@ DevSeqs dev_seqs(umiclust_ctx* c) {
 // (re)build one index tile over sequences map[first .. first+n) with ordinals xoff + c; postings
 // vbase + ((xoff + c) % seg_mod) / kParts (umiclust_internal.h), in the tile's arena slot
 void build_tile(umiclust_ctx* c, Tile& t, const int32_t* map, int32_t first, int32_t n, int32_t xoff, int32_t vbase,
-                int32_t seg_mod) {
+                int32_t seg_mod, hipStream_t st = nullptr) {
+  if (!st) st = c->st;
   if (!t.hist.p) {
     c->hip(t.hist.ensure(kBins), "tile alloc");
-    c->hip(hipMemsetAsync(t.hist.p, 0, (size_t)kBins * 4, c->st), "tile memset");
+    c->hip(hipMemsetAsync(t.hist.p, 0, (size_t)kBins * 4, st), "tile memset");
   }
   c->hip(t.off.ensure(kBins + 1), "tile alloc");
   c->hip(t.cursor.ensure(kBins), "tile alloc");
   c->hip(t.partial.ensure(kScanBlocks), "tile alloc");
   if (tile_cap(n) > t.post_cap) c->fail(UMICLUST_EDEVICE, "internal: index tile slot too small");
   uint16_t* post = c->arena.p + t.post_base;
-  c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, t.hist.p, c->st), "index count");
-  c->hip(launch_index_scan(t.hist.p, t.partial.p, t.off.p, t.cursor.p, post, c->st), "index scan");
-  c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, vbase, seg_mod, t.cursor.p, post, c->st),
+  c->hip(launch_index_count(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, t.hist.p, st), "index count");
+  c->hip(launch_index_scan(t.hist.p, t.partial.p, t.off.p, t.cursor.p, post, st), "index scan");
+  c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, vbase, seg_mod, t.cursor.p, post, st),
          "index fill");
   t.n = n;
   t.built_n = n;
@@ -620,6 +627,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   const int both = c->both;
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
+  if (c->ix_st && c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");  // index / peer tiles
   P.q0 = q0;
   P.nq = nq;
   P.w0 = w0;
@@ -734,6 +742,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     c->hip(launch_prefilter(a, st, 0), "prefilter");
   }
   c->hip(hipEventRecord(P.ev[1], st), "event");
+  c->last_r_ev = P.ev[1];
   P.a_timed = second_half;
   P.t_slot = P.a_slot;
   P.a_live = false;
@@ -803,10 +812,16 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   // on its own stream, gated by the main stream's work so far (index append, peer tiles, this buffer set's
   // last merge): the main stream's next append and second half do not queue behind it
   hipStream_t st = c->st;
+  if (c->ix_st && c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");  // index / peer tiles
   if (c->split_stream) {
     // created on first use, after the others: HIP hands streams hardware queues in creation order, and an
     // extra stream created earlier would push the alignment stream onto the main stream's queue
-    if (!c->st_pf) c->hip(hipStreamCreateWithFlags(&c->st_pf, hipStreamNonBlocking), "stream");
+    if (!c->st_pf) {
+      // the least priority: the pass chain the host waits for is dispatched first
+      int lo = 0, hi = 0;
+      c->hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
+      c->hip(hipStreamCreateWithPriority(&c->st_pf, hipStreamNonBlocking, lo), "stream");
+    }
     c->hip(hipEventRecord(c->a_ev[slot][2], c->st), "event");
     st = c->st_pf;
     c->hip(hipStreamWaitEvent(st, c->a_ev[slot][2], 0), "wait");
@@ -1291,7 +1306,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
 // behind any queued pass (which keeps reading the tiles as they were when it was enqueued).
 void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   if (new_cents.empty()) return;
-  hipStream_t st = c->st;
+  hipStream_t st = c->ix_st ? c->ix_st : c->st;
+  if (c->ix_st && c->last_r_ev) c->hip(hipStreamWaitEvent(st, c->last_r_ev, 0), "wait");
   const int32_t ord0 = (int32_t)c->cent.size();
   for (int32_t q : new_cents) {  // capacity reserved: no reallocation
     c->cent.push_back(q);
@@ -1329,7 +1345,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     t->seg = t->base / kSegCentroids;
     t->post_cap = tile_cap(kTile);
     t->post_base = c->sealed_slot0 + (uint64_t)c->tiles.size() * t->post_cap;
-    build_tile(c, *t, c->d_cent.p, t->base, kTile, t->base, kCentBase, kSegCentroids);
+    build_tile(c, *t, c->d_cent.p, t->base, kTile, t->base, kCentBase, kSegCentroids, st);
     c->tiles.push_back(t);
     c->sealed_end += kTile;
     c->base_end = std::max(c->base_end, c->sealed_end);
@@ -1341,7 +1357,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     c->base_tile.base = c->sealed_end;
     c->base_tile.seg = c->sealed_end / kSegCentroids;
     build_tile(c, c->base_tile, c->d_cent.p, c->sealed_end, ordend - c->sealed_end, c->sealed_end, kCentBase,
-               kSegCentroids);
+               kSegCentroids, st);
     c->base_end = ordend;
   }
   // the other delta slot was last read by a counting half the main stream has already waited for (the
@@ -1351,11 +1367,15 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   dt.base = c->base_end;
   dt.seg = c->base_end / kSegCentroids;
   if (ordend > c->base_end)
-    build_tile(c, dt, c->d_cent.p, c->base_end, ordend - c->base_end, c->base_end, kCentBase, kSegCentroids);
+    build_tile(c, dt, c->d_cent.p, c->base_end, ordend - c->base_end, c->base_end, kCentBase, kSegCentroids, st);
   else
     dt.n = 0;
   c->index_end = ordend;
   c->hip(hipEventRecord(ev.second, st), "event");
+  if (c->ix_st) {
+    if (!c->ix_done) c->hip(hipEventCreate(&c->ix_done), "event");
+    c->hip(hipEventRecord(c->ix_done, st), "event");
+  }
 }
 
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
@@ -1478,6 +1498,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   // multi-bin sets run several lanes on one GPU, which is throughput-bound: there the whole passes win
   // (configs 2 / 5: +12 % / +2 %, config 3: -6 %; profiles/r02/split_ab.json)
   const bool split = c->split_env >= 0 ? c->split_env != 0 : !multi_bin;
+  c->ix_st = (split && D == 2 && c->ix_side) ? c->st_b : nullptr;
+  c->last_r_ev = nullptr;
   if (split && D == 2) {
     // Split passes.  Pass j = counting half A(j) (index of blocks <= j-3, window j-2 .. j with block j-2
     // flagged) enqueued after block j-3 is resolved, and second half R(j) (the full kernel over A's
@@ -1485,11 +1507,21 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     // centroids, then walk / align / pack) after block j-2 is.  Block j's peer tile: blk_tile[j % 4],
     // counter region j % 3 (three consecutive blocks share a counting window).
     auto stile = [&](int32_t j) -> Tile& { return c->blk_tile[j % (kPeerTiles + 1)]; };
-    auto build_peer = [&](int32_t j) {
+    auto build_peer = [&](int32_t j, bool side) {
       Tile& t = stile(j);
       const int32_t region = j % kPeerTiles;
-      if (!(t.prebuilt && t.base == blocks[j].first && t.n == blocks[j].second && t.seg == region))
-        build_tile(c, t, c->d_iota.p, blocks[j].first, blocks[j].second, 0, region * kPeerRegion, 1 << 30);
+      if (!(t.prebuilt && t.base == blocks[j].first && t.n == blocks[j].second && t.seg == region)) {
+        hipStream_t bs = c->st;
+        if (side && c->ix_st) {
+          bs = c->ix_st;
+          if (c->last_r_ev) c->hip(hipStreamWaitEvent(bs, c->last_r_ev, 0), "wait");
+        }
+        build_tile(c, t, c->d_iota.p, blocks[j].first, blocks[j].second, 0, region * kPeerRegion, 1 << 30, bs);
+        if (bs != c->st) {
+          if (!c->ix_done) c->hip(hipEventCreate(&c->ix_done), "event");
+          c->hip(hipEventRecord(c->ix_done, bs), "event");
+        }
+      }
       t.base = blocks[j].first;
       t.seg = region;
       t.len = c->hlen[blocks[j].first];
@@ -1512,7 +1544,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     // the index holds the blocks before r and nothing is queued: classic passes r (window r) and r+1 (window
     // r, r+1), then A(r+2) with block r flagged
     auto prime = [&](int32_t r) {
-      for (int32_t j = r; j < r + 3 && j < nb; j++) build_peer(j);
+      for (int32_t j = r; j < r + 3 && j < nb; j++) build_peer(j, false);
       if (r < nb) second_half(r, r, false);
       if (r + 1 < nb) second_half(r + 1, r, false);
       if (r + 2 < nb) count_half(r + 2, r, 0);
@@ -1520,11 +1552,12 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     prime(0);
     for (int32_t k = 0; k < nb; k++) {
       Pass& P = c->pass[k % 2];
-      if (k + 3 < nb) build_peer(k + 3);  // queries only: built while the host resolves block k
+      if (k + 3 < nb) build_peer(k + 3, true);  // queries only: built while the host resolves block k
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         // drain everything queued (its windows include block k) and restart the pipeline after block k
         c->hip(hipStreamSynchronize(c->st_al), "sync");
         if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
+        c->hip(hipStreamSynchronize(c->st_b), "sync");
         c->hip(hipStreamSynchronize(c->st), "sync");
         for (Pass& Q : c->pass) {
           Q.live = false;
@@ -1596,6 +1629,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   }
   c->b_hint = b_eff;
   if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
+  c->hip(hipStreamSynchronize(c->st_b), "sync");
+  c->ix_st = nullptr;
   c->hip(hipStreamSynchronize(c->st_al), "sync");
   c->hip(hipStreamSynchronize(c->st), "sync");
   for (size_t i = 0; i < c->nix; i++) {
@@ -2502,6 +2537,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     return nullptr;
   }
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
+  if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_SPLIT")) {
     c->split_env = atoi(e) != 0 ? 1 : 0;
     c->split_stream = atoi(e) == 2;
@@ -2543,6 +2579,10 @@ void umiclust_destroy(umiclust_ctx* c) {
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st_al) (void)hipStreamDestroy(c->st_al);
+  if (c->ix_done) (void)hipEventDestroy(c->ix_done);
+  for (auto& r : c->a_ev)
+    for (hipEvent_t e : r)
+      if (e) (void)hipEventDestroy(e);
   if (c->st_pf) (void)hipStreamDestroy(c->st_pf);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
