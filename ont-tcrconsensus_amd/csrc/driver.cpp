@@ -2051,6 +2051,37 @@ bool write_file(const std::string& path, const std::string& data) {
   return ok;
 }
 
+// a file made of parts written side by side: each part at its offset (pwrite), on one thread per part
+bool write_parts(const std::string& path, const std::vector<std::string>& parts) {
+  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (fd < 0) return false;
+  const int T = (int)parts.size();
+  std::vector<off_t> at(T + 1, 0);
+  for (int t = 0; t < T; t++) at[t + 1] = at[t] + (off_t)parts[t].size();
+  bool ok = at[T] == 0 || ftruncate(fd, at[T]) == 0;
+  std::vector<char> good(T, 1);
+  if (ok)
+    parallel_for(T, [&](int t) {
+      const char* p = parts[t].data();
+      size_t n = parts[t].size();
+      off_t o = at[t];
+      while (n > 0) {
+        const ssize_t w = pwrite(fd, p, n, o);
+        if (w < 0) {
+          if (errno == EINTR) continue;
+          good[t] = 0;
+          return;
+        }
+        p += w;
+        n -= (size_t)w;
+        o += w;
+      }
+    });
+  for (int t = 0; t < T; t++) ok = ok && good[t];
+  ok = (close(fd) == 0) && ok;
+  return ok;
+}
+
 // clusters [0, K) split over T threads by member count
 std::vector<int32_t> cluster_slices(const std::vector<int32_t>& ostart, int32_t K, int T) {
   std::vector<int32_t> cut(T + 1, K);
@@ -2103,6 +2134,11 @@ void split_fields(Sv name, std::vector<Sv>& f) {  // name.split(";")
     }
 }
 
+// parse_umi_clusters over the in-memory clusters (parse_umi_clusters.py:10-242).  Clusters are independent
+// except for the loop's early exit (`max_clusters`) and its first error, so the work runs in three phases:
+// every cluster's counts and first format error on io_threads() threads; in cluster order, the exit and the
+// first error (which the reference raises after writing the files of the clusters before it); then the
+// cluster files and the per-cluster text of the kept range on the threads, concatenated in order.
 void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp, const char* work_dir_c,
                 umiclust_parse_result* pr) {
   if (!c->p.clusterout_sort || !c->p.clusterout_id)
@@ -2114,109 +2150,184 @@ void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp
   if (stat(fa_dir.c_str(), &sb) == 0) c->fail(UMICLUST_EEXIST, "%s should not exist yet but does exist!", fa_dir.c_str());
   if (mkdir(fa_dir.c_str(), 0777) != 0) c->fail(UMICLUST_EIO, "cannot create %s", fa_dir.c_str());
   const int32_t K = c->nclusters;
-  std::string stats_out = "id_cluster\tn_fwd\tn_rev\twritten_fwd\twritten_rev\tn\twritten\tcluster_written\n";
-  std::string smol, log, lines, fn;
-  int64_t n_written = 0, reads_found = 0, reads_written = 0;
-  std::vector<Sv> fields;
-  // kept[strand]: insertion-ordered dict read id -> record (:61-65); ids of one cluster
-  std::vector<std::pair<Sv, int32_t>> kept[2];
-  std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position), per cluster
-  for (int32_t k = 0; k < K; k++) {  // consout in file order; clusterid = k (:197-200)
-    const std::string out_fasta = pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta");  // :34
-    kept[0].clear();
-    kept[1].clear();
-    index.clear();
-    int64_t seen[2] = {0, 0}, found = 0;
+  struct PClus {
+    int64_t n_fwd = 0, n_rev = 0, found = 0, max_fwd = 0, max_rev = 0, w_fwd = 0, w_rev = 0, w_all = 0;
+    int written = 0, err = 0;
+    std::string msg;
+  };
+  struct Scratch {
+    std::vector<Sv> fields;
+    std::vector<std::pair<Sv, int32_t>> kept[2];  // insertion-ordered dict read id -> record (:61-65)
+    std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position)
+  };
+  // one cluster's counts (and its kept records in sc.kept); false on the first malformed record
+  auto analyze = [&](int32_t k, PClus& r, Scratch& sc) -> bool {
+    sc.kept[0].clear();
+    sc.kept[1].clear();
+    sc.index.clear();
+    int64_t seen[2] = {0, 0};
     for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {  // cluster<N> file order (:36)
       const int32_t i = c->perm[c->omemb[x]];
       const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
-      split_fields(name, fields);
-      if (fields.size() != 7)  // :38-47
-        c->fail(UMICLUST_EFORMAT, "cluster %d: header has %d cols while it should contain 7: %s", k,
-                (int)fields.size(), name.str().c_str());
+      split_fields(name, sc.fields);
+      if (sc.fields.size() != 7) {  // :38-47
+        r.err = UMICLUST_EFORMAT;
+        r.msg = "cluster " + std::to_string(k) + ": header has " + std::to_string(sc.fields.size()) +
+                " cols while it should contain 7: " + name.str();
+        return false;
+      }
       Sv strand;
-      if (!split1(fields[1], "strand=", strand)) c->fail(UMICLUST_EFORMAT, "no strand= field: %s", name.str().c_str());
-      found++;
+      if (!split1(sc.fields[1], "strand=", strand)) {
+        r.err = UMICLUST_EFORMAT;
+        r.msg = "no strand= field: " + name.str();
+        return false;
+      }
+      r.found++;
       int st = 0;
       if (strand == "+") st = 0;
       else if (strand == "-") st = 1;
-      else c->fail(UMICLUST_EFORMAT, "Strand annotation is %s but only - or + are allowed!", strand.str().c_str());
+      else {
+        r.err = UMICLUST_EFORMAT;
+        r.msg = "Strand annotation is " + strand.str() + " but only - or + are allowed!";
+        return false;
+      }
       if (seen[st] < max_reads) {  // kept[strand][id] = rec: a repeated id keeps its first position
-        std::string key = fields[0].str();
+        std::string key = sc.fields[0].str();
         key.push_back((char)('0' + st));
         int32_t pos = -1;
-        for (auto& e : index)
-          if (e.first == key) { pos = e.second; break; }
+        for (auto& e : sc.index)
+          if (e.first == key) {
+            pos = e.second;
+            break;
+          }
         if (pos < 0) {
-          index.emplace_back(std::move(key), (int32_t)kept[st].size());
-          kept[st].emplace_back(fields[0], i);
+          sc.index.emplace_back(std::move(key), (int32_t)sc.kept[st].size());
+          sc.kept[st].emplace_back(sc.fields[0], i);
         } else {
-          kept[st][pos].second = i;
+          sc.kept[st][pos].second = i;
         }
       }
       seen[st]++;
     }
     // strand caps (:66-87)
-    const int64_t n_fwd = seen[0], n_rev = seen[1];
-    int64_t min_fwd, min_rev, max_fwd, max_rev;
+    r.n_fwd = seen[0];
+    r.n_rev = seen[1];
+    int64_t min_fwd, min_rev;
     if (pp->balance_strands) {
       min_fwd = min_rev = min_reads / 2;
-      const int64_t capped = std::min(std::min(n_fwd * 2, n_rev * 2), max_reads);
-      max_fwd = max_rev = capped / 2;
-    } else if (n_fwd > n_rev) {
+      const int64_t capped = std::min(std::min(r.n_fwd * 2, r.n_rev * 2), max_reads);
+      r.max_fwd = r.max_rev = capped / 2;
+    } else if (r.n_fwd > r.n_rev) {
       min_fwd = min_rev = 0;
-      max_rev = std::min(n_rev, max_reads / 2);
-      max_fwd = std::min(max_reads - max_rev, n_fwd);
+      r.max_rev = std::min(r.n_rev, max_reads / 2);
+      r.max_fwd = std::min(max_reads - r.max_rev, r.n_fwd);
     } else {
       min_fwd = min_rev = 0;
-      max_fwd = std::min(n_fwd, max_reads / 2);
-      max_rev = std::min(max_reads - max_fwd, n_rev);
+      r.max_fwd = std::min(r.n_fwd, max_reads / 2);
+      r.max_rev = std::min(max_reads - r.max_fwd, r.n_rev);
     }
-    const int64_t n_reads = max_fwd + max_rev;
-    if (n_reads > max_reads) c->fail(UMICLUST_EINVAL, "n_reads is higher than max_reads_per_cluster");  // :89-92
-    log += "Cluster: " + out_fasta + " has " + std::to_string(n_fwd) + "/" + std::to_string(max_fwd) + " fwd and " +
-           std::to_string(n_rev) + "/" + std::to_string(max_rev) + " rev reads\n";
-    int64_t w_fwd = 0, w_rev = 0, w_all = 0, written = 0;
-    if (n_fwd >= min_fwd && n_rev >= min_rev && n_reads >= min_reads) {  // :95-120
-      w_fwd = std::min<int64_t>((int64_t)kept[0].size(), max_fwd);
-      w_rev = std::min<int64_t>((int64_t)kept[1].size(), max_rev);
-      w_all = std::min<int64_t>(w_fwd + w_rev, max_reads);
-      written = 1;
-      lines.clear();
-      for (int64_t y = 0; y < w_all; y++) {
-        const auto& e = y < w_fwd ? kept[0][y] : kept[1][y - w_fwd];
-        const int32_t i = e.second;
-        split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, fields);
-        Sv read;
-        if (!split1(fields[6], "seq=", read)) c->fail(UMICLUST_EFORMAT, "no seq= field in record %d", i);
-        lines.push_back('>');
-        lines.append(fields[0].p, fields[0].n);
-        lines.push_back('\n');
-        lines.append(read.p, read.n);
-        lines.push_back('\n');
-        smol += ">" + std::to_string(k) + "\n";
-        smol.append(read.p, read.n);
-        smol.push_back('\n');
-      }
-      if (!write_file(out_fasta, lines)) c->fail(UMICLUST_EIO, "cannot write %s", out_fasta.c_str());
-    } else {
-      log += "Cluster " + std::to_string(k) + " skipped\n";
+    const int64_t n_reads = r.max_fwd + r.max_rev;
+    if (n_reads > max_reads) {  // :89-92
+      r.err = UMICLUST_EINVAL;
+      r.msg = "n_reads is higher than max_reads_per_cluster";
+      return false;
     }
-    log += "Cluster: " + out_fasta + " has " + std::to_string(w_all) + " reads written: " + std::to_string(w_fwd) +
-           " fwd - " + std::to_string(w_rev) + " rev\n";
-    stats_out += "cluster" + std::to_string(k) + "\t" + std::to_string(n_fwd) + "\t" + std::to_string(n_rev) + "\t" +
-                 std::to_string(w_fwd) + "\t" + std::to_string(w_rev) + "\t" + std::to_string(found) + "\t" +
-                 std::to_string(w_all) + "\t" + std::to_string(written) + "\n";
-    n_written += written;
+    if (r.n_fwd >= min_fwd && r.n_rev >= min_rev && n_reads >= min_reads) {  // :95-120
+      r.w_fwd = std::min<int64_t>((int64_t)sc.kept[0].size(), r.max_fwd);
+      r.w_rev = std::min<int64_t>((int64_t)sc.kept[1].size(), r.max_rev);
+      r.w_all = std::min<int64_t>(r.w_fwd + r.w_rev, max_reads);
+      r.written = 1;
+    }
+    return true;
+  };
+  const int T = K < 256 ? 1 : io_threads();
+  const std::vector<int32_t> cut = cluster_slices(c->ostart, K, T);
+  std::vector<PClus> res((size_t)K);
+  parallel_for(T, [&](int t) {
+    Scratch sc;
+    for (int32_t k = cut[t]; k < cut[t + 1]; k++) analyze(k, res[k], sc);
+  });
+  // the reference's loop in order: its first error, its early exit
+  int64_t n_written = 0, reads_found = 0, reads_written = 0;
+  int32_t kend = K, kerr = -1;
+  for (int32_t k = 0; k < K; k++) {
+    if (res[k].err) {
+      kerr = k;
+      kend = k;
+      break;
+    }
+    n_written += res[k].written;
     // the reference's quirk (:206, :219-221): the totals are overwritten by this cluster's counts, then doubled
-    reads_found = 2 * found;
-    reads_written = 2 * w_all;
+    reads_found = 2 * res[k].found;
+    reads_written = 2 * res[k].w_all;
     // `if max_clusters and n_written > max_clusters` (:222-223): any non-zero value applies, as in Python
-    if (pp->max_clusters != 0 && n_written > pp->max_clusters) break;
+    if (pp->max_clusters != 0 && n_written > pp->max_clusters) {
+      kend = k + 1;
+      break;
+    }
+  }
+  // cluster files and the text of clusters [0, kend), on the threads
+  const std::vector<int32_t> wcut = cluster_slices(c->ostart, kend, T);
+  std::vector<std::string> smol_p(T), log_p(T), stats_p(T);
+  std::vector<int32_t> bad(T, -1), noseq(T, -1);
+  parallel_for(T, [&](int t) {
+    Scratch sc;
+    std::string lines, &smol = smol_p[t], &log = log_p[t], &stats_out = stats_p[t];
+    for (int32_t k = wcut[t]; k < wcut[t + 1]; k++) {
+      PClus r;
+      analyze(k, r, sc);
+      const std::string out_fasta = pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta");  // :34
+      log += "Cluster: " + out_fasta + " has " + std::to_string(r.n_fwd) + "/" + std::to_string(r.max_fwd) +
+             " fwd and " + std::to_string(r.n_rev) + "/" + std::to_string(r.max_rev) + " rev reads\n";
+      if (r.written) {
+        lines.clear();
+        for (int64_t y = 0; y < r.w_all; y++) {
+          const auto& e = y < r.w_fwd ? sc.kept[0][y] : sc.kept[1][y - r.w_fwd];
+          const int32_t i = e.second;
+          split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
+          Sv read;
+          if (!split1(sc.fields[6], "seq=", read)) {
+            noseq[t] = i;
+            return;
+          }
+          lines.push_back('>');
+          lines.append(sc.fields[0].p, sc.fields[0].n);
+          lines.push_back('\n');
+          lines.append(read.p, read.n);
+          lines.push_back('\n');
+          smol += ">" + std::to_string(k) + "\n";
+          smol.append(read.p, read.n);
+          smol.push_back('\n');
+        }
+        if (!write_file(out_fasta, lines)) {
+          if (bad[t] < 0) bad[t] = k;
+          return;
+        }
+      } else {
+        log += "Cluster " + std::to_string(k) + " skipped\n";
+      }
+      log += "Cluster: " + out_fasta + " has " + std::to_string(r.w_all) + " reads written: " + std::to_string(r.w_fwd) +
+             " fwd - " + std::to_string(r.w_rev) + " rev\n";
+      stats_out += "cluster" + std::to_string(k) + "\t" + std::to_string(r.n_fwd) + "\t" + std::to_string(r.n_rev) +
+                   "\t" + std::to_string(r.w_fwd) + "\t" + std::to_string(r.w_rev) + "\t" + std::to_string(r.found) +
+                   "\t" + std::to_string(r.w_all) + "\t" + std::to_string(r.written) + "\n";
+    }
+  });
+  for (int t = 0; t < T; t++) {
+    if (noseq[t] >= 0) c->fail(UMICLUST_EFORMAT, "no seq= field in record %d", noseq[t]);
+    if (bad[t] >= 0) c->fail(UMICLUST_EIO, "cannot write %s", pjoin(fa_dir, "cluster" + std::to_string(bad[t]) + ".fasta").c_str());
+  }
+  if (kerr >= 0) c->fail(res[kerr].err, "%s", res[kerr].msg.c_str());
+  std::string stats_out = "id_cluster\tn_fwd\tn_rev\twritten_fwd\twritten_rev\tn\twritten\tcluster_written\n", log;
+  for (int t = 0; t < T; t++) {
+    stats_out += stats_p[t];
+    log += log_p[t];
   }
   if (!write_file(pjoin(work_dir, "vsearch_cluster_stats.tsv"), stats_out))
     c->fail(UMICLUST_EIO, "cannot write the stats table");
-  if (!write_file(pjoin(work_dir, "smolecule_clusters.fa"), smol)) c->fail(UMICLUST_EIO, "cannot write smolecule_clusters.fa");
+  // every read once more (GBs at production depth): the threads' parts side by side
+  if (!write_parts(pjoin(work_dir, "smolecule_clusters.fa"), smol_p))
+    c->fail(UMICLUST_EIO, "cannot write smolecule_clusters.fa");
   pr->n_clusters = K;
   pr->n_written = n_written;
   pr->reads_found = reads_found;

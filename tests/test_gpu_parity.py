@@ -280,16 +280,19 @@ def _tree(d):
 
 
 PARSE_CASES = [
-    # (round, min_reads, max_reads, balance, max_clusters, dup_ids)
-    (1, 4, 60, False, None, False),
-    (1, 2, 5, True, None, True),
-    (1, 3, 8, False, 5, True),
-    (2, 1, 4, False, None, False),
-    (1, 100000, 60, False, None, False),  # nothing written: the empty-region branch
+    # (round, min_reads, max_reads, balance, max_clusters, dup_ids, molecules)
+    (1, 4, 60, False, None, False, 120),
+    (1, 2, 5, True, None, True, 120),
+    (1, 3, 8, False, 5, True, 120),
+    (2, 1, 4, False, None, False, 120),
+    (1, 100000, 60, False, None, False, 120),  # nothing written: the empty-region branch
+    # >= 256 clusters: the parse runs on io_threads() threads (early exit inside a later thread's range)
+    (1, 4, 60, False, None, True, 900),
+    (1, 2, 8, True, 400, False, 900),
 ]
 
 
-@pytest.mark.parametrize("case", PARSE_CASES, ids=[f"r{c[0]}_min{c[1]}_max{c[2]}_b{int(c[3])}_mc{c[4]}_d{int(c[5])}"
+@pytest.mark.parametrize("case", PARSE_CASES, ids=[f"r{c[0]}_min{c[1]}_max{c[2]}_b{int(c[3])}_mc{c[4]}_d{int(c[5])}_m{c[6]}"
                                                   for c in PARSE_CASES])
 def test_fused_parse_matches_two_step(tmp_path, case):
     """§8f f2: vsearch_cluster_and_parse writes the same bytes as vsearch_cluster followed by the
@@ -297,8 +300,9 @@ def test_fused_parse_matches_two_step(tmp_path, case):
     intermediate cluster<N> files."""
     from umiclust.parse_umi_clusters import parse_umi_clusters, vsearch_cluster_and_parse
     from umiclust.vsearch_umi_cluster import vsearch_cluster, vsearch_cluster_consensus
-    round_, mn, mx, bal, mc, dup = case
-    u = synth.make_umis(120, seed=41 + mn, max_reads=2000, orient_mix=0.1, error_rate=0.015 if round_ == 1 else 0.002)
+    round_, mn, mx, bal, mc, dup, nmol = case
+    u = synth.make_umis(nmol, seed=41 + mn, max_reads=2000 * nmol // 120, orient_mix=0.1,
+                        error_rate=0.015 if round_ == 1 else 0.002)
     fa = tmp_path / "in.fasta"
     synth.write_umi_fasta(str(fa), u)
     if dup:  # repeated read ids (kept once per strand, at the first position, with the last record)
