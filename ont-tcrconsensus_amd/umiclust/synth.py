@@ -346,3 +346,21 @@ def write_umi_fasta_fast(path: str, umis: UmiSet, seed: int = 7, read_len: int =
                                        u[:half], b";umi_rev_seq=", u[half:], b";seq=",
                                        pool[starts[j]:starts[j] + read_len], b"\n", u, b"\n")))
             f.write(b"".join(parts))
+
+
+def segment_stress(n_rand: int = 470_000, n_copy: int = 3000, seed: int = 91, length: int = 64):
+    """A bin past one counter segment (> 7 x 65,536 centroids, the prefilter's LDS counter range): n_rand
+    random `length`-mers (nearly all their own centroids) followed by 1-substitution copies of sequences
+    from both segments.  Returns (buf uint8, off int64) in input order."""
+    rng = np.random.default_rng(seed)
+    base = ACGT[rng.integers(0, 4, (n_rand, length))]
+    half = n_copy // 2
+    src = np.concatenate([rng.integers(0, min(n_rand, 400_000), half),
+                          rng.integers(max(0, n_rand - 10_000), n_rand, n_copy - half)])
+    cp = base[src].copy()
+    rows = np.arange(n_copy)
+    pos = rng.integers(0, length, n_copy)
+    cp[rows, pos] = ACGT[(np.searchsorted(ACGT, cp[rows, pos]) + rng.integers(1, 4, n_copy)) % 4]
+    buf = np.ascontiguousarray(np.concatenate([base, cp])).reshape(-1)
+    off = np.arange(0, (n_rand + n_copy) * length + 1, length, dtype=np.int64)
+    return buf, off

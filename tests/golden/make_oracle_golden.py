@@ -3,7 +3,8 @@ BASELINE config-1 bin (100k reads, the reference's CPU-runnable case) and of sam
 stress bin (~96-nt UMIs, 15 % indels, clusters of >1k members), so the GPU parity test can check them
 without re-running the CPU oracle (~1 min per config-1 case) on the GPU box.
 
-Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py [config ...]
+Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py [config ...] | multibin [name ...] |
+segments
 """
 import hashlib
 import json
@@ -130,9 +131,28 @@ def main(configs):
             json.dump(cases, f, indent=1, sort_keys=True)
 
 
+def main_segments():
+    """oracle_segments.json: synth.segment_stress() (a bin past one 7 x 65,536-centroid counter segment)."""
+    import orc
+    from umiclust import synth
+    buf, off = synth.segment_stress()
+    raw = buf.tobytes()
+    seqs = [raw[off[i]:off[i + 1]].decode() for i in range(len(off) - 1)]
+    t0 = time.perf_counter()
+    r = orc.cluster(orc.params(1, 0.90, 58, 68), seqs)
+    dt = time.perf_counter() - t0
+    d = digest(r)
+    d.update(preset=1, identity=0.90, minlen=58, maxlen=68, n_reads=len(seqs), alignments=r["stats"]["alignments"],
+             cells=r["stats"]["cells"], oracle_seconds=round(dt, 2), oracle_threads=1, host_cpu=_cpu_model())
+    with open(os.path.join(HERE, "oracle_segments.json"), "w") as f:
+        json.dump({"segments_round1_id090": d}, f, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
-    if args and args[0] == "multibin":
+    if args and args[0] == "segments":
+        main_segments()
+    elif args and args[0] == "multibin":
         main_multibin(args[1:] or sorted(MULTIBIN_CASES))
     else:
         main([int(a) for a in args] or sorted({c[0] for c in CASES.values()}))

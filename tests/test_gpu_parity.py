@@ -218,6 +218,32 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
     assert st["n_reruns"] > 0  # the overflow re-run and the pipeline restart were exercised
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_two_counter_segments(split, monkeypatch):
+    """A bin past one counter segment (> 7 x 65,536 centroids: synth.segment_stress, 470k random 64-mers and
+    1-substitution copies of sequences from both segments): the full kernel counts both segments and keeps a
+    running top-41 across them (the split pipeline falls back to whole passes once the index spans two
+    segments).  Alignment count, cells and the membership / strand / centroid / consensus digests equal the
+    oracle's (tests/golden/oracle_segments.json, make_oracle_golden.py segments)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_oracle_golden import digest
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                       "oracle_segments.json")))["segments_round1_id090"]
+    buf, off = synth.segment_stress()
+    monkeypatch.setenv("UMICLUST_SPLIT", split)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.90, 58, 68), buf=buf, off=off)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    assert st["n_clusters"] > 7 * 65536  # two counter segments
+    d = digest(g)
+    assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
+    for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
+        assert d[k] == gold[k], k
+
+
 def test_edge_inputs(gpu_ctx):
     p = _lib.params(1, 0.93, 58, 68)
     op = orc.params(1, 0.93, 58, 68)
