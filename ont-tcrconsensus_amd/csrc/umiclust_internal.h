@@ -26,7 +26,7 @@ constexpr int kTile = 65536;        // centroids per sealed index tile
 //   [r*kPeerRegion, (r+1)*kPeerRegion)  peer tile of a block in region r = block % depth (r < kPeerTiles)
 //                                       (x - base) / kParts
 //   [kDummy, kDummy + 64)         padding postings
-//   [kTrash, kTrash + 256)        lanes past the end of the posting stream, one word per lane (never read)
+//   [kTrash, kTrash + 256)        spare (lanes past the end of the posting stream add 0 instead)
 //   [kCentBase, ...)              centroids: kCentBase + (ordinal % kSegCentroids) / kParts
 // Centroids beyond kSegCentroids live in further counter segments, processed one after another.
 constexpr int kParts = 8;
