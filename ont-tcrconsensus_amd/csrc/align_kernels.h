@@ -345,18 +345,229 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
 }
 
+// ------------------------------------------------------------------ K3B: banded packed alignment
+// k_align_pk's recurrences, summaries and strict priorities with one pair spread over a group of G lanes
+// (inside one 16-lane DPP row), for launches too small to fill the GPU with one lane per pair: deep
+// clusters cut greedy blocks to a few hundred query-strands, ~10k pairs = 150 waves for 1,024 SIMDs, each
+// wave bound by one alignment's QL x TL cells in series.  Lane g of a group holds the B = ceil(QL / G)
+// query rows [g B - P, (g + 1) B - P) as k_align_pk's top and bottom halves.  The P = G B - QL virtual
+// rows on top of lane 0 end in one forced to the boundary row -1, so the last lane ends exactly at row
+// QL - 1 and its last-row penalties and trailing-run counters stay compile-time rows.  Lane g runs two
+// columns behind lane g - 1 and takes, by DPP row_shr:1, the carries lane g - 1's last row left in the
+// previous step (the role k_align_pk's top-to-bottom carries play inside a lane): TL + 2G - 1 steps of
+// B / 2 packed rows per pair.
+constexpr int band_lanes(int ql) { return ql >= 57 ? 8 : 4; }  // keeps P < B (virtual rows in lane 0)
+
+__device__ __forceinline__ uint32_t row_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+}
+
+template <int QL, int G>
+__global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __restrict__ pq,
+                                                   const uint32_t* __restrict__ pt, int32_t npairs,
+                                                   const uint32_t* __restrict__ dev_npairs,
+                                                   const uint32_t* __restrict__ outidx, Scoring sc,
+                                                   uint32_t* __restrict__ out) {
+  constexpr int B = (QL + G - 1) / G;
+  constexpr int P = G * B - QL;  // virtual rows on top of lane 0
+  constexpr int TOP = (B + 1) / 2, BOT = B - TOP;
+  constexpr int NG = (TOP + 15) / 16;
+  constexpr int KL = BOT - 1;                              // register holding the lane's last row (high half)
+  constexpr int VR = P - 1;                                // lane 0's local row standing for row -1
+  constexpr int VK = VR < TOP ? VR : VR - TOP;             // its register
+  constexpr uint32_t VM = VR < TOP ? 0x0000ffffu : 0xffff0000u;  // and half
+  static_assert(16 % G == 0 && P < B && BOT >= 1, "band layout");
+  const int gid = (int)(blockIdx.x * 64 + threadIdx.x);
+  const int k = gid / G, g = gid % G;
+  if (k >= npairs) return;  // group-uniform
+  if (dev_npairs && k >= (int)*dev_npairs) return;
+  const bool first = g == 0, last = g == G - 1;
+  const uint32_t fm = first ? 0xffffffffu : 0u;
+  const int r0 = g * B - P;  // global row of local row 0
+  const uint32_t qv = pq[k];
+  const int32_t q = (int32_t)(qv >> 1);
+  const int qstr = (int)(qv & 1u);
+  const int32_t t = (int32_t)pt[k];
+  const int tl = s.lens[t];
+  uint64_t MT[NG], MB[NG];
+#pragma unroll
+  for (int gg = 0; gg < NG; gg++) MT[gg] = MB[gg] = 0;
+  {
+    const uint32_t* qc = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      const int r = r0 + i;
+      const int rc = r < 0 ? 0 : r;  // virtual rows read row 0's word (never before the sequence)
+      const uint32_t w = qc[rc >> 3] >> ((rc & 7) * 4);
+      const uint64_t bit = r >= 0 ? 1ull : 0ull;
+      const uint32_t b = (uint32_t)__builtin_ctz((w & 15u) | 16u) & 3u;
+      if (i < TOP) MT[i >> 4] |= bit << (16 * b + (i & 15));
+      else MB[(i - TOP) >> 4] |= bit << (16 * b + ((i - TOP) & 15));
+    }
+  }
+  const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
+  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
+  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
+  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  const v2s MM = as_v2(pk2(sc.mismatch, sc.mismatch));
+  const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
+  const v2s R0 = as_v2(pk2(r0, r0));
+  const uint32_t qrqL = pk2(QRqi, last ? QRqr : QRqi), rqL = pk2(Rqi, last ? Rqr : Rqi);
+  v2s H[TOP], E[TOP];
+  uint32_t SH[TOP], SE[TOP];  // summaries; SH stored +1 (every consumer adds the move)
+  auto init_rows = [&](uint32_t keep_mask) {
+    // boundary column -1 (k_align_pk's init_rows at global rows); lane 0's row -1 stand-in holds H(-1,-1) = 0
+#pragma unroll
+    for (int kk = 0; kk < TOP; kk++) {
+      const int i0 = r0 + kk, i1 = r0 + TOP + kk;
+      const int h0 = -sc.go[1] - (i0 + 1) * sc.ge[1];
+      const int h1 = -sc.go[1] - (i1 + 1) * sc.ge[1];
+      const int q1 = (kk == KL && last) ? QRqr : QRqi;
+      const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
+      const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
+      uint32_t hp = pk2(h0, h1);
+      if constexpr (P > 0)
+        if (kk == VK) hp &= ~(VM & fm);
+      H[kk] = as_v2(bfi(keep_mask, hp, as_u(H[kk])));
+      E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
+      SH[kk] = bfi(keep_mask, 0x00010001u, SH[kk]);
+      SE[kk] = bfi(keep_mask, 0x00010001u, SE[kk]);
+    }
+  };
+#pragma unroll
+  for (int kk = 0; kk < TOP; kk++) {
+    H[kk] = as_v2(0u);
+    E[kk] = as_v2(0u);
+    SH[kk] = SE[kk] = 0;
+  }
+  init_rows(0xffffffffu);
+  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDF = 0;  // top half's last row -> bottom half (next step)
+  uint32_t xHF = 0, xSS = 0, xDF = 0;                    // last row (Hd | F, SHd | SF, DF) -> lane g+1
+  int Lext = 0, trail = 0;
+  uint32_t tword = 0, tprev = 1;
+  const int nsteps = tl + 2 * G - 1;
+  for (int st = 0; st < nsteps; st++) {
+    const int j = st - 2 * g;  // top half's column; the bottom half's is j - 1
+    const uint32_t rHF = row_shr1(xHF), rSS = row_shr1(xSS), rDF = row_shr1(xDF);
+    uint32_t tcode = 0;
+    if (j >= 0 && j <= tl) {
+      if ((j & 7) == 0) tword = tcp[j >> 3];
+      tcode = tword & 15u;
+      tword >>= 4;
+    }
+    const uint32_t bl = (uint32_t)__builtin_ctz(tcode | 16u) & 3u, bh = (uint32_t)__builtin_ctz(tprev | 16u) & 3u;
+    tprev = tcode;
+    uint32_t M[NG];
+#pragma unroll
+    for (int gg = 0; gg < NG; gg++)
+      M[gg] = ((uint32_t)(MT[gg] >> (16 * bl)) & 0xffffu) | ((uint32_t)(MB[gg] >> (16 * bh)) << 16);
+    const bool lc0 = (j == tl - 1), lc1 = (j == tl);
+    const uint32_t QRt = pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti);
+    const uint32_t Rt = pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti);
+    // the row above the top half: the boundary row -1 (lane 0) or lane g-1's last row | carry (bottom half)
+    const int hd0 = (j <= 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
+    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
+    v2s Hd = as_v2(bfi(fm, (uint32_t)hd0 & 0xffffu, rHF & 0xffffu) | (cHd << 16));
+    uint32_t SHd = bfi(fm, 1u, rSS & 0xffffu) | (cSHd << 16);
+    v2s F = as_v2(bfi(fm, (uint32_t)f0 & 0xffffu, rHF >> 16) | (cF << 16));
+    uint32_t SF = bfi(fm, 1u, rSS >> 16) | (cSF << 16);
+    uint32_t DF = bfi(fm, 0xffffu, rDF & 0xffffu) | (cDF << 16);  // row the current D run opened from
+#pragma unroll
+    for (int kk = 0; kk < TOP; kk++) {
+      const uint32_t e = (M[kk >> 4] >> (kk & 15)) & 0x00010001u;
+      v2s h = Hd + MM + as_v2(e) * DELTA;
+      uint32_t sh = SHd + (e << 8);
+      const uint32_t mF = gt_mask(F, h);
+      h = __builtin_elementwise_max(h, F);
+      sh = bfi(mF, SF, sh);
+      const v2s Ec = E[kk];
+      const uint32_t mE = gt_mask(Ec, h);
+      h = __builtin_elementwise_max(h, Ec);
+      sh = bfi(mE, SE[kk], sh);
+      const uint32_t sh1 = sh + 0x00010001u;
+      int dr_last = 0;
+      bool eb_last = false;
+      if (kk == KL) {
+        eb_last = (mE >> 31) != 0;
+        dr_last = (mF >> 31) != 0 ? (QL - 1) - (int)(short)(DF >> 16) : 0;
+      }
+      const v2s fo = h - as_v2(QRt), fe = F - as_v2(Rt);
+      const uint32_t mfx = gt_mask(fe, fo);
+      F = __builtin_elementwise_max(fo, fe);
+      DF = bfi(mfx | (mF & ~mE), DF, as_u(as_v2(pk2(kk, TOP + kk)) + R0));
+      SF = bfi(mfx, SF + 0x00010001u, sh1);
+      const uint32_t qrq = kk == KL ? qrqL : pk2(QRqi, QRqi);
+      const uint32_t rq = kk == KL ? rqL : pk2(Rqi, Rqi);
+      const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
+      const uint32_t mex = gt_mask(ee, eo);
+      if (kk == KL) {
+        const bool ex = (mex >> 31) != 0;
+        const int lh = eb_last ? 1 + Lext : 0;
+        trail = eb_last ? lh : dr_last;
+        Lext = ex ? 1 + Lext : lh;
+      }
+      E[kk] = __builtin_elementwise_max(eo, ee);
+      SE[kk] = bfi(mex, SE[kk] + 0x00010001u, sh1);
+      Hd = H[kk];
+      SHd = SH[kk];
+      H[kk] = h;
+      SH[kk] = sh1;
+      if constexpr (P > 0) {
+        if (kk == VK) {
+          // lane 0's stand-in row leaves exactly what the boundary row -1 gives the row below it
+          const int cv = VR < TOP ? j : j - 1;
+          const int hb = cv < 0 ? 0 : -(sc.go[0] + (cv + 1) * sc.ge[0]);
+          const int fb = sc.boundary_open ? hb - (cv == tl - 1 ? QRtr : QRti) : kNegInf;
+          const uint32_t vm = VM & fm;
+          H[kk] = as_v2(bfi(vm, pk2(hb, hb), as_u(H[kk])));
+          SH[kk] = bfi(vm, 0x00010001u, SH[kk]);
+          F = as_v2(bfi(vm, pk2(fb, fb), as_u(F)));
+          SF = bfi(vm, 0x00010001u, SF);
+          DF |= vm;
+        }
+      }
+      if (kk == KL) {
+        // carries for lane g+1: H(last, j-2) and S_H before this step's update, F / S_F / DF out of it
+        xHF = (as_u(Hd) >> 16) | (as_u(F) & 0xffff0000u);
+        xSS = (SHd >> 16) | (SF & 0xffff0000u);
+        xDF = DF >> 16;
+      }
+    }
+    cHd = as_u(Hd) & 0xffffu;
+    cSHd = SHd & 0xffffu;
+    cF = as_u(F) & 0xffffu;
+    cSF = SF & 0xffffu;
+    cDF = DF & 0xffffu;
+    if (j <= 0) {
+      // columns before 0 (this lane has not started) and the bottom half's column -1: restore
+      init_rows(j < 0 ? 0xffffffffu : 0xffff0000u);
+      Lext = 0;
+      trail = 0;
+    }
+  }
+  if (!last) return;
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16);
+  const uint32_t S = ((SH[KL] >> 16) - 1u) & 0xffffu;
+  const uint32_t m = S >> 8, acols = S & 0xffu;
+  const uint32_t internal = acols - (uint32_t)trail;
+  out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
+}
+
 typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
                         const uint32_t*, Scoring, uint32_t*);
 
-// launch table: align[3 L + v] (v: 0 packed, 1 one-cell-per-op, 2 IUPAC)
+// launch table: align[kAlignSlots L + v] (v: 0 packed, 1 one-cell-per-op, 2 IUPAC, 3 banded packed)
+constexpr int kAlignSlots = 4;
 template <int L, int LO>
 struct AlignRange {
   static void fill(AlignFn* a) {
-    a[3 * L] = k_align_pk<L>;
+    a[kAlignSlots * L] = k_align_pk<L>;
     // the one-cell-per-op kernel for one-hot inputs is a cross-check of the packed one (<= kShortLen)
-    if constexpr (L <= kShortLen) a[3 * L + 1] = k_align<L, false>;
-    else a[3 * L + 1] = k_align_pk<L>;
-    a[3 * L + 2] = k_align<L, true>;
+    if constexpr (L <= kShortLen) a[kAlignSlots * L + 1] = k_align<L, false>;
+    else a[kAlignSlots * L + 1] = k_align_pk<L>;
+    a[kAlignSlots * L + 2] = k_align<L, true>;
+    a[kAlignSlots * L + 3] = k_align_band<L, band_lanes(L)>;
     if constexpr (L > LO) AlignRange<L - 1, LO>::fill(a);
   }
 };

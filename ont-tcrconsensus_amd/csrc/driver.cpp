@@ -322,6 +322,8 @@ struct umiclust_ctx {
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
   int32_t split_env = -1;
+  int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
+                                   // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
@@ -762,8 +764,9 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   // unfinished walk together with the relevant in-window peers (their relevance is taken from the walk
   // state after round 0, which only widens it: a superset of what the final state needs)
   const uint32_t peer_out0 = (uint32_t)nqs * kWalk;
+  // small passes (deep clusters cut blocks small) spread every pair over a lane group
   c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * kWalk, P.d_counters.p + 1, P.d_outidx.p, c->sc,
-                      P.d_res.p, st),
+                      P.d_res.p, st, c->band_pairs),
          "align 0");
   c->hip(launch_walk(0, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
                      P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2,
@@ -775,7 +778,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
                            st),
          "peer pairs");
   c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * (kWalk + kPeerCap), P.d_counters.p + 2,
-                      P.d_outidx.p, c->sc, P.d_res.p, st),
+                      P.d_outidx.p, c->sc, P.d_res.p, st, c->band_pairs),
          "align 1");
   c->hip(launch_walk(1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
                      P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 3,
@@ -1274,7 +1277,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
       c->hip(hipEventRecord(c->evb[0], sb), "event");
       c->hip(launch_align(dev_seqs(c), c->hlen[q0], c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc,
-                          c->d_bres.p, sb),
+                          c->d_bres.p, sb, c->band_pairs),
              "align B");
       c->hip(hipEventRecord(c->evb[1], sb), "event");
       c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
@@ -2649,6 +2652,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   }
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_SPLIT")) {
     c->split_env = atoi(e) != 0 ? 1 : 0;
     c->split_stream = atoi(e) == 2;
@@ -2919,7 +2923,7 @@ int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const ch
                "traceback");
       else
         c->hip(launch_align(ds, ql, amb != 0, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), nullptr, nullptr, sc,
-                            d_out.p + b0, c->st),
+                            d_out.p + b0, c->st, c->band_pairs),
                "align");
       b0 = e;
     }

@@ -1320,7 +1320,7 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   return hipGetLastError();
 }
 
-static AlignFn g_align[3 * (kMaxLen + 1)];
+static AlignFn g_align[kAlignSlots * (kMaxLen + 1)];
 static int g_align_variant0 = 0;
 static std::once_flag g_align_once;
 static void init_align_tables() {
@@ -1339,13 +1339,16 @@ static void init_align_tables() {
 
 hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq,
                         const uint32_t* pt, int32_t npairs, const uint32_t* dev_npairs,
-                        const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st) {
+                        const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st,
+                        int32_t band_max) {
   init_align_tables();
   const int variant0 = g_align_variant0;
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(g_align[3 * qlen + (ambig ? 2 : variant0)], dim3((npairs + 63) / 64), dim3(64), 0, st, s,
-                     pq, pt, npairs, dev_npairs, outidx, sc, out);
+  const bool band = !ambig && variant0 == 0 && npairs <= band_max;
+  const int64_t lanes = (int64_t)npairs * (band ? band_lanes(qlen) : 1);
+  hipLaunchKernelGGL(g_align[kAlignSlots * qlen + (ambig ? 2 : band ? 3 : variant0)], dim3((unsigned)((lanes + 63) / 64)),
+                     dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
 }
 

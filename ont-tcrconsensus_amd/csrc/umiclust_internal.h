@@ -160,10 +160,11 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode = 0
 
 // alignment of pairs whose queries all have length qlen; pq = (query seqno << 1) | strand, pt = target seqno (plus strand)
 // out[outidx ? outidx[k] : k] = matches | internal << 8 | (score & 0xffff) << 16.
-// If dev_npairs != NULL only pairs k < *dev_npairs run (npairs is the launch bound).
+// If dev_npairs != NULL only pairs k < *dev_npairs run (npairs is the launch bound).  Launches of at most
+// band_max pairs (one-hot codes) spread each pair over a lane group (k_align_band) instead of one lane.
 hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
                         const uint32_t* dev_npairs, const uint32_t* outidx, const Scoring& sc,
-                        uint32_t* out, hipStream_t st);
+                        uint32_t* out, hipStream_t st, int32_t band_max = 0);
 
 constexpr int kTabL = 2 * kMaxLen + 1;  // internal alignment length 0..2*kMaxLen
 constexpr int kTabM = kMaxLen + 1;      // matches 0..kMaxLen

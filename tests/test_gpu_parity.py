@@ -73,6 +73,45 @@ def test_align_pairs_vs_oracle(gpu_ctx, preset, ambig, hi):
         assert (int(tb["score"][k]), int(tb["matches"][k]), int(tb["internal_len"][k])) == got
 
 
+@pytest.mark.parametrize("preset,hi", [(1, 72), (2, _lib.MAX_LEN), (1, _lib.MAX_LEN)])
+def test_align_pairs_banded_vs_oracle(preset, hi, monkeypatch):
+    """The banded packed kernel (one pair over a group of 4 or 8 lanes, virtual rows on top of lane 0,
+    DPP carries between lanes), forced for every launch: every query length 32..hi, targets 1..hi."""
+    monkeypatch.setenv("UMICLUST_BAND", str(1 << 30))
+    p = _lib.params(preset, 0.93, 32, hi)
+    op = orc.params(preset, 0.93, 32, hi)
+    qs, ts = _pairs(700 + preset + hi, 4000, list(range(32, hi + 1)), tl_lo=1, tl_hi=hi)
+    with _lib.Context(0) as ctx:
+        r = ctx.align_pairs(p, qs, ts)
+    for k, (q, t) in enumerate(zip(qs, ts)):
+        o = orc.align(op, q, t)
+        got = (int(r["score"][k]), int(r["matches"][k]), int(r["internal_len"][k]))
+        assert got == (o["score"], o["matches"], o["internal_len"]), (k, q, t, got, o)
+
+
+@pytest.mark.parametrize("deep", [False, True])
+def test_cluster_banded_vs_oracle(deep, monkeypatch):
+    """Every walk launch on the banded kernel: short UMIs (config-2 style) and config-5 deep clusters."""
+    monkeypatch.setenv("UMICLUST_BAND", str(1 << 30))
+    if deep:
+        u = synth.make_umis(8, seed=37, max_reads=2500, orient_mix=0.3, mean_reads=1500.0, error_rate=0.15,
+                            split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                            pattern_rev=synth.UMI_REV_LONG)
+        args = (1, 0.75, 80, 110)
+    else:
+        u = synth.make_umis(200, seed=29, max_reads=2500, orient_mix=0.2)
+        args = (1, 0.93, 58, 68)
+    seqs = u.as_list()
+    monkeypatch.setenv("UMICLUST_BLOCK", "256")
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(*args), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(*args), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+
+
 def test_align_known_answers(gpu_ctx):
     p = _lib.params(1, 0.93, 32, 72)
     base = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
