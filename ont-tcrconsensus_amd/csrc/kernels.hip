@@ -1347,7 +1347,8 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
   const bool band = !ambig && variant0 == 0 && npairs <= band_max;
   const int64_t lanes = (int64_t)npairs * (band ? band_lanes(qlen) : 1);
-  hipLaunchKernelGGL(g_align[kAlignSlots * qlen + (ambig ? 2 : band ? 3 : variant0)], dim3((unsigned)((lanes + 63) / 64)),
+  const int v = ambig ? 2 : band ? 3 : variant0;
+  hipLaunchKernelGGL(g_align[kAlignSlots * qlen + v], dim3((unsigned)((lanes + 63) / 64)),
                      dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
 }
