@@ -137,6 +137,15 @@ struct Fail {
 
 // One greedy block in flight: its own peer tile, device outputs and pinned mirrors, so the device
 // runs block k+1 while the host resolves block k.
+// Outcome of one strand's walk.
+struct Outcome {
+  bool acc = false;
+  uint16_t rank = 0;
+  uint32_t t = 0xffffffffu;
+  int walked = 0;
+  int64_t cells = 0;
+};
+
 struct Pass {
   int32_t q0 = 0, nq = 0, w0 = 0;  // block [q0, q0+nq), peer window [w0, q0+nq)
   bool live = false;
@@ -168,8 +177,9 @@ struct Pass {
   // parallel classification of the pass's query-strands (resolve_pass): 0 the device outcome is final,
   // 1 final unless one of its in-block relevant peers (deps) turns out a centroid or is undetermined,
   // 2 resolved sequentially in full
-  std::vector<uint8_t> kind, ndeps;
+  std::vector<uint8_t> kind, ndeps, pre_cert;
   std::vector<uint16_t> deps;
+  std::vector<Outcome> pre;  // outcomes the classify threads resolved (kind 3) or found needing round B (kind 4)
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   // split passes: the counting half (enqueue_count) of the block this buffer set serves next
   PinBuf<TileView> h_tiles_a;
@@ -322,6 +332,7 @@ struct umiclust_ctx {
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
   int32_t split_env = -1;
+  bool pre_resolve = true;          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
                                    // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
@@ -386,6 +397,8 @@ struct umiclust_ctx {
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
   int64_t dbg_q[4] = {0, 0, 0, 0};
+  double dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // UMICLUST_DEBUG: resolve_pass phases (s): event wait, outcome copy,
+                                               // record copy, classify, in-order resolve, round B + rest, total
   int64_t dbg_p[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: strands on the inline path / with > kInlineRel relevant
                                     // peers / reading their record / peers scanned there  // UMICLUST_DEBUG: queries without records / records with only earlier-block
                                     // relevant peers / with an in-block relevant peer / host ns in pass 1
@@ -518,15 +531,6 @@ struct MCand {
   uint32_t seqno;
   uint32_t res;  // alignment result (matches | internal << 8), valid if have
   bool have;
-};
-
-// Outcome of one strand's walk.
-struct Outcome {
-  bool acc = false;
-  uint16_t rank = 0;
-  uint32_t t = 0xffffffffu;
-  int walked = 0;
-  int64_t cells = 0;
 };
 
 // vsearch search_onequery over a merged, sorted candidate list (maxaccepts 1, maxrejects 32).
@@ -908,6 +912,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   const double tsync0 = now_s();
   c->hip(hipEventSynchronize(P.ev[4]), "sync");
   c->stats.t_sync_s += now_s() - tsync0;
+  c->dbg_t[0] += now_s() - tsync0;
+  struct DAcc { double* p; double t0; ~DAcc() { *p += now_s() - t0; } } dtot{&c->dbg_t[6], tsync0};
   P.live = false;
   float ms = 0;
   c->hip(hipEventElapsedTime(&ms, P.ev[0], P.ev[1]), "elapsed");
@@ -943,6 +949,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   const double tc0 = now_s();
   P.hq_copy.assign(P.h_hq.p, P.h_hq.p + nqs);
   c->stats.t_sync_s += now_s() - tc0;
+  c->dbg_t[1] += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
   for (int32_t qs = 0; qs < nqs; qs++)
     if (hq[qs].flags & 2u) return false;
@@ -950,8 +957,6 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   const double th0 = now_s();
   constexpr int kSlots = kWalk + kPeerCap;  // round-B result slots per query-strand: T_old, peers
   std::vector<int32_t> deferred;
-  std::vector<MCand> L;
-  std::vector<std::pair<unsigned long long, int>> cp;
   std::vector<uint32_t> extra_res;   // [row*kSlots + slot] results of round B (valid if flag)
   std::vector<uint8_t> extra_have;
   std::vector<int32_t> extra_row;    // qs -> row of the round-B arrays (-1: none)
@@ -969,6 +974,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     P.rec_copy.assign(P.h_rec.p, P.h_rec.p + *P.h_reccount.p);
     recs = P.rec_copy.data();
     c->stats.t_sync_s += now_s() - tc1;
+    c->dbg_t[2] += now_s() - tc1;
   }
   auto rec_of = [&](const HostQs& h) {
     const uint32_t* r = recs + h.rec;
@@ -994,15 +1000,25 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // Such a query is a member whichever centroid it ends up joining, so later queries that only need to
   // know "centroid or not" are not held up by it.
   auto cert_device = [](const HostQs& h) { return (h.flags & 1u) && (int)h.w + (int)h.nrel <= kWalk; };
-  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert) -> int {
+  struct Scratch {
+    std::vector<std::pair<unsigned long long, int>> cp;
+    std::vector<MCand> L;
+    int64_t merged = 0;
+  };
+  // seq: the in-order phase (debug counters, merged-walk timer); otherwise a classify thread resolving a strand
+  // whose peers' states are all final, with its own scratch
+  auto strand_outcome_s = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert, Scratch& scr,
+                              bool seq) -> int {
     // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed
+    auto& cp = scr.cp;
+    auto& L = scr.L;
     const HostQs& h = hq[qs];
     cert = false;
     if (h.rec == 0xffffffffu) {
       device_outcome(h, o);
       return 0;
     }
-    if (c->debug) c->dbg_p[h.nrel <= (uint32_t)kInlineRel ? 0 : 1]++;
+    if (seq && c->debug) c->dbg_p[h.nrel <= (uint32_t)kInlineRel ? 0 : 1]++;
     if (h.nrel <= (uint32_t)kInlineRel) {
       bool cent = false;
       for (uint32_t i = 0; i < h.nrel; i++) {
@@ -1018,21 +1034,21 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
         return 0;
       }
     }
-    if (c->debug) c->dbg_p[2]++;
+    if (seq && c->debug) c->dbg_p[2]++;
     const Rec R = rec_of(h);
-    if (c->debug) c->dbg_p[3] += R.np;
+    if (seq && c->debug) c->dbg_p[3] += R.np;
     bool affects = false, undet = false;
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
       const uint8_t st = state[(uint32_t)w0 + (pw & 0xffffu)];
       if ((pw >> 24) & 1u) {
         if (st == ST_UNDET) {
-          c->dbg[2]++;
+          if (seq) c->dbg[2]++;
           cert = cert_device(h);
           return 1;
         }
         affects |= st == ST_CENT;
-        if (!((pw >> 25) & 1u)) c->dbg[st == ST_CENT ? 0 : 1]++;  // mispredicted / saved
+        if (seq && !((pw >> 25) & 1u)) c->dbg[st == ST_CENT ? 0 : 1]++;  // mispredicted / saved
       } else {
         undet |= st == ST_UNDET;
       }
@@ -1045,9 +1061,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       cert = cert_device(h);
       return 1;
     }
-    c->stats.n_merged_walks++;
-    const double tm0 = now_s();
-    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{&c->stats.t_merged_s, tm0};
+    scr.merged++;
+    double t_unused = 0;
+    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{seq ? &c->stats.t_merged_s : &t_unused,
+                                                                               now_s()};
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
     const int32_t row = allow_extra ? extra_row[qs] : -1;
@@ -1105,6 +1122,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
         cert = c->h_acc[(size_t)Li * kTabM + m] != 0;
       }
     return 2;
+  };
+  Scratch scr0;
+  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert) -> int {
+    return strand_outcome_s(qs, q, allow_extra, o, cert, scr0, true);
   };
   auto resolve = [&](int32_t ql, bool allow_extra, auto&& strand_fn) -> bool {
     const int32_t q = q0 + ql;
@@ -1168,7 +1189,12 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   P.kind.resize((size_t)nqs);
   P.ndeps.resize((size_t)nqs);
   P.deps.resize((size_t)nqs * kDeps);
-  auto classify = [&](int32_t qs) {
+  P.pre.resize((size_t)nqs);
+  P.pre_cert.resize((size_t)nqs);
+  // kind 0: the device outcome is final; 1: final unless an in-block dependency becomes a centroid or is
+  // deferred; 2: full resolution in order; 3 / 4: every peer lies in an earlier (resolved) block, so the
+  // full resolution needs no in-order state and ran here: resolved (3) or needing round B (4)
+  auto classify = [&](int32_t qs, Scratch& scr) {
     const HostQs& h = hq[qs];
     uint8_t& kd = P.kind[qs];
     if (h.rec == 0xffffffffu) {
@@ -1195,17 +1221,34 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
     kd = !ok ? 2 : nd ? 1 : 0;
     P.ndeps[qs] = (uint8_t)nd;
+    if (kd == 2 && c->pre_resolve) {
+      const Rec R = rec_of(h);
+      bool early = true;
+      for (int y = 0; y < R.np && early; y++) early = (R.peer[y] & 0xffffu) < inb;
+      if (early) {
+        bool cert = false;
+        const int r = strand_outcome_s(qs, q0 + qs / both, false, P.pre[qs], cert, scr, false);
+        if (r != 1) {
+          kd = r == 0 ? 3 : 4;
+          P.pre_cert[qs] = cert;
+        }
+      }
+    }
   };
   if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
   const int T = nqs < 2048 ? 1 : c->pool->size();
+  std::vector<Scratch> scr_t((size_t)T);
   if (T == 1) {
-    for (int32_t qs = 0; qs < nqs; qs++) classify(qs);
+    for (int32_t qs = 0; qs < nqs; qs++) classify(qs, scr_t[0]);
   } else {
     c->pool->run([&](int t) {
       const int32_t lo = (int32_t)((int64_t)nqs * t / T), hi = (int32_t)((int64_t)nqs * (t + 1) / T);
-      for (int32_t qs = lo; qs < hi; qs++) classify(qs);
+      for (int32_t qs = lo; qs < hi; qs++) classify(qs, scr_t[(size_t)t]);
     });
   }
+  for (const Scratch& x : scr_t) c->stats.n_merged_walks += x.merged;
+  const double tp1 = now_s();
+  c->dbg_t[3] += tp1 - tp0;
   // Phase 2 (sequential, sorted order): confirm the device outcomes against the in-block peers' states
   auto strand_fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
     const HostQs& h = hq[qs];
@@ -1213,6 +1256,14 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     if (P.kind[qs] == 0) {
       device_outcome(h, o);
       return 0;
+    }
+    if (P.kind[qs] == 3) {
+      o = P.pre[qs];
+      return 0;
+    }
+    if (P.kind[qs] == 4) {
+      cert = P.pre_cert[qs] != 0;
+      return 2;
     }
     if (P.kind[qs] == 1) {
       const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
@@ -1235,6 +1286,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   for (int32_t ql = 0; ql < nq; ql++)
     if (!resolve(ql, false, strand_fast)) deferred.push_back(ql);
   c->dbg_q[3] += (int64_t)((now_s() - tp0) * 1e9);
+  c->dbg_t[4] += now_s() - tp1;
   t_host += now_s() - th0;
   c->stats.t_host_pass1_s += now_s() - th0;
   c->stats.n_deferred += (int64_t)deferred.size();
@@ -1302,6 +1354,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     t_host += now_s() - th2;
     std::sort(new_cents.begin(), new_cents.end());
   }
+  c->stats.n_merged_walks += scr0.merged;
   return true;
 }
 
@@ -1773,6 +1826,11 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: strands inline %lld many-relevant %lld record-read %lld peers-scanned %lld\n", bin,
             (long long)c->dbg_p[0], (long long)c->dbg_p[1], (long long)c->dbg_p[2], (long long)c->dbg_p[3]);
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: resolve wait %.3f hq-copy %.3f rec-copy %.3f classify %.3f in-order %.3f total %.3f s "
+            "(round B and the rest %.3f)\n", bin, c->dbg_t[0], c->dbg_t[1], c->dbg_t[2], c->dbg_t[3], c->dbg_t[4],
+            c->dbg_t[6], c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[3] - c->dbg_t[4]);
+  for (double& x : c->dbg_t) x = 0;
   c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
   c->dbg_p[0] = c->dbg_p[1] = c->dbg_p[2] = c->dbg_p[3] = 0;
   c->dbg[0] = c->dbg[1] = c->dbg[2] = 0;
@@ -2653,6 +2711,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_SPLIT")) {
     c->split_env = atoi(e) != 0 ? 1 : 0;
     c->split_stream = atoi(e) == 2;
