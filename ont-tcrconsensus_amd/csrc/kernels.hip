@@ -1681,6 +1681,9 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
   const uint32_t* qcp = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
   for (int j = lane; j < tl + 64; j += 64) S.tcode[j] = j < tl ? (uint8_t)((tcp[j >> 3] >> ((j & 7) * 4)) & 15u) : 0;
+  // both sequences' code words in VGPRs (lane w holds word w): the backtrack reads them by v_readlane
+  // instead of a global / LDS load per diagonal step
+  const uint32_t qword = lane < kCodeWords ? qcp[lane] : 0u, tword = lane < kCodeWords ? tcp[lane] : 0u;
   const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
   const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
   const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
@@ -1774,8 +1777,9 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
       i--;
       op = 'D';
     } else {
-      const uint32_t qc = (qcp[i >> 3] >> ((i & 7) * 4)) & 15u;
-      if (qc & S.tcode[j]) matches++;
+      const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
+      const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
+      if (qc & tc) matches++;
       i--;
       j--;
       op = 'M';
