@@ -40,6 +40,8 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <pthread.h>
+#include <sched.h>
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
@@ -214,6 +216,9 @@ class WorkPool {
     for (auto& t : th_) t.join();
   }
   int size() const { return (int)th_.size() + 1; }
+  void set_affinity(const cpu_set_t& set) {
+    for (auto& t : th_) pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+  }
   void run(const std::function<void(int)>& f) {
     if (th_.empty()) {
       f(0);
@@ -332,6 +337,7 @@ struct umiclust_ctx {
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
   int32_t split_env = -1;
+  bool pin = false;                // UMICLUST_PIN=1: host resolve threads kept in the caller's L3 domain (L3Pin)
   bool pre_resolve = true;          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
                                    // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
@@ -2712,6 +2718,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PIN")) c->pin = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_SPLIT")) {
     c->split_env = atoi(e) != 0 ? 1 : 0;
     c->split_stream = atoi(e) == 2;
@@ -2826,10 +2833,48 @@ int32_t umiclust_load(umiclust_ctx* c, const umiclust_params* p, const char* seq
   });
 }
 
+// UMICLUST_PIN=1: keep the host resolve -- the calling thread and the resolve pool -- inside the L3 domain the
+// caller runs on, for the duration of one call (the caller's affinity is restored afterwards)
+struct L3Pin {
+  cpu_set_t saved;
+  bool on = false;
+  explicit L3Pin(umiclust_ctx* c) {
+    if (!c->pin || sched_getaffinity(0, sizeof saved, &saved) != 0) return;
+    const int cpu = sched_getcpu();
+    char path[96], buf[256];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+    FILE* f = cpu >= 0 ? fopen(path, "r") : nullptr;
+    if (!f) return;
+    const bool got = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!got) return;
+    cpu_set_t want;
+    CPU_ZERO(&want);
+    for (char* p = buf; *p;) {  // "a-b,c,d-e"
+      char* e;
+      const long a = strtol(p, &e, 10);
+      if (e == p) break;
+      long b = a;
+      if (*e == '-') b = strtol(e + 1, &e, 10);
+      for (long x = a; x <= b && x < CPU_SETSIZE; x++)
+        if (CPU_ISSET((int)x, &saved)) CPU_SET((int)x, &want);
+      p = *e == ',' ? e + 1 : e;
+      if (*p == '\n') break;
+    }
+    if (CPU_COUNT(&want) == 0 || sched_setaffinity(0, sizeof want, &want) != 0) return;
+    if (c->pool) c->pool->set_affinity(want);  // a pool created below inherits the caller's mask
+    on = true;
+  }
+  ~L3Pin() {
+    if (on) sched_setaffinity(0, sizeof saved, &saved);
+  }
+};
+
 int64_t umiclust_cluster(umiclust_ctx* c, umiclust_stats* stats) {
   UC_GUARD(c, {
     if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster before umiclust_load");
     if (c->bin_s.size() != 2) c->fail(UMICLUST_EINVAL, "umiclust_cluster: the load holds several bins");
+    L3Pin pin(c);
     cluster_all(c, 0);
     if (stats) *stats = c->stats;
     return c->nclusters;
