@@ -337,7 +337,8 @@ struct umiclust_ctx {
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
   int32_t split_env = -1;
-  bool pin = false;                // UMICLUST_PIN=1: host resolve threads kept in the caller's L3 domain (L3Pin)
+  bool pin = true;                 // UMICLUST_PIN=0: host resolve threads not kept in the caller's L3 domain (L3Pin;
+                                   // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json)
   bool pre_resolve = true;          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
                                    // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
@@ -2833,8 +2834,8 @@ int32_t umiclust_load(umiclust_ctx* c, const umiclust_params* p, const char* seq
   });
 }
 
-// UMICLUST_PIN=1: keep the host resolve -- the calling thread and the resolve pool -- inside the L3 domain the
-// caller runs on, for the duration of one call (the caller's affinity is restored afterwards)
+// Keep the host resolve -- the calling thread and the resolve pool -- inside the L3 domain the caller runs on,
+// for the duration of one call (the caller's affinity is restored afterwards; UMICLUST_PIN=0 turns it off)
 struct L3Pin {
   cpu_set_t saved;
   bool on = false;
