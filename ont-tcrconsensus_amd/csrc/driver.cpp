@@ -1755,7 +1755,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     c->hip(hipEventRecord(c->tev[0], c->st), "event");
     DevSeqs ds = dev_seqs(c);
     // every member's chosen hit in one launch (one wave per alignment, any query length)
-    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st),
+    // the bin's longest sequence bounds every pair's lengths (one pass over its lengths)
+    const int32_t maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
+    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl),
            "traceback");
     // consensus inputs in output-cluster order
     std::vector<int32_t> mseq(n), mops(n);
@@ -3024,7 +3026,7 @@ int32_t umiclust_align_pairs(umiclust_ctx* c, const umiclust_params* p, const ch
       while (e < npairs && off[ord[e] + 1] - off[ord[e]] == ql) e++;
       if (cigar_ops)
         c->hip(launch_traceback(ds, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), sc, d_ops.p + (size_t)b0 * kOpsStride,
-                                d_nops.p + b0, d_out.p + b0, c->st),
+                                d_nops.p + b0, d_out.p + b0, c->st, kMaxLen),
                "traceback");
       else
         c->hip(launch_align(ds, ql, amb != 0, d_pq.p + b0, d_pt.p + b0, (int32_t)(e - b0), nullptr, nullptr, sc,

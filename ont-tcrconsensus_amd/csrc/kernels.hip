@@ -1649,15 +1649,18 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
 // (bit 0 up = D chosen, bit 1 left = I chosen, bit 2 D-extension, bit 3 I-extension) goes to LDS, 8 steps
 // per word, and lane 0 runs backtrack16 over it.  Any query length up to kMaxLen in one launch; latency
 // ~(ql + tl) steps instead of ql * tl serial cells.
+// A wave's LDS is sized by the longest sequence of the launch (maxl): dir[stripes][words][64] (cell
+// (64 s + l, t - l): word t / 8 of lane l, nibble t % 8), botH[maxl] (H(64 s - 1, j) for the next stripe),
+// botF[maxl] (F(64 s, j)), hend, tcode[maxl + 64] -- 9.4 KB for 68-nt UMIs instead of 12.4 KB at kMaxLen
+// (16 waves per CU instead of 12).
 constexpr int kTwWaves = 4;
-constexpr int kTwStripes = (kMaxLen + 63) / 64;
-constexpr int kTwWords = (kMaxLen + 63 + 7) / 8;
-struct TwShared {
-  uint32_t dir[kTwStripes][kTwWords][64];  // cell (64 s + l, t - l): word t / 8 of lane l, nibble t % 8
-  int32_t botH[kMaxLen];                   // H(64 s - 1, j) for the next stripe
-  int32_t botF[kMaxLen];                   // F(64 s, j)
-  uint8_t tcode[kMaxLen + 64];
-  int32_t hend;
+struct TwLayout {
+  int words, dir_u32, wave_bytes;
+  __host__ __device__ explicit TwLayout(int maxl) {
+    words = (maxl + 63 + 7) / 8;
+    dir_u32 = ((maxl + 63) / 64) * words * 64;
+    wave_bytes = (dir_u32 * 4 + 2 * maxl * 4 + 4 + maxl + 64 + 15) & ~15;
+  }
 };
 
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
@@ -1667,12 +1670,24 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
 __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const uint32_t* __restrict__ pq,
                                                               const uint32_t* __restrict__ pt, int32_t npairs,
                                                               Scoring sc, uint8_t* __restrict__ ops,
-                                                              uint16_t* __restrict__ nops, uint32_t* __restrict__ out) {
-  __shared__ TwShared SH[kTwWaves];
+                                                              uint16_t* __restrict__ nops, uint32_t* __restrict__ out,
+                                                              int32_t maxl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tw_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int k = (int)blockIdx.x * kTwWaves + wave;
   if (k >= npairs) return;  // wave-uniform
-  TwShared& S = SH[wave];
+  const TwLayout lay(maxl);
+  struct {
+    uint32_t* dir;
+    int32_t *botH, *botF, *hendp;
+    uint8_t* tcode;
+  } S;
+  S.dir = (uint32_t*)(tw_smem + (size_t)wave * lay.wave_bytes);
+  S.botH = (int32_t*)(S.dir + lay.dir_u32);
+  S.botF = S.botH + maxl;
+  S.hendp = S.botF + maxl;
+  S.tcode = (uint8_t*)(S.hendp + 1);
+  const int TW = lay.words;
   const uint32_t qv = pq[k];
   const int32_t q = (int32_t)(qv >> 1);
   const int qstr = (int)(qv & 1u);
@@ -1739,7 +1754,7 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
         E = En;
         hout = h;
         fout = Fn;
-        if (i == ql - 1 && j == tl - 1) S.hend = h;
+        if (i == ql - 1 && j == tl - 1) *S.hendp = h;
         if (lane == 63 && st + 1 < nstripe) {
           S.botH[j] = h;
           S.botF[j] = Fn;
@@ -1749,7 +1764,7 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
       (void)Hl;
       dword |= d << ((tt & 7) * 4);
       if ((tt & 7) == 7 || tt == nsteps - 1) {
-        S.dir[st][tt >> 3][lane] = dword;
+        S.dir[(st * TW + (tt >> 3)) * 64 + lane] = dword;
         dword = 0;
       }
     }
@@ -1765,7 +1780,7 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   while (i >= 0 && j >= 0) {
     aligned++;
     const int l = i & 63, tt = j + l;
-    const uint32_t d = (S.dir[i >> 6][tt >> 3][l] >> ((tt & 7) * 4)) & 15u;
+    const uint32_t d = (S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
     if (op == 'I' && (d & 8u)) {
       j--;
     } else if (op == 'D' && (d & 4u)) {
@@ -1797,14 +1812,17 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
   if (tlft >= aligned) trgt = 0;
   const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
-  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)S.hend & 0xffffu) << 16);
+  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)*S.hendp & 0xffffu) << 16);
 }
 
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
-                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st) {
+                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
+                            int32_t maxl) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_trace_wave, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves), 0, st, s, pq, pt,
-                     npairs, sc, ops, nops, out);
+  if (maxl < 1 || maxl > kMaxLen) return hipErrorInvalidValue;
+  const TwLayout lay(maxl);
+  hipLaunchKernelGGL(k_trace_wave, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
+                     (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl);
   return hipGetLastError();
 }
 

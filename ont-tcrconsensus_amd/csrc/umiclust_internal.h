@@ -219,8 +219,10 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st);
 // traceback (one wave per pair, any query length): ops[k*kOpsStride...] ('M','D','I' in alignment order,
 // right-aligned in the slot), nops[k], out[k] as launch_align's
+// maxl: the longest query or target length among the pairs (sizes the kernel's LDS)
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
-                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st);
+                            const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
+                            int32_t maxl);
 // consensus: cluster c members member_seqno[cstart[c] .. cstart[c+1]) (centroid first),
 // member_ops index per member (-1 for centroid), member strand.
 hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t nclusters,
