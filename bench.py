@@ -11,17 +11,27 @@ Workloads (BASELINE.json configs):
   --config 5: the long-UMI high-error stress bin (300k ~96-nt UMIs, 15 % indels, >1k-member clusters).
 A step = one full pass of the hot path over the rank's bins with the sequences already resident in HBM:
 K1 prep/DUST/k-mers, greedy blocks of K2 prefilter + K3 walk alignment + host resolution, K3T traceback
-for members, K4 consensus, and the result download.  --e2e adds the file leg: the same config-2 bin
-written as a FASTA with 1,500-nt `seq=` reads, then read FASTA -> cluster -> files written, timed end to end.
+for members, K4 consensus, and the result download.  Config 2 (N = 1) also runs the file leg (`e2e`, on by
+default, --no-e2e skips it): the same bin written as a FASTA with 1,500-nt `seq=` reads, then read FASTA ->
+cluster -> files written (umiclust_run_fasta, the reference's boundary: vsearch_umi_cluster.py:17-56) and the
+fused drop-in (umiclust_run_fasta_parse), each beside a write probe of the same file count and bytes on the same
+filesystem (tools/io_probe.c), so the writers' share of the disk's rate is a measured fraction.
 
-    python bench.py --gpus N --steps K --warmup W [--config 2|3|4|5] [--e2e]
+    python bench.py --gpus N --steps K --warmup W [--config 2|3|4|5] [--no-e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+--gpus N without a launcher (no WORLD_SIZE in the environment) starts N ranks itself through
+torch.distributed.run before anything touches a GPU; under a launcher WORLD_SIZE must equal N.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import ctypes
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -149,6 +159,37 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
     return roof, align
 
 
+def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
+    """Per-CU LDS-array and VALU busy of `kernel`, from the committed rocprofv3 PMC CSV
+    (profiles/r03/pmc_busy_<kernel>.csv: SQ_LDS_IDX_ACTIVE, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_WAVES,
+    GRBM_GUI_ACTIVE, ...; one pass, tools/gpu_pmc_r03.sh) with the unit factors measured by the calibration
+    kernels of tools/pmc_calib.hip (profiles/r03/pmc_calib.json): LDS busy = LDS-array cycles per CU / kernel
+    cycles, VALU busy = VALU issue cycles per SIMD / kernel cycles, kernel cycles = GRBM_GUI_ACTIVE / XCDs."""
+    csv_path = os.path.join(ROOT, "profiles", "r03", f"pmc_busy_{kernel}.csv")
+    cal_path = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
+    if not (os.path.exists(csv_path) and os.path.exists(cal_path)):
+        return None
+    cal = json.load(open(cal_path))
+    tot, disp = {}, set()
+    for r in csv.DictReader(open(csv_path, newline="")):
+        if r["Kernel_Name"].split("(")[0].split("<")[0] != kernel:
+            continue
+        disp.add(r["Dispatch_Id"])
+        tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if not disp:
+        return None
+    n = len(disp)
+    per = {k: v / n for k, v in tot.items()}
+    cyc = per["GRBM_GUI_ACTIVE"] / cal["xcds"]
+    lds = per["SQ_LDS_IDX_ACTIVE"] * cal["lds_idx_active_cycles_per_unit"] / cal["cus"] / cyc
+    valu = per["SQ_ACTIVE_INST_VALU"] * cal["active_inst_valu_cycles_per_unit"] / (cal["cus"] * 4) / cyc
+    out = dict(source=os.path.relpath(csv_path, ROOT), calibration=os.path.relpath(cal_path, ROOT), dispatches=n,
+               kernel_cycles=cyc, lds_array_busy_per_cu=lds, valu_busy_per_simd=valu,
+               lds_bank_conflict_frac=per.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, per["SQ_LDS_IDX_ACTIVE"]),
+               waves_resident_per_cu=per["SQ_WAVE_CYCLES"] * cal["wave_cycles_per_unit"] / cal["cus"] / cyc)
+    return out
+
+
 def breakdown(stats: list) -> dict:
     k = ["t_total_s", "t_prefilter_s", "t_align_s", "t_consensus_s", "t_index_s", "t_host_s",
          "t_host_pass1_s", "t_sync_s", "t_merged_s"]
@@ -166,13 +207,24 @@ def main() -> None:
                     help="default 0.90 (config 2), 0.93 (configs 3, 4 round 1), 0.75 (config 5)")
     ap.add_argument("--cpu-sample", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="also time FASTA read -> cluster -> files written")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the file leg (config 2, N = 1)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="configs 3/4: bins clustered concurrently per GPU (one device context per lane)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one rank per GPU, started before anything here touches a GPU; exit with the launcher's status
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        raise SystemExit(subprocess.call(cmd))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')} "
+                         "(the launcher's rank count must equal --gpus)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -305,24 +357,16 @@ def main() -> None:
             "blocks": sum(s["n_blocks"] for s in last), "block_reruns": sum(s["n_reruns"] for s in last),
             "roofline": roof, "align": align,
         }
-        if args.config in (3, 4) and world == 1:
-            # modelled multi-GPU time of the same bins: the LPT plan bench.py uses for N ranks, each rank's
-            # share weighted by the measured per-bin times of the last step (bins are independent); the
-            # 1-GPU wall scaled by the largest rank's share
+        if args.config == 2:
+            busy = pmc_busy("k_pf_count")
+            if busy:
+                roof["pmc"] = busy
+        if args.config in (3, 4):
+            # per-bin wall times of the last step, measured while `lanes` bins share the GPU (so they do not
+            # add up to the step): the largest bin bounds any split of these bins over GPUs
             per_bin = [s["t_total_s"] for s in last]
-            nb1 = runners[0].nbins
-            w = [per_bin[i] + (per_bin[nb1 + i] if len(runners) > 1 else 0.0) for i in range(nb1)]
-            costs = [shard.bin_cost(b.umis.n) for b in runners[0].binset.bins]
-            wall = t_max / args.steps
-            model = {}
-            for g in (2, 4, 8):
-                plan = shard.lpt_assign(costs, g)
-                share = max(sum(w[i] for i in p) for p in plan) / max(sum(w), 1e-12)
-                span = wall * share
-                model[str(g)] = dict(makespan_s=span, umis_per_s=tot_umis / span if span else None,
-                                     efficiency=1.0 / (g * share) if share else None)
-            out["lpt_model_from_measured_bins"] = model
             out["largest_bin_s"] = max(per_bin) if per_bin else 0.0
+            out["bins_timed"] = len(per_bin)
             out["lanes"] = args.lanes
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -334,7 +378,7 @@ def main() -> None:
             else:
                 cpu = cpu_baseline_bins(runners[0].binset.bins, args.identity, lens)
         out["cpu_baseline"] = cpu
-        if args.e2e and args.config == 2 and world == 1:
+        if not args.no_e2e and args.config == 2 and world == 1:
             out["e2e"] = e2e_leg(ctx, umis, args.identity, lens)
         print(json.dumps(out), flush=True)
     ctx.close()
@@ -344,12 +388,44 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def _tree_bytes(d: str) -> tuple[int, int]:
+    n = b = 0
+    for root, _, files in os.walk(d):
+        for f in files:
+            n += 1
+            b += os.path.getsize(os.path.join(root, f))
+    return n, b
+
+
+def write_probe(d: str, nfiles: int, nbytes: int, threads: int, fsync: bool = False) -> dict:
+    """tools/io_probe.c: nbytes into nfiles equal files (or slices of one file) from `threads` threads on the
+    filesystem of d, the shape the writers use; seconds, GB/s (and the fsync'd commit rate when asked)."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libioprobe.so"))
+    lib.io_probe.restype = ctypes.c_double
+    lib.io_probe.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    pd = os.path.join(d, "probe")
+    os.mkdir(pd)
+    fs = ctypes.c_double(0.0)
+    t = lib.io_probe(pd.encode(), max(1, nfiles), nbytes, threads, ctypes.byref(fs) if fsync else None)
+    os.rmdir(pd)
+    if t < 0:
+        raise RuntimeError("io_probe failed")
+    out = dict(files=nfiles, bytes=nbytes, threads=threads, seconds=t, gbps=nbytes / t / 1e9 if t > 0 else None)
+    if fsync:
+        out.update(fsync_s=fs.value, committed_gbps=nbytes / (t + fs.value) / 1e9)
+    return out
+
+
 def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
-    """§8d's UMIs/s: read FASTA -> cluster -> cluster<N> files + consout written (the drop-in's file
-    boundary, umiclust_run_fasta), on the same bin written with 1,500-nt `seq=` reads."""
+    """§8d's UMIs/s at the drop-in's file boundary (vsearch_umi_cluster.py:17-56: FASTA in, cluster<N> files +
+    consout out; umiclust_run_fasta) and for the fused drop-in (umiclust_run_fasta_parse:
+    clustering + parse_umi_clusters' outputs, no cluster<N> files), on the same bin written with 1,500-nt `seq=`
+    reads.  Each writer is followed by a write probe of its own file count and bytes on the same filesystem, so
+    write_frac = probe seconds / writer seconds is the writer's share of what the disk takes for that shape."""
     import shutil
     import tempfile
     from umiclust import _lib, synth
+    io_t = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
     d = tempfile.mkdtemp(prefix="umiclust_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
         fa = os.path.join(d, "region_cluster0_detected_umis.fasta")
@@ -364,9 +440,10 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
         st = ctx.run_fasta(p, fa, os.path.join(out, "cluster"), os.path.join(out, "umi_clusters_consensus.fasta"),
                            os.path.join(out, "vsearch_cluster.log"))
         t_run = time.perf_counter() - t0
+        nf, nb = _tree_bytes(out)
         shutil.rmtree(out, ignore_errors=True)
-        # the fused drop-in: clustering + parse_umi_clusters' outputs written from memory, no
-        # cluster<N> files (run_config.json:17-19 defaults: >= 4 reads, <= 60 per cluster, no strand balancing)
+        probe = write_probe(d, nf, nb, io_t)
+        # the fused drop-in (run_config.json:17-19 defaults: >= 4 reads, <= 60 per cluster, no strand balancing)
         work = os.path.join(d, "work")
         os.mkdir(work)
         pp = _lib.ParseParams(min_reads_per_cluster=4, max_reads_per_cluster=60, balance_strands=0, max_clusters=0)
@@ -374,14 +451,32 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
         st2, pr = ctx.run_fasta_parse(p, fa, None, os.path.join(work, "umi_clusters_consensus.fasta"),
                                       os.path.join(work, "vsearch_cluster.log"), pp, work)
         t_fused = time.perf_counter() - t0
-        return dict(umis_per_s=st["n_kept"] / t_run, seconds=t_run, fasta_bytes=size, n_kept=st["n_kept"],
-                    clusters=st["n_clusters"], cluster_files=st["n_clusters"], t_read_s=st.get("t_read_s"),
-                    t_cluster_s=st["t_total_s"], t_write_s=st.get("t_write_s"), fasta_write_s=t_gen,
-                    fused_parse=dict(umis_per_s=st2["n_kept"] / t_fused, seconds=t_fused, t_read_s=st2.get("t_read_s"),
-                                     t_cluster_s=st2["t_total_s"], t_write_s=st2.get("t_write_s"),
-                                     clusters_written=pr["n_written"], reads_written=pr["reads_written"]),
-                    note="page-cache-warm input; outputs on the box's local disk; fused_parse = umiclust_run_fasta_parse "
-                         "(the clustering plus parse_umi_clusters' outputs, no cluster<N> files)")
+        nf2, nb2 = _tree_bytes(os.path.join(work, "clusters_fa"))
+        smol = os.path.getsize(os.path.join(work, "smolecule_clusters.fa"))
+        _, nb_all = _tree_bytes(work)
+        shutil.rmtree(work, ignore_errors=True)
+        probe_f = write_probe(d, nf2, nb2, io_t)
+        probe_s = write_probe(d, 1, smol, io_t)
+        disk = write_probe(d, 1, 2 << 30, io_t, fsync=True)
+        fused_probe_s = probe_f["seconds"] + probe_s["seconds"]
+        return dict(
+            umis_per_s=st["n_kept"] / t_run, seconds=t_run, fasta_bytes=size, n_kept=st["n_kept"],
+            clusters=st["n_clusters"], t_read_s=st.get("t_read_s"), t_cluster_s=st["t_total_s"],
+            t_write_s=st.get("t_write_s"), files_written=nf, bytes_written=nb,
+            write_gbps=nb / st["t_write_s"] / 1e9 if st.get("t_write_s") else None,
+            probe=probe, write_frac=probe["seconds"] / st["t_write_s"] if st.get("t_write_s") else None,
+            fasta_write_s=t_gen,
+            fused_parse=dict(umis_per_s=st2["n_kept"] / t_fused, seconds=t_fused, t_read_s=st2.get("t_read_s"),
+                             t_cluster_s=st2["t_total_s"], t_write_s=st2.get("t_write_s"),
+                             clusters_written=pr["n_written"], cluster_files=nf2, cluster_file_bytes=nb2,
+                             smolecule_bytes=smol, bytes_written=nb_all,
+                             write_gbps=nb_all / st2["t_write_s"] / 1e9 if st2.get("t_write_s") else None,
+                             probe_files=probe_f, probe_smolecule=probe_s,
+                             write_frac=fused_probe_s / st2["t_write_s"] if st2.get("t_write_s") else None),
+            disk_commit=disk,
+            note="page-cache-warm input; outputs on the box's local disk ($TMPDIR); write_frac = seconds of the "
+                 "write probe (same files and bytes, same threads, no fsync, as the writers) / the writer's seconds; "
+                 "disk_commit = a 2 GiB file written and fsync'd (the rate once the page cache must drain)")
     finally:
         shutil.rmtree(d, ignore_errors=True)
 

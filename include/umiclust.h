@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 3
+#define UMICLUST_ABI_VERSION 4
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -61,6 +61,15 @@ typedef struct umiclust_params {
   int32_t fasta_width;    /* --fasta_width (80) */
   int32_t policy_boundary_open; /* E(i,0)/F(0,j) opened from the DP
                                    boundary (1, default) or -inf (0) */
+  int32_t threads;        /* --threads n (vsearch_umi_cluster.py:33-34,83-84; n >= 25 in the pipeline,
+                             utils.py:56-63).  Only read under policy_threads = 1. */
+  int32_t policy_threads; /* SURVEY Appendix C O4 [L]: 0 (default) = the sequential definition (vsearch
+                             --threads 1, cluster_core_serial); 1 = vsearch's multithreaded cluster_fast
+                             restated (cluster_core_parallel): rounds of `threads` queries, each searched
+                             against the index frozen at the round's start, then re-checked in order against
+                             the round's new centroids (inserted into its hit list by k-mer count and
+                             re-walked one alignment at a time).  umiclust_params_from_argv sets 1 when the
+                             environment has UMICLUST_O4=batched (the reference's argv stays unchanged). */
 } umiclust_params;
 
 /* presets */

@@ -330,6 +330,7 @@ struct umiclust_ctx {
   // two passes in flight (software pipeline over blocks) + round B on a side stream
   Pass pass[kPeerTiles];          // passes in flight (the pipeline depth: UMICLUST_DEPTH, <= kPeerTiles)
   Tile blk_tile[kPeerTiles + 1], solo_tile;  // per-block peer tiles (ring of depth + 1), overflow re-runs
+  Tile round_tile[2];             // O4 batched rounds: a pass's window from its first query's round start
   // passes in flight: 2 by default; 3 (window of three blocks) hides more host time but its extra peers cost
   // more than that on configs 2/3/5 (profiles/r02/pipeline_depth_sweep.json)
   int32_t depth = 2;
@@ -400,6 +401,7 @@ struct umiclust_ctx {
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
   int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
+  int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
@@ -453,6 +455,9 @@ void validate(umiclust_ctx* c, const umiclust_params& p) {
     c->fail(UMICLUST_EINVAL, "bad length window [%d,%d]", p.minseqlength, p.maxseqlength);
   if (!(p.id > 0.0 && p.id <= 1.0)) c->fail(UMICLUST_EINVAL, "--id must be in (0,1]");
   if (p.minwordmatches < 0) c->fail(UMICLUST_EINVAL, "minwordmatches < 0");
+  if (p.policy_threads != 0 && p.policy_threads != 1) c->fail(UMICLUST_EINVAL, "policy_threads must be 0 or 1");
+  if (p.policy_threads && (p.threads < 1 || p.threads > kMaxBlock))
+    c->fail(UMICLUST_EINVAL, "policy_threads = 1 needs 1 <= threads <= %d", kMaxBlock);
   int mx = std::abs(p.match) + std::abs(p.mismatch);
   for (int k = 0; k < 6; k++) mx = std::max(mx, p.gap_open[k] + p.gap_ext[k]);
   if (mx * 2 * kMaxLen > 15000) c->fail(UMICLUST_EINVAL, "scores too large for 16-bit DP");
@@ -1008,7 +1013,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // know "centroid or not" are not held up by it.
   auto cert_device = [](const HostQs& h) { return (h.flags & 1u) && (int)h.w + (int)h.nrel <= kWalk; };
   struct Scratch {
-    std::vector<std::pair<unsigned long long, int>> cp;
+    std::vector<std::pair<unsigned long long, int>> cp, cx;
     std::vector<MCand> L;
     int64_t merged = 0;
   };
@@ -1075,11 +1080,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
     const int32_t row = allow_extra ? extra_row[qs] : -1;
+    // O4 batched rounds: centroids created before q's round join its search (the merged walk); those of its
+    // own round are the extras of the re-check below.  Sequential: every centroid peer joins the walk.
+    const uint32_t rb = c->o4_T ? (uint32_t)(state.s0 + (q - state.s0) / c->o4_T * c->o4_T) : UINT32_MAX;
+    auto& cx = scr.cx;
     cp.clear();
+    cx.clear();
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
       const uint32_t ps = (uint32_t)w0 + (pw & 0xffffu);
-      if (state[ps] == ST_CENT) cp.push_back({cand_key((pw >> 16) & 0xffu, c->hlen[ps], ps), y});
+      if (state[ps] == ST_CENT) (ps < rb ? cp : cx).push_back({cand_key((pw >> 16) & 0xffu, c->hlen[ps], ps), y});
     }
     std::sort(cp.begin(), cp.end());
     L.clear();
@@ -1121,7 +1131,52 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       }
       L.push_back(m);
     }
-    if (merged_walk(c, L, c->hlen[q], o)) return 0;
+    if (merged_walk(c, L, c->hlen[q], o)) {
+      if (cx.empty()) return 0;
+      // cluster_core_parallel's re-check (policy O4): the round's new centroids over the k-mer threshold are
+      // inserted into the hit list (the walked candidates, all aligned) by (count desc, shorter first, then
+      // seqno), and the list is walked again one alignment at a time from the top until an accept or
+      // maxrejects rejects; the best hit is then the best accepted one of every aligned hit
+      std::sort(cx.begin(), cx.end());
+      int acc = 0, rej = 0;
+      size_t a = 0, b = 0;
+      const size_t w = (size_t)o.walked;
+      while (acc < c->p.maxaccepts && rej < c->p.maxrejects && (a < w || b < cx.size())) {
+        uint32_t res, t;
+        if (a < w && (b >= cx.size() || L[a].key < cx[b].first)) {
+          res = L[a].res;
+          t = L[a].seqno;
+          a++;
+        } else {
+          const int y = cx[b].second;
+          t = (uint32_t)w0 + (R.peer[y] & 0xffffu);
+          if ((R.peer[y] >> 25) & 1u) {
+            res = R.pres[y];
+          } else if (row >= 0 && extra_have[(size_t)row * kSlots + kWalk + y]) {
+            res = extra_res[(size_t)row * kSlots + kWalk + y];
+          } else {
+            cert = o.acc;  // an accepted hit of the search stays a candidate whatever the re-check finds
+            return 2;
+          }
+          b++;
+          o.walked++;
+          o.cells += (int64_t)c->hlen[q] * c->hlen[t];
+        }
+        const uint32_t m = res & 0xffu, Li = (res >> 8) & 0xffu;
+        if (c->h_acc[(size_t)Li * kTabM + m]) {
+          acc++;
+          const uint16_t rk = c->h_rank[(size_t)Li * kTabM + m];
+          if (!o.acc || rk > o.rank || (rk == o.rank && t < o.t)) {
+            o.rank = rk;
+            o.t = t;
+          }
+          o.acc = true;
+        } else {
+          rej++;
+        }
+      }
+      return 0;
+    }
     // an accept already known within the first kWalk candidates ends the walk by its batch at the latest
     for (int x = 0; x < std::min<int>((int)L.size(), kWalk) && !cert; x++)
       if (L[x].have) {
@@ -1206,6 +1261,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     uint8_t& kd = P.kind[qs];
     if (h.rec == 0xffffffffu) {
       kd = 0;
+      return;
+    }
+    if (c->o4_T) {  // O4 batched rounds: every strand with a record resolves in order (strand_outcome_s)
+      kd = 2;
       return;
     }
     int nd = 0;
@@ -1501,6 +1560,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     slot(c->delta_tile[1], kDelta);
     for (Tile& t : c->blk_tile) slot(t, kMaxBlock);
     slot(c->solo_tile, kMaxBlock);
+    if (c->o4_T)
+      for (Tile& t : c->round_tile) slot(t, c->o4_T);
     c->sealed_slot0 = off;
     off += (uint64_t)(n / kTile) * tile_cap(kTile);
     c->hip(c->arena.ensure((size_t)off + 64), "alloc arena");
@@ -1515,6 +1576,38 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
       q0 += same;
     }
   };
+  // Policy O4 batched rounds (c->o4_T queries each, counted from the bin's first sorted query): query q's search
+  // sees only the centroids before its round start rstart(q), and the centroids of its round before it are the
+  // re-check's extras -- both must be in its pass's peer window, and the index must hold nothing from the round.
+  // So a pass's window starts at min(nominal window start, round start of its first query) (a round tile over
+  // [round start, block start) replaces the nominal previous tiles when the round began earlier), and resolved
+  // centroids wait in `pending` until every later pass's window starts after them.
+  const int32_t T4 = c->o4_T;
+  auto rstart = [&](int32_t q) { return T4 ? s0 + (q - s0) / T4 * T4 : q; };
+  std::vector<int32_t> pending;
+  auto sync_index = [&](int32_t X) {  // the index gets the pending centroids before seqno X
+    size_t m = 0;
+    while (m < pending.size() && pending[m] < X) m++;
+    if (!m) return;
+    std::vector<int32_t> a(pending.begin(), pending.begin() + (ptrdiff_t)m);
+    append_centroids(c, a);
+    pending.erase(pending.begin(), pending.begin() + (ptrdiff_t)m);
+  };
+  // prevs/nprev of a pass starting at query q with the nominal window start wnom, adjusted for its round
+  auto round_window = [&](int32_t q, int32_t wnom, const Tile** prevs, int& nprev, int32_t region, int slot) {
+    const int32_t rs = rstart(q);
+    if (rs < wnom) {
+      Tile& rt = c->round_tile[slot & 1];
+      build_tile(c, rt, c->d_iota.p, rs, q - rs, 0, region * kPeerRegion, 1 << 30);
+      rt.base = rs;
+      rt.seg = region;
+      rt.len = 0;  // several lengths
+      rt.prebuilt = false;
+      prevs[0] = &rt;
+      nprev = 1;
+    }
+    sync_index(std::min(wnom, rs));
+  };
   // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
   int32_t b_eff = std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
   split_blocks(s0, b_eff);
@@ -1527,14 +1620,18 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     int32_t piece = nq;
     for (int32_t q = q0; q < q0 + nq;) {
       const int32_t m = std::min(piece, q0 + nq - q);
-      enqueue_pass(c, P, q, m, nullptr, 0, c->solo_tile, 0);
+      const Tile* prevs[kPeerTiles];
+      int nprev = 0;
+      if (T4) round_window(q, q, prevs, nprev, 1, 0);
+      enqueue_pass(c, P, q, m, prevs, nprev, c->solo_tile, 0);
       c->stats.n_reruns++;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
         piece = std::max(1, m / 2);
         continue;
       }
-      append_centroids(c, new_cents);
+      if (T4) pending.insert(pending.end(), new_cents.begin(), new_cents.end());
+      else append_centroids(c, new_cents);
       c->stats.n_blocks++;
       q += m;
     }
@@ -1545,7 +1642,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   // before j: the merged walk is exact.  Invariant at the top of iteration k: passes k .. k+D-1 (those that
   // exist) are queued, the index holds blocks < k.  Block k's peer tile lives in blk_tile[k % (D + 1)]
   // (read by passes k .. k+D-1) and counts into peer region k % D of the prefilter counters.
-  const int D = c->depth;
+  const int D = T4 ? 2 : c->depth;
   auto tile_of = [&](int32_t k) -> Tile& { return c->blk_tile[k % (D + 1)]; };
   // Lazy peers: once new centroids have become rare (the last resolved block created fewer than
   // lazy_permille per mille), in-window peers are not aligned speculatively; a query whose relevant peer
@@ -1555,12 +1652,14 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   auto enqueue = [&](int32_t k, int nprev) {
     const Tile* prevs[kPeerTiles];
     for (int i = 0; i < nprev; i++) prevs[i] = &tile_of(k - nprev + i);
+    if (T4) round_window(blocks[k].first, nprev ? blocks[k - nprev].first : blocks[k].first, prevs, nprev,
+                         (k + D - 1) % D, k);
     enqueue_pass(c, c->pass[k % D], blocks[k].first, blocks[k].second, prevs, nprev, tile_of(k), k % D, lazy);
   };
   // split passes shorten the host <-> device cycle of one bin at the price of a wider counting window;
   // multi-bin sets run several lanes on one GPU, which is throughput-bound: there the whole passes win
   // (configs 2 / 5: +12 % / +2 %, config 3: -6 %; profiles/r02/split_ab.json)
-  const bool split = c->split_env >= 0 ? c->split_env != 0 : !multi_bin;
+  const bool split = !T4 && (c->split_env >= 0 ? c->split_env != 0 : !multi_bin);
   c->ix_st = (split && D == 2 && c->ix_side) ? c->st_b : nullptr;
   c->last_r_ev = nullptr;
   if (split && D == 2) {
@@ -1683,7 +1782,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
         if (k + i < nb) enqueue(k + i, i - 1);
       continue;
     }
-    append_centroids(c, new_cents);
+    if (T4) pending.insert(pending.end(), new_cents.begin(), new_cents.end());
+    else append_centroids(c, new_cents);
     c->stats.n_blocks++;
     lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
@@ -1691,6 +1791,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   }
   }
   c->b_hint = b_eff;
+  // centroids still pending (O4): creation numbers only, no index is needed any more
+  c->cent.insert(c->cent.end(), pending.begin(), pending.end());
   if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
   c->hip(hipStreamSynchronize(c->st_b), "sync");
   c->ix_st = nullptr;
@@ -1856,6 +1958,7 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
   c->p = *p;
   c->sc = to_scoring(*p);
   c->both = p->strand_both ? 2 : 1;
+  c->o4_T = (p->policy_threads && p->threads > 1) ? p->threads : 0;
   build_tables(c);
   c->n_input = n;
   c->bin_in.assign((size_t)nbins + 1, 0);
@@ -2590,6 +2693,8 @@ int32_t umiclust_params_init(umiclust_params* p, int32_t preset, double identity
   p->clusterout_id = 1;
   p->fasta_width = 80;
   p->policy_boundary_open = 1;
+  p->threads = 1;
+  p->policy_threads = 0;
   for (int k = 0; k < 6; k++) p->gap_ext[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 2 : 1;
   if (preset == UMICLUST_PRESET_ROUND1) {
     p->match = 10;
@@ -2639,7 +2744,11 @@ int32_t umiclust_params_from_argv(umiclust_params* p, int32_t argc, const char* 
     else if (!strcmp(a, "--cluster_fast")) { const char* v = val(); if (!v || !put(in_fasta, v)) return UMICLUST_EINVAL; have_in = true; }
     else if (!strcmp(a, "--minseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->minseqlength = atoi(v); }
     else if (!strcmp(a, "--maxseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxseqlength = atoi(v); }
-    else if (!strcmp(a, "--threads")) { if (!val()) return UMICLUST_EINVAL; }
+    else if (!strcmp(a, "--threads")) {
+      const char* v = val();
+      if (!v) return UMICLUST_EINVAL;
+      p->threads = std::max(1, atoi(v));
+    }
     else if (!strcmp(a, "--strand")) {
       const char* v = val();
       if (!v) return UMICLUST_EINVAL;
@@ -2672,6 +2781,12 @@ int32_t umiclust_params_from_argv(umiclust_params* p, int32_t argc, const char* 
     else return UMICLUST_EINVAL;
   }
   if (!have_in) return UMICLUST_EINVAL;
+  // O4: the reference's argv is kept as is; the batched restatement of vsearch's multithreaded clustering is
+  // chosen from the environment (UMICLUST_O4=batched), the sequential definition otherwise
+  if (const char* e = getenv("UMICLUST_O4")) {
+    if (!strcmp(e, "batched")) p->policy_threads = 1;
+    else if (strcmp(e, "sequential") != 0) return UMICLUST_EINVAL;
+  }
   return UMICLUST_OK;
 }
 

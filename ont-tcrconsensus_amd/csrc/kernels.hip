@@ -852,7 +852,8 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
             mk &= mk - 1u;
             const uint32_t cv = (w >> (8 * byte)) & 0xffu;
             const int32_t sq = pv.base + ((4 * x + (int)byte) << kPartShift) + part;
-            const uint32_t key = ((127u - cv) << 23) | ((uint32_t)pv.len << 16) | (uint32_t)(sq - a.peer_base);
+            // the peer's own length (an O4 round tile spans several lengths; k_pf_merge keys peers the same way)
+            const uint32_t key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[sq] << 16) | (uint32_t)(sq - a.peer_base);
             if (slot <= (uint32_t)kPeerCap) S.pcand[slot] = key;
             slot++;
           }

@@ -38,6 +38,8 @@ class OrcParams(C.Structure):
         ("clusterout_id", C.c_int32),
         ("fasta_width", C.c_int32),
         ("policy_boundary_open", C.c_int32),
+        ("threads", C.c_int32),
+        ("policy_threads", C.c_int32),
     ]
 
 

@@ -80,6 +80,8 @@ void orc_params_preset(orc_params *p, int preset, double id, int minlen, int max
   p->clusterout_id = 1;
   p->fasta_width = 80;
   p->policy_boundary_open = 1;
+  p->threads = 1;
+  p->policy_threads = 0;
   for (int k = 0; k < 6; k++) p->gap_ext[k] = (k == ORC_QI || k == ORC_TI) ? 2 : 1; /* 2I/1E */
   if (preset == 1) {
     /* --gapopen 0E/40I --mismatch -40 --match 10 (vsearch_umi_cluster.py:44-50) */
@@ -365,6 +367,8 @@ typedef struct {
   int accepted;
   double id;
   char *cigar;
+  int32_t count;   /* shared unique k-mers */
+  int aligned;     /* O4 recheck: hits inserted from the round's new centroids start unaligned */
 } hit_t;
 
 typedef struct {
@@ -398,6 +402,25 @@ static void index_add(ctx_t *c, int32_t seqno, const orc_params *p, uint32_t *kb
   }
 }
 
+/* align one hit (search16 semantics) and apply search_acceptable_aligned; returns accepted */
+static int align_hit(ctx_t *c, const orc_params *p, const char *qs, int ql, hit_t *h) {
+  int32_t ts = h->target;
+  aln_result r;
+  char *cg = (char *)malloc((size_t)(2 * (ql + c->len[ts]) + 2));
+  align_core(p, qs, ql, c->seq[ts], c->len[ts], &r, cg);
+  c->alignments++;
+  c->cells += (int64_t)ql * c->len[ts];
+  h->id = r.id2;
+  free(h->cigar);
+  h->cigar = cg;
+  h->aligned = 1;
+  /* search_acceptable_aligned: defaults leave only the id / weak-id tests */
+  int mm = r.matches + r.mismatches;
+  int ok = (r.id2 >= 100.0 * p->weak_id) && mm > 0 && (100.0 * r.matches / mm >= 0.0);
+  h->accepted = ok && r.id2 >= 100.0 * p->id;
+  return h->accepted;
+}
+
 /* search_onequery (searchcore.cc) for one strand: top scores + batched-8 alignment. */
 static int search_strand(ctx_t *c, const orc_params *p, const char *qs, int ql, int strand,
                          uint32_t *kbuf, int32_t *counts, hit_t *hits) {
@@ -428,8 +451,10 @@ static int search_strand(ctx_t *c, const orc_params *p, const char *qs, int ql, 
   for (;;) {
     while (finalized + delayed < p->maxaccepts + p->maxrejects - 1 && rejects < p->maxrejects &&
            accepts < p->maxaccepts && pos < nc) {
-      hits[hit_count].target = cand[pos++].seqno;
+      hits[hit_count].target = cand[pos].seqno;
+      hits[hit_count].count = cand[pos++].count;
       hits[hit_count].accepted = 0;
+      hits[hit_count].aligned = 1;  /* align_delayed aligns every popped candidate */
       hits[hit_count].cigar = NULL;
       hit_count++;
       delayed++;
@@ -438,25 +463,8 @@ static int search_strand(ctx_t *c, const orc_params *p, const char *qs, int ql, 
     if (delayed == 0) break;
     /* align_delayed */
     for (int x = finalized; x < hit_count; x++) {
-      hit_t *h = &hits[x];
-      int32_t ts = h->target;
-      aln_result r;
-      char *cg = (char *)malloc((size_t)(2 * (ql + c->len[ts]) + 2));
-      align_core(p, qs, ql, c->seq[ts], c->len[ts], &r, cg);
-      c->alignments++;
-      c->cells += (int64_t)ql * c->len[ts];
-      h->id = r.id2;
-      h->cigar = cg;
-      /* search_acceptable_aligned: defaults leave only the id / weak-id tests */
-      int mm = r.matches + r.mismatches;
-      int ok = (r.id2 >= 100.0 * p->weak_id) && mm > 0 &&
-               (100.0 * r.matches / mm >= 0.0);
-      if (ok && r.id2 >= 100.0 * p->id) {
-        h->accepted = 1;
-        accepts++;
-      } else {
-        rejects++;
-      }
+      if (align_hit(c, p, qs, ql, &hits[x])) accepts++;
+      else rejects++;
       finalized++;
     }
     delayed = 0;
@@ -625,41 +633,131 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
   hit_t *hm = (hit_t *)malloc(sizeof(hit_t) * (size_t)tophits);
   char *rcq = (char *)malloc((size_t)maxl + 2);
   int32_t clusters = 0;
-  /* cluster_core_serial (cluster.cc) */
-  for (int32_t s = 0; s < nk; s++) {
-    int np = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, hp);
-    int nm = 0;
-    if (p->strand_both) {
-      revcomp(rcq, c.seq[s], c.len[s]);
-      nm = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, hm);
-    }
-    /* search_findbest2_byid: accepted hit with max id; tie -> lower target; plus first */
-    hit_t *best = NULL;
-    int best_strand = 0;
-    for (int x = 0; x < np; x++)
-      if (hp[x].accepted && (!best || hp[x].id > best->id ||
-                             (hp[x].id == best->id && hp[x].target < best->target))) {
-        best = &hp[x];
-        best_strand = 0;
+  /* assign s from its hits: search_findbest2_byid (accepted hit with max id; tie -> lower target; plus
+   * first), then a member of that centroid's cluster or a new centroid */
+  #define ASSIGN(s, hp, np, hm, nm) do {                                                            \
+    hit_t *best_ = NULL;                                                                            \
+    int bs_ = 0;                                                                                    \
+    for (int x = 0; x < (np); x++)                                                                  \
+      if ((hp)[x].accepted && (!best_ || (hp)[x].id > best_->id ||                                  \
+                               ((hp)[x].id == best_->id && (hp)[x].target < best_->target))) {      \
+        best_ = &(hp)[x];                                                                           \
+        bs_ = 0;                                                                                    \
+      }                                                                                             \
+    for (int x = 0; x < (nm); x++)                                                                  \
+      if ((hm)[x].accepted && (!best_ || (hm)[x].id > best_->id ||                                  \
+                               ((hm)[x].id == best_->id && (hm)[x].target < best_->target))) {      \
+        best_ = &(hm)[x];                                                                           \
+        bs_ = 1;                                                                                    \
+      }                                                                                             \
+    if (best_) {                                                                                    \
+      c.clusterno[s] = c.clusterno[best_->target];                                                  \
+      c.strand[s] = (uint8_t)bs_;                                                                   \
+      c.cigar[s] = best_->cigar;                                                                    \
+      best_->cigar = NULL;                                                                          \
+    } else {                                                                                        \
+      c.clusterno[s] = clusters++;                                                                  \
+      index_add(&c, s, p, kbuf);                                                                    \
+    }                                                                                               \
+    for (int x = 0; x < (np); x++) free((hp)[x].cigar);                                             \
+    for (int x = 0; x < (nm); x++) free((hm)[x].cigar);                                             \
+  } while (0)
+  const int32_t T = (p->policy_threads && p->threads > 1) ? p->threads : 1;
+  if (T == 1) {
+    /* cluster_core_serial (cluster.cc) */
+    for (int32_t s = 0; s < nk; s++) {
+      int np = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, hp);
+      int nm = 0;
+      if (p->strand_both) {
+        revcomp(rcq, c.seq[s], c.len[s]);
+        nm = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, hm);
       }
-    for (int x = 0; x < nm; x++)
-      if (hm[x].accepted && (!best || hm[x].id > best->id ||
-                             (hm[x].id == best->id && hm[x].target < best->target))) {
-        best = &hm[x];
-        best_strand = 1;
-      }
-    if (best) {
-      c.clusterno[s] = c.clusterno[best->target];
-      c.strand[s] = (uint8_t)best_strand;
-      c.cigar[s] = best->cigar;
-      best->cigar = NULL;
-    } else {
-      c.clusterno[s] = clusters++;
-      index_add(&c, s, p, kbuf);
+      ASSIGN(s, hp, np, hm, nm);
     }
-    for (int x = 0; x < np; x++) free(hp[x].cigar);
-    for (int x = 0; x < nm; x++) free(hm[x].cigar);
+  } else {
+    /* cluster_core_parallel (cluster.cc), policy O4 [L]: rounds of T queries.  The round's searches run
+     * against the index as it stood at the round's start (the worker threads), then the results are
+     * analysed in order: a query whose k-mers reach minwordmatches (or all of its own) against a centroid
+     * created earlier in the round gets that centroid inserted into its hit list by (count desc, shorter
+     * target first; after equal ones), and the list is walked again from the top one alignment at a time
+     * (accepts/rejects recounted; hits already aligned keep their results, new ones are aligned) until an
+     * accept, maxrejects rejects or its end; the best hit is then chosen over every aligned hit. */
+    const int cap = tophits + T;
+    hit_t *bh = (hit_t *)calloc((size_t)T * 2 * (size_t)cap, sizeof(hit_t));
+    int *bn = (int *)calloc((size_t)T * 2, sizeof(int));
+    int32_t *extra = (int32_t *)malloc(sizeof(int32_t) * (size_t)T);
+    uint32_t *ekm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(maxl + 8));
+    uint64_t *qset = (uint64_t *)calloc(((size_t)1 << (2 * p->wordlength)) / 64 + 1, 8);
+    for (int32_t b0 = 0; b0 < nk; b0 += T) {
+      const int32_t nb = (nk - b0 < T) ? nk - b0 : T;
+      for (int32_t i = 0; i < nb; i++) {
+        const int32_t s = b0 + i;
+        bn[2 * i] = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, bh + (size_t)(2 * i) * cap);
+        bn[2 * i + 1] = 0;
+        if (p->strand_both) {
+          revcomp(rcq, c.seq[s], c.len[s]);
+          bn[2 * i + 1] = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, bh + (size_t)(2 * i + 1) * cap);
+        }
+      }
+      int nextra = 0;
+      for (int32_t i = 0; i < nb; i++) {
+        const int32_t s = b0 + i;
+        for (int st = 0; st < (p->strand_both ? 2 : 1) && nextra > 0; st++) {
+          hit_t *h = bh + (size_t)(2 * i + st) * cap;
+          int *nh = &bn[2 * i + st];
+          const char *qs = c.seq[s];
+          if (st) {
+            revcomp(rcq, c.seq[s], c.len[s]);
+            qs = rcq;
+          }
+          const int nq = orc_unique_kmers(qs, c.len[s], p->wordlength, p->qmask_dust, kbuf);
+          for (int k = 0; k < nq; k++) qset[kbuf[k] >> 6] |= 1ULL << (kbuf[k] & 63);
+          const int minmatches = p->minwordmatches < nq ? p->minwordmatches : nq;
+          int added = 0;
+          for (int j = 0; j < nextra; j++) {
+            const int32_t e = extra[j];
+            const int ne = orc_unique_kmers(c.seq[e], c.len[e], p->wordlength, p->qmask_dust, ekm);
+            int shared = 0;
+            for (int k = 0; k < ne; k++) shared += (int)((qset[ekm[k] >> 6] >> (ekm[k] & 63)) & 1ULL);
+            if (shared < minmatches) continue;
+            int x = *nh;
+            while (x > 0 && (h[x - 1].count < shared ||
+                             (h[x - 1].count == shared && c.len[h[x - 1].target] > c.len[e]))) {
+              h[x] = h[x - 1];
+              x--;
+            }
+            h[x].target = e;
+            h[x].count = shared;
+            h[x].accepted = 0;
+            h[x].aligned = 0;
+            h[x].id = 0.0;
+            h[x].cigar = NULL;
+            (*nh)++;
+            added++;
+          }
+          for (int k = 0; k < nq; k++) qset[kbuf[k] >> 6] = 0;
+          if (added) {
+            int accepts = 0, rejects = 0;
+            for (int t = 0; accepts < p->maxaccepts && rejects < p->maxrejects && t < *nh; t++) {
+              if (!h[t].aligned) align_hit(&c, p, qs, c.len[s], &h[t]);
+              if (h[t].accepted) accepts++;
+              else rejects++;
+            }
+          }
+        }
+        hit_t *hpi = bh + (size_t)(2 * i) * cap, *hmi = bh + (size_t)(2 * i + 1) * cap;
+        const int32_t before = clusters;
+        ASSIGN(s, hpi, bn[2 * i], hmi, bn[2 * i + 1]);
+        if (clusters > before) extra[nextra++] = s;
+      }
+    }
+    free(qset);
+    free(ekm);
+    free(extra);
+    free(bn);
+    free(bh);
   }
+  #undef ASSIGN
   /* cluster sizes and output numbering (--clusterout_sort: size desc, creation order) */
   csz_t *cs = (csz_t *)calloc((size_t)clusters + 1, sizeof(csz_t));
   for (int32_t k = 0; k < clusters; k++) cs[k].cno = k;

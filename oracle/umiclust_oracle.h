@@ -47,6 +47,12 @@ typedef struct orc_params {
   int32_t clusterout_id;
   int32_t fasta_width;   /* 80 */
   int32_t policy_boundary_open; /* O3b: E(i,0)/F(0,j) opened from the boundary H (1) or -inf (0) */
+  int32_t threads;       /* --threads (vsearch_umi_cluster.py:33-34; >= 25 in the pipeline, utils.py:56-63) */
+  int32_t policy_threads;/* O4 [L]: 0 = the sequential definition (cluster_core_serial, --threads 1);
+                            1 = cluster_core_parallel restated: rounds of `threads` queries searched
+                            against the index frozen at the round's start, then, in order, each query
+                            re-checked against the round's new centroids (inserted into its hit list by
+                            k-mer count and re-walked one alignment at a time) */
 } orc_params;
 
 /* presets: 1 = round 1 (vsearch_umi_cluster.py:44-50: --gapopen 0E/40I --mismatch -40

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(lib, name), name
-    assert _lib.lib().umiclust_abi_version() == 3
+    assert _lib.lib().umiclust_abi_version() == 4
 
 
 def test_argv_matches_reference():
@@ -48,13 +48,34 @@ def test_params_from_round2_argv():
     assert paths["log"] == "/tmp/out2/vsearch_cluster_consensus.log"
 
 
-def test_presets_equal_argv_decoding():
+def test_presets_equal_argv_decoding(monkeypatch):
+    monkeypatch.delenv("UMICLUST_O4", raising=False)
     a, _ = _lib.params_from_argv(ARGV["calls"][0]["argv"])
     b = _lib.params(_lib.PRESET_ROUND1, 0.93, 58, 68)
+    b.threads = 25  # the captured argv's --threads 25 (informational under the default O4 policy)
     assert bytes(a) == bytes(b)
     a, _ = _lib.params_from_argv(ARGV["calls"][1]["argv"])
     b = _lib.params(_lib.PRESET_VSEARCH_DEFAULT, 0.97, 58, 68)
+    b.threads = 25
     assert bytes(a) == bytes(b)
+
+
+@pytest.mark.parametrize("env,policy", [(None, 0), ("sequential", 0), ("batched", 1)])
+def test_o4_policy_from_environment(monkeypatch, env, policy):
+    """the reference's argv (--threads 25) is kept as is; UMICLUST_O4 chooses between
+    the sequential definition (default) and the batched restatement of vsearch's multithreaded clustering."""
+    if env is None:
+        monkeypatch.delenv("UMICLUST_O4", raising=False)
+    else:
+        monkeypatch.setenv("UMICLUST_O4", env)
+    p, _ = _lib.params_from_argv(ARGV["calls"][0]["argv"])
+    assert (p.threads, p.policy_threads) == (25, policy)
+
+
+def test_o4_policy_bad_environment(monkeypatch):
+    monkeypatch.setenv("UMICLUST_O4", "sometimes")
+    with pytest.raises(_lib.UmiclustError):
+        _lib.params_from_argv(ARGV["calls"][0]["argv"])
 
 
 @pytest.mark.parametrize("bad", [["vsearch", "--cluster_fast"], ["vsearch", "--bogus", "--cluster_fast", "a"],

@@ -162,3 +162,54 @@ def test_cluster_invariants():
         # greedy on length-sorted input: the centroid is the longest, earliest record
         assert lens[cen[0]] == max(lens[i] for i in mem)
     assert all(cl[i] == -1 for i in range(len(seqs)) if not 58 <= lens[i] <= 68)
+
+
+# ---- vsearch --threads n (cluster_core_parallel) vs the sequential definition ----
+def _partition(r):
+    groups = {}
+    for i, c in enumerate(r["cluster"]):
+        groups.setdefault(int(c), []).append(i)
+    return {tuple(v) for v in groups.values()}
+
+
+def _o4(preset, idn, threads, lens=(58, 68)):
+    p = orc.params(preset, idn, *lens)
+    p.threads, p.policy_threads = threads, 1
+    return p
+
+
+def test_o4_round_of_one_is_sequential():
+    """policy_threads = 1 with rounds of one query is the sequential definition, alignment for alignment."""
+    seqs = synth.make_umis(200, seed=41, max_reads=3000, orient_mix=0.2).as_list()
+    a = orc.cluster(orc.params(1, 0.93), seqs)
+    b = orc.cluster(_o4(1, 0.93, 1), seqs)
+    assert _partition(a) == _partition(b) and a["consensus"] == b["consensus"]
+    assert a["stats"]["alignments"] == b["stats"]["alignments"] and a["stats"]["cells"] == b["stats"]["cells"]
+
+
+def test_o4_threads25_on_config1_inputs():
+    """Where --threads 25 and --threads 1 differ on config-1 inputs (the first 30k reads of the config-1 bin,
+    seed 1001, --id 0.93, round-1 scoring): the round's searches miss the round's new centroids, so the re-check
+    aligns them one at a time instead of in batches of 8 -- fewer alignments -- but every cluster, strand,
+    centroid and consensus is the same.  (Over the whole 100k-read bin: 664,470 vs 664,448 alignments, identical
+    clusters)"""
+    seqs = synth.config_umis(1).as_list()[:30000]
+    a = orc.cluster(orc.params(1, 0.93), seqs)
+    b = orc.cluster(_o4(1, 0.93, 25), seqs)
+    assert _partition(a) == _partition(b)
+    assert (a["cluster"] == b["cluster"]).all() and (a["strand"] == b["strand"]).all()
+    assert a["consensus"] == b["consensus"]
+    assert b["stats"]["alignments"] < a["stats"]["alignments"]
+
+
+def test_o4_threads25_changes_membership_at_high_error():
+    """At 4 % per-base error the same --threads 25 moves a few reads between clusters: the round's searches do
+    not see the round's new centroids, and the re-check walks them one alignment at a time, so a query can end up
+    with a different best hit than the sequential walk gives it."""
+    seqs = synth.make_umis(1000, seed=7, max_reads=20000, error_rate=0.04).as_list()
+    a = orc.cluster(orc.params(1, 0.93), seqs)
+    b = orc.cluster(_o4(1, 0.93, 25), seqs)
+    assert a["n_clusters"] == b["n_clusters"]
+    moved = _partition(a) - _partition(b)
+    assert len(moved) > 0
+    assert sum(len(g) for g in moved) < len(seqs) // 100  # a handful of reads

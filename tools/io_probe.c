@@ -1,0 +1,141 @@
+/*
+ * io_probe.c -- filesystem write-bandwidth probe for bench.py's e2e leg (measurement only; not product code).
+ *
+ * Writes `total` bytes into `nfiles` files (probe<i>, equal sizes, one open/write/close each) under `dir`
+ * from `threads` threads -- the same shape as the drop-in's writers (one file per cluster, written on the
+ * I/O threads) -- and returns the seconds taken.  With nfiles == 1 the threads pwrite disjoint slices of
+ * one file (the shape of consout / smolecule_clusters.fa).  If `fsync_s` is not NULL every file is then
+ * fsync'd and the extra seconds reported there (the disk-commit cost the writers never pay: they close
+ * without fsync, as vsearch and Python's file objects do).  Files are removed afterwards (not timed).
+ *
+ * Built by __graft_entry__.build() into tools/libioprobe.so; loaded by bench.py with ctypes.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+typedef struct {
+  const char *dir;
+  int64_t nfiles, total;
+  int threads, t;
+  const char *buf;
+  int64_t bufsz;
+  int err;
+} job_t;
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int write_all(int fd, const char *p, int64_t n, int64_t off, int positional) {
+  while (n > 0) {
+    ssize_t w = positional ? pwrite(fd, p, (size_t)n, off) : write(fd, p, (size_t)n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    p += w;
+    n -= w;
+    off += w;
+  }
+  return 0;
+}
+
+static void *files_worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  char path[4096];
+  const int64_t per = j->total / j->nfiles;
+  for (int64_t i = j->t; i < j->nfiles; i += j->threads) {
+    snprintf(path, sizeof path, "%s/probe%lld", j->dir, (long long)i);
+    int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (fd < 0) { j->err = errno; return NULL; }
+    int64_t left = per + (i == j->nfiles - 1 ? j->total - per * j->nfiles : 0);
+    while (left > 0 && !j->err) {
+      int64_t n = left < j->bufsz ? left : j->bufsz;
+      if (write_all(fd, j->buf, n, 0, 0)) j->err = errno;
+      left -= n;
+    }
+    if (close(fd)) j->err = errno;
+  }
+  return NULL;
+}
+
+static void *slice_worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  char path[4096];
+  snprintf(path, sizeof path, "%s/probe0", j->dir);
+  int fd = open(path, O_WRONLY);
+  if (fd < 0) { j->err = errno; return NULL; }
+  int64_t a = j->total * j->t / j->threads, b = j->total * (j->t + 1) / j->threads;
+  while (a < b && !j->err) {
+    int64_t n = b - a < j->bufsz ? b - a : j->bufsz;
+    if (write_all(fd, j->buf, n, a, 1)) j->err = errno;
+    a += n;
+  }
+  close(fd);
+  return NULL;
+}
+
+double io_probe(const char *dir, int64_t nfiles, int64_t total, int threads, double *fsync_s) {
+  if (!dir || nfiles < 1 || total < 0 || threads < 1) return -1.0;
+  const int64_t bufsz = 1 << 20;
+  char *buf = (char *)malloc((size_t)bufsz);
+  if (!buf) return -1.0;
+  for (int64_t i = 0; i < bufsz; i++) buf[i] = "ACGT\n"[i % 5];
+  char path[4096];
+  if (nfiles == 1) {  /* one file, pre-sized, threads writing disjoint slices */
+    snprintf(path, sizeof path, "%s/probe0", dir);
+    int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (fd < 0) { free(buf); return -1.0; }
+    close(fd);
+  }
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  job_t *jobs = (job_t *)calloc((size_t)threads, sizeof(job_t));
+  const double t0 = now_s();
+  if (nfiles == 1) {
+    int fd = open(path, O_WRONLY);
+    if (fd >= 0) {
+      if (ftruncate(fd, total)) jobs[0].err = errno;
+      close(fd);
+    }
+  }
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (job_t){dir, nfiles, total, threads, t, buf, bufsz, 0};
+    pthread_create(&th[t], NULL, nfiles == 1 ? slice_worker : files_worker, &jobs[t]);
+  }
+  int err = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].err) err = jobs[t].err;
+  }
+  const double dt = now_s() - t0;
+  if (fsync_s) {
+    const double t1 = now_s();
+    for (int64_t i = 0; i < nfiles; i++) {
+      snprintf(path, sizeof path, "%s/probe%lld", dir, (long long)i);
+      int fd = open(path, O_WRONLY);
+      if (fd >= 0) {
+        if (fsync(fd)) err = errno;
+        close(fd);
+      }
+    }
+    *fsync_s = now_s() - t1;
+  }
+  for (int64_t i = 0; i < nfiles; i++) {
+    snprintf(path, sizeof path, "%s/probe%lld", dir, (long long)i);
+    unlink(path);
+  }
+  free(jobs);
+  free(th);
+  free(buf);
+  return err ? -1.0 : dt;
+}
