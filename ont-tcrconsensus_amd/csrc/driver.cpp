@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -49,9 +50,16 @@
 #include <zlib.h>
 
 #include "../../include/umiclust.h"
+#include "host_io.h"
 #include "umiclust_internal.h"
 
 using namespace uc;
+using uc::io::Fasta;
+using uc::io::io_threads;
+using uc::io::parallel_for;
+using uc::io::pjoin;
+using uc::io::Sv;
+using uc::io::split1;
 
 namespace {
 
@@ -267,6 +275,8 @@ class WorkPool {
 
 }  // namespace
 
+static std::atomic<int> g_live_ctx{0};  // contexts alive in this process (L3Pin)
+
 struct umiclust_ctx {
   int dev = 0;
   hipStream_t st = nullptr;
@@ -339,7 +349,9 @@ struct umiclust_ctx {
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
   int32_t split_env = -1;
   bool pin = true;                 // UMICLUST_PIN=0: host resolve threads not kept in the caller's L3 domain (L3Pin;
-                                   // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json)
+                                   // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json);
+                                   // off by default when LOCAL_WORLD_SIZE > 1
+  bool pin_forced = false;         // UMICLUST_PIN=1: pinned even beside other contexts / ranks
   bool pre_resolve = true;          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
                                    // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
@@ -434,6 +446,53 @@ struct umiclust_ctx {
 };
 
 namespace {
+
+// Keep the host resolve -- the calling thread and the resolve pool -- inside the L3 domain the caller runs on,
+// for the duration of one call; the caller's and the pool's affinity are restored afterwards.  Only while this
+// is the process's one live context and the process is its node's only rank (LOCAL_WORLD_SIZE <= 1): several
+// contexts (bin-set lanes) or ranks pinned by where their callers happen to run could all land on one CCD.
+// UMICLUST_PIN=0 turns it off, UMICLUST_PIN=1 forces it on.
+struct L3Pin {
+  cpu_set_t saved;
+  bool on = false;
+  umiclust_ctx* c = nullptr;
+  explicit L3Pin(umiclust_ctx* ctx) : c(ctx) {
+    if (!c->pin || (g_live_ctx.load() > 1 && !c->pin_forced) || sched_getaffinity(0, sizeof saved, &saved) != 0)
+      return;
+    // the pool is created with the caller's own mask before the caller is narrowed, so restoring `saved` on
+    // both undoes the call's pinning completely
+    if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
+    const int cpu = sched_getcpu();
+    char path[96], buf[256];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+    FILE* f = cpu >= 0 ? fopen(path, "r") : nullptr;
+    if (!f) return;
+    const bool got = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!got) return;
+    cpu_set_t want;
+    CPU_ZERO(&want);
+    for (char* p = buf; *p;) {  // "a-b,c,d-e"
+      char* e;
+      const long a = strtol(p, &e, 10);
+      if (e == p) break;
+      long b = a;
+      if (*e == '-') b = strtol(e + 1, &e, 10);
+      for (long x = a; x <= b && x < CPU_SETSIZE; x++)
+        if (CPU_ISSET((int)x, &saved)) CPU_SET((int)x, &want);
+      p = *e == ',' ? e + 1 : e;
+      if (*p == '\n') break;
+    }
+    if (CPU_COUNT(&want) == 0 || sched_setaffinity(0, sizeof want, &want) != 0) return;
+    c->pool->set_affinity(want);
+    on = true;
+  }
+  ~L3Pin() {
+    if (!on) return;
+    sched_setaffinity(0, sizeof saved, &saved);
+    c->pool->set_affinity(saved);
+  }
+};
 
 Scoring to_scoring(const umiclust_params& p) {
   Scoring s{};
@@ -2058,470 +2117,13 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
   c->clustered = false;
 }
 
-// ---------------------------------------------------------------- FASTA I/O
-// Host threads for file I/O (the box gives a GPU process ~16 cores; UMICLUST_IO_THREADS overrides).
-int io_threads() {
-  static const int n = [] {
-    const char* e = getenv("UMICLUST_IO_THREADS");
-    int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(v > 0 ? v : 1, 16));
-  }();
-  return n;
-}
-
-// run f(t) for t in [0, T) on T threads (the caller's thread runs t = 0)
-template <typename F>
-void parallel_for(int T, F&& f) {
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
-  f(0);
-  for (auto& x : th) x.join();
-}
-
-// The input FASTA, memory-mapped; records are parsed by io_threads() threads, each taking the records
-// that start in its slice of the file.
-struct Fasta {
-  const char* data = nullptr;     // file contents (mapping)
-  size_t size = 0;
-  void* map = nullptr;
-  std::vector<int64_t> hdr_off;   // label start (after '>')
-  std::vector<int32_t> hdr_len;   // label length (truncated at whitespace)
-  std::vector<char> seq;          // concatenated sequences
-  std::vector<int64_t> seq_off;   // n+1
-  Fasta() = default;
-  Fasta(const Fasta&) = delete;
-  Fasta& operator=(const Fasta&) = delete;
-  ~Fasta() {
-    if (map) munmap(map, size);
-  }
-};
-
-struct FastaPart {
-  std::vector<int64_t> hdr_off;
-  std::vector<int32_t> hdr_len;
-  std::vector<char> seq;
-  std::vector<int64_t> seq_off;
-};
-
-// records starting in [a, b) (a is a record start or 0): headers are truncated at the first whitespace
-// (vsearch without --notrunclabels); sequence lines keep letters only; lines before the first '>' are
-// ignored
-void parse_fasta_range(const char* d, size_t a, size_t b, FastaPart& P) {
-  size_t i = a;
-  bool in = false;
-  P.seq_off.push_back(0);
-  while (i < b) {
-    const char* nl = (const char*)memchr(d + i, '\n', b - i);
-    const size_t e = nl ? (size_t)(nl - d) : b;
-    if (d[i] == '>') {
-      if (in) P.seq_off.push_back((int64_t)P.seq.size());
-      const size_t j = i + 1;
-      size_t k = j;
-      while (k < e && d[k] != '\r' && d[k] != ' ' && d[k] != '\t') k++;
-      P.hdr_off.push_back((int64_t)j);
-      P.hdr_len.push_back((int32_t)(k - j));
-      in = true;
-    } else if (in) {
-      for (size_t k = i; k < e; k++) {
-        const char ch = d[k];
-        if ((ch >= 'A' && ch <= 'Z') || (ch >= 'a' && ch <= 'z')) P.seq.push_back(ch);
-      }
-    }
-    i = e + 1;
-  }
-  if (in) P.seq_off.push_back((int64_t)P.seq.size());
-}
-
-bool read_fasta(const char* path, Fasta& f) {
-  int fd = open(path, O_RDONLY);
-  if (fd < 0) return false;
-  struct stat sb;
-  if (fstat(fd, &sb) != 0) {
-    close(fd);
-    return false;
-  }
-  f.size = (size_t)sb.st_size;
-  if (f.size > 0) {
-    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-    if (f.map == MAP_FAILED) {
-      f.map = nullptr;
-      close(fd);
-      return false;
-    }
-    f.data = (const char*)f.map;
-  }
-  close(fd);
-  const char* d = f.data;
-  const size_t N = f.size;
-  const int T = N < (1u << 20) ? 1 : io_threads();
-  // slice starts: the first record start at or after t*N/T
-  std::vector<size_t> cut(T + 1, N);
-  cut[0] = 0;
-  for (int t = 1; t < T; t++) {
-    size_t p = std::max(cut[t - 1], N / T * t);
-    while (p < N && !(d[p] == '>' && d[p - 1] == '\n')) {
-      const char* q = (const char*)memchr(d + p, '>', N - p);
-      if (!q) { p = N; break; }
-      p = (size_t)(q - d);
-      if (d[p - 1] != '\n') p++;
-    }
-    cut[t] = p;
-  }
-  std::vector<FastaPart> parts(T);
-  parallel_for(T, [&](int t) { parse_fasta_range(d, cut[t], cut[t + 1], parts[t]); });
-  size_t nrec = 0, nseq = 0;
-  for (auto& P : parts) {
-    nrec += P.hdr_off.size();
-    nseq += P.seq.size();
-  }
-  f.hdr_off.reserve(nrec);
-  f.hdr_len.reserve(nrec);
-  f.seq.reserve(nseq);
-  f.seq_off.reserve(nrec + 1);
-  f.seq_off.push_back(0);
-  for (auto& P : parts) {
-    const int64_t base = (int64_t)f.seq.size();
-    f.hdr_off.insert(f.hdr_off.end(), P.hdr_off.begin(), P.hdr_off.end());
-    f.hdr_len.insert(f.hdr_len.end(), P.hdr_len.begin(), P.hdr_len.end());
-    f.seq.insert(f.seq.end(), P.seq.begin(), P.seq.end());
-    for (size_t r = 1; r < P.seq_off.size(); r++) f.seq_off.push_back(base + P.seq_off[r]);
-  }
-  if (f.seq_off.size() != f.hdr_off.size() + 1) return false;
-  return true;
-}
-
-void put_wrapped(std::string& out, const char* s, int64_t len, int width) {
-  if (width <= 0) {
-    out.append(s, (size_t)len);
-    out.push_back('\n');
-    return;
-  }
-  if (len == 0) out.push_back('\n');
-  for (int64_t i = 0; i < len; i += width) {
-    out.append(s + i, (size_t)std::min<int64_t>(width, len - i));
-    out.push_back('\n');
-  }
-}
-
-bool write_all(int fd, const char* p, size_t n) {
-  while (n > 0) {
-    const ssize_t w = write(fd, p, n);
-    if (w < 0) {
-      if (errno == EINTR) continue;
-      return false;
-    }
-    p += w;
-    n -= (size_t)w;
-  }
-  return true;
-}
-
-bool write_file(const std::string& path, const std::string& data) {
-  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
-  if (fd < 0) return false;
-  bool ok = write_all(fd, data.data(), data.size());
-  ok = (close(fd) == 0) && ok;
-  return ok;
-}
-
-// a file made of parts written side by side: each part at its offset (pwrite), on one thread per part
-bool write_parts(const std::string& path, const std::vector<std::string>& parts) {
-  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
-  if (fd < 0) return false;
-  const int T = (int)parts.size();
-  std::vector<off_t> at(T + 1, 0);
-  for (int t = 0; t < T; t++) at[t + 1] = at[t] + (off_t)parts[t].size();
-  bool ok = at[T] == 0 || ftruncate(fd, at[T]) == 0;
-  std::vector<char> good(T, 1);
-  if (ok)
-    parallel_for(T, [&](int t) {
-      const char* p = parts[t].data();
-      size_t n = parts[t].size();
-      off_t o = at[t];
-      while (n > 0) {
-        const ssize_t w = pwrite(fd, p, n, o);
-        if (w < 0) {
-          if (errno == EINTR) continue;
-          good[t] = 0;
-          return;
-        }
-        p += w;
-        n -= (size_t)w;
-        o += w;
-      }
-    });
-  for (int t = 0; t < T; t++) ok = ok && good[t];
-  ok = (close(fd) == 0) && ok;
-  return ok;
-}
-
-// clusters [0, K) split over T threads by member count
-std::vector<int32_t> cluster_slices(const std::vector<int32_t>& ostart, int32_t K, int T) {
-  std::vector<int32_t> cut(T + 1, K);
-  cut[0] = 0;
-  const int64_t tot = ostart[K];
-  int32_t k = 0;
-  for (int t = 1; t < T; t++) {
-    const int64_t want = tot * t / T;
-    while (k < K && ostart[k] < want) k++;
-    cut[t] = std::max(k, cut[t - 1]);
-  }
-  return cut;
-}
-
-// ---------------------------------------------------------------- in-process parse (§8f f2)
-// parse_umi_clusters / polish_cluster (/root/reference/ont_tcr_consensus/parse_umi_clusters.py:10-242)
-// evaluated on the in-memory clusters instead of re-reading consout and the cluster<N> files.  Every
-// string operation restates the Python it replaces; the comments cite the lines.
-std::string pjoin(const std::string& a, const std::string& b) {  // os.path.join(a, b), b relative
-  if (a.empty()) return b;
-  return a.back() == '/' ? a + b : a + "/" + b;
-}
-
-struct Sv {
-  const char* p;
-  size_t n;
-  std::string str() const { return std::string(p, n); }
-  bool operator==(const char* s) const { return n == strlen(s) && !memcmp(p, s, n); }
-};
-
-// Python `s.split(sep)[1]`: the text between the first and the second occurrence of sep
-bool split1(Sv s, const char* sep, Sv& out) {
-  const size_t m = strlen(sep);
-  const char* e = s.p + s.n;
-  const char* a = std::search(s.p, e, sep, sep + m);
-  if (a == e) return false;
-  a += m;
-  const char* b = std::search(a, e, sep, sep + m);
-  out = Sv{a, (size_t)(b - a)};
-  return true;
-}
-
-void split_fields(Sv name, std::vector<Sv>& f) {  // name.split(";")
-  f.clear();
-  size_t st = 0;
-  for (size_t i = 0; i <= name.n; i++)
-    if (i == name.n || name.p[i] == ';') {
-      f.push_back(Sv{name.p + st, i - st});
-      st = i + 1;
-    }
-}
-
-// parse_umi_clusters over the in-memory clusters (parse_umi_clusters.py:10-242).  Clusters are independent
-// except for the loop's early exit (`max_clusters`) and its first error, so the work runs in three phases:
-// every cluster's counts and first format error on io_threads() threads; in cluster order, the exit and the
-// first error (which the reference raises after writing the files of the clusters before it); then the
-// cluster files and the per-cluster text of the kept range on the threads, concatenated in order.
-void parse_impl(umiclust_ctx* c, const Fasta& f, const umiclust_parse_params* pp, const char* work_dir_c,
-                umiclust_parse_result* pr) {
-  if (!c->p.clusterout_sort || !c->p.clusterout_id)
-    c->fail(UMICLUST_EINVAL, "in-process parse needs --clusterout_sort and --clusterout_id numbering");
-  const int64_t min_reads = pp->min_reads_per_cluster, max_reads = pp->max_reads_per_cluster;
-  const std::string work_dir = work_dir_c ? work_dir_c : "";
-  const std::string fa_dir = pjoin(work_dir, "clusters_fa");  // :177
-  struct stat sb;
-  if (stat(fa_dir.c_str(), &sb) == 0) c->fail(UMICLUST_EEXIST, "%s should not exist yet but does exist!", fa_dir.c_str());
-  if (mkdir(fa_dir.c_str(), 0777) != 0) c->fail(UMICLUST_EIO, "cannot create %s", fa_dir.c_str());
-  const int32_t K = c->nclusters;
-  struct PClus {
-    int64_t n_fwd = 0, n_rev = 0, found = 0, max_fwd = 0, max_rev = 0, w_fwd = 0, w_rev = 0, w_all = 0;
-    int written = 0, err = 0;
-    std::string msg;
-  };
-  struct Scratch {
-    std::vector<Sv> fields;
-    std::vector<std::pair<Sv, int32_t>> kept[2];  // insertion-ordered dict read id -> record (:61-65)
-    std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position)
-  };
-  // one cluster's counts (and its kept records in sc.kept); false on the first malformed record
-  auto analyze = [&](int32_t k, PClus& r, Scratch& sc) -> bool {
-    sc.kept[0].clear();
-    sc.kept[1].clear();
-    sc.index.clear();
-    int64_t seen[2] = {0, 0};
-    for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {  // cluster<N> file order (:36)
-      const int32_t i = c->perm[c->omemb[x]];
-      const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
-      split_fields(name, sc.fields);
-      if (sc.fields.size() != 7) {  // :38-47
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "cluster " + std::to_string(k) + ": header has " + std::to_string(sc.fields.size()) +
-                " cols while it should contain 7: " + name.str();
-        return false;
-      }
-      Sv strand;
-      if (!split1(sc.fields[1], "strand=", strand)) {
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "no strand= field: " + name.str();
-        return false;
-      }
-      r.found++;
-      int st = 0;
-      if (strand == "+") st = 0;
-      else if (strand == "-") st = 1;
-      else {
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "Strand annotation is " + strand.str() + " but only - or + are allowed!";
-        return false;
-      }
-      if (seen[st] < max_reads) {  // kept[strand][id] = rec: a repeated id keeps its first position
-        std::string key = sc.fields[0].str();
-        key.push_back((char)('0' + st));
-        int32_t pos = -1;
-        for (auto& e : sc.index)
-          if (e.first == key) {
-            pos = e.second;
-            break;
-          }
-        if (pos < 0) {
-          sc.index.emplace_back(std::move(key), (int32_t)sc.kept[st].size());
-          sc.kept[st].emplace_back(sc.fields[0], i);
-        } else {
-          sc.kept[st][pos].second = i;
-        }
-      }
-      seen[st]++;
-    }
-    // strand caps (:66-87)
-    r.n_fwd = seen[0];
-    r.n_rev = seen[1];
-    int64_t min_fwd, min_rev;
-    if (pp->balance_strands) {
-      min_fwd = min_rev = min_reads / 2;
-      const int64_t capped = std::min(std::min(r.n_fwd * 2, r.n_rev * 2), max_reads);
-      r.max_fwd = r.max_rev = capped / 2;
-    } else if (r.n_fwd > r.n_rev) {
-      min_fwd = min_rev = 0;
-      r.max_rev = std::min(r.n_rev, max_reads / 2);
-      r.max_fwd = std::min(max_reads - r.max_rev, r.n_fwd);
-    } else {
-      min_fwd = min_rev = 0;
-      r.max_fwd = std::min(r.n_fwd, max_reads / 2);
-      r.max_rev = std::min(max_reads - r.max_fwd, r.n_rev);
-    }
-    const int64_t n_reads = r.max_fwd + r.max_rev;
-    if (n_reads > max_reads) {  // :89-92
-      r.err = UMICLUST_EINVAL;
-      r.msg = "n_reads is higher than max_reads_per_cluster";
-      return false;
-    }
-    if (r.n_fwd >= min_fwd && r.n_rev >= min_rev && n_reads >= min_reads) {  // :95-120
-      r.w_fwd = std::min<int64_t>((int64_t)sc.kept[0].size(), r.max_fwd);
-      r.w_rev = std::min<int64_t>((int64_t)sc.kept[1].size(), r.max_rev);
-      r.w_all = std::min<int64_t>(r.w_fwd + r.w_rev, max_reads);
-      r.written = 1;
-    }
-    return true;
-  };
-  const int T = K < 256 ? 1 : io_threads();
-  const std::vector<int32_t> cut = cluster_slices(c->ostart, K, T);
-  std::vector<PClus> res((size_t)K);
-  parallel_for(T, [&](int t) {
-    Scratch sc;
-    for (int32_t k = cut[t]; k < cut[t + 1]; k++) analyze(k, res[k], sc);
-  });
-  // the reference's loop in order: its first error, its early exit
-  int64_t n_written = 0, reads_found = 0, reads_written = 0;
-  int32_t kend = K, kerr = -1;
-  for (int32_t k = 0; k < K; k++) {
-    if (res[k].err) {
-      kerr = k;
-      kend = k;
-      break;
-    }
-    n_written += res[k].written;
-    // the reference's quirk (:206, :219-221): the totals are overwritten by this cluster's counts, then doubled
-    reads_found = 2 * res[k].found;
-    reads_written = 2 * res[k].w_all;
-    // `if max_clusters and n_written > max_clusters` (:222-223): any non-zero value applies, as in Python
-    if (pp->max_clusters != 0 && n_written > pp->max_clusters) {
-      kend = k + 1;
-      break;
-    }
-  }
-  // cluster files and the text of clusters [0, kend), on the threads
-  const std::vector<int32_t> wcut = cluster_slices(c->ostart, kend, T);
-  std::vector<std::string> smol_p(T), log_p(T), stats_p(T);
-  std::vector<int32_t> bad(T, -1), noseq(T, -1);
-  parallel_for(T, [&](int t) {
-    Scratch sc;
-    std::string lines, &smol = smol_p[t], &log = log_p[t], &stats_out = stats_p[t];
-    for (int32_t k = wcut[t]; k < wcut[t + 1]; k++) {
-      PClus r;
-      analyze(k, r, sc);
-      const std::string out_fasta = pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta");  // :34
-      log += "Cluster: " + out_fasta + " has " + std::to_string(r.n_fwd) + "/" + std::to_string(r.max_fwd) +
-             " fwd and " + std::to_string(r.n_rev) + "/" + std::to_string(r.max_rev) + " rev reads\n";
-      if (r.written) {
-        lines.clear();
-        for (int64_t y = 0; y < r.w_all; y++) {
-          const auto& e = y < r.w_fwd ? sc.kept[0][y] : sc.kept[1][y - r.w_fwd];
-          const int32_t i = e.second;
-          split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
-          Sv read;
-          if (!split1(sc.fields[6], "seq=", read)) {
-            noseq[t] = i;
-            return;
-          }
-          lines.push_back('>');
-          lines.append(sc.fields[0].p, sc.fields[0].n);
-          lines.push_back('\n');
-          lines.append(read.p, read.n);
-          lines.push_back('\n');
-          smol += ">" + std::to_string(k) + "\n";
-          smol.append(read.p, read.n);
-          smol.push_back('\n');
-        }
-        if (!write_file(out_fasta, lines)) {
-          if (bad[t] < 0) bad[t] = k;
-          return;
-        }
-      } else {
-        log += "Cluster " + std::to_string(k) + " skipped\n";
-      }
-      log += "Cluster: " + out_fasta + " has " + std::to_string(r.w_all) + " reads written: " + std::to_string(r.w_fwd) +
-             " fwd - " + std::to_string(r.w_rev) + " rev\n";
-      stats_out += "cluster" + std::to_string(k) + "\t" + std::to_string(r.n_fwd) + "\t" + std::to_string(r.n_rev) +
-                   "\t" + std::to_string(r.w_fwd) + "\t" + std::to_string(r.w_rev) + "\t" + std::to_string(r.found) +
-                   "\t" + std::to_string(r.w_all) + "\t" + std::to_string(r.written) + "\n";
-    }
-  });
-  for (int t = 0; t < T; t++) {
-    if (noseq[t] >= 0) c->fail(UMICLUST_EFORMAT, "no seq= field in record %d", noseq[t]);
-    if (bad[t] >= 0) c->fail(UMICLUST_EIO, "cannot write %s", pjoin(fa_dir, "cluster" + std::to_string(bad[t]) + ".fasta").c_str());
-  }
-  if (kerr >= 0) c->fail(res[kerr].err, "%s", res[kerr].msg.c_str());
-  std::string stats_out = "id_cluster\tn_fwd\tn_rev\twritten_fwd\twritten_rev\tn\twritten\tcluster_written\n", log;
-  for (int t = 0; t < T; t++) {
-    stats_out += stats_p[t];
-    log += log_p[t];
-  }
-  if (!write_file(pjoin(work_dir, "vsearch_cluster_stats.tsv"), stats_out))
-    c->fail(UMICLUST_EIO, "cannot write the stats table");
-  // every read once more (GBs at production depth): the threads' parts side by side
-  if (!write_parts(pjoin(work_dir, "smolecule_clusters.fa"), smol_p))
-    c->fail(UMICLUST_EIO, "cannot write smolecule_clusters.fa");
-  pr->n_clusters = K;
-  pr->n_written = n_written;
-  pr->reads_found = reads_found;
-  pr->reads_written = reads_written;
-  pr->empty_region = (n_written == 0 || reads_found == 0) ? 1 : 0;
-  pr->pad = 0;
-  if (pr->empty_region) return;  // :224-231 (the caller appends the region: it may need the JSON map)
-  log += "Clusters: " + std::to_string((int64_t)(n_written * 100.0 / K)) + "% written (" + std::to_string(n_written) +
-         ")\n";
-  log += "Reads: " + std::to_string(reads_found) + " found\n";
-  log += "Reads: " + std::to_string((int64_t)(reads_written * 100.0 / reads_found)) + "% in written clusters\n";
-  if (!write_file(pjoin(work_dir, "parse_cluster.log"), log)) c->fail(UMICLUST_EIO, "cannot write parse_cluster.log");
-}
-
 int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
                        const char* clusters_prefix, const char* consout, const char* log_path,
                        umiclust_stats* stats, const umiclust_parse_params* pp = nullptr,
                        const char* work_dir = nullptr, umiclust_parse_result* pr = nullptr) {
   const double t0 = now_s();
   Fasta f;
-  if (!in_fasta || !read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
+  if (!in_fasta || !io::read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
   const int64_t n = (int64_t)f.hdr_off.size();
   for (int64_t i = 0; i < n; i++) {
     const int64_t L = f.seq_off[i + 1] - f.seq_off[i];
@@ -2530,63 +2132,22 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   const double t_read = now_s() - t0;
   load_impl(c, p, f.seq.data(), f.seq_off.data(), n);
   if (c->bin_s.size() != 2) c->fail(UMICLUST_EINVAL, "file path: one bin per load");
-  cluster_all(c, 0);
+  {
+    L3Pin pin(c);  // the same host placement as the session API (umiclust_cluster)
+    cluster_all(c, 0);
+  }
   const double t1 = now_s();
   const int32_t K = c->nclusters;
   const int width = p->fasta_width;
+  const io::ClusterView cv{K, c->ostart.data(), c->omemb.data(), c->perm.data()};
   // both writers build and write disjoint cluster ranges on io_threads() threads
-  const int T = K < 256 ? 1 : io_threads();
-  const std::vector<int32_t> cut = cluster_slices(c->ostart, K, T);
-  if (consout) {
-    std::vector<std::string> part(T);
-    parallel_for(T, [&](int t) {
-      std::string& out = part[t];
-      out.reserve((size_t)(cut[t + 1] - cut[t]) * 256);
-      for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
-        const int32_t cs = c->omemb[c->ostart[k]];
-        const int32_t ci = c->perm[cs];
-        out += ">centroid=";
-        out.append(f.data + f.hdr_off[ci], (size_t)f.hdr_len[ci]);
-        out += ";seqs=" + std::to_string(c->ostart[k + 1] - c->ostart[k]);
-        if (p->clusterout_id) out += ";clusterid=" + std::to_string(k);
-        out.push_back('\n');
-        put_wrapped(out, c->cons.data() + c->cons_off[k], c->cons_off[k + 1] - c->cons_off[k], width);
-      }
-    });
-    const int fd = open(consout, O_WRONLY | O_CREAT | O_TRUNC, 0666);
-    bool ok = fd >= 0;
-    for (int t = 0; ok && t < T; t++) ok = write_all(fd, part[t].data(), part[t].size());
-    if (fd >= 0) ok = (close(fd) == 0) && ok;
-    if (!ok) c->fail(UMICLUST_EIO, "cannot write %s", consout);
-  }
+  if (consout) io::write_consout(consout, f, cv, c->cons.data(), c->cons_off.data(), p->clusterout_id != 0, width);
   if (clusters_prefix) {
     // masked sequences (vsearch prints the DUST-masked db sequence): only the cluster<N> files need them
     std::vector<char> masked((size_t)c->n * kMaxLen);
     if (c->n > 0)
       c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
-    std::vector<int32_t> bad(T, -1);
-    parallel_for(T, [&](int t) {
-      std::string fn, out;
-      for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
-        out.clear();
-        for (int32_t x = c->ostart[k]; x < c->ostart[k + 1]; x++) {
-          const int32_t s = c->omemb[x];
-          const int32_t i = c->perm[s];
-          out.push_back('>');
-          out.append(f.data + f.hdr_off[i], (size_t)f.hdr_len[i]);
-          out.push_back('\n');
-          put_wrapped(out, masked.data() + (size_t)s * kMaxLen, c->hlen[s], width);
-        }
-        fn = clusters_prefix;
-        fn += std::to_string(k);
-        if (!write_file(fn, out)) {
-          bad[t] = k;
-          return;
-        }
-      }
-    });
-    for (int t = 0; t < T; t++)
-      if (bad[t] >= 0) c->fail(UMICLUST_EIO, "cannot write %s%d", clusters_prefix, bad[t]);
+    io::write_cluster_files(clusters_prefix, f, cv, masked.data(), kMaxLen, c->hlen.data(), width);
   }
   const double t_write = now_s() - t1;
   if (log_path) {
@@ -2618,54 +2179,18 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
              c->n ? 100.0 * singles / c->n : 0.0, K ? 100.0 * singles / K : 0.0,
              (long long)s.n_alignments, (long long)s.cells, (long long)s.kmer_postings, (long long)s.n_blocks,
              t_read, s.t_total_s, s.t_prefilter_s, s.t_align_s, s.t_consensus_s, s.t_host_s, t_write);
-    if (!write_file(log_path, buf)) c->fail(UMICLUST_EIO, "cannot write %s", log_path);
+    io::write_text(log_path, buf);
   }
-  if (pp) parse_impl(c, f, pp, work_dir, pr);
+  if (pp) {
+    if (!c->p.clusterout_sort || !c->p.clusterout_id)
+      c->fail(UMICLUST_EINVAL, "in-process parse needs --clusterout_sort and --clusterout_id numbering");
+    io::parse_clusters(f, cv, pp, work_dir, pr);
+  }
   c->stats.t_read_s = t_read;
   c->stats.t_write_s = t_write + (pp ? now_s() - t1 - t_write : 0.0);
   c->stats.t_run_s = now_s() - t0;
   if (stats) *stats = c->stats;
   return K;
-}
-
-// ---------------------------------------------------------------- argv
-// vsearch --gapopen/--gapext strings: "/"-separated tokens "<int>[QT][ILRE]*"
-// (no letter = all positions; E = both ends; Q/T restrict to query/target gaps).
-bool parse_gap(const char* s, int32_t* dst) {
-  const char* p = s;
-  while (*p) {
-    char* e = nullptr;
-    long v = strtol(p, &e, 10);
-    if (e == p) return false;
-    p = e;
-    bool q = false, t = false, I = false, L = false, R = false;
-    while (*p && *p != '/') {
-      switch (*p) {
-        case 'Q': q = true; break;
-        case 'T': t = true; break;
-        case 'I': I = true; break;
-        case 'E': L = R = true; break;
-        case 'L': L = true; break;
-        case 'R': R = true; break;
-        default: return false;
-      }
-      p++;
-    }
-    if (!q && !t) q = t = true;
-    if (!I && !L && !R) I = L = R = true;
-    if (q) {
-      if (L) dst[UMICLUST_QL] = (int32_t)v;
-      if (I) dst[UMICLUST_QI] = (int32_t)v;
-      if (R) dst[UMICLUST_QR] = (int32_t)v;
-    }
-    if (t) {
-      if (L) dst[UMICLUST_TL] = (int32_t)v;
-      if (I) dst[UMICLUST_TI] = (int32_t)v;
-      if (R) dst[UMICLUST_TR] = (int32_t)v;
-    }
-    if (*p == '/') p++;
-  }
-  return true;
 }
 
 }  // namespace
@@ -2675,120 +2200,6 @@ extern "C" {
 
 int32_t umiclust_abi_version(void) { return UMICLUST_ABI_VERSION; }
 
-int32_t umiclust_params_init(umiclust_params* p, int32_t preset, double identity, int32_t minlen,
-                             int32_t maxlen) {
-  if (!p) return UMICLUST_EINVAL;
-  memset(p, 0, sizeof(*p));
-  p->id = identity;
-  p->weak_id = identity < 0.10 ? identity : 0.10;
-  p->minseqlength = minlen;
-  p->maxseqlength = maxlen;
-  p->wordlength = 8;
-  p->minwordmatches = 12;
-  p->maxaccepts = 1;
-  p->maxrejects = 32;
-  p->strand_both = 1;
-  p->qmask_dust = 1;
-  p->clusterout_sort = 1;
-  p->clusterout_id = 1;
-  p->fasta_width = 80;
-  p->policy_boundary_open = 1;
-  p->threads = 1;
-  p->policy_threads = 0;
-  for (int k = 0; k < 6; k++) p->gap_ext[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 2 : 1;
-  if (preset == UMICLUST_PRESET_ROUND1) {
-    p->match = 10;
-    p->mismatch = -40;
-    for (int k = 0; k < 6; k++) p->gap_open[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 40 : 0;
-  } else if (preset == UMICLUST_PRESET_VSEARCH_DEFAULT) {
-    p->match = 2;
-    p->mismatch = -4;
-    for (int k = 0; k < 6; k++) p->gap_open[k] = (k == UMICLUST_QI || k == UMICLUST_TI) ? 20 : 2;
-  } else {
-    return UMICLUST_EINVAL;
-  }
-  return UMICLUST_OK;
-}
-
-int32_t umiclust_params_from_argv(umiclust_params* p, int32_t argc, const char* const* argv,
-                                  char* in_fasta, char* clusters_prefix, char* consout,
-                                  char* log_path, int32_t pathcap) {
-  if (!p || argc < 0 || (argc > 0 && !argv)) return UMICLUST_EINVAL;
-  umiclust_params_init(p, UMICLUST_PRESET_VSEARCH_DEFAULT, 0.97, 32, 50000);
-  p->clusterout_sort = 0;
-  p->clusterout_id = 0;
-  p->strand_both = 0;
-  p->maxseqlength = 50000;
-  bool have_in = false;
-  auto put = [&](char* dst, const char* v) -> bool {
-    if (!dst) return true;
-    if ((int32_t)strlen(v) + 1 > pathcap) return false;
-    strcpy(dst, v);
-    return true;
-  };
-  if (in_fasta) in_fasta[0] = 0;
-  if (clusters_prefix) clusters_prefix[0] = 0;
-  if (consout) consout[0] = 0;
-  if (log_path) log_path[0] = 0;
-  int i = 0;
-  if (argc > 0 && argv[0] && argv[0][0] != '-') i = 1;  // program name
-  for (; i < argc; i++) {
-    const char* a = argv[i];
-    auto val = [&]() -> const char* { return (i + 1 < argc) ? argv[++i] : nullptr; };
-    if (!strcmp(a, "--clusterout_id")) p->clusterout_id = 1;
-    else if (!strcmp(a, "--clusterout_sort")) p->clusterout_sort = 1;
-    else if (!strcmp(a, "--quiet") || !strcmp(a, "--no_progress")) {}
-    else if (!strcmp(a, "--clusters")) { const char* v = val(); if (!v || !put(clusters_prefix, v)) return UMICLUST_EINVAL; }
-    else if (!strcmp(a, "--consout")) { const char* v = val(); if (!v || !put(consout, v)) return UMICLUST_EINVAL; }
-    else if (!strcmp(a, "--log")) { const char* v = val(); if (!v || !put(log_path, v)) return UMICLUST_EINVAL; }
-    else if (!strcmp(a, "--cluster_fast")) { const char* v = val(); if (!v || !put(in_fasta, v)) return UMICLUST_EINVAL; have_in = true; }
-    else if (!strcmp(a, "--minseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->minseqlength = atoi(v); }
-    else if (!strcmp(a, "--maxseqlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxseqlength = atoi(v); }
-    else if (!strcmp(a, "--threads")) {
-      const char* v = val();
-      if (!v) return UMICLUST_EINVAL;
-      p->threads = std::max(1, atoi(v));
-    }
-    else if (!strcmp(a, "--strand")) {
-      const char* v = val();
-      if (!v) return UMICLUST_EINVAL;
-      if (!strcmp(v, "both")) p->strand_both = 1;
-      else if (!strcmp(v, "plus")) p->strand_both = 0;
-      else return UMICLUST_EINVAL;
-    }
-    else if (!strcmp(a, "--gapopen")) { const char* v = val(); if (!v || !parse_gap(v, p->gap_open)) return UMICLUST_EINVAL; }
-    else if (!strcmp(a, "--gapext")) { const char* v = val(); if (!v || !parse_gap(v, p->gap_ext)) return UMICLUST_EINVAL; }
-    else if (!strcmp(a, "--match")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->match = atoi(v); }
-    else if (!strcmp(a, "--mismatch")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->mismatch = atoi(v); }
-    else if (!strcmp(a, "--id")) {
-      const char* v = val();
-      if (!v) return UMICLUST_EINVAL;
-      p->id = atof(v);
-      p->weak_id = p->id < 0.10 ? p->id : 0.10;
-    }
-    else if (!strcmp(a, "--qmask")) {
-      const char* v = val();
-      if (!v) return UMICLUST_EINVAL;
-      if (!strcmp(v, "dust")) p->qmask_dust = 1;
-      else if (!strcmp(v, "none")) p->qmask_dust = 0;
-      else return UMICLUST_EINVAL;
-    }
-    else if (!strcmp(a, "--wordlength")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->wordlength = atoi(v); }
-    else if (!strcmp(a, "--minwordmatches")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->minwordmatches = atoi(v); }
-    else if (!strcmp(a, "--maxaccepts")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxaccepts = atoi(v); }
-    else if (!strcmp(a, "--maxrejects")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->maxrejects = atoi(v); }
-    else if (!strcmp(a, "--fasta_width")) { const char* v = val(); if (!v) return UMICLUST_EINVAL; p->fasta_width = atoi(v); }
-    else return UMICLUST_EINVAL;
-  }
-  if (!have_in) return UMICLUST_EINVAL;
-  // O4: the reference's argv is kept as is; the batched restatement of vsearch's multithreaded clustering is
-  // chosen from the environment (UMICLUST_O4=batched), the sequential definition otherwise
-  if (const char* e = getenv("UMICLUST_O4")) {
-    if (!strcmp(e, "batched")) p->policy_threads = 1;
-    else if (strcmp(e, "sequential") != 0) return UMICLUST_EINVAL;
-  }
-  return UMICLUST_OK;
-}
 
 // The alignment stream is created with an explicit priority, the highest by default: a pass's walk/align/pack
 // chain gates the host's resolution of its block and through it the next passes.  A prioritised stream also
@@ -2836,7 +2247,12 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_PIN")) c->pin = atoi(e) != 0;
+  if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
+  if (const char* e = getenv("UMICLUST_PIN")) {
+    c->pin = atoi(e) != 0;
+    c->pin_forced = atoi(e) == 1;
+  }
+  g_live_ctx++;
   if (const char* e = getenv("UMICLUST_SPLIT")) {
     c->split_env = atoi(e) != 0 ? 1 : 0;
     c->split_stream = atoi(e) == 2;
@@ -2864,6 +2280,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
 
 void umiclust_destroy(umiclust_ctx* c) {
   if (!c) return;
+  g_live_ctx--;
   (void)hipSetDevice(c->dev);
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();
@@ -2897,6 +2314,9 @@ const char* umiclust_last_error(const umiclust_ctx* c) { return c ? c->err.c_str
       __VA_ARGS__                                       \
     } catch (const Fail& f__) {                         \
       return f__.code;                                  \
+    } catch (const uc::io::IoError& e__) {              \
+      (c)->err = e__.msg;                               \
+      return e__.code;                                  \
     } catch (const std::bad_alloc&) {                   \
       (c)->err = "host allocation failed";              \
       return UMICLUST_ENOMEM;                           \
@@ -2951,42 +2371,6 @@ int32_t umiclust_load(umiclust_ctx* c, const umiclust_params* p, const char* seq
   });
 }
 
-// Keep the host resolve -- the calling thread and the resolve pool -- inside the L3 domain the caller runs on,
-// for the duration of one call (the caller's affinity is restored afterwards; UMICLUST_PIN=0 turns it off)
-struct L3Pin {
-  cpu_set_t saved;
-  bool on = false;
-  explicit L3Pin(umiclust_ctx* c) {
-    if (!c->pin || sched_getaffinity(0, sizeof saved, &saved) != 0) return;
-    const int cpu = sched_getcpu();
-    char path[96], buf[256];
-    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
-    FILE* f = cpu >= 0 ? fopen(path, "r") : nullptr;
-    if (!f) return;
-    const bool got = fgets(buf, sizeof buf, f) != nullptr;
-    fclose(f);
-    if (!got) return;
-    cpu_set_t want;
-    CPU_ZERO(&want);
-    for (char* p = buf; *p;) {  // "a-b,c,d-e"
-      char* e;
-      const long a = strtol(p, &e, 10);
-      if (e == p) break;
-      long b = a;
-      if (*e == '-') b = strtol(e + 1, &e, 10);
-      for (long x = a; x <= b && x < CPU_SETSIZE; x++)
-        if (CPU_ISSET((int)x, &saved)) CPU_SET((int)x, &want);
-      p = *e == ',' ? e + 1 : e;
-      if (*p == '\n') break;
-    }
-    if (CPU_COUNT(&want) == 0 || sched_setaffinity(0, sizeof want, &want) != 0) return;
-    if (c->pool) c->pool->set_affinity(want);  // a pool created below inherits the caller's mask
-    on = true;
-  }
-  ~L3Pin() {
-    if (on) sched_setaffinity(0, sizeof saved, &saved);
-  }
-};
 
 int64_t umiclust_cluster(umiclust_ctx* c, umiclust_stats* stats) {
   UC_GUARD(c, {
@@ -3050,6 +2434,7 @@ int32_t umiclust_load_bins(umiclust_ctx* c, const umiclust_params* p, const char
 int64_t umiclust_cluster_bin(umiclust_ctx* c, int32_t bin, umiclust_stats* stats) {
   UC_GUARD(c, {
     if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster_bin before umiclust_load_bins");
+    L3Pin pin(c);  // only with one live context (a bin-set runner's lanes each own one: then it stays off)
     cluster_all(c, bin, true);
     if (stats) *stats = c->stats;
     return c->nclusters;
@@ -3186,7 +2571,7 @@ struct OvRun {
   DevBuf<uint64_t> d_hash;
   DevBuf<int32_t> d_reg;
   DevBuf<unsigned long long> d_keys, d_rep;
-  DevBuf<uint32_t> d_cnt, d_start, d_cursor, d_bsum, d_members, d_coll;
+  DevBuf<uint32_t> d_cnt, d_start, d_cursor, d_bsum, d_members, d_coll, d_big, d_nbig;
   OvBuffers B{};
   uint64_t mask = 0;
 };
@@ -3218,11 +2603,13 @@ void overlap_table(umiclust_ctx* c, OvRun& R, const char* seqs, const int64_t* o
   c->hip(R.d_bsum.ensure(m / 1024 + 1), "alloc");
   c->hip(R.d_members.ensure((size_t)n + 1), "alloc");
   c->hip(R.d_coll.ensure(1), "alloc");
+  c->hip(R.d_big.ensure((size_t)n / (kOvSmallBucket + 1) + 1), "alloc");
+  c->hip(R.d_nbig.ensure(1), "alloc");
   if (bytes > 0) c->hip(hipMemcpyAsync(R.d_seq.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
   c->hip(hipMemcpyAsync(R.d_off.p, rel.data(), rel.size() * 8, hipMemcpyHostToDevice, c->st), "h2d");
   c->hip(hipMemcpyAsync(R.d_rs.p, rstart, ((size_t)nreg + 1) * 8, hipMemcpyHostToDevice, c->st), "h2d");
   R.B = OvBuffers{R.d_hash.p, R.d_reg.p, R.d_keys.p, R.d_rep.p, R.d_slot.p, R.d_cnt.p, R.d_start.p, R.d_cursor.p,
-                  R.d_bsum.p, R.d_members.p, R.d_coll.p};
+                  R.d_bsum.p, R.d_members.p, R.d_coll.p, R.d_big.p, R.d_nbig.p};
   // a 64-bit collision between two different sequences is detected exactly; the next seed is tried
   const uint64_t seeds[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull,
                              0x082efa98ec4e6c89ull};
@@ -3295,24 +2682,31 @@ int32_t umiclust_overlap_regions(umiclust_ctx* c, const char* seqs, const int64_
 // ---------------------------------------------------------------- UMI extraction (§8f f1)
 namespace {
 // additionalEqualities of extract_umis.py:26-87 (either order), plus identity
-const char* const kIupacEq[] = {"MA", "MC", "RA", "RG", "WA", "WT", "SC", "SG", "YC", "YT", "KG", "KT", "VA", "VC",
+constexpr const char* kIupacEq[] = {"MA", "MC", "RA", "RG", "WA", "WT", "SC", "SG", "YC", "YT", "KG", "KT", "VA", "VC",
                                 "VG", "HA", "HC", "HT", "DA", "DG", "DT", "BC", "BG", "BT", "NA", "NC", "NG", "NT",
                                 "ma", "mc", "ra", "rg", "wa", "wt", "sc", "sg", "yc", "yt", "kg", "kt", "va", "vc",
                                 "vg", "ha", "hc", "ht", "da", "dg", "dt", "bc", "bg", "bt", "na", "nc", "ng", "nt",
                                 "aA", "cC", "tT", "gG"};
 
-void build_patterns(umiclust_ctx* c, const char* fwd, const char* rev, ExtractPatterns& P) {
-  static bool eqt[256][256];
-  static bool init = false;
-  if (!init) {
-    for (int a = 0; a < 256; a++)
-      for (int b = 0; b < 256; b++) eqt[a][b] = a == b;
-    for (const char* e : kIupacEq) {
-      eqt[(uint8_t)e[0]][(uint8_t)e[1]] = true;
-      eqt[(uint8_t)e[1]][(uint8_t)e[0]] = true;
-    }
-    init = true;
+// symbol equality of edlib with the reference's additionalEqualities, built at compile time (constant
+// initialisation: contexts on different threads share it without a lazy first-use race)
+struct EqTable {
+  bool eq[256][256];
+};
+constexpr EqTable make_eq_table() {
+  EqTable t{};
+  for (int a = 0; a < 256; a++)
+    for (int b = 0; b < 256; b++) t.eq[a][b] = a == b;
+  for (const char* e : kIupacEq) {
+    t.eq[(uint8_t)e[0]][(uint8_t)e[1]] = true;
+    t.eq[(uint8_t)e[1]][(uint8_t)e[0]] = true;
   }
+  return t;
+}
+constexpr EqTable kEqTable = make_eq_table();
+
+void build_patterns(umiclust_ctx* c, const char* fwd, const char* rev, ExtractPatterns& P) {
+  const auto& eqt = kEqTable.eq;
   memset(&P, 0, sizeof(P));
   const char* pats[2] = {fwd, rev};
   for (int w = 0; w < 2; w++) {
@@ -3393,74 +2787,6 @@ void extract_device(umiclust_ctx* c, const char* seqs, const int64_t* offs, int6
   c->hip(hipStreamSynchronize(c->st), "sync");
 }
 
-// FASTQ records (pysam.FastxFile): '@' header (name up to whitespace), sequence lines up to the '+' line, then
-// as many quality characters as sequence ones
-bool read_fastq(const char* path, Fasta& f) {
-  int fd = open(path, O_RDONLY);
-  if (fd < 0) return false;
-  struct stat sb;
-  if (fstat(fd, &sb) != 0) {
-    close(fd);
-    return false;
-  }
-  f.size = (size_t)sb.st_size;
-  if (f.size > 0) {
-    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-    if (f.map == MAP_FAILED) {
-      f.map = nullptr;
-      close(fd);
-      return false;
-    }
-    f.data = (const char*)f.map;
-  }
-  close(fd);
-  const char* d = f.data;
-  const size_t N = f.size;
-  size_t i = 0;
-  f.seq_off.push_back(0);
-  auto line_end = [&](size_t x) {
-    const char* nl = (const char*)memchr(d + x, '\n', N - x);
-    return nl ? (size_t)(nl - d) : N;
-  };
-  while (i < N) {
-    if (d[i] == '\n' || d[i] == '\r') { i++; continue; }
-    if (d[i] != '@') return false;
-    const size_t e = line_end(i);
-    size_t k = i + 1;
-    while (k < e && d[k] != '\r' && d[k] != ' ' && d[k] != '\t') k++;
-    f.hdr_off.push_back((int64_t)(i + 1));
-    f.hdr_len.push_back((int32_t)(k - i - 1));
-    i = e + 1;
-    size_t nseq = 0;
-    while (i < N && d[i] != '+') {
-      const size_t le = line_end(i);
-      for (size_t x = i; x < le; x++)
-        if (d[x] != '\r') {
-          f.seq.push_back(d[x]);
-          nseq++;
-        }
-      i = le + 1;
-    }
-    if (i >= N) return false;
-    i = line_end(i) + 1;  // the '+' line
-    size_t nq = 0;
-    while (i < N && nq < nseq) {
-      const size_t le = line_end(i);
-      for (size_t x = i; x < le; x++) nq += d[x] != '\r';
-      i = le + 1;
-    }
-    f.seq_off.push_back((int64_t)f.seq.size());
-  }
-  return true;
-}
-
-// the reverse_complement of extract_umis.py:10-12: str.translate("ACTG" -> "TGAC"), reversed
-void revcomp_ref(const char* s, size_t n, std::string& out) {
-  for (size_t x = n; x-- > 0;) {
-    const char ch = s[x];
-    out.push_back(ch == 'A' ? 'T' : ch == 'C' ? 'G' : ch == 'T' ? 'A' : ch == 'G' ? 'C' : ch);
-  }
-}
 }  // namespace
 
 int32_t umiclust_extract_umis(umiclust_ctx* c, const char* seqs, const int64_t* offsets, int64_t n,
@@ -3488,7 +2814,7 @@ int64_t umiclust_extract_umis_file(umiclust_ctx* c, const char* fastx_file, cons
       fastq = ch == '@';
       fclose(fp);
     }
-    if (!(fastq ? read_fastq(fastx_file, f) : read_fasta(fastx_file, f)))
+    if (!(fastq ? io::read_fastq(fastx_file, f) : io::read_fasta(fastx_file, f)))
       c->fail(UMICLUST_EIO, "cannot parse %s", fastx_file);
     const int64_t n = (int64_t)f.hdr_off.size();
     std::vector<int32_t> res((size_t)std::max<int64_t>(n, 1) * 6);
@@ -3496,131 +2822,19 @@ int64_t umiclust_extract_umis_file(umiclust_ctx* c, const char* fastx_file, cons
                    umi_fwd, umi_rev, res.data());
     // records in input order; the reference raises at the first record without a strand annotation, after
     // writing the records before it: those are written, then the error is returned
-    std::vector<std::string> strand(n), rid(n);
     int64_t ngood = n;
-    for (int64_t i = 0; i < n; i++) {
-      const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
+    for (int64_t i = 0; i < n && ngood == n; i++) {
       Sv st;
-      if (!split1(name, "strand=", st)) {
-        ngood = i;
-        break;
-      }
-      strand[i] = st.str();
-      const char* semi = (const char*)memchr(name.p, ';', name.n);
-      rid[i] = std::string(name.p, semi ? (size_t)(semi - name.p) : name.n);
+      if (!split1(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, "strand=", st)) ngood = i;
     }
-    const int T = ngood < 4096 ? 1 : io_threads();
-    std::vector<std::string> part(T);
-    std::vector<int64_t> cnt(T, 0);
-    parallel_for(T, [&](int t) {
-      std::string& o = part[t];
-      for (int64_t i = ngood * t / T; i < ngood * (t + 1) / T; i++) {
-        const int32_t* r = res.data() + i * 6;
-        if (r[0] < 0 || r[3] < 0) continue;  // `if not umi_5p or not umi_3p`
-        const char* s = f.seq.data() + f.seq_off[i];
-        const int64_t len = f.seq_off[i + 1] - f.seq_off[i];
-        const int64_t w3 = (adapter_length_3_end == 0 || adapter_length_3_end > len) ? len : adapter_length_3_end;
-        const char* u5 = s + r[1];
-        const size_t l5 = (size_t)(r[2] - r[1] + 1);
-        const char* u3 = s + (len - w3) + r[4];
-        const size_t l3 = (size_t)(r[5] - r[4] + 1);
-        cnt[t]++;
-        o += ">" + rid[i] + ";strand=" + strand[i] + ";umi_fwd_dist=" + std::to_string(r[0]) + ";umi_rev_dist=" +
-             std::to_string(r[3]) + ";umi_fwd_seq=";
-        o.append(u5, l5);
-        o += ";umi_rev_seq=";
-        o.append(u3, l3);
-        o += ";seq=";
-        o.append(s, (size_t)len);
-        o.push_back('\n');
-        if (strand[i] == "+") {
-          o.append(u5, l5);
-          o.append(u3, l3);
-        } else {
-          revcomp_ref(u3, l3, o);
-          revcomp_ref(u5, l5, o);
-        }
-        o.push_back('\n');
-      }
-    });
-    const int fd = open(out_fasta, O_WRONLY | O_CREAT | O_TRUNC, 0666);
-    bool ok = fd >= 0;
-    for (int t = 0; ok && t < T; t++) ok = write_all(fd, part[t].data(), part[t].size());
-    if (fd >= 0) ok = (close(fd) == 0) && ok;
-    if (!ok) c->fail(UMICLUST_EIO, "cannot write %s", out_fasta);
+    const int64_t tot = io::write_detected_umis(out_fasta, f, res.data(), ngood, adapter_length_3_end);
     if (ngood < n) c->fail(UMICLUST_EFORMAT, "Read strand not annotated!");
-    int64_t tot = 0;
-    for (int64_t v : cnt) tot += v;
     return tot;
   });
 }
 
 // ---------------------------------------------------------------- region binning (§8f f4)
 namespace {
-// BGZF (SAM/BAM specification §4.1): gzip members with a BC extra field holding BSIZE; every block is
-// inflated independently, so the blocks are split over the host threads
-bool inflate_bgzf(umiclust_ctx* c, const char* path, std::vector<uint8_t>& raw) {
-  int fd = open(path, O_RDONLY);
-  if (fd < 0) return false;
-  struct stat sb;
-  if (fstat(fd, &sb) != 0) {
-    close(fd);
-    return false;
-  }
-  const size_t N = (size_t)sb.st_size;
-  void* map = N ? mmap(nullptr, N, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0) : nullptr;
-  close(fd);
-  if (N && map == MAP_FAILED) return false;
-  const uint8_t* d = (const uint8_t*)map;
-  std::vector<size_t> boff, bsz;
-  std::vector<uint32_t> isz;
-  size_t o = 0;
-  bool ok = true;
-  while (o + 18 <= N) {
-    if (d[o] != 31 || d[o + 1] != 139 || d[o + 2] != 8 || !(d[o + 3] & 4)) { ok = false; break; }
-    const size_t xlen = (size_t)d[o + 10] | ((size_t)d[o + 11] << 8);
-    size_t bs = 0;
-    for (size_t x = o + 12; x + 4 <= o + 12 + xlen;) {
-      const size_t sl = (size_t)d[x + 2] | ((size_t)d[x + 3] << 8);
-      if (d[x] == 66 && d[x + 1] == 67 && sl == 2) bs = ((size_t)d[x + 4] | ((size_t)d[x + 5] << 8)) + 1;
-      x += 4 + sl;
-    }
-    if (!bs || o + bs > N) { ok = false; break; }
-    boff.push_back(o);
-    bsz.push_back(bs);
-    isz.push_back((uint32_t)d[o + bs - 4] | ((uint32_t)d[o + bs - 3] << 8) | ((uint32_t)d[o + bs - 2] << 16) |
-                  ((uint32_t)d[o + bs - 1] << 24));
-    o += bs;
-  }
-  if (ok && o != N) ok = false;
-  std::vector<size_t> uo(boff.size() + 1, 0);
-  for (size_t b = 0; b < boff.size(); b++) uo[b + 1] = uo[b] + isz[b];
-  if (ok) {
-    raw.resize(uo.back());
-    const int T = std::max(1, std::min<int>(io_threads(), (int)boff.size()));
-    std::vector<int> bad(T, 0);
-    parallel_for(T, [&](int t) {
-      for (size_t b = (size_t)t; b < boff.size(); b += (size_t)T) {
-        if (!isz[b]) continue;
-        const size_t xlen = (size_t)d[boff[b] + 10] | ((size_t)d[boff[b] + 11] << 8);
-        z_stream zs{};
-        if (inflateInit2(&zs, -15) != Z_OK) { bad[t] = 1; return; }
-        zs.next_in = const_cast<Bytef*>(d + boff[b] + 12 + xlen);
-        zs.avail_in = (uInt)(bsz[b] - 12 - xlen - 8);
-        zs.next_out = raw.data() + uo[b];
-        zs.avail_out = isz[b];
-        const int rc = inflate(&zs, Z_FINISH);
-        inflateEnd(&zs);
-        if (rc != Z_STREAM_END || zs.avail_out != 0) { bad[t] = 1; return; }
-      }
-    });
-    for (int v : bad) ok = ok && !v;
-  }
-  if (map) munmap(map, N);
-  (void)c;
-  return ok;
-}
-
 int32_t rd_i32(const uint8_t* p) { int32_t v; memcpy(&v, p, 4); return v; }
 }  // namespace
 
@@ -3634,7 +2848,7 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
         !counts || ncluster_cap < 0 || (ncluster_cap > 0 && !reads_per_cluster))
       c->fail(UMICLUST_EINVAL, "bad argument");
     std::vector<uint8_t> raw;
-    if (!inflate_bgzf(c, bam_file, raw)) c->fail(UMICLUST_EIO, "cannot read BGZF/BAM %s", bam_file);
+    if (!io::inflate_bgzf(bam_file, raw)) c->fail(UMICLUST_EIO, "cannot read BGZF/BAM %s", bam_file);
     if (raw.size() < 12 || memcmp(raw.data(), "BAM\1", 4) != 0) c->fail(UMICLUST_EFORMAT, "%s is not BAM", bam_file);
     // header: text, then the reference names, matched to the regions of the reference FASTA
     std::unordered_map<std::string, int32_t> rid;
@@ -3736,7 +2950,7 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
         const int32_t k = used[u];
         const std::string fn = pjoin(out_dir, "region_cluster" + std::to_string(k) + ".fasta");
         const int fd = open(fn.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0666);
-        bool ok = fd >= 0 && write_all(fd, outb.data() + cbase[k], (size_t)(cbase[k + 1] - cbase[k]));
+        bool ok = fd >= 0 && io::write_all(fd, outb.data() + cbase[k], (size_t)(cbase[k + 1] - cbase[k]));
         if (fd >= 0) ok = (close(fd) == 0) && ok;
         if (!ok) bad[t] = k;
       }

@@ -1,0 +1,106 @@
+// host_io.h -- the HIP-free host side of the drop-in boundary: FASTA/FASTQ input, the vsearch output
+// writers (--consout, --clusters), the in-process parse_umi_clusters, the vsearch argv
+// grammar, BGZF inflation (f4) and the detected-UMI writer (f1).  Compiled by g++ (no HIP), so the CPU
+// suite builds it with ASan/UBSan (tests/test_sanitizers_cpu.py, tools/host_asan_main.cpp).  Not part of the
+// C ABI except umiclust_params_init / umiclust_params_from_argv, which it defines.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/umiclust.h"
+
+namespace uc {
+namespace io {
+
+// A failure of an I/O-side step: an UMICLUST_E* code and a message (driver.cpp turns it into the context's
+// error; nothing is thrown across the C ABI).
+struct IoError {
+  int code;
+  std::string msg;
+};
+
+// host threads for file I/O (the box gives a GPU process ~16 cores; UMICLUST_IO_THREADS overrides)
+int io_threads();
+
+// run f(t) for t in [0, T) on T threads (the caller's thread runs t = 0)
+template <typename F>
+void parallel_for(int T, F&& f) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back([&f, t] { f(t); });
+  f(0);
+  for (auto& x : th) x.join();
+}
+
+// The input FASTA (or FASTQ), memory-mapped; labels point into the mapping, sequences are copied out.
+struct Fasta {
+  const char* data = nullptr;     // file contents (mapping)
+  size_t size = 0;
+  void* map = nullptr;
+  std::vector<int64_t> hdr_off;   // label start (after '>' / '@')
+  std::vector<int32_t> hdr_len;   // label length (truncated at whitespace)
+  std::vector<char> seq;          // concatenated sequences
+  std::vector<int64_t> seq_off;   // n+1
+  Fasta() = default;
+  Fasta(const Fasta&) = delete;
+  Fasta& operator=(const Fasta&) = delete;
+  ~Fasta();
+};
+// vsearch's FASTA reader: labels truncated at the first whitespace, sequence lines keep letters only, lines
+// before the first '>' ignored; parsed by io_threads() threads over slices of the mapping
+bool read_fasta(const char* path, Fasta& f);
+// pysam.FastxFile's FASTQ records: '@' name, sequence lines up to '+', as many quality characters
+bool read_fastq(const char* path, Fasta& f);
+
+// clusters in output order: cluster k = sorted seqnos omemb[ostart[k] .. ostart[k+1]) (centroid first), input
+// record of sorted seqno s = perm[s]
+struct ClusterView {
+  int32_t K = 0;
+  const int32_t* ostart = nullptr;
+  const int32_t* omemb = nullptr;
+  const int32_t* perm = nullptr;
+};
+
+// clusters [0, K) split over T threads by member count
+std::vector<int32_t> cluster_slices(const int32_t* ostart, int32_t K, int T);
+
+// --consout: >centroid=<label>;seqs=<m>[;clusterid=<k>] + the consensus of cluster k, wrapped at width
+void write_consout(const char* path, const Fasta& f, const ClusterView& cv, const char* cons, const int64_t* cons_off,
+                   bool clusterout_id, int width);
+// --clusters: <prefix><k> per cluster, the members' labels and masked sequences (masked[s * stride], length
+// hlen[s]) in cluster order
+void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& cv, const char* masked, int stride,
+                         const uint8_t* hlen, int width);
+// a small text file (the log)
+void write_text(const char* path, const std::string& text);
+// whole-buffer write / create-write-close (false on an I/O error)
+bool write_all(int fd, const char* p, size_t n);
+bool write_file(const std::string& path, const std::string& data);
+
+// parse_umi_clusters / polish_cluster (/root/reference/ont_tcr_consensus/parse_umi_clusters.py:10-242) on the
+// in-memory clusters: <work_dir>/clusters_fa/cluster<k>.fasta, smolecule_clusters.fa, vsearch_cluster_stats.tsv,
+// parse_cluster.log; byte-identical to the reference run on the vsearch files
+void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_params* pp, const char* work_dir,
+                    umiclust_parse_result* pr);
+
+// write_fasta of extract_umis (/root/reference/ont_tcr_consensus/extract_umis.py:154-186) for records [0, ngood):
+// res[i*6 ..] = (dist, start, end) of the 5' and 3' UMI in their windows; returns the reads with both UMIs
+int64_t write_detected_umis(const char* path, const Fasta& f, const int32_t* res, int64_t ngood, int32_t a3);
+
+// BGZF (SAM/BAM specification §4.1) inflated on the host threads
+bool inflate_bgzf(const char* path, std::vector<uint8_t>& raw);
+
+// the reference's string helpers
+struct Sv {
+  const char* p;
+  size_t n;
+  std::string str() const { return std::string(p, n); }
+  bool operator==(const char* s) const;
+};
+bool split1(Sv s, const char* sep, Sv& out);  // Python s.split(sep)[1]
+std::string pjoin(const std::string& a, const std::string& b);  // os.path.join(a, b), b relative
+
+}  // namespace io
+}  // namespace uc

@@ -16,6 +16,7 @@
 
 #include <stdint.h>
 
+#include "../../include/umiclust.h"
 #include "umiclust_internal.h"
 
 namespace uc {
@@ -171,14 +172,21 @@ __global__ void k_ov_fill(const int64_t* __restrict__ slot, int64_t n, uint32_t*
   members[atomicAdd(&cursor[slot[i]], 1u)] = (uint32_t)i;
 }
 
-// one thread per slot: members in index (= region) order, run lengths per region, then every region pair
+// one thread per slot: members in index (= region) order, run lengths per region, then every region pair.
+// Buckets of more than kOvSmallBucket members (one UMI present many times: an artifact shared by many regions)
+// are handed to k_ov_pairs_big, so no thread runs a quadratic sort or pair loop over a large bucket.
 __global__ void k_ov_pairs(const uint32_t* __restrict__ start, int64_t m, uint32_t* __restrict__ members,
                            const int32_t* __restrict__ region, int32_t nreg,
-                           unsigned long long* __restrict__ total, uint32_t* __restrict__ maxc) {
+                           unsigned long long* __restrict__ total, uint32_t* __restrict__ maxc,
+                           uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= m) return;
   const uint32_t a = start[s], b = start[s + 1];
   if (b - a < 2) return;
+  if (b - a > (uint32_t)kOvSmallBucket) {
+    big[atomicAdd(nbig, 1u)] = (uint32_t)s;
+    return;
+  }
   uint32_t* mb = members + a;
   const uint32_t nb = b - a;
   // insertion sort (buckets are small: one distinct consensus UMI)
@@ -209,6 +217,66 @@ __global__ void k_ov_pairs(const uint32_t* __restrict__ start, int64_t m, uint32
       j0 = j1;
     }
     i0 = i1;
+  }
+}
+
+// large buckets: one workgroup per bucket (persistent grid over the list k_ov_pairs built).  A region histogram
+// in LDS replaces the sort (regions are index ranges, so the nonzero entries in region order are the runs), a
+// block scan compacts it, and the pairs of runs are spread over the threads row by row.
+constexpr int kOvMaxRegions = UMICLUST_OVERLAP_MAX_REGIONS;
+__global__ __launch_bounds__(kOvThreads) void k_ov_pairs_big(const uint32_t* __restrict__ start,
+                                                           const uint32_t* __restrict__ members,
+                                                           const int32_t* __restrict__ region, int32_t nreg,
+                                                           const uint32_t* __restrict__ big,
+                                                           const uint32_t* __restrict__ nbig,
+                                                           unsigned long long* __restrict__ total,
+                                                           uint32_t* __restrict__ maxc) {
+  __shared__ uint32_t hist[kOvMaxRegions];
+  __shared__ uint16_t rr[kOvMaxRegions];
+  __shared__ uint32_t rc[kOvMaxRegions];
+  __shared__ uint32_t part[kOvThreads];
+  __shared__ uint32_t nz_s;
+  const int tid = threadIdx.x;
+  const uint32_t nbuckets = *nbig;
+  for (uint32_t q = blockIdx.x; q < nbuckets; q += gridDim.x) {
+    const uint32_t s = big[q];
+    const uint32_t a = start[s], nb = start[s + 1] - a;
+    for (int r = tid; r < nreg; r += kOvThreads) hist[r] = 0;
+    if (tid == 0) nz_s = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += kOvThreads) atomicAdd(&hist[region[members[a + i]]], 1u);
+    __syncthreads();
+    // compaction in region order: chunks of kOvThreads regions, an exclusive scan of the nonzero flags
+    for (int r0 = 0; r0 < nreg; r0 += kOvThreads) {
+      const int r = r0 + tid;
+      const uint32_t f = (r < nreg && hist[r] != 0u) ? 1u : 0u;
+      part[tid] = f;
+      __syncthreads();
+      for (int d = 1; d < kOvThreads; d <<= 1) {
+        const uint32_t v = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+      }
+      const uint32_t base = nz_s;
+      if (f) {
+        rr[base + part[tid] - 1u] = (uint16_t)r;
+        rc[base + part[tid] - 1u] = hist[r];
+      }
+      __syncthreads();
+      if (tid == kOvThreads - 1) nz_s = base + part[tid];
+      __syncthreads();
+    }
+    const uint32_t nz = nz_s;
+    for (uint32_t i = 0; i + 1 < nz; i++) {
+      const uint32_t ra = rr[i], ca = rc[i];
+      for (uint32_t j = i + 1 + tid; j < nz; j += kOvThreads) {
+        const int64_t cell = (int64_t)ra * nreg + rr[j];
+        atomicAdd(&total[cell], (unsigned long long)ca * rc[j]);
+        atomicMax(&maxc[cell], rc[j]);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -258,8 +326,13 @@ hipError_t launch_overlap_table(const char* seqs, const int64_t* offs, int64_t n
 hipError_t launch_overlap_pairs(const OvBuffers& B, uint64_t mask, int32_t nreg, unsigned long long* total,
                                 uint32_t* maxc, hipStream_t st) {
   const int64_t m = (int64_t)mask + 1;
+  if (nreg > kOvMaxRegions) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(B.nbig, 0, 4, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_ov_pairs, dim3((unsigned)((m + kOvThreads - 1) / kOvThreads)), dim3(kOvThreads), 0, st,
-                     B.start, m, B.members, B.region, nreg, total, maxc);
+                     B.start, m, B.members, B.region, nreg, total, maxc, B.big, B.nbig);
+  hipLaunchKernelGGL(k_ov_pairs_big, dim3(512), dim3(kOvThreads), 0, st, B.start, B.members, B.region, nreg, B.big,
+                     B.nbig, total, maxc);
   return hipGetLastError();
 }
 

@@ -244,7 +244,10 @@ struct OvBuffers {
   uint32_t* bsum;                 // [m / 1024 + 1]
   uint32_t* members;              // [n]
   uint32_t* collision;            // [1]
+  uint32_t* big;                  // [n / (kOvSmallBucket + 1) + 1] slots whose buckets k_ov_pairs hands on
+  uint32_t* nbig;                 // [1]
 };
+constexpr int kOvSmallBucket = 32;  // larger buckets (a UMI in many regions): one workgroup each, region histogram
 // one hash-table pass over n sequences of nreg regions (region r = [rstart[r], rstart[r+1])), table of
 // mask + 1 slots; csr also buckets the members by slot.  Synchronous; *collided != 0 means two different
 // sequences shared a 64-bit hash (re-run with another seed).

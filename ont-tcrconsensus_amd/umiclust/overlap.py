@@ -12,18 +12,21 @@ Same names, arguments, files and return values as the reference:
     an empty region 1 raises ValueError (upstream's max() of an empty list);
   * count_overlapping_umis_between_all_regions(smolecule_filtered_fa_list, overlapping_umi_edit_threshold,
     logs_dir) (:345-369): the TSV header, then every itertools.combinations pair -- all pairs in ONE GPU hash
-    join (umiclust_overlap_regions) instead of one Ray task per pair and one per UMI.
+    join (umiclust_overlap_regions) instead of one Ray task per pair and one per UMI; past
+    UMICLUST_OVERLAP_MAX_REGIONS regions, row blocks of regions joined with every later block.  A pair with an
+    empty region 1 raises ValueError, as upstream's task does, after every other pair has been reported (the
+    other Ray tasks still run and append their rows before ray.get raises).
 Rows are written in combinations order (upstream: Ray completion order).  No CPU fallback: without the
 library or a device every call raises.
 """
 from __future__ import annotations
 
-import itertools
 import os
 from typing import Union
 
 import numpy as np
 
+from . import _lib
 from . import vsearch_umi_cluster as _v
 
 CONSOUT = "umi_clusters_consensus.fasta"
@@ -83,12 +86,30 @@ def count_overlapping_umis_between_all_regions(smolecule_filtered_fa_list: list,
     out = []
     if R < 2:
         return out
-    total, maxc = _v.context().overlap_regions(seqs)
-    for a, b in itertools.combinations(range(R), 2):
-        if not seqs[a]:  # upstream: max() of an empty region 1 raises inside the pair's task
-            raise ValueError("max() arg is an empty sequence")
-        out.append(_report(os.path.basename(region_dirs[a]), os.path.basename(region_dirs[b]), int(total[a, b]),
-                           int(maxc[a, b]), logs_dir, tsv))
+    names = [os.path.basename(d) for d in region_dirs]
+    empty_region_1 = False
+    # one GPU join over every region when they fit one call; beyond that, row blocks of regions joined with each
+    # later block (every pair of the union is counted; the pairs of the row block are kept)
+    B = _lib.OVERLAP_MAX_REGIONS // 2 if R > _lib.OVERLAP_MAX_REGIONS else R
+    for i0 in range(0, R, B):
+        rows = range(i0, min(R, i0 + B))
+        tot = np.zeros((len(rows), R), np.int64)
+        mxc = np.zeros((len(rows), R), np.int32)
+        for j0 in range(i0, R, B):
+            cols = list(rows) if j0 == i0 else list(rows) + list(range(j0, min(R, j0 + B)))
+            t, m = _v.context().overlap_regions([seqs[x] for x in cols])
+            tot[:, cols] = np.maximum(tot[:, cols], t[:len(rows)])
+            mxc[:, cols] = np.maximum(mxc[:, cols], m[:len(rows)])
+        for r, a in enumerate(rows):
+            for b in range(a + 1, R):
+                if not seqs[a]:
+                    # upstream: max() of an empty region 1 raises inside that pair's task; the other tasks still run
+                    # and append their rows, and ray.get raises afterwards
+                    empty_region_1 = True
+                    continue
+                out.append(_report(names[a], names[b], int(tot[r, b]), int(mxc[r, b]), logs_dir, tsv))
+    if empty_region_1:
+        raise ValueError("max() arg is an empty sequence")
     return out
 
 
@@ -110,4 +131,3 @@ class _LocalRemote:
 
 count_single_umi_overlaps_task = _LocalRemote(count_single_umi_overlaps)
 count_overlapping_umis_between_2_regions_task = _LocalRemote(count_overlapping_umis_between_2_regions)
-del np

@@ -72,10 +72,18 @@ def count_overlapping_umis_between_2_regions(region_1_dir, region_2_dir, regions
 
 def count_overlapping_umis_between_all_regions(smolecule_filtered_fa_list, overlapping_umi_edit_threshold,
                                                logs_dir):
-    """extract_umis.py:345-369: header row, then one call per unordered region pair."""
+    """extract_umis.py:345-369: header row, then one task per unordered region pair; ray.get raises the first
+    task's exception (an empty region 1's ValueError) after every task has run and appended its rows."""
     region_dirs = [os.path.dirname(fa) for fa in smolecule_filtered_fa_list]
     tsv = os.path.join(logs_dir, "regions_w_overlapping_umis.tsv")
     with open(tsv, "a") as tsv_out:
         print("region_1", "region_2", "umi_overlap_count", sep="\t", file=tsv_out)
-    return [count_overlapping_umis_between_2_regions(r1, r2, tsv, overlapping_umi_edit_threshold)
-            for r1, r2 in itertools.combinations(region_dirs, 2)]
+    out, first_exc = [], None
+    for r1, r2 in itertools.combinations(region_dirs, 2):
+        try:
+            out.append(count_overlapping_umis_between_2_regions(r1, r2, tsv, overlapping_umi_edit_threshold))
+        except ValueError as e:
+            first_exc = first_exc or e
+    if first_exc is not None:
+        raise first_exc
+    return out

@@ -4,7 +4,9 @@ outputs of count_overlapping_umis_between_all_regions / count_overlapping_umis_b
 
 `ray`, `pysam` and `edlib` are not installed (ordinary ModuleNotFoundError).  They are
 replaced by stand-ins that execute nothing from the data: ray.remote(...) returns an object whose .remote()
-calls the function directly and ray.get() returns its argument (so TSV rows come in
+calls the function directly and returns a future holding its value or its exception, and ray.get() of a list
+of futures returns their values or, after every task has run, raises the first exception in list order --
+Ray's semantics: one failing task does not stop the others from appending their TSV rows (TSV rows come in
 itertools.combinations order); pysam.FastxFile is the FASTA iterator of make_golden.py; edlib.align is never
 called (its call is commented out upstream) and raises if it were.  Only data is written to the fixtures.
 
@@ -28,12 +30,19 @@ import make_golden  # noqa: E402  (the pysam stand-in and the module loader)
 def _stubs():
     make_golden._stub_modules()  # pysam + a pass-through ray, replaced below
 
+    class _Future:
+        def __init__(self, f, a, k):
+            try:
+                self.value, self.exc = f(*a, **k), None
+            except Exception as e:  # noqa: BLE001 -- held until ray.get, as Ray does
+                self.value, self.exc = None, e
+
     class _Remote:
         def __init__(self, f):
             self.f = f
 
         def remote(self, *a, **k):
-            return self.f(*a, **k)
+            return _Future(self.f, a, k)
 
         def options(self, **_k):
             return self
@@ -43,7 +52,20 @@ def _stubs():
 
     ray = types.ModuleType("ray")
     ray.remote = lambda *a, **k: (_Remote(a[0]) if a and callable(a[0]) else (lambda f: _Remote(f)))
-    ray.get = lambda x: x
+    def _get(x):
+        if isinstance(x, list):
+            vals = [_get(y) if not isinstance(y, _Future) or y.exc is None else y for y in x]
+            for y in vals:
+                if isinstance(y, _Future):
+                    raise y.exc
+            return vals
+        if isinstance(x, _Future):
+            if x.exc is not None:
+                raise x.exc
+            return x.value
+        return x
+
+    ray.get = _get
     sys.modules["ray"] = ray
     edlib = types.ModuleType("edlib")
 
@@ -119,6 +141,7 @@ def main():
         _case(rng, "empty_region_2", 3, [20], 10, 0.9, empty=(2,)),
         _case(rng, "empty_region_1", 3, [20], 10, 0.9, empty=(0,)),
         _case(rng, "many_regions", 12, [10, 50, 120], 200, 0.6),
+        _case(rng, "empty_region_mid", 5, [20, 30], 10, 0.9, empty=(2,)),
     ]
     od = os.path.join(HERE, "overlap")
     os.makedirs(od, exist_ok=True)

@@ -59,3 +59,50 @@ def test_hash_collision_reseeds_exactly(monkeypatch):
     with _lib.Context(0) as ctx:
         got = ctx.overlap_counts(s1, s2)
     assert got.tolist() == oracle.overlap_counts(s1, s2)
+
+
+def test_regions_shared_artifact_umi(gpu_ctx):
+    """one consensus UMI present in hundreds of regions (an adapter artifact) -- its bucket goes to the
+    workgroup-per-bucket path (k_ov_pairs_big) instead of one thread's quadratic loops; exact against the oracle."""
+    rng = random.Random(13)
+    art = "ACGT" * 16
+    pool = ["".join(rng.choice("ACG") for _ in range(60)) for _ in range(300)]
+    regions = []
+    for r in range(400):
+        seqs = [rng.choice(pool) for _ in range(rng.randint(0, 6))] + [art] * rng.randint(0, 3)
+        rng.shuffle(seqs)
+        regions.append(seqs)
+    total, maxc = gpu_ctx.overlap_regions(regions)
+    for a in range(len(regions)):
+        for b in range(a + 1, len(regions)):
+            c = oracle.overlap_counts(regions[a], regions[b])
+            assert total[a, b] == sum(c) and maxc[a, b] == (max(c) if c else 0), (a, b)
+
+
+def test_all_regions_in_blocks_past_the_region_cap(tmp_path, monkeypatch):
+    """More regions than one join holds (UMICLUST_OVERLAP_MAX_REGIONS; lowered here to 8): row blocks joined with
+    every later block give the same files and results as the oracle, and an empty region 1 in the middle still
+    lets every other pair report before the ValueError."""
+    from test_overlap_cpu import materialize
+    from umiclust import _lib
+    monkeypatch.setattr(_lib, "OVERLAP_MAX_REGIONS", 8)
+    rng = random.Random(17)
+    pool = ["".join(rng.choice("ACGT") for _ in range(rng.randint(56, 70))) for _ in range(40)]
+    for empty in (None, 7):
+        regions = [dict(name=f"region_cluster{r}", seqs=[] if r == empty else
+                        [rng.choice(pool) for _ in range(rng.randint(1, 12))]) for r in range(21)]
+        case = dict(width=80, regions=regions)
+        d_gpu, d_orc = tmp_path / f"g{empty}", tmp_path / f"o{empty}"
+        d_gpu.mkdir()
+        d_orc.mkdir()
+        res = {}
+        for d, fn in ((d_gpu, overlap.count_overlapping_umis_between_all_regions),
+                      (d_orc, oracle.count_overlapping_umis_between_all_regions)):
+            fas, logs = materialize(d, case)
+            try:
+                res[str(d)] = ("ok", fn(fas, 2, logs))
+            except ValueError:
+                res[str(d)] = ("ValueError", None)
+            res[str(d)] += (tuple(open(os.path.join(logs, f)).read() for f in sorted(os.listdir(logs))),)
+        assert res[str(d_gpu)] == res[str(d_orc)]
+        assert res[str(d_gpu)][0] == ("ok" if empty is None else "ValueError")
