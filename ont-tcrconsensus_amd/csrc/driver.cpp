@@ -2913,7 +2913,7 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
     // the reference raises KeyError at the first record whose region is unknown, after the records before it
     int64_t stop = n;
     for (int64_t r = 0; r < n && stop == n; r++)
-      if (cls[r] == kBamNoRegion || cls[r] == kBamNoCluster) stop = r;
+      if (cls[r] == kBamNoRegion || cls[r] == kBamNoCluster || cls[r] == kBamNoCigar) stop = r;
     int32_t ncl = 0;
     for (int64_t r = 0; r < stop; r++)
       if (cls[r] == kBamKept) ncl = std::max(ncl, clu[r] + 1);
@@ -2975,6 +2975,8 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
       }
     }
     for (int x = 0; x < 4; x++) counts[x] = cnt[x];
+    if (stop < n && cls[stop] == kBamNoCigar)
+      c->fail(UMICLUST_EFORMAT, "TypeError: '<' not supported between instances of 'NoneType' and 'float'");
     if (stop < n) {
       const int32_t ref = rd_i32(raw.data() + roff[stop] + 4);
       const std::string nm = ref >= 0 && ref < nref ? refname[ref] : std::string("None");

@@ -43,6 +43,8 @@ __global__ void k_bam_classify(const uint8_t* __restrict__ raw, const int64_t* _
     c = kBamSecondary;
   } else if (ref < 0 || ref >= nref || ref_len[ref] < 0) {
     c = kBamNoRegion;  // region_length_dict[entry.reference_name] raises
+  } else if (ncig == 0) {
+    c = kBamNoCigar;  // pysam's reference_length is None without a CIGAR: `None < float` raises TypeError (:261)
   } else {
     const uint8_t* cg = p + 32 + lrn;
     int64_t rl = 0;
@@ -50,7 +52,6 @@ __global__ void k_bam_classify(const uint8_t* __restrict__ raw, const int64_t* _
       const uint32_t v = ld_u32(cg + 4 * x), op = v & 15u;
       if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += v >> 4;
     }
-    if (ncig == 0) rl = 1;  // pysam: bam_endpos() - pos is pos + 1 - pos without a CIGAR
     const double L = (double)ref_len[ref];
     if ((double)rl < L * minov) {
       c = kBamShort;

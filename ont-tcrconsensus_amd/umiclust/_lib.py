@@ -387,6 +387,8 @@ class Context:
                                          det.ctypes.data_as(P(C.c_uint8)), miss, 4096)
         if rc == -74 and miss.value:
             raise KeyError(miss.value.decode())
+        if rc == -74 and (lib().umiclust_last_error(self._h) or b"").startswith(b"TypeError: "):
+            raise TypeError(lib().umiclust_last_error(self._h).decode()[len("TypeError: "):])
         self._check(rc, "region_split")
         return counts, rpc[:cap], det[:R]
 

@@ -69,8 +69,8 @@ class AlignedSegment:
     def reference_length(self):
         if self.is_unmapped:
             return None
-        if not self.cigartuples:  # htslib bam_endpos: pos + 1 without a CIGAR
-            return 1
+        if not self.cigartuples:  # pysam: reference_end (hence reference_length) is None without a CIGAR
+            return None
         return sum(ln for op, ln in self.cigartuples if op in (0, 2, 3, 7, 8))
 
     def get_forward_sequence(self):

@@ -9,7 +9,9 @@ records read by oracle/bam.py (pysam is not installed):
     region_length * (2 - minimal_region_overlap) + max_softclip_5_end + max_softclip_3_end (:264-269);
   - a kept record goes to region_cluster<k>.fasta as `>{query_name};strand={+|-}` and its forward sequence
     (`None` when the record stores none, as print() writes it) (:271-283);
-  - the region-length and cluster lookups raise KeyError for a reference missing from them (:261, :271).
+  - the region-length and cluster lookups raise KeyError for a reference missing from them (:261, :271);
+  - a mapped primary record without a CIGAR has no reference_length (pysam: None) and the comparison at :261
+    raises TypeError, after the records before it.
 Pinned by tests/golden/region_split/*.json, the reference's own outputs (tests/test_region_split_cpu.py).
 With `out_dir` the records are appended one open() per record, as the reference does (:273-280): the
 CPU baseline of bench_rows.py times exactly that loop.

@@ -26,7 +26,7 @@ import make_golden  # noqa: E402
 
 
 def make_case(rng, name, n_regions, n_reads, minimal_region_overlap=0.95, s5=73, s3=68, pre_existing=False,
-              unknown_ref=False):
+              unknown_ref=False, no_cigar_at=None):
     regions = []
     for r in range(n_regions):
         suffix = rng.choice(["", "", "", "_v_n", "cdr3j_n", "full_n"]) if r > 1 else ""
@@ -70,6 +70,8 @@ def make_case(rng, name, n_regions, n_reads, minimal_region_overlap=0.95, s5=73,
             seq = ""  # secondary without a stored sequence
         records.append(dict(name=f"read{i:05d}", flag=flag, ref=ref if not flag & 4 or rng.random() < 0.5 else -1,
                             pos=rng.randint(0, 20), cigar=cigar, seq=seq))
+        if i == no_cigar_at:  # a mapped primary record without a CIGAR: pysam's reference_length is None
+            records[-1].update(flag=16, ref=0, cigar=[])
     pre = {}
     if pre_existing:  # the reference appends to region_cluster<k>.fasta
         pre = {f"region_cluster{clusters[regions[0][0]]}.fasta": ">old;strand=+\nACGT\n"}
@@ -116,6 +118,9 @@ def run_reference(mod, case):
         except KeyError as e:
             res["result"] = None
             res["error"] = f"KeyError: {e}"
+        except TypeError as e:  # None < float: a mapped primary record without a CIGAR
+            res["result"] = None
+            res["error"] = f"TypeError: {e}"
         res["out_files"] = {fn: open(os.path.join(out, fn)).read() for fn in sorted(os.listdir(out))}
         res["log_files"] = {fn: open(os.path.join(logs, fn)).read() for fn in sorted(os.listdir(logs))}
         return res
@@ -131,7 +136,8 @@ def main():
     cases = [make_case(rng, "small", 6, 150), make_case(rng, "many_regions", 30, 500),
              make_case(rng, "loose_overlap", 8, 250, minimal_region_overlap=0.5, s5=10, s3=10),
              make_case(rng, "append_existing", 5, 150, pre_existing=True),
-             make_case(rng, "unknown_reference", 5, 150, unknown_ref=True)]
+             make_case(rng, "unknown_reference", 5, 150, unknown_ref=True),
+             make_case(rng, "no_cigar", 5, 150, no_cigar_at=97)]
     od = os.path.join(HERE, "region_split")
     os.makedirs(od, exist_ok=True)
     for c in cases:

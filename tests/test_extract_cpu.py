@@ -57,3 +57,57 @@ def test_records_and_strand():
     assert txt.endswith(ox.reverse_complement(u3) + ox.reverse_complement(u5) + "\n")
     with pytest.raises(Exception):
         ox.extract_records([("r1", seq)], 73, 68, 3, FWD, rev)
+
+
+# ---- pinned by the reference itself: tests/golden/extract (make_golden_extract.py ran extract_umis.py here) ----
+import glob as _glob
+import json as _json
+import os as _os
+
+EXTRACT_FIX = sorted(_glob.glob(_os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "golden", "extract",
+                                              "*.json")))
+
+
+def _records(text):
+    """pysam.FastxFile's view of a FASTA/FASTQ text: (name up to whitespace, joined sequence)."""
+    lines = [x.rstrip("\r") for x in text.split("\n")]
+    fastq = any(x for x in lines) and next(x for x in lines if x).startswith("@")
+    recs, i = [], 0
+    while i < len(lines):
+        if not lines[i]:
+            i += 1
+            continue
+        name = lines[i][1:].split()[0]
+        i += 1
+        seq = []
+        while i < len(lines) and not lines[i].startswith(">") and not (fastq and lines[i].startswith("+")):
+            seq.append(lines[i].strip())
+            i += 1
+        s = "".join(seq)
+        if fastq:
+            i += 1
+            q = 0
+            while i < len(lines) and q < len(s):
+                q += len(lines[i])
+                i += 1
+        recs.append((name, s))
+    return recs
+
+
+@pytest.mark.parametrize("path", EXTRACT_FIX, ids=[_os.path.basename(p)[:-5] for p in EXTRACT_FIX])
+def test_oracle_glue_matches_reference_fixtures(path):
+    """The oracle's restated glue (oracle/extract.extract_records: strand split, read name, windows, skips,
+    header and combined-UMI format) reproduces the reference's output records."""
+    case = _json.load(open(path))
+    a = dict(case["args"])
+    a.pop("write_region")
+    recs = _records(case["input"])
+    want = list(case["files"].values())[0]
+    if case["error"]:
+        bad = next(i for i, (n, _s) in enumerate(recs) if "strand=" not in n)
+        got, _n = ox.extract_records(recs[:bad], **a)
+        with pytest.raises(Exception, match="Read strand not annotated!"):
+            ox.extract_records(recs, **a)
+    else:
+        got, _n = ox.extract_records(recs, **a)
+    assert got == want

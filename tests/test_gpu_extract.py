@@ -120,3 +120,32 @@ def test_no_umi_returns_none(tmp_path):
     src.write_text(">a;strand=+\n" + "ACGT" * 50 + "\n")
     assert ge.extract_umis(str(src), str(tmp_path), True) is None
     assert (tmp_path / "r_detected_umis.fasta").read_text() == ""
+
+
+# ---- pinned by the reference itself: tests/golden/extract (make_golden_extract.py ran extract_umis.py here) ----
+import glob as _glob
+import json as _json
+
+_EXTRACT_FIX = sorted(_glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "extract",
+                                              "*.json")))
+
+
+@pytest.mark.parametrize("path", _EXTRACT_FIX, ids=[os.path.basename(p)[:-5] for p in _EXTRACT_FIX])
+def test_extract_umis_vs_reference_fixtures(tmp_path, path):
+    """umiclust.extract_umis byte for byte against the reference's extract_umis outputs: FASTA and multi-line
+    FASTQ input, write_region True/False (the output-path rule), a zero 3' window (`seq[-0:]` = the whole read),
+    a zero 5' window, the run_config.json patterns at k = 0 and 3, extra `;` fields after strand=, lowercase
+    reads, `N`s, no read with both UMIs (returns None, empty file), and a record without `strand=` (the records
+    before it written, then the exception)."""
+    case = _json.load(open(path))
+    src = tmp_path / case["file_name"]
+    src.write_text(case["input"])
+    out = tmp_path / "out"
+    out.mkdir()
+    if case["error"]:
+        with pytest.raises(Exception):
+            ge.extract_umis(str(src), str(out), **case["args"])
+    else:
+        ret = ge.extract_umis(str(src), str(out), **case["args"])
+        assert (None if ret is None else os.path.relpath(ret, out)) == case["returned"]
+    assert {f: open(os.path.join(out, f)).read() for f in sorted(os.listdir(out))} == case["files"]

@@ -31,6 +31,7 @@ def test_bam_round_trip(tmp_path, case):
 def test_fixtures_cover_the_branches():
     cs = {c["name"]: c for c in cases()}
     assert cs["unknown_reference"]["error"].startswith("KeyError")
+    assert cs["no_cigar"]["error"].startswith("TypeError")
     assert cs["append_existing"]["out_files"][next(iter(cs["append_existing"]["pre_existing"]))].startswith(">old")
     flags = {r["flag"] & 0x914 for c in cs.values() for r in c["records"]}
     assert {0, 4, 16, 256, 2048} <= flags | {x & ~16 for x in flags}
@@ -47,9 +48,10 @@ def test_oracle_restatement_vs_reference_fixtures(case):
     kw = dict(minimal_region_overlap=case["minimal_region_overlap"], max_softclip_5_end=case["max_softclip_5_end"],
               max_softclip_3_end=case["max_softclip_3_end"])
     if case["error"]:
-        with pytest.raises(KeyError) as e:
+        exc = KeyError if case["error"].startswith("KeyError") else TypeError
+        with pytest.raises(exc) as e:
             ors.split_records(recs, lengths, case["clusters"], **kw)
-        assert f"KeyError: {e.value}" == case["error"]
+        assert f"{exc.__name__}: {e.value}" == case["error"]
         return
     counts, per_cluster, texts, _ = ors.split_records(recs, lengths, case["clusters"], **kw)
     want = {fn: t[len(case["pre_existing"].get(fn, "")):] for fn, t in case["out_files"].items()}
