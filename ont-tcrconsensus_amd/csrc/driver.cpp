@@ -1977,13 +1977,19 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   c->stats.t_consensus_s = t_cons;
   c->stats.t_host_s = t_host;
   if (c->pf_prof.p) {
-    unsigned long long h[9];
+    unsigned long long h[16];
     c->hip(hipMemcpy(h, c->pf_prof.p, sizeof(h), hipMemcpyDeviceToHost), "d2h");
     const double nwg = h[8] ? (double)h[8] : 1.0;
     fprintf(stderr,
             "prefilter phase clocks per workgroup (%llu): query %.0f views %.0f offsets %.0f table %.0f count %.0f "
             "scan %.0f select %.0f out %.0f\n",
             h[8], h[5] / nwg, h[6] / nwg, h[7] / nwg, h[0] / nwg, h[1] / nwg, h[2] / nwg, h[3] / nwg, h[4] / nwg);
+    const double nc = h[14] ? (double)h[14] : 1.0;
+    fprintf(stderr,
+            "k_pf_count phase clocks per workgroup (%llu sampled): zero %.0f table %.0f count %.0f scan %.0f "
+            "peers+out %.0f; chunks per workgroup %.1f\n",
+            h[14], h[9] / nc, h[10] / nc, h[11] / nc, h[12] / nc, h[13] / nc, h[15] / nc);
+    c->hip(hipMemset(c->pf_prof.p, 0, 16 * sizeof(unsigned long long)), "memset");
   }
   c->stats.t_total_s = now_s() - t0;
   c->clustered = true;
@@ -2268,7 +2274,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
-    if (c->pf_prof.ensure(9) != hipSuccess || hipMemset(c->pf_prof.p, 0, 9 * sizeof(unsigned long long)) != hipSuccess) {
+    if (c->pf_prof.ensure(16) != hipSuccess || hipMemset(c->pf_prof.p, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;
       if (err) *err = UMICLUST_EDEVICE;
       return nullptr;

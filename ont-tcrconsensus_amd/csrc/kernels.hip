@@ -1046,6 +1046,16 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   const int ncnt = kCentBase + ((nsubC + 15) & ~15);
   const uint64_t pbase = a.seg_base[0];
   const __amdgpu_buffer_rsrc_t arena = arena_rsrc(uniform_ptr(a.arena + pbase));
+  // optional phase timing (UMICLUST_PFPROF: a.prof != nullptr): thread 0's shader-clock deltas between the
+  // phase barriers of sampled workgroups, into a.prof[9 + i] (k_pf_full uses [0, 9))
+  const bool prof = a.prof != nullptr && tid == 0 && (blockIdx.x % 61u) == 0u;
+  unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[5] = {0, 0, 0, 0, 0};
+#define PFC_MARK(i)                                             \
+  if (prof) {                                                   \
+    const unsigned long long tn = __builtin_readcyclecounter(); \
+    tacc[i] += tn - tprev;                                      \
+    tprev = tn;                                                 \
+  }
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
   for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) {
@@ -1053,10 +1063,13 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     H.npc = 0;
   }
   uint32_t T, nlc;
+  PFC_MARK(0)
   pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
                 km0, km1, wv, lane, tid, T, nlc);
+  PFC_MARK(1)
   if (T > 0) pf_count_stream<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
   __syncthreads();
+  PFC_MARK(2)
   if (wv == 0) {
     // postings touched (stats): every chunk posting minus the padding ones (the spare counters)
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
@@ -1092,6 +1105,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
       }
     }
   }
+  PFC_MARK(3)
   // peers: the window queries before q, every count >= thr (all of them when thr == 0)
 #pragma unroll
   for (int v = 0; v < kPeerTiles; v++) {
@@ -1151,6 +1165,13 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     a.pnpeer[pq_] = (uint8_t)(np > (uint32_t)kPeerCap ? 255u : np);
     if (ovf) a.units[atomicAdd(a.nunits, 1u)] = (uint32_t)pq_;
   }
+  PFC_MARK(4)
+  if (prof) {
+    for (int i = 0; i < 5; i++) atomicAdd(&a.prof[9 + i], tacc[i]);
+    atomicAdd(&a.prof[14], 1ull);
+    atomicAdd(&a.prof[15], (unsigned long long)T);
+  }
+#undef PFC_MARK
 }
 
 // One wave per query-strand.  Candidates: the parts' lists (distinct ordinals) get their u64 keys
