@@ -397,6 +397,20 @@ def _tree_bytes(d: str) -> tuple[int, int]:
     return n, b
 
 
+def write_probe_mmap(d: str, nbytes: int, threads: int) -> dict:
+    """tools/io_probe.c io_probe_mmap: nbytes into one file through a shared mapping from `threads` threads."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libioprobe.so"))
+    lib.io_probe_mmap.restype = ctypes.c_double
+    lib.io_probe_mmap.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int]
+    pd = os.path.join(d, "probe")
+    os.mkdir(pd)
+    t = lib.io_probe_mmap(pd.encode(), nbytes, threads)
+    os.rmdir(pd)
+    if t < 0:
+        raise RuntimeError("io_probe_mmap failed")
+    return dict(files=1, bytes=nbytes, threads=threads, seconds=t, gbps=nbytes / t / 1e9 if t > 0 else None)
+
+
 def write_probe(d: str, nfiles: int, nbytes: int, threads: int, fsync: bool = False) -> dict:
     """tools/io_probe.c: nbytes into nfiles equal files (or slices of one file) from `threads` threads on the
     filesystem of d, the shape the writers use; seconds, GB/s (and the fsync'd commit rate when asked)."""
@@ -433,6 +447,8 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
         synth.write_umi_fasta_fast(fa, umis, read_len=read_len)
         t_gen = time.perf_counter() - t0
         size = os.path.getsize(fa)
+        # every timed write below starts with no dirty pages of an earlier phase still draining (untimed sync)
+        os.sync()
         out = os.path.join(d, "out")
         os.mkdir(out)
         p = _lib.params(_lib.PRESET_ROUND1, identity, *lens)
@@ -442,7 +458,9 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
         t_run = time.perf_counter() - t0
         nf, nb = _tree_bytes(out)
         shutil.rmtree(out, ignore_errors=True)
+        os.sync()
         probe = write_probe(d, nf, nb, io_t)
+        os.sync()
         # the fused drop-in (run_config.json:17-19 defaults: >= 4 reads, <= 60 per cluster, no strand balancing)
         work = os.path.join(d, "work")
         os.mkdir(work)
@@ -455,8 +473,13 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
         smol = os.path.getsize(os.path.join(work, "smolecule_clusters.fa"))
         _, nb_all = _tree_bytes(work)
         shutil.rmtree(work, ignore_errors=True)
+        os.sync()
         probe_f = write_probe(d, nf2, nb2, io_t)
+        os.sync()
         probe_s = write_probe(d, 1, smol, io_t)
+        os.sync()
+        probe_s_mmap = write_probe_mmap(d, smol, io_t)
+        os.sync()
         disk = write_probe(d, 1, 2 << 30, io_t, fsync=True)
         fused_probe_s = probe_f["seconds"] + probe_s["seconds"]
         return dict(
@@ -471,12 +494,13 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
                              clusters_written=pr["n_written"], cluster_files=nf2, cluster_file_bytes=nb2,
                              smolecule_bytes=smol, bytes_written=nb_all,
                              write_gbps=nb_all / st2["t_write_s"] / 1e9 if st2.get("t_write_s") else None,
-                             probe_files=probe_f, probe_smolecule=probe_s,
+                             probe_files=probe_f, probe_smolecule=probe_s, probe_smolecule_mmap=probe_s_mmap,
                              write_frac=fused_probe_s / st2["t_write_s"] if st2.get("t_write_s") else None),
             disk_commit=disk,
-            note="page-cache-warm input; outputs on the box's local disk ($TMPDIR); write_frac = seconds of the "
-                 "write probe (same files and bytes, same threads, no fsync, as the writers) / the writer's seconds; "
-                 "disk_commit = a 2 GiB file written and fsync'd (the rate once the page cache must drain)")
+            note="page-cache-warm input; outputs on the box's local disk ($TMPDIR); every timed write (writers and "
+                 "probes) starts after an untimed sync; write_frac = seconds of the write probe (same files and bytes, "
+                 "same threads, no fsync, as the writers) / the writer's seconds; probe_smolecule_mmap = the one-file "
+                 "probe through a shared mapping instead of pwrite; disk_commit = a 2 GiB file written and fsync'd")
     finally:
         shutil.rmtree(d, ignore_errors=True)
 

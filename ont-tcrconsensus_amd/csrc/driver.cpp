@@ -187,7 +187,7 @@ struct Pass {
   // parallel classification of the pass's query-strands (resolve_pass): 0 the device outcome is final,
   // 1 final unless one of its in-block relevant peers (deps) turns out a centroid or is undetermined,
   // 2 resolved sequentially in full
-  std::vector<uint8_t> kind, ndeps, pre_cert;
+  std::vector<uint8_t> kind, ndeps, pre_cert, done;
   std::vector<uint16_t> deps;
   std::vector<Outcome> pre;  // outcomes the classify threads resolved (kind 3) or found needing round B (kind 4)
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
@@ -955,6 +955,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;
   a.ppost = P.d_ppost.p;
+  a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
   c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
   c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
   c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
@@ -1360,18 +1361,65 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       }
     }
   };
+  // A query whose strands are all final here (kinds 0 and 3: no in-block dependency) is resolved here too: its
+  // outcome needs no in-order state, and only in-block queries ever read its state, in phase 2, after this
+  // phase.  P.done: 0 pending (phase 2), 1 member, 2 centroid.
+  P.done.resize((size_t)nq);
+  struct Acc {
+    int64_t aln = 0, cells = 0;
+  };
+  auto classify_query = [&](int32_t ql, Scratch& scr, Acc& acc) {
+    bool det = true;
+    for (int s = 0; s < both; s++) {
+      const int32_t qs = ql * both + s;
+      classify(qs, scr);
+      det &= P.kind[qs] == 0 || P.kind[qs] == 3;
+    }
+    if (!det) {
+      P.done[ql] = 0;
+      return;
+    }
+    Outcome best, os[2];
+    int bs = 0;
+    for (int s = 0; s < both; s++) {
+      const int32_t qs = ql * both + s;
+      if (P.kind[qs] == 0) device_outcome(hq[qs], os[s]);
+      else os[s] = P.pre[qs];
+      acc.aln += os[s].walked;
+      acc.cells += os[s].cells;
+      if (better(os[s], best)) {
+        best = os[s];
+        bs = s;
+      }
+    }
+    const int32_t q = q0 + ql;
+    if (best.acc) {
+      state[q] = ST_MEMBER;
+      c->target[q] = (int32_t)best.t;
+      c->strand[q] = (uint8_t)bs;
+      P.done[ql] = 1;
+    } else {
+      state[q] = ST_CENT;
+      P.done[ql] = 2;
+    }
+  };
   if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
   const int T = nqs < 2048 ? 1 : c->pool->size();
   std::vector<Scratch> scr_t((size_t)T);
+  std::vector<Acc> acc_t((size_t)T);
   if (T == 1) {
-    for (int32_t qs = 0; qs < nqs; qs++) classify(qs, scr_t[0]);
+    for (int32_t ql = 0; ql < nq; ql++) classify_query(ql, scr_t[0], acc_t[0]);
   } else {
     c->pool->run([&](int t) {
-      const int32_t lo = (int32_t)((int64_t)nqs * t / T), hi = (int32_t)((int64_t)nqs * (t + 1) / T);
-      for (int32_t qs = lo; qs < hi; qs++) classify(qs, scr_t[(size_t)t]);
+      const int32_t lo = (int32_t)((int64_t)nq * t / T), hi = (int32_t)((int64_t)nq * (t + 1) / T);
+      for (int32_t ql = lo; ql < hi; ql++) classify_query(ql, scr_t[(size_t)t], acc_t[(size_t)t]);
     });
   }
   for (const Scratch& x : scr_t) c->stats.n_merged_walks += x.merged;
+  for (const Acc& x : acc_t) {
+    c->stats.n_alignments += x.aln;
+    c->stats.cells += x.cells;
+  }
   const double tp1 = now_s();
   c->dbg_t[3] += tp1 - tp0;
   // Phase 2 (sequential, sorted order): confirm the device outcomes against the in-block peers' states
@@ -1408,8 +1456,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
     return strand_outcome(qs, q, false, o, cert);
   };
-  for (int32_t ql = 0; ql < nq; ql++)
-    if (!resolve(ql, false, strand_fast)) deferred.push_back(ql);
+  for (int32_t ql = 0; ql < nq; ql++) {
+    const uint8_t d = P.done[ql];
+    if (d == 2) new_cents.push_back(q0 + ql);
+    else if (d == 0 && !resolve(ql, false, strand_fast)) deferred.push_back(ql);
+  }
   c->dbg_q[3] += (int64_t)((now_s() - tp0) * 1e9);
   c->dbg_t[4] += now_s() - tp1;
   t_host += now_s() - th0;

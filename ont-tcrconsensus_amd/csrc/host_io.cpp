@@ -446,6 +446,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     int64_t n_fwd = 0, n_rev = 0, found = 0, max_fwd = 0, max_rev = 0, w_fwd = 0, w_rev = 0, w_all = 0;
     int written = 0, err = 0;
     int64_t noseq_at = -1;  // the first entry to write without a seq= field (an IndexError mid-cluster)
+    int64_t smol_bytes = 0; // this cluster's smolecule_clusters.fa records (">{k}\n{read}\n" per entry written)
     std::string msg;
   };
   struct Scratch {
@@ -533,6 +534,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       r.w_rev = std::min<int64_t>((int64_t)sc.kept[1].size(), r.max_rev);
       r.w_all = std::min<int64_t>(r.w_fwd + r.w_rev, max_reads);
       r.written = 1;
+      const int64_t head = 3 + (int64_t)std::to_string(k).size();  // '>' k '\n' ... '\n'
       for (int64_t y = 0; y < r.w_all; y++) {  // `cols[6].split("seq=")[1]` of every entry written (:106)
         const int32_t i = entry(r, sc, y);
         split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
@@ -543,6 +545,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
           r.msg = "IndexError: no seq= field in " + Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}.str();
           return false;
         }
+        r.smol_bytes += head + (int64_t)read.n;
       }
     }
     return true;
@@ -576,15 +579,61 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   // a missing seq= field interrupts cluster kerr after its first noseq_at entries: written like the others
   const bool partial = kerr >= 0 && res[kerr].noseq_at >= 0;
   const int32_t kwrite = partial ? kerr + 1 : kend;
+  if (partial) {  // the bytes of its first noseq_at entries (analyze stopped counting at the failing one)
+    const int64_t head = 3 + (int64_t)std::to_string(kerr).size();
+    PClus r;
+    Scratch sc;
+    analyze(kerr, r, sc);
+    res[kerr].smol_bytes = 0;
+    for (int64_t y = 0; y < res[kerr].noseq_at; y++) {
+      const int32_t i = entry(r, sc, y);
+      split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
+      Sv read;
+      split1(sc.fields[6], "seq=", read);
+      res[kerr].smol_bytes += head + (int64_t)read.n;
+    }
+  }
+  // smolecule_clusters.fa: every read written once more (GBs at production depth).  Its records are laid out
+  // by cluster in advance (offsets from the counts above), and each writing thread pwrites its clusters' records
+  // at their offset as soon as its range is done, beside the other threads' cluster files.  (A shared mapping of
+  // the file was measured 5x slower than pwrite on the GPU box's filesystem: 2.2 vs 10.4 GB/s,
+  // profiles/r03/e2e_probes.json.)
+  std::vector<int64_t> smol_off((size_t)kwrite + 1, 0);
+  for (int32_t k = 0; k < kwrite; k++) smol_off[k + 1] = smol_off[k] + res[k].smol_bytes;
+  const std::string smol_path = pjoin(work_dir, "smolecule_clusters.fa");
+  const int smol_fd = open(smol_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  if (smol_fd < 0) throw IoError{UMICLUST_EIO, "cannot write smolecule_clusters.fa"};
   // cluster files and the text of clusters [0, kwrite), on the threads
   const std::vector<int32_t> wcut = cluster_slices(cv.ostart, kwrite, T);
-  std::vector<std::string> smol_p(T), log_p(T), stats_p(T);
+  std::vector<std::string> log_p(T), stats_p(T);
+  std::vector<size_t> stats_beg((size_t)kwrite + 1, 0);  // a cluster's line starts here in its thread's part
   std::vector<int32_t> bad(T, -1);
-  std::vector<uint8_t> wrote((size_t)kwrite, 0);
+  std::vector<uint8_t> wrote((size_t)kwrite, 0), smol_bad(T, 0);
   parallel_for(T, [&](int t) {
     Scratch sc;
-    std::string lines, &smol = smol_p[t], &log = log_p[t], &stats_out = stats_p[t];
+    std::string lines, smol, &log = log_p[t], &stats_out = stats_p[t];
+    // this thread's records, contiguous in the file from its first cluster's offset (also on an early return:
+    // the clusters before a failing one keep their records, as the reference's buffered file does)
+    struct Flush {
+      std::string& s;
+      int fd;
+      off_t at;
+      uint8_t& bad;
+      ~Flush() {
+        size_t o = 0;
+        while (o < s.size()) {
+          const ssize_t w = pwrite(fd, s.data() + o, s.size() - o, at + (off_t)o);
+          if (w < 0) {
+            if (errno == EINTR) continue;
+            bad = 1;
+            return;
+          }
+          o += (size_t)w;
+        }
+      }
+    } flush{smol, smol_fd, (off_t)smol_off[wcut[t]], smol_bad[t]};
     for (int32_t k = wcut[t]; k < wcut[t + 1]; k++) {
+      stats_beg[k] = stats_out.size();
       PClus r;
       analyze(k, r, sc);
       const int64_t nw = (partial && k == kerr) ? res[k].noseq_at : r.w_all;
@@ -623,25 +672,30 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
                    "\t" + std::to_string(r.w_all) + "\t" + std::to_string(r.written) + "\n";
     }
   });
-  // an unwritable cluster file: the reference stops there (OSError) -- files the other threads wrote past it go
+  // an unwritable cluster file: the reference stops there (OSError) -- files the other threads wrote past it go,
+  // and the stats and smolecule records end before it, as the reference's `with` blocks leave them
   int32_t kbad = -1;
   for (int t = 0; t < T; t++)
     if (bad[t] >= 0 && (kbad < 0 || bad[t] < kbad)) kbad = bad[t];
-  if (kbad >= 0) {
+  const int32_t kkeep = kbad >= 0 ? kbad : kwrite;
+  if (kbad >= 0)
     for (int32_t k = kbad + 1; k < kwrite; k++)
       if (wrote[k]) unlink(pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta").c_str());
-    throw IoError{UMICLUST_EIO, "cannot write " + pjoin(fa_dir, "cluster" + std::to_string(kbad) + ".fasta")};
-  }
+  bool smol_ok = true;
+  for (int t = 0; t < T; t++) smol_ok = smol_ok && !smol_bad[t];
+  if (kbad >= 0) smol_ok = ftruncate(smol_fd, (off_t)smol_off[kkeep]) == 0 && smol_ok;
+  smol_ok = close(smol_fd) == 0 && smol_ok;
   std::string stats_out = "id_cluster\tn_fwd\tn_rev\twritten_fwd\twritten_rev\tn\twritten\tcluster_written\n", log;
   for (int t = 0; t < T; t++) {
-    stats_out += stats_p[t];
+    if (wcut[t] >= kkeep) break;
+    stats_out.append(stats_p[t], 0, kkeep < wcut[t + 1] ? stats_beg[kkeep] : stats_p[t].size());
     log += log_p[t];
   }
   if (!write_file(pjoin(work_dir, "vsearch_cluster_stats.tsv"), stats_out))
     throw IoError{UMICLUST_EIO, "cannot write the stats table"};
-  // every read once more (GBs at production depth): the threads' parts side by side
-  if (!write_parts(pjoin(work_dir, "smolecule_clusters.fa"), smol_p))
-    throw IoError{UMICLUST_EIO, "cannot write smolecule_clusters.fa"};
+  if (!smol_ok) throw IoError{UMICLUST_EIO, "cannot write smolecule_clusters.fa"};
+  if (kbad >= 0)
+    throw IoError{UMICLUST_EIO, "cannot write " + pjoin(fa_dir, "cluster" + std::to_string(kbad) + ".fasta")};
   if (kerr >= 0) throw IoError{res[kerr].err, res[kerr].msg};
   pr->n_clusters = K;
   pr->n_written = n_written;

@@ -730,6 +730,64 @@ __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, ui
   }
 }
 
+// The same count with the window addresses computed ahead, kPfPre windows at a time: window() reads the list
+// table in LDS, and an LDS read waits for every LDS operation the wave issued before it -- in the loop above
+// that is the counting atomics of the previous windows, so each pair of windows drained the wave's atomics
+// before its next loads could even be addressed.  Here a round's addresses come first (the table reads of a
+// whole round in flight together, behind no atomics at the start of the stream), then the round's chunks
+// stream through kPfAhead loads in flight while the atomics are issued without any LDS read between them.
+constexpr int kPfPre = 16, kPfAhead = 4;
+template <uint32_t kBase>
+__device__ __forceinline__ void pf_count_stream_pre(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
+                                                    const uint32_t* lstart, const uint32_t* lbias,
+                                                    const uint16_t* wbase, const uint32_t* wlo, const uint32_t* whi,
+                                                    int lane, int wv) {
+  const uint32_t nwin = (T + 63u) >> 6;
+  const unsigned long long below = (2ull << lane) - 1ull;
+  const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
+  const uint32_t below_hi = lane < 32 ? 0u : (2u << (lane - 32)) - 1u;
+  auto window = [&](uint32_t w) -> uint32_t {
+    if (w >= nwin) return 0xffffffffu;
+    const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
+    if (w < (uint32_t)kPfWinBase) {
+      const uint32_t L0 = wbase[w] + (uint32_t)__builtin_popcount(wlo[w] & below_lo) +
+                          (uint32_t)__builtin_popcount(whi[w] & below_hi);
+      return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
+    }
+    int lo = 0, hi = (int)nlc - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (lstart[mid] <= g0) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t m = (uint32_t)lo;
+    const uint32_t bit = lstart[m + 1 + lane] - g0;
+    uint32_t lo32 = bit < 32u ? 1u << bit : 0u, hi32 = bit - 32u < 32u ? 1u << (bit - 32u) : 0u;
+    wave_or2_dpp(lo32, hi32);
+    const unsigned long long sm = ((unsigned long long)lane63(hi32) << 32) | lane63(lo32);
+    const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
+    return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
+  };
+  constexpr uint32_t S1 = kPfWaves;
+  for (uint32_t w0 = (uint32_t)wv; w0 < nwin; w0 += kPfPre * S1) {  // wave-uniform
+    const uint32_t nb = min((uint32_t)kPfPre, (nwin - w0 + S1 - 1) / S1);  // windows of this round
+    uint32_t ad[kPfPre];
+#pragma unroll
+    for (int i = 0; i < kPfPre; i++) ad[i] = (uint32_t)i < nb ? window(w0 + i * S1) : 0xffffffffu;
+    uint4 v[kPfAhead];
+#pragma unroll
+    for (int i = 0; i < kPfAhead; i++) v[i] = ld_chunk(arena, ad[i] == 0xffffffffu ? 0u : ad[i]);
+#pragma unroll
+    for (int i = 0; i < kPfPre; i++) {
+      if ((uint32_t)i >= nb) break;
+      const uint4 cur = v[i % kPfAhead];
+      if (i + kPfAhead < kPfPre && (uint32_t)(i + kPfAhead) < nb)
+        v[i % kPfAhead] = ld_chunk(arena, ad[i + kPfAhead] == 0xffffffffu ? 0u : ad[i + kPfAhead]);
+      pf_chunk<kBase>(cur, ad[i] != 0xffffffffu ? 1u : 0u);
+    }
+  }
+}
+
 // The full counting kernel: every counter segment (bins beyond kSegCentroids centroids) and the exact
 // selection of a part's top-41 for any candidate count (it also re-runs the units the lean kernel could
 // not finish: more than kPartCand candidates, or a threshold of 0).  One (query-strand, part) unit.
@@ -1020,6 +1078,7 @@ struct PfCountHdr {
 __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
   return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 2 + 2 * kPfWinBase * 4 + (2 * nlist_cap + 66) * 4);
 }
+template <int CM>
 __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
@@ -1067,7 +1126,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
                 km0, km1, wv, lane, tid, T, nlc);
   PFC_MARK(1)
-  if (T > 0) pf_count_stream<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
+  if (T > 0) {
+    if (CM == 1) pf_count_stream_pre<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
+    else pf_count_stream<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
+  }
   __syncthreads();
   PFC_MARK(2)
   if (wv == 0) {
@@ -1314,7 +1376,9 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   if (!attr_set_on_device(k_attr_prefilter)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_pf_count, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+      e = hipFuncSetAttribute((const void*)k_pf_count<0>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_pf_count<1>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
     if (e != hipSuccess) return e;
     mark_attr_set(k_attr_prefilter);
   }
@@ -1327,8 +1391,15 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     // lean counting (one counter segment)
     if (a.nseg > 1 || a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
     const uint32_t tab_off = (uint32_t)(kCentBase + sub);
-    hipLaunchKernelGGL(k_pf_count, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
-                       st, a, tab_off);
+    // UMICLUST_PFCOUNT: 0 (default) the paired loop, 1 addresses computed a round ahead (pf_count_stream_pre:
+    // measured slower on config 2, 2.13 vs 1.55 ms per launch, profiles/r03/pfcount_ab.json)
+    static const int cm = getenv("UMICLUST_PFCOUNT") ? atoi(getenv("UMICLUST_PFCOUNT")) : 0;
+    if (cm == 1)
+      hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
+                         st, a, tab_off);
+    else
+      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
+                         st, a, tab_off);
     if (mode == 1) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {

@@ -29,6 +29,12 @@ for st in "$@"; do
     write) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B \
              > "$out/write.log" 2>&1; rc=$? ;;
     pfprof) UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof.json" 2> "$out/pfprof.err"; rc=$? ;;
+    pfab) for cm in 0 1; do
+            UMICLUST_PFCOUNT=$cm timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+              > "$out/pfab$cm.json" 2> "$out/pfab$cm.err" || { rc=$?; break; }
+            UMICLUST_PFCOUNT=$cm UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof$cm.json" \
+              2> "$out/pfprof$cm.err" || { rc=$?; break; }
+          done ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 $B > "$out/trace.log" 2>&1; rc=$? ;;
     c3) timeout -k 10 500 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;

@@ -7,6 +7,8 @@
  * one file (the shape of consout / smolecule_clusters.fa).  If `fsync_s` is not NULL every file is then
  * fsync'd and the extra seconds reported there (the disk-commit cost the writers never pay: they close
  * without fsync, as vsearch and Python's file objects do).  Files are removed afterwards (not timed).
+ * io_probe_mmap: the one-file shape written through a shared mapping instead (ftruncate, mmap, the threads
+ * copy their slices, munmap, close): buffered write()/pwrite() into one file serialise on its inode lock.
  *
  * Built by __graft_entry__.build() into tools/libioprobe.so; loaded by bench.py with ctypes.
  */
@@ -14,6 +16,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <sys/mman.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -136,6 +139,61 @@ double io_probe(const char *dir, int64_t nfiles, int64_t total, int threads, dou
   }
   free(jobs);
   free(th);
+  free(buf);
+  return err ? -1.0 : dt;
+}
+
+typedef struct {
+  char *map;
+  int64_t total;
+  int threads, t;
+  const char *buf;
+  int64_t bufsz;
+} mjob_t;
+
+static void *mmap_worker(void *arg) {
+  mjob_t *j = (mjob_t *)arg;
+  int64_t a = j->total * j->t / j->threads, b = j->total * (j->t + 1) / j->threads;
+  while (a < b) {
+    int64_t n = b - a < j->bufsz ? b - a : j->bufsz;
+    memcpy(j->map + a, j->buf, (size_t)n);
+    a += n;
+  }
+  return NULL;
+}
+
+double io_probe_mmap(const char *dir, int64_t total, int threads) {
+  if (!dir || total <= 0 || threads < 1) return -1.0;
+  const int64_t bufsz = 1 << 20;
+  char *buf = (char *)malloc((size_t)bufsz);
+  if (!buf) return -1.0;
+  for (int64_t i = 0; i < bufsz; i++) buf[i] = "ACGT\n"[i % 5];
+  char path[4096];
+  snprintf(path, sizeof path, "%s/probe0", dir);
+  const double t0 = now_s();
+  int fd = open(path, O_RDWR | O_CREAT | O_TRUNC, 0666);
+  int err = fd < 0;
+  char *map = NULL;
+  if (!err && ftruncate(fd, total)) err = 1;
+  if (!err) {
+    map = (char *)mmap(NULL, (size_t)total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (map == MAP_FAILED) err = 1;
+  }
+  if (!err) {
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    mjob_t *jobs = (mjob_t *)calloc((size_t)threads, sizeof(mjob_t));
+    for (int t = 0; t < threads; t++) {
+      jobs[t] = (mjob_t){map, total, threads, t, buf, bufsz};
+      pthread_create(&th[t], NULL, mmap_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    munmap(map, (size_t)total);
+    free(jobs);
+    free(th);
+  }
+  if (fd >= 0) close(fd);
+  const double dt = now_s() - t0;
+  unlink(path);
   free(buf);
   return err ? -1.0 : dt;
 }
