@@ -161,8 +161,8 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
 
 def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     """Per-CU LDS-array and VALU busy of `kernel`, from the committed rocprofv3 PMC CSV
-    (profiles/r03/pmc_busy_<kernel>.csv: SQ_LDS_IDX_ACTIVE, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_WAVES,
-    GRBM_GUI_ACTIVE, ...; one pass, tools/gpu_pmc_r03.sh) with the unit factors measured by the calibration
+    (profiles/r03/pmc_busy_<kernel>.csv: SQ_LDS_IDX_ACTIVE, SQ_ACTIVE_INST_VALU, SQ_INSTS_LDS, SQ_INSTS_VALU,
+    GRBM_GUI_ACTIVE, ...; one pass, step `busy` of tools/gpu_r03.sh) with the unit factors measured by the calibration
     kernels of tools/pmc_calib.hip (profiles/r03/pmc_calib.json): LDS busy = LDS-array cycles per CU / kernel
     cycles, VALU busy = VALU issue cycles per SIMD / kernel cycles, kernel cycles = GRBM_GUI_ACTIVE / XCDs."""
     csv_path = os.path.join(ROOT, "profiles", "r03", f"pmc_busy_{kernel}.csv")
@@ -172,7 +172,8 @@ def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     cal = json.load(open(cal_path))
     tot, disp = {}, set()
     for r in csv.DictReader(open(csv_path, newline="")):
-        if r["Kernel_Name"].split("(")[0].split("<")[0] != kernel:
+        name = r["Kernel_Name"].replace("void ", "").split("(")[0].split("<")[0].split("::")[-1]
+        if name != kernel:
             continue
         disp.add(r["Dispatch_Id"])
         tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -186,7 +187,8 @@ def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     out = dict(source=os.path.relpath(csv_path, ROOT), calibration=os.path.relpath(cal_path, ROOT), dispatches=n,
                kernel_cycles=cyc, lds_array_busy_per_cu=lds, valu_busy_per_simd=valu,
                lds_bank_conflict_frac=per.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, per["SQ_LDS_IDX_ACTIVE"]),
-               waves_resident_per_cu=per["SQ_WAVE_CYCLES"] * cal["wave_cycles_per_unit"] / cal["cus"] / cyc)
+               lds_array_cycles_per_instr=per["SQ_LDS_IDX_ACTIVE"] / max(1.0, per.get("SQ_INSTS_LDS", 0.0)),
+               valu_instrs_per_lds_instr=per["SQ_INSTS_VALU"] / max(1.0, per.get("SQ_INSTS_LDS", 0.0)))
     return out
 
 

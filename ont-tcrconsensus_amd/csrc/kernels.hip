@@ -779,11 +779,12 @@ __device__ __forceinline__ void pf_count_stream_pre(__amdgpu_buffer_rsrc_t arena
     for (int i = 0; i < kPfAhead; i++) v[i] = ld_chunk(arena, ad[i] == 0xffffffffu ? 0u : ad[i]);
 #pragma unroll
     for (int i = 0; i < kPfPre; i++) {
-      if ((uint32_t)i >= nb) break;
-      const uint4 cur = v[i % kPfAhead];
-      if (i + kPfAhead < kPfPre && (uint32_t)(i + kPfAhead) < nb)
-        v[i % kPfAhead] = ld_chunk(arena, ad[i + kPfAhead] == 0xffffffffu ? 0u : ad[i + kPfAhead]);
-      pf_chunk<kBase>(cur, ad[i] != 0xffffffffu ? 1u : 0u);
+      if ((uint32_t)i < nb) {  // wave-uniform; no break, so the loop unrolls and v[] stays in registers
+        const uint4 cur = v[i % kPfAhead];
+        if (i + kPfAhead < kPfPre && (uint32_t)(i + kPfAhead) < nb)
+          v[i % kPfAhead] = ld_chunk(arena, ad[i + kPfAhead] == 0xffffffffu ? 0u : ad[i + kPfAhead]);
+        pf_chunk<kBase>(cur, ad[i] != 0xffffffffu ? 1u : 0u);
+      }
     }
   }
 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 GPU session: parity tests, the default bench line (config 2 + e2e), PMC calibration and the
 # k_pf_count busy pass, kernel trace.  Every GPU step has its own time limit; the first failure ends the call.
-# Usage: bash tools/gpu_r03.sh <tag> <steps...>   steps: tests | bench | calib | busy | trace | c3 | c4 | c5
+# Usage: bash tools/gpu_r03.sh <tag> <steps...>   steps: tests | bench | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5
 set -o pipefail
 tag=${1:-r03}
 shift
@@ -38,6 +38,9 @@ for st in "$@"; do
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 $B > "$out/trace.log" 2>&1; rc=$? ;;
     c3) timeout -k 10 500 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
+    c3trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c3trace" -o run -- \
+             python3 bench.py --config 3 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c3trace.log" 2>&1; rc=$?
+             rm -f "$out/c3trace/run_kernel_trace.csv" ;;  # ~10^5 dispatches: the stats file is what is kept
     c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
     c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
@@ -45,5 +48,6 @@ for st in "$@"; do
   echo "== $st rc=$rc $(date +%T)"
   [ $rc -ne 0 ] && break
 done
+du -sh "$out"
 for f in "$out"/*.json; do [ -f "$f" ] && { echo "--- $f"; cut -c1-400 "$f"; }; done
 exit $rc
