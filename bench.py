@@ -127,7 +127,12 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
     n_blocks = sum(s["n_blocks"] for s in stats)
     if n_cnt == 0:  # multi-segment bins only: the full kernel counts
         t_cnt, n_cnt = t_pf, n_blocks
-    pf_bytes = sum(s["kmer_postings"] for s in stats) * 2
+    # algorithmic postings = every posting of the query-strands' k-mer lists (what vsearch's count touches, as
+    # `cells` is the full rectangle however the kernel bands): the ones streamed + the deferred lists' (frequent
+    # k-mers whose matches the kernel adds per surviving target: PrefilterArgs::fmask)
+    streamed = sum(s["kmer_postings"] for s in stats)
+    deferred = sum(s.get("kmer_postings_deferred", 0) for s in stats)
+    pf_bytes = (streamed + deferred) * 2
     traffic = None
     if os.path.exists(traffic_json):
         try:
@@ -141,9 +146,14 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
                 frac=achieved / L2_GATHER_GBS, traffic=traffic,
                 hbm_frac=achieved / HBM_PEAK_GBS, hbm_peak=HBM_PEAK_GBS,
                 bytes_per_launch=pf_bytes / max(1, n_cnt), launches=n_cnt,
+                streamed_bytes_per_launch=2 * streamed / max(1, n_cnt),
+                deferred_share=deferred / max(1, streamed + deferred),
+                streamed_frac=(2 * streamed / t_cnt / 1e9 if t_cnt > 0 else 0.0) / L2_GATHER_GBS,
                 avg_launch_ms=1e3 * t_cnt / max(1, n_cnt),
                 prefilter_ms_per_block=1e3 * t_pf / max(1, n_blocks),
-                note="2 B per u16 posting streamed (postings served from the XCD-partitioned L2; measured HBM "
+                note="2 B per u16 posting of the query-strands' k-mer lists (algorithmic: streamed + deferred, "
+                     "the deferred lists' share in deferred_share; streamed_frac counts only what was streamed; "
+                     "postings served from the XCD-partitioned L2; measured HBM "
                      "traffic is `traffic`); peak = L2-served gather rate, MI355X_MICROARCH.md (1,152-B rows). "
                      "What binds it is instruction issue, not bytes: VALU and LDS-atomic issue per posting "
                      "(profiles/r02/pmc_pf_count_c2.json)")

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 4
+#define UMICLUST_ABI_VERSION 5
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -106,6 +106,8 @@ typedef struct umiclust_stats {
   int64_t n_lazy_passes;  /* passes whose in-window peers were aligned on demand (round B) only */
   double t_count_s;       /* kernel time, the prefilter's counting kernel alone (k_pf_count, HIP events) */
   int64_t n_count_launches; /* its launches (one per pass over one counter segment) */
+  int64_t kmer_postings_deferred; /* postings of the lists the counting kernel deferred (frequent k-mers whose
+                                     matches it adds per surviving target instead; x 8 chunks, incl. padding) */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

@@ -166,6 +166,8 @@ struct Pass {
   DevBuf<uint32_t> d_pcand, d_units;  // per-(query-strand, part) prefilter candidates, overflowed units
   DevBuf<uint8_t> d_pncand, d_ppeer_count, d_pnpeer;
   DevBuf<uint32_t> d_ppost;  // postings touched per (query-strand, part), summed by k_pf_merge
+  DevBuf<uint32_t> d_pdef;   // postings of deferred lists per (query-strand, part) (frequent-k-mer deferral)
+  DevBuf<uint32_t> d_pdm;    // deferred k-mer bits of each (query-strand, part)'s candidates (k_pf_merge)
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
@@ -321,6 +323,18 @@ struct umiclust_ctx {
   DevBuf<uint8_t> d_strong;       // [seqno * 2 + strand] prefilter's near-identical-peer flags (speculation)
   DevBuf<char> d_masked;
   DevBuf<int32_t> d_iota;
+  // frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask; exact): the load's most frequent
+  // + strand k-mers (>= defer_freq of the sampled sequences, at most kFKmers) and every (sequence, strand)'s mask
+  // of them; UMICLUST_DEFER = the most k-mers a query-strand defers (default 0: off -- on config 2 deferring 2-4
+  // k-mers streams 14-22 % fewer postings but the counting kernel's launch time is unchanged within noise:
+  // 1.575 ms off, 1.589-1.600 ms at 2-4, profiles/r03/defer_ab.json)
+  DevBuf<uint32_t> d_fmask;
+  DevBuf<uint32_t> d_cent_fm;     // ordinal -> fmask of its + strand (PrefilterArgs::fmask_ord)
+  uint16_t fkmer[kFKmers] = {};
+  int32_t nfk = 0;
+  int32_t defer_max = 0;
+  int32_t defer_min_thr = 6;
+  double defer_freq = 0.02;
   // device: tables
   DevBuf<uint8_t> d_acc;
   DevBuf<uint16_t> d_rank;
@@ -660,6 +674,8 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_ppeer_count.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_pnpeer.ensure(nqs * kParts), "alloc");
   c->hip(P.d_ppost.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_pdef.ensure(nqs * kParts), "alloc");
+  c->hip(P.d_pdm.ensure(nqs * kParts), "alloc");
   c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
@@ -698,6 +714,17 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // threshold, and one download of the walk states, top lists, walked results and peer results.
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
+// the frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask)
+void set_defer(const umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
+  a.fmask = c->d_fmask.p;
+  a.fmask_ord = c->d_cent_fm.p;
+  a.pdef = P.d_pdef.p;
+  a.pdm = P.d_pdm.p;
+  a.defer_max = c->nfk > 0 ? c->defer_max : 0;
+  a.defer_min_thr = c->defer_min_thr;
+  for (int i = 0; i < kFKmers; i++) a.fkmer[i] = c->fkmer[i];
+}
+
 void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* const* prevs, int nprev, Tile& own,
                   int32_t region, bool lazy_peers = false, bool after_count = false) {
   const int32_t w0 = nprev > 0 ? prevs[0]->base : q0;
@@ -801,6 +828,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.strong_eighths = c->strong_eighths;
   a.postings_touched = P.d_counters.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
+  set_defer(c, a, P);
   if (second_half) c->hip(hipStreamWaitEvent(st, c->a_ev[P.a_slot][1], 0), "wait");
   c->hip(hipEventRecord(P.ev[0], st), "event");
   P.c_timed = false;
@@ -956,6 +984,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   a.pnpeer = P.d_pnpeer.p;
   a.ppost = P.d_ppost.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
+  set_defer(c, a, P);
   c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
   c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
   c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
@@ -1013,6 +1042,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     P.rec_est = (uint32_t)std::max<size_t>(1u << 16, used + used / 2 + 4096);
   }
   c->stats.kmer_postings += P.h_counters.p[0];
+  c->stats.kmer_postings_deferred += P.h_counters.p[11];
   c->stats.pairs_peer += P.h_counters.p[8];
   // every alignment the device computed for this pass (walk rounds + speculative peers)
   c->stats.cells_computed += (int64_t)c->hlen[q0] * ((int64_t)P.h_counters.p[9] + (int64_t)P.h_counters.p[10]);
@@ -1562,6 +1592,9 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
          "h2d cent");
   c->hip(hipMemcpyAsync(c->d_cent_len.p + ord0, c->h_cent_len.p + ord0, new_cents.size(), hipMemcpyHostToDevice, st),
          "h2d cent len");
+  if (c->nfk > 0)
+    c->hip(launch_fmask_ord(c->d_fmask.p, c->d_cent.p + ord0, (int32_t)new_cents.size(), c->d_cent_fm.p + ord0, st),
+           "centroid k-mer masks");
   const int32_t ordend = (int32_t)c->cent.size();
   if (c->nix >= c->ix_events.size()) {
     hipEvent_t e0, e1;
@@ -1640,6 +1673,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
+  c->hip(c->d_cent_fm.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->h_cent.ensure((size_t)n + 1), "pin cent");
   c->hip(c->h_cent_len.ensure((size_t)n + 1), "pin cent");
   c->hip(c->d_seq2ord.ensure((size_t)n + 1), "alloc seq2ord");
@@ -2028,7 +2062,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   c->stats.t_consensus_s = t_cons;
   c->stats.t_host_s = t_host;
   if (c->pf_prof.p) {
-    unsigned long long h[16];
+    unsigned long long h[24];
     c->hip(hipMemcpy(h, c->pf_prof.p, sizeof(h), hipMemcpyDeviceToHost), "d2h");
     const double nwg = h[8] ? (double)h[8] : 1.0;
     fprintf(stderr,
@@ -2038,9 +2072,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     const double nc = h[14] ? (double)h[14] : 1.0;
     fprintf(stderr,
             "k_pf_count phase clocks per workgroup (%llu sampled): zero %.0f table %.0f count %.0f scan %.0f "
-            "peers+out %.0f; chunks per workgroup %.1f\n",
-            h[14], h[9] / nc, h[10] / nc, h[11] / nc, h[12] / nc, h[13] / nc, h[15] / nc);
-    c->hip(hipMemset(c->pf_prof.p, 0, 16 * sizeof(unsigned long long)), "memset");
+            "peers+out %.0f; chunks per workgroup %.1f; table = offsets %.0f + block scan %.0f + writes\n",
+            h[14], h[9] / nc, h[10] / nc, h[11] / nc, h[12] / nc, h[13] / nc, h[15] / nc, h[16] / nc, h[17] / nc);
+    c->hip(hipMemset(c->pf_prof.p, 0, 24 * sizeof(unsigned long long)), "memset");
   }
   c->stats.t_total_s = now_s() - t0;
   c->clustered = true;
@@ -2166,8 +2200,40 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
          "prep");
   uint32_t amb = 0;
   c->hip(hipMemcpyAsync(&amb, d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
-  c->hip(hipStreamSynchronize(c->st), "sync load");
+  // frequent k-mers (the lean counting kernel's deferral): + strand counts over <= 2^18 sampled sequences
+  const int32_t stride = std::max<int32_t>(1, c->n >> 18);
+  std::vector<uint32_t> hist(kBins / kParts);
+  {
+    DevBuf<uint32_t> d_hist;
+    c->hip(d_hist.ensure(hist.size()), "alloc");
+    c->hip(hipMemsetAsync(d_hist.p, 0, hist.size() * 4, c->st), "memset");
+    c->hip(launch_kmer_hist(c->d_kmers.p, c->d_nk.p, c->n, stride, d_hist.p, c->st), "k-mer counts");
+    c->hip(hipMemcpyAsync(hist.data(), d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync load");
+  }
   c->ambig = amb != 0;
+  {
+    const int64_t sampled = c->n > 0 ? ((int64_t)c->n + stride - 1) / stride : 0;
+    const double min_count = std::max(1.0, c->defer_freq * (double)sampled);
+    std::vector<uint32_t> order;
+    for (uint32_t k = 0; k < (uint32_t)hist.size(); k++)
+      if (hist[k] >= min_count) order.push_back(k);
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hist[x] != hist[y] ? hist[x] > hist[y] : x < y; });
+    c->nfk = (int32_t)std::min<size_t>(order.size(), kFKmers);
+    std::vector<uint8_t> lut(hist.size(), 0xff);
+    for (int i = 0; i < kFKmers; i++) {
+      c->fkmer[i] = i < c->nfk ? (uint16_t)order[i] : 0;
+      if (i < c->nfk) lut[order[i]] = (uint8_t)i;
+    }
+    c->hip(c->d_fmask.ensure(ns * 2), "alloc");
+    if (c->nfk > 0 && c->n > 0) {
+      DevBuf<uint8_t> d_lut;
+      c->hip(d_lut.ensure(lut.size()), "alloc");
+      c->hip(hipMemcpyAsync(d_lut.p, lut.data(), lut.size(), hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(launch_fmask(c->d_kmers.p, c->d_nk.p, c->n, d_lut.p, c->d_fmask.p, c->st), "k-mer masks");
+      c->hip(hipStreamSynchronize(c->st), "sync load");
+    }
+  }
   for (int32_t s = 0; s < c->n; s++)
     if (c->hlen[s] < kMinTplLen) c->fail(UMICLUST_ERANGE, "sequence shorter than %d (minseqlength)", kMinTplLen);
   c->loaded = true;
@@ -2303,6 +2369,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
@@ -2325,7 +2392,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
-    if (c->pf_prof.ensure(16) != hipSuccess || hipMemset(c->pf_prof.p, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
+    if (c->pf_prof.ensure(24) != hipSuccess || hipMemset(c->pf_prof.p, 0, 24 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;
       if (err) *err = UMICLUST_EDEVICE;
       return nullptr;

@@ -613,7 +613,9 @@ struct PfTable {
 };
 __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, int t0, int nct, int ntl,
                                               uint64_t pbase, int part, int thr, int nk, uint32_t km0, uint32_t km1,
-                                              int wv, int lane, int tid, uint32_t& T, uint32_t& nlc) {
+                                              int wv, int lane, int tid, uint32_t& T, uint32_t& nlc,
+                                              bool skip0 = false, bool skip1 = false, uint32_t* def_ch = nullptr,
+                                              unsigned long long* clk = nullptr) {
   TileView tvs[kPfTilesPerWave];
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
@@ -622,7 +624,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
     else if (ti < ntl) tvs[it] = a.peer[ti - nct];
     else tvs[it].n = 0;
   }
-  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
+  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0, dch = 0;
   u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
@@ -635,22 +637,31 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
   for (int it = 0; it < kPfTilesPerWave; it++) {
     const bool live = thr > 0 && tvs[it].n > 0;
     const uint32_t tbase = (uint32_t)(tvs[it].post_base - pbase);
-    nch[2 * it] = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
+    const uint32_t c0 = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
+    const uint32_t c1 = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
+    // deferred k-mers (k_pf_count's frequent-k-mer deferral): their lists are not streamed
+    // (centroid tiles only: peer tiles are counted in full, so peers and flagged hits stay exact)
+    const bool cen = wv + it * kPfWaves < nct, s0 = skip0 && cen, s1 = skip1 && cen;
+    nch[2 * it] = s0 ? 0u : c0;
     bse[2 * it] = tbase + o0[it].x;
-    nch[2 * it + 1] = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
+    nch[2 * it + 1] = s1 ? 0u : c1;
     bse[2 * it + 1] = tbase + o1[it].x;
+    dch += (s0 ? c0 : 0u) + (s1 ? c1 : 0u);
   }
 #pragma unroll
   for (int j = 0; j < kPfSlots; j++) {
     sum_ch += nch[j];
     sum_ne += nch[j] ? 1u : 0u;
   }
+  if (clk) clk[0] = __builtin_readcyclecounter();  // phase probe: the list offsets have arrived
   // window start masks (set below, after block_excl_scan's barriers)
   if (tid < kPfWinBase) tb.wlo[tid] = 0u;
   else if (tid < 2 * kPfWinBase) tb.whi[tid - kPfWinBase] = 0u;
   // packed scan: chunks << kListBits | lists (see kListBits)
   uint32_t tot;
   const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
+  if (def_ch && dch) atomicAdd(def_ch, dch);  // after the scan's barriers: *def_ch was zeroed before the call
+  if (clk) clk[1] = __builtin_readcyclecounter();
   T = tot >> kListBits;
   nlc = tot & kListMask;
   uint32_t li = ex & kListMask, ci = ex >> kListBits;
@@ -1074,7 +1085,7 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_pf_full(PrefilterArgs a, int 
 // the kernel keeps few registers, so up to 8 workgroups share a CU.
 struct PfCountHdr {
   uint32_t wsum[kPfWaves];
-  uint32_t ncand, npc, pad0, pad1;
+  uint32_t ncand, npc, ndef, pad1;
 };
 __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
   return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 2 + 2 * kPfWinBase * 4 + (2 * nlist_cap + 66) * 4);
@@ -1101,6 +1112,24 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
   const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
   const int64_t pq_ = (int64_t)qs * kParts + part;
+  // frequent-k-mer deferral (PrefilterArgs::fmask): D = the lowest set bits of the query-strand's F mask, at most
+  // defer_max of them and thr - |D| >= defer_min_thr; the lanes holding D's k-mers skip their lists
+  uint32_t dmask = 0u;
+  if (a.defer_max > 0 && thr > 0) {
+    uint32_t m = a.fmask[(int64_t)q * 2 + strand];
+    for (int i = 0; i < a.defer_max && m != 0u && thr - (i + 1) >= a.defer_min_thr; i++) {
+      dmask |= m & (0u - m);
+      m &= m - 1u;
+    }
+  }
+  dmask = (uint32_t)__builtin_amdgcn_readfirstlane((int)dmask);
+  const int fd = __builtin_popcount(dmask);
+  bool skip0 = false, skip1 = false;
+  for (uint32_t m = dmask; m != 0u; m &= m - 1u) {
+    const uint32_t fk = a.fkmer[__builtin_ctz(m)];
+    skip0 |= lane < nk && km0 == fk;
+    skip1 |= lane + 64 < nk && km1 == fk;
+  }
   const int nct = a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0;
   const int nsubC = a.ncent > part ? (a.ncent - part + kParts - 1) >> kPartShift : 0;
   const int ncnt = kCentBase + ((nsubC + 15) & ~15);
@@ -1110,6 +1139,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   // phase barriers of sampled workgroups, into a.prof[9 + i] (k_pf_full uses [0, 9))
   const bool prof = a.prof != nullptr && tid == 0 && (blockIdx.x % 61u) == 0u;
   unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[5] = {0, 0, 0, 0, 0};
+  unsigned long long clk[2] = {0, 0}, tsub[2] = {0, 0};  // table sub-phases: offsets arrived, block scan done
 #define PFC_MARK(i)                                             \
   if (prof) {                                                   \
     const unsigned long long tn = __builtin_readcyclecounter(); \
@@ -1121,11 +1151,16 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   if (tid == 0) {
     H.ncand = 0;
     H.npc = 0;
+    H.ndef = 0;
   }
   uint32_t T, nlc;
   PFC_MARK(0)
   pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
-                km0, km1, wv, lane, tid, T, nlc);
+                km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof ? clk : nullptr);
+  if (prof) {
+    tsub[0] += clk[0] - tprev;
+    tsub[1] += clk[1] - clk[0];
+  }
   PFC_MARK(1)
   if (T > 0) {
     if (CM == 1) pf_count_stream_pre<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
@@ -1137,21 +1172,27 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     // postings touched (stats): every chunk posting minus the padding ones (the spare counters)
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
     const uint32_t pads = lane63(wave_scan_dpp((uint32_t)cb[kDummy + lane], OpAdd()));
-    if (lane == 0) a.ppost[pq_] = 8u * T - pads;
+    if (lane == 0) {
+      a.ppost[pq_] = 8u * T - pads;
+      if (a.pdef) a.pdef[pq_] = 8u * H.ndef;
+    }
   }
   // centroid counters >= thr (SWAR: bytes <= 112, so byte + 128 - thr sets bit 7 iff >= thr); a sweep
-  // of 64 counter vectors with no candidate costs one OR and a ballot
+  // of 64 counter vectors with no candidate costs one OR and a ballot.  With deferred k-mers (fd > 0) the
+  // centroid counters lack at most |D| matches: every counter >= thr - |D| is emitted with its partial count and
+  // k_pf_merge adds the deferred matches (PrefilterArgs::pdm).  Peer tiles are counted in full (exact).
   const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
+  const uint32_t cadd = (uint32_t)(128 - (thr - fd)) * 0x01010101u;
   if (thr > 0) {
     const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
     const uint4* c4 = cnt4 + kCentBase / 16;
     for (int x0 = wv * 64; x0 < lim4; x0 += kPfThreads) {
       const int x = x0 + lane;
       const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
-      if (__ballot((((v.x + add) | (v.y + add) | (v.z + add) | (v.w + add)) & 0x80808080u) != 0u) == 0ull) continue;
+      if (__ballot((((v.x + cadd) | (v.y + cadd) | (v.z + cadd) | (v.w + cadd)) & 0x80808080u) != 0u) == 0ull) continue;
       const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-      uint32_t mk[4] = {(v.x + add) & 0x80808080u, (v.y + add) & 0x80808080u, (v.z + add) & 0x80808080u,
-                        (v.w + add) & 0x80808080u};
+      uint32_t mk[4] = {(v.x + cadd) & 0x80808080u, (v.y + cadd) & 0x80808080u, (v.z + cadd) & 0x80808080u,
+                        (v.w + cadd) & 0x80808080u};
       const uint32_t n = (uint32_t)(__builtin_popcount(mk[0]) + __builtin_popcount(mk[1]) +
                                     __builtin_popcount(mk[2]) + __builtin_popcount(mk[3]));
       uint32_t slot = wave_alloc(n, &H.ncand);
@@ -1226,6 +1267,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const bool ovf = thr == 0 || nc > (uint32_t)kPartCand;
     a.pncand[pq_] = (uint8_t)(ovf ? 255u : nc);
     a.pnpeer[pq_] = (uint8_t)(np > (uint32_t)kPeerCap ? 255u : np);
+    if (a.pdm) a.pdm[pq_] = ovf ? 0u : dmask;  // the full kernel's candidates (ovf) are exact
     if (ovf) a.units[atomicAdd(a.nunits, 1u)] = (uint32_t)pq_;
   }
   PFC_MARK(4)
@@ -1233,6 +1275,8 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     for (int i = 0; i < 5; i++) atomicAdd(&a.prof[9 + i], tacc[i]);
     atomicAdd(&a.prof[14], 1ull);
     atomicAdd(&a.prof[15], (unsigned long long)T);
+    atomicAdd(&a.prof[16], tsub[0]);
+    atomicAdd(&a.prof[17], tsub[1]);
   }
 #undef PFC_MARK
 }
@@ -1244,10 +1288,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
 // part top-41: top-41 of a union = top-41 of the parts' top-41s).  Peers: sorted within each part by
 // (count desc, length asc, window id asc) and concatenated in part order.
 constexpr int kMergeWaves = 4;
-__global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs) {
+__global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs, int32_t use_pdm) {
   __shared__ unsigned long long keys[kMergeWaves][kParts * kPartCand];
   __shared__ uint32_t pkeys[kMergeWaves][kPeerCap];
-  __shared__ uint32_t wpost[kMergeWaves];
+  __shared__ uint32_t wpost[kMergeWaves], wdef[kMergeWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qs = (int)blockIdx.x * kMergeWaves + wave;
   const bool live = qs < nqs;
@@ -1256,15 +1300,27 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   // postings touched (stats): the parts' counts, one atomic per workgroup into one of kPostSpread lines
   {
     uint32_t pp = (live && lane < kParts) ? a.ppost[p0 + lane] : 0u;
+    uint32_t pd = (live && lane < kParts && a.pdef) ? a.pdef[p0 + lane] : 0u;
 #pragma unroll
-    for (int d = 1; d < kParts; d <<= 1) pp += __shfl_xor(pp, d, 64);
-    if (lane == 0) wpost[wave] = pp;
+    for (int d = 1; d < kParts; d <<= 1) {
+      pp += __shfl_xor(pp, d, 64);
+      pd += __shfl_xor(pd, d, 64);
+    }
+    if (lane == 0) {
+      wpost[wave] = pp;
+      wdef[wave] = pd;
+    }
     __syncthreads();
     if (threadIdx.x == 0 && a.postings_touched) {
-      uint32_t t = 0;
+      uint32_t t = 0, td = 0;
 #pragma unroll
-      for (int w = 0; w < kMergeWaves; w++) t += wpost[w];
+      for (int w = 0; w < kMergeWaves; w++) {
+        t += wpost[w];
+        td += wdef[w];
+      }
       if (t) atomicAdd(a.postings_touched + 16 + 32 * (blockIdx.x % kPostSpread), t);
+      // deferred postings (k_pf_count's frequent-k-mer deferral): the next word of the same line
+      if (td) atomicAdd(a.postings_touched + 17 + 32 * (blockIdx.x % kPostSpread), td);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nunits = 0;  // the full kernel has read it (stream order)
@@ -1279,9 +1335,18 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
   const int o_l = inc - n_l;
   const int total = __shfl(inc, kParts - 1, 64);
+  // frequent-k-mer deferral (PrefilterArgs::pdm): the part's centroid candidates hold partial counts
+  const uint32_t dm_l = (use_pdm && lane < kParts) ? a.pdm[p0 + lane] : 0u;
+  int thr = 0;
+  if (use_pdm) {
+    const int32_t q = a.q0 + qs / a.both;
+    const int nkq = a.seqs.nk[(int64_t)q * 2 + qs % a.both];
+    thr = nkq < a.minwordmatches ? nkq : a.minwordmatches;
+  }
 #pragma unroll
   for (int l = 0; l < kParts; l++) {
     const int n = __shfl(n_l, l, 64), o = __shfl(o_l, l, 64);
+    const uint32_t dm = (uint32_t)__shfl((int)dm_l, l, 64);
     for (int x = lane; x < n; x += 64) {
       const uint32_t e = a.pcand[(p0 + l) * kPartCand + x];
       unsigned long long key = ~0ull;  // a flagged hit that turned out a member: no candidate
@@ -1294,23 +1359,35 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       } else {
         const uint32_t ord = e & 0xffffffu;
         const uint32_t len = a.seqs.lens[a.cent_seqno[ord]];
-        key = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)len << 48) | ord;
+        uint32_t cv = e >> 24;
+        if (dm) cv += (uint32_t)__builtin_popcount(a.fmask_ord[ord] & dm);  // the deferred matches
+        if (!dm || cv >= (uint32_t)thr)
+          key = ((unsigned long long)(127u - cv) << 56) | ((unsigned long long)len << 48) | ord;
       }
       K[o + x] = key;
     }
   }
-  int nvalid = 0;
-  for (int e = lane; e < total; e += 64) nvalid += K[e] != ~0ull;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) nvalid += __shfl_xor(nvalid, d, 64);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int e = lane; e < total; e += 64) {
+  // compact the valid keys in place (chunk i reads [64 i, 64 i + 64) and writes below its own start, after its
+  // reads: LDS operations of a wave complete in order)
+  int nvalid = 0;
+  for (int e0 = 0; e0 < total; e0 += 64) {
+    const int e = e0 + lane;
+    const unsigned long long key = e < total ? K[e] : ~0ull;
+    const unsigned long long vb = __ballot(key != ~0ull);
+    if (key != ~0ull) K[nvalid + (int)__builtin_popcountll(vb & ((1ull << lane) - 1ull))] = key;
+    nvalid += (int)__builtin_popcountll(vb);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int e = lane; e < nvalid; e += 64) {
     const unsigned long long key = K[e];
     int rank = 0;
-    for (int y = 0; y < total; y++) rank += K[y] < key;
-    if (rank < kTopHits && key != ~0ull) {
+    for (int y = 0; y < nvalid; y++) rank += K[y] < key;
+    if (rank < kTopHits) {
       a.top_seqno[(int64_t)qs * kTopHits + rank] = (uint32_t)a.cent_seqno[(uint32_t)(key & 0xffffffu)];
       a.top_count[(int64_t)qs * kTopHits + rank] = (uint8_t)(127u - (uint32_t)(key >> 56));
     }
@@ -1369,6 +1446,56 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
 }
 
+// ------------------------------------------------------------------ frequent k-mers (PrefilterArgs::fmask)
+// + strand k-mer frequencies over every stride-th sequence of a load (one wave per sequence), then per
+// (sequence, strand) the mask of the frequent k-mers (lut[k-mer] = bit or 0xff) it holds (one wave each).
+__global__ __launch_bounds__(256) void k_kmer_hist(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
+                                                   int32_t n, int32_t stride, uint32_t* __restrict__ hist) {
+  const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * stride;
+  const int x = threadIdx.x & 63;
+  if (s >= n) return;
+  const int m = nk[s * 2];
+  const uint16_t* k = kmers + s * 2 * kKmerStride;
+  if (x < m) atomicAdd(&hist[k[x]], 1u);
+  if (x + 64 < m) atomicAdd(&hist[k[x + 64]], 1u);
+}
+__global__ __launch_bounds__(256) void k_fmask(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
+                                               int64_t n2, const uint8_t* __restrict__ lut, uint32_t* __restrict__ fmask) {
+  const int64_t ss = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // sequence * 2 + strand (wave-uniform)
+  const int x = threadIdx.x & 63;
+  if (ss >= n2) return;
+  const int m = nk[ss];
+  const uint16_t* k = kmers + ss * kKmerStride;
+  const uint32_t b0 = x < m ? lut[k[x]] : 0xffu, b1 = x + 64 < m ? lut[k[x + 64]] : 0xffu;
+  uint32_t v = (b0 < 32u ? 1u << b0 : 0u) | (b1 < 32u ? 1u << b1 : 0u);
+  v = wave_scan_dpp(v, OpOr());
+  if (x == 63) fmask[ss] = v;
+}
+__global__ __launch_bounds__(256) void k_fmask_ord(const uint32_t* __restrict__ fmask, const int32_t* __restrict__ cent,
+                                                   int32_t n, uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = fmask[(int64_t)cent[i] * 2];
+}
+hipError_t launch_fmask_ord(const uint32_t* fmask, const int32_t* cent, int32_t n, uint32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fmask_ord, dim3((n + 255) / 256), dim3(256), 0, st, fmask, cent, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_kmer_hist(const uint16_t* kmers, const uint8_t* nk, int32_t n, int32_t stride, uint32_t* hist,
+                            hipStream_t st) {
+  const int64_t ns = stride > 0 ? ((int64_t)n + stride - 1) / stride : 0;
+  if (ns <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_kmer_hist, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, st, kmers, nk, n, stride, hist);
+  return hipGetLastError();
+}
+hipError_t launch_fmask(const uint16_t* kmers, const uint8_t* nk, int32_t n, const uint8_t* lut, uint32_t* fmask,
+                        hipStream_t st) {
+  const int64_t n2 = (int64_t)n * 2;
+  if (n2 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fmask, dim3((unsigned)((n2 + 3) / 4)), dim3(256), 0, st, kmers, nk, n2, lut, fmask);
+  return hipGetLastError();
+}
+
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
@@ -1409,8 +1536,10 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   } else {
     hipLaunchKernelGGL(k_pf_full, dim3(nqs * kParts), dim3(kPfThreads), smem_full, st, a, 0);
   }
+  // the lean kernel's candidates (and its per-unit D) exist unless this is a multi-segment whole prefilter
+  const int32_t use_pdm = (a.pdm && a.defer_max > 0 && (mode != 0 || a.nseg <= 1)) ? 1 : 0;
   hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st,
-                     a, nqs);
+                     a, nqs, use_pdm);
   return hipGetLastError();
 }
 
@@ -1633,10 +1762,15 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
   const int qs = (int)blockIdx.x * kPackWaves + wave;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // counters[0] = the postings partial sums (k_pf_merge spreads its atomics over kPostSpread lines)
+    // counters[11] = the deferred postings' partial sums (the next word of each line)
     uint32_t v = threadIdx.x < kPostSpread ? counters[16 + 32 * threadIdx.x] : 0u;
+    uint32_t vd = threadIdx.x < kPostSpread ? counters[17 + 32 * threadIdx.x] : 0u;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
-    if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : counters[threadIdx.x];
+    for (int d = 1; d < 64; d <<= 1) {
+      v += __shfl_xor(v, d, 64);
+      vd += __shfl_xor(vd, d, 64);
+    }
+    if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : threadIdx.x == 11 ? vd : counters[threadIdx.x];
   }
   const bool live = qs < nqs;
   const WalkState w = ws[live ? qs : 0];

@@ -75,6 +75,14 @@ struct DevSeqs {
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
                        char* masked, uint32_t* ambig, hipStream_t st);
+// frequent k-mers of a load (PrefilterArgs::fmask): + strand k-mer counts of every stride-th sequence into
+// hist[65536] (zero on entry); then fmask[s * 2 + strand] = the bits lut[k-mer] (< 32; 0xff = none) it holds
+hipError_t launch_kmer_hist(const uint16_t* kmers, const uint8_t* nk, int32_t n, int32_t stride, uint32_t* hist,
+                            hipStream_t st);
+hipError_t launch_fmask(const uint16_t* kmers, const uint8_t* nk, int32_t n, const uint8_t* lut, uint32_t* fmask,
+                        hipStream_t st);
+// out[i] = fmask[cent[i] * 2] (the + strand masks of centroid ordinals, PrefilterArgs::fmask_ord)
+hipError_t launch_fmask_ord(const uint32_t* fmask, const int32_t* cent, int32_t n, uint32_t* out, hipStream_t st);
 // index tile build over sequences c in [0, count) with seqno map[first + c] and ordinal
 // x = xoff + c (centroid tiles: the centroid ordinal; peer tiles: c): count (hist[kBins], all zero
 // on entry), scan (padded offsets off[kBins+1], fill cursors, padding postings written into post,
@@ -95,6 +103,7 @@ constexpr int kPartCand = 64;  // candidates a (query-strand, part) passes to th
 // pass counters: [0..15] stats and pair counts, the postings partial sums, the overflowed-unit count
 constexpr int kUnitsSlot = 16 + kPostSpread * 32;
 constexpr int kCountersLen = kUnitsSlot + 32;
+constexpr int kFKmers = 32;  // frequent k-mers of a load eligible for deferral (PrefilterArgs::fkmer)
 struct PrefilterArgs {
   DevSeqs seqs;
   const uint16_t* arena;   // postings of every tile
@@ -151,6 +160,20 @@ struct PrefilterArgs {
   uint32_t* postings_touched;  // counters[0]; the merge adds into kPostSpread slots 128 B apart after
                                // counters[16], which k_pack sums into the host copy of counters[0]
   unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
+  // Frequent-k-mer deferral (k_pf_count + k_pf_merge; exact).  F = fkmer[0..kFKmers), the load's most frequent
+  // + strand k-mers, most frequent first; fmask[seqno * 2 + strand] bit b = that strand's unique k-mers hold
+  // fkmer[b].  A query-strand defers D = the (at most defer_max) lowest bits of its own mask: their posting lists
+  // in the centroid tiles are not streamed, so a centroid counter misses at most |D| and the counters >= thr - |D|
+  // are the only possible candidates; the merge adds popcount(fmask_ord[ordinal] & D) to each and drops the ones
+  // still < thr.  defer_max = 0 turns it off; thr - |D| stays >= defer_min_thr.
+  const uint32_t* fmask;
+  const uint32_t* fmask_ord;  // [ordinal] fmask of centroid ordinal's + strand (fmask[cent_seqno[o] * 2])
+  uint32_t* pdef;            // [nqs*kParts] postings of the deferred lists (chunks x 8, incl. list padding)
+  uint32_t* pdm;             // [nqs*kParts] D of the unit's candidates for k_pf_merge (0: exact, e.g. the full
+                             // kernel's); centroid candidates then hold partial counts >= thr - |D|
+  int32_t defer_max;
+  int32_t defer_min_thr;
+  uint16_t fkmer[kFKmers];
 };
 // two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
 // mode 0: the whole prefilter (lean counting + the full kernel over its overflowed units, or the full

@@ -83,6 +83,7 @@ class Stats(C.Structure):
         ("n_lazy_passes", C.c_int64),
         ("t_count_s", C.c_double),
         ("n_count_launches", C.c_int64),
+        ("kmer_postings_deferred", C.c_int64),
     ]
 
     def as_dict(self) -> dict:

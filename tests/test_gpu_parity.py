@@ -237,6 +237,35 @@ def test_pipeline_modes(split, block, monkeypatch):
     assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("defer", ["1", "4"])
+def test_kmer_deferral(defer, split, monkeypatch):
+    """The lean counting kernel's frequent-k-mer deferral (PrefilterArgs::fmask): a query-strand skips the posting
+    lists of up to UMICLUST_DEFER of its most frequent k-mers and adds them per surviving target -- membership,
+    strands, centroids, consensus, alignments and cells equal the oracle's; the postings it streams plus the
+    deferred lists cover exactly what the undeferred count streams (deferred lists are counted with their
+    padding, <= 7 postings per list)."""
+    u = synth.make_umis(300, seed=27, max_reads=4000, orient_mix=0.2)
+    seqs = u.as_list()
+    monkeypatch.setenv("UMICLUST_BLOCK", "512")
+    monkeypatch.setenv("UMICLUST_SPLIT", split)
+    o = orc.cluster(orc.params(1, 0.90, 58, 68), seqs)
+    out = {}
+    for d in ("0", defer):
+        monkeypatch.setenv("UMICLUST_DEFER", d)
+        with _lib.Context(0) as ctx:
+            ctx.load(_lib.params(1, 0.90, 58, 68), seqs)
+            st = ctx.cluster()
+            g = ctx.fetch()
+        _cmp_cluster(g, o)
+        assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+        out[d] = st
+    s0, sd = out["0"], out[defer]
+    assert s0["kmer_postings_deferred"] == 0
+    assert sd["kmer_postings_deferred"] > 0 and sd["kmer_postings"] < s0["kmer_postings"]
+    assert sd["kmer_postings"] + sd["kmer_postings_deferred"] >= s0["kmer_postings"]
+
+
 @pytest.mark.parametrize("split", ["0", "1", "2"])
 def test_pipeline_modes_deep_clusters(split, monkeypatch):
     """Config-5 style deep clusters (long UMIs, 15 % indels) with small blocks: peer lists overflow, blocks

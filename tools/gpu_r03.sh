@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 GPU session: parity tests, the default bench line (config 2 + e2e), PMC calibration and the
 # k_pf_count busy pass, kernel trace.  Every GPU step has its own time limit; the first failure ends the call.
-# Usage: bash tools/gpu_r03.sh <tag> <steps...>   steps: tests | bench | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5
+# Usage: bash tools/gpu_r03.sh <tag> <steps...>   steps: tests | bench | defer (DEFERS="0 3") | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5
 set -o pipefail
 tag=${1:-r03}
 shift
@@ -34,6 +34,10 @@ for st in "$@"; do
               > "$out/pfab$cm.json" 2> "$out/pfab$cm.err" || { rc=$?; break; }
             UMICLUST_PFCOUNT=$cm UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof$cm.json" \
               2> "$out/pfprof$cm.err" || { rc=$?; break; }
+          done ;;
+    defer) for dm in ${DEFERS:-0 3}; do
+            UMICLUST_DEFER=$dm timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+              > "$out/defer$dm.json" 2> "$out/defer$dm.err" || { rc=$?; break; }
           done ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 $B > "$out/trace.log" 2>&1; rc=$? ;;
