@@ -423,6 +423,10 @@ struct umiclust_ctx {
   // UMICLUST_BLOCK unset: a bin of n queries uses blocks of about n / block_div (>= 2048): a small bin's
   // window then holds fewer same-molecule peers (fewer speculative peer alignments and overflows)
   int32_t block_div = 16;
+  int32_t block_min = 2048;       // UMICLUST_BLOCK_MIN: the smallest default block (bins of < 16 x this)
+  // UMICLUST_MIXLEN=0: blocks end at every query-length change (one alignment launch per round); =1: a block spans
+  // up to kSegLens lengths (one launch per length and round): a small bin is then a few passes, not one per length
+  int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
@@ -741,7 +745,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   own.prebuilt = false;
   own.base = q0;
   own.seg = region;
-  own.len = c->hlen[q0];  // blocks hold one query length
+  own.len = c->hlen[q0];  // the block's longest query
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -857,10 +861,32 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipStreamWaitEvent(c->st_al, P.ev[1], 0), "wait");
   st = c->st_al;
   DevSeqs ds = dev_seqs(c);
-  const int32_t qlen = c->hlen[q0];
+  // the block's query lengths (sorted, non-increasing): one pair segment and one alignment launch per length
+  const int32_t lmax = c->hlen[q0], nsg = lmax - c->hlen[q0 + nq - 1] + 1;
+  if (nsg > kSegLens) c->fail(UMICLUST_EINVAL, "block spans %d query lengths (> %d)", nsg, kSegLens);
+  int32_t nql[kSegLens] = {};
+  for (int32_t q = q0; q < q0 + nq; q++) nql[lmax - c->hlen[q]]++;
+  SegTab sg0{}, sg1{};
+  sg0.lmax = sg1.lmax = lmax;
+  sg0.nseg = sg1.nseg = nsg;
+  for (int32_t i = 0, b0 = 0, b1 = 0; i < nsg; i++) {
+    sg0.base[i] = (uint32_t)b0;
+    sg1.base[i] = (uint32_t)b1;
+    b0 += nql[i] * both * kWalk;
+    b1 += nql[i] * both * (kWalk + kPeerCap);
+  }
+  uint32_t* segc = P.d_counters.p + kSegSlot;  // [walk round][segment]
+  unsigned long long* cells_w = reinterpret_cast<unsigned long long*>(P.d_counters.p + 12);
+  unsigned long long* cells_p = reinterpret_cast<unsigned long long*>(P.d_counters.p + 14);
+  auto align_round = [&](const SegTab& sg, int per_qs, uint32_t* cnt, const char* what) {
+    for (int32_t i = 0; i < nsg; i++)
+      if (nql[i])
+        c->hip(launch_align(ds, lmax - i, c->ambig, P.d_pq.p + sg.base[i], P.d_pt.p + sg.base[i], nql[i] * both * per_qs,
+                            cnt + i, P.d_outidx.p + sg.base[i], c->sc, P.d_res.p, st, c->band_pairs),
+               what);
+  };
   c->hip(launch_walk(-1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p, P.d_res.p,
-                     c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 1,
-                     P.d_counters.p + 9, st),
+                     c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg0, segc, cells_w, st),
          "walk");
   c->hip(hipEventRecord(P.ev[2], st), "event");
   // two dependent alignment launches: batch 0 (or a speculative whole walk), then the rest of every
@@ -868,24 +894,20 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   // state after round 0, which only widens it: a superset of what the final state needs)
   const uint32_t peer_out0 = (uint32_t)nqs * kWalk;
   // small passes (deep clusters cut blocks small) spread every pair over a lane group
-  c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * kWalk, P.d_counters.p + 1, P.d_outidx.p, c->sc,
-                      P.d_res.p, st, c->band_pairs),
-         "align 0");
+  align_round(sg0, kWalk, segc, "align 0");
   c->hip(launch_walk(0, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
-                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2,
-                     P.d_counters.p + 9, st),
+                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1, segc + kSegLens,
+                     cells_w, st),
          "walk 0");
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
-                           P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 2, P.d_counters.p + 10, P.d_counters.p + 8,
+                           P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1, segc + kSegLens, cells_p, P.d_counters.p + 8,
                            peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, lazy_peers ? 0 : 1,
                            st),
          "peer pairs");
-  c->hip(launch_align(ds, qlen, c->ambig, P.d_pq.p, P.d_pt.p, nqs * (kWalk + kPeerCap), P.d_counters.p + 2,
-                      P.d_outidx.p, c->sc, P.d_res.p, st, c->band_pairs),
-         "align 1");
+  align_round(sg1, kWalk + kPeerCap, segc + kSegLens, "align 1");
   c->hip(launch_walk(1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
-                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, P.d_counters.p + 3,
-                     P.d_counters.p + 9, st),
+                     P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1,
+                     segc + 2 * kSegLens, cells_w, st),
          "walk 1");
   c->hip(hipEventRecord(P.ev[3], st), "event");
   // what the host needs goes straight to pinned host memory; the pass that next reuses these
@@ -1045,7 +1067,12 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   c->stats.kmer_postings_deferred += P.h_counters.p[11];
   c->stats.pairs_peer += P.h_counters.p[8];
   // every alignment the device computed for this pass (walk rounds + speculative peers)
-  c->stats.cells_computed += (int64_t)c->hlen[q0] * ((int64_t)P.h_counters.p[9] + (int64_t)P.h_counters.p[10]);
+  {
+    unsigned long long cw = 0, cp = 0;  // u64 cells of the walk pairs / the peer pairs (counters 12-13 / 14-15)
+    memcpy(&cw, P.h_counters.p + 12, 8);
+    memcpy(&cp, P.h_counters.p + 14, 8);
+    c->stats.cells_computed += (int64_t)(cw + cp);
+  }
   // a pageable copy of the per-query-strand outcomes (sequential, revisited below); the records
   // are read in place, only for the query-strands whose relevant peers include a centroid
   const double tc0 = now_s();
@@ -1524,7 +1551,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     t_host += now_s() - th1;
     const int32_t nb = (int32_t)bpq.size();
     c->stats.pairs_round_b += nb;
-    for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[q0] * c->hlen[bpt[x]];
+    for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[bpq[x] >> 1] * c->hlen[bpt[x]];
     std::vector<uint32_t> bres(nb);
     if (nb > 0) {
       hipStream_t sb = c->st_b;
@@ -1534,9 +1561,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
       c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
       c->hip(hipEventRecord(c->evb[0], sb), "event");
-      c->hip(launch_align(dev_seqs(c), c->hlen[q0], c->ambig, c->d_bpq.p, c->d_bpt.p, nb, nullptr, nullptr, c->sc,
-                          c->d_bres.p, sb, c->band_pairs),
-             "align B");
+      // the pairs are in query order: one launch per run of one query length
+      for (int32_t x0 = 0; x0 < nb;) {
+        const int32_t L = c->hlen[bpq[x0] >> 1];
+        int32_t x1 = x0 + 1;
+        while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
+        c->hip(launch_align(dev_seqs(c), L, c->ambig, c->d_bpq.p + x0, c->d_bpt.p + x0, x1 - x0, nullptr, nullptr, c->sc,
+                            c->d_bres.p + x0, sb, c->band_pairs),
+               "align B");
+        x0 = x1;
+      }
       c->hip(hipEventRecord(c->evb[1], sb), "event");
       c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
       c->hip(hipStreamSynchronize(sb), "sync");
@@ -1592,7 +1626,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
          "h2d cent");
   c->hip(hipMemcpyAsync(c->d_cent_len.p + ord0, c->h_cent_len.p + ord0, new_cents.size(), hipMemcpyHostToDevice, st),
          "h2d cent len");
-  if (c->nfk > 0)
+  if (c->nfk > 0 && c->defer_max > 0)
     c->hip(launch_fmask_ord(c->d_fmask.p, c->d_cent.p + ord0, (int32_t)new_cents.size(), c->d_cent_fm.p + ord0, st),
            "centroid k-mer masks");
   const int32_t ordend = (int32_t)c->cent.size();
@@ -1686,7 +1720,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   // blocks of at most B queries of one length (the aligner is compiled per query length); a block's
   // peer tile fills one kPeerRegion of the prefilter counters, so B <= kMaxBlock
   int32_t B = std::max(1, std::min<int32_t>(c->block_size, kMaxBlock));
-  if (c->block_div > 0) B = std::min<int32_t>(B, std::max<int32_t>(2048, ((s1 - s0) / c->block_div + 255) & ~255));
+  if (c->block_div > 0) B = std::min<int32_t>(B, std::max<int32_t>(c->block_min, ((s1 - s0) / c->block_div + 255) & ~255));
   c->pass_B = B;
   for (Pass& P : c->pass) ensure_pass_buffers(c, P, B);
   // postings arena: the base, delta, peer-ring and solo slots, then the sealed tile slots in creation
@@ -1711,11 +1745,21 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     c->hip(c->arena.ensure((size_t)off + 64), "alloc arena");
   }
   std::vector<std::pair<int32_t, int32_t>> blocks;
-  // the blocks from query `from` on, at most `bmax` queries of one length each
+  // blocks across length changes: bins below the full block size (config 3: 4.15 vs 3.61 M UMIs/s; a 2M-read bin
+  // gains nothing, its length runs are many blocks long: profiles/r03/mixlen_ab.json)
+  const bool mix = c->mix_len > 0 || (c->mix_len < 0 && B < kMaxBlock);
+  // the blocks from query `from` on, at most `bmax` queries (of one length each unless mix)
   auto split_blocks = [&](int32_t from, int32_t bmax) {
     for (int32_t q0 = from; q0 < s1;) {
       int32_t same = 1;
-      while (q0 + same < s1 && same < bmax && c->hlen[q0 + same] == c->hlen[q0]) same++;
+      if (mix && !c->o4_T) {  // across length changes, at most kSegLens lengths (one pair segment each);
+                                     // O4 batched rounds keep one length per block (mixed blocks there: 21 more
+                                     // alignments than the oracle on test_batched_rounds_deep_clusters, unresolved)
+        const int32_t lim = std::min<int32_t>(bmax, s1 - q0);
+        while (same < lim && c->hlen[q0] - c->hlen[q0 + same] < kSegLens) same++;
+      } else {
+        while (q0 + same < s1 && same < bmax && c->hlen[q0 + same] == c->hlen[q0]) same++;
+      }
       blocks.push_back({q0, same});
       q0 += same;
     }
@@ -2370,6 +2414,8 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
+  if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {

@@ -1583,21 +1583,47 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
 // are resolved later by the host): round r evaluates batch r of every unfinished query-strand and
 // emits the pairs of batch r+1.  Acceptance and the id order come from host-built tables, so the
 // IEEE-double test `100.0*matches/internal >= 100.0*id` is exactly vsearch's.
-__global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
-                       const uint32_t* __restrict__ top_seqno, const uint8_t* __restrict__ top_count,
-                       const uint8_t* __restrict__ ntop, const uint8_t* __restrict__ lens,
-                       const uint32_t* __restrict__ res, const uint8_t* __restrict__ acc_tab,
-                       const uint16_t* __restrict__ rank_tab, WalkState* __restrict__ ws,
-                       uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
-                       uint32_t* __restrict__ outidx, uint32_t* __restrict__ npairs,
-                       uint32_t* __restrict__ tsum) {
+// Pairs are appended to per-query-length segments (SegTab: a block may hold several lengths, and the aligner is
+// compiled per query length): segment i = query length sg.lmax - i, its pairs from sg.base[i], its counter cnt[i].
+// Slots are allocated per wave (queries are length-sorted, so a wave's lanes hold one or two segments): one atomic
+// per segment present in the wave.  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t seg_alloc(uint32_t n, uint32_t si, uint32_t* cnt) {
+  uint32_t start = 0;
+  unsigned long long pending = __ballot(n > 0u);
+  while (pending) {
+    const int lead = __builtin_ctzll(pending);
+    const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)si, lead);
+    const bool mine = n > 0u && si == L;
+    const unsigned long long grp = __ballot(mine);
+    const uint32_t v = mine ? n : 0u;
+    const uint32_t incl = wave_scan_dpp(v, OpAdd());
+    const uint32_t tot = lane63(incl);
+    uint32_t b = 0;
+    if ((int)(threadIdx.x & 63) == lead) b = atomicAdd(cnt + L, tot);
+    b = (uint32_t)__builtin_amdgcn_readlane((int)b, lead);
+    if (mine) start = b + incl - v;
+    pending &= ~grp;
+  }
+  return start;
+}
+
+__global__ __launch_bounds__(256) void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
+                                              const uint32_t* __restrict__ top_seqno, const uint8_t* __restrict__ top_count,
+                                              const uint8_t* __restrict__ ntop, const uint8_t* __restrict__ lens,
+                                              const uint32_t* __restrict__ res, const uint8_t* __restrict__ acc_tab,
+                                              const uint16_t* __restrict__ rank_tab, WalkState* __restrict__ ws,
+                                              uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
+                                              uint32_t* __restrict__ outidx, SegTab sg, uint32_t* __restrict__ seg_cnt,
+                                              unsigned long long* __restrict__ cells) {
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
-  if (qs >= nqs) return;
-  const int32_t q = q0 + qs / both;
-  const uint32_t strand = (uint32_t)(qs % both);
-  const int nt = ntop[qs];
-  WalkState w;
-  int emit_to;  // emit candidates [w.e, emit_to)
+  const bool live = qs < nqs;  // every lane stays to the slot allocation
+  const int32_t q = q0 + (live ? qs : 0) / both;
+  const uint32_t strand = (uint32_t)((live ? qs : 0) % both);
+  const int nt = live ? ntop[qs] : 0;
+  const int ql = lens[q];
+  WalkState w{};
+  bool act = live;
+  int emit_to = 0;  // emit candidates [w.e, emit_to)
   if (round < 0) {
     w.w = 0;
     w.done = (nt == 0) ? 1 : 0;
@@ -1607,42 +1633,46 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int
     w.cells = 0;
     w.lastkey = 0;
     w.e = 0;
-    const bool spec = nt > 0 && (int)top_count[(int64_t)qs * kTopHits] < spec_thr;
+    const bool spec = nt > 0 && (int)top_count[(int64_t)(live ? qs : 0) * kTopHits] < spec_thr;
     emit_to = min(nt, spec ? kWalk : kBatch);
-  } else {
+  } else if (live) {
     w = ws[qs];
-    if (w.done) return;
-    const int ql = lens[q];
-    // every batch whose results exist, in order
-    while (!w.done && w.w < w.e) {
-      const int b0 = w.w, b1 = min(nt, b0 + kBatch);
-      for (int x = b0; x < b1; x++) {
-        const uint32_t r = res[(int64_t)qs * kWalk + x];
-        const uint32_t m = r & 0xffu, L = (r >> 8) & 0xffu;
-        const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
-        w.cells += (uint32_t)(ql * lens[t]);
-        if (acc_tab[L * kTabM + m]) {
-          const uint16_t rk = rank_tab[L * kTabM + m];
-          if (!w.acc || rk > w.best_rank || (rk == w.best_rank && t < w.best_t)) {
-            w.best_rank = rk;
-            w.best_t = t;
+    act = !w.done;
+    if (act) {
+      // every batch whose results exist, in order
+      while (!w.done && w.w < w.e) {
+        const int b0 = w.w, b1 = min(nt, b0 + kBatch);
+        for (int x = b0; x < b1; x++) {
+          const uint32_t r = res[(int64_t)qs * kWalk + x];
+          const uint32_t m = r & 0xffu, L = (r >> 8) & 0xffu;
+          const uint32_t t = top_seqno[(int64_t)qs * kTopHits + x];
+          w.cells += (uint32_t)(ql * lens[t]);
+          if (acc_tab[L * kTabM + m]) {
+            const uint16_t rk = rank_tab[L * kTabM + m];
+            if (!w.acc || rk > w.best_rank || (rk == w.best_rank && t < w.best_t)) {
+              w.best_rank = rk;
+              w.best_t = t;
+            }
+            w.acc = 1;
           }
-          w.acc = 1;
         }
+        w.w = (uint8_t)b1;
+        const uint32_t tl = lens[top_seqno[(int64_t)qs * kTopHits + b1 - 1]];
+        w.lastkey = ((unsigned long long)(127u - top_count[(int64_t)qs * kTopHits + b1 - 1]) << 56) |
+                    ((unsigned long long)tl << 48) | top_seqno[(int64_t)qs * kTopHits + b1 - 1];
+        if (w.acc || b1 >= nt || b1 >= kWalk) w.done = 1;
       }
-      w.w = (uint8_t)b1;
-      const uint32_t tl = lens[top_seqno[(int64_t)qs * kTopHits + b1 - 1]];
-      w.lastkey = ((unsigned long long)(127u - top_count[(int64_t)qs * kTopHits + b1 - 1]) << 56) |
-                  ((unsigned long long)tl << 48) | top_seqno[(int64_t)qs * kTopHits + b1 - 1];
-      if (w.acc || b1 >= nt || b1 >= kWalk) w.done = 1;
+      // the rest of an unfinished walk is emitted at once (one more align launch instead of up to three
+      // dependent ones); walks are still evaluated batch by batch
+      emit_to = w.done ? (int)w.e : min(nt, kWalk);
     }
-    // the rest of an unfinished walk is emitted at once (one more align launch instead of up to three
-    // dependent ones); walks are still evaluated batch by batch
-    emit_to = w.done ? (int)w.e : min(nt, kWalk);
   }
-  if (emit_to > (int)w.e) {
+  const uint32_t n = (act && emit_to > (int)w.e) ? (uint32_t)(emit_to - (int)w.e) : 0u;
+  const uint32_t si = (uint32_t)(sg.lmax - ql);
+  const uint32_t k0 = seg_alloc(n, si, seg_cnt);
+  if (n) {
     const int b0 = w.e, b1 = emit_to;
-    const uint32_t base = atomicAdd(npairs, (uint32_t)(b1 - b0));
+    const uint32_t base = sg.base[si] + k0;
     uint32_t tl = 0;
     for (int x = b0; x < b1; x++) {
       const uint32_t k = base + (uint32_t)(x - b0);
@@ -1652,21 +1682,22 @@ __global__ void k_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int
       outidx[k] = (uint32_t)qs * kWalk + (uint32_t)x;
       tl += lens[t];
     }
-    atomicAdd(tsum, tl);  // target residues of the pairs emitted (cells computed = qlen * this)
+    atomicAdd(cells, (unsigned long long)ql * tl);  // cells the device computes for these pairs
     w.e = (uint8_t)b1;
   }
-  ws[qs] = w;
+  if (act) ws[qs] = w;
 }
 
 hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
-                       uint32_t* outidx, uint32_t* npairs, uint32_t* tsum, hipStream_t st) {
+                       uint32_t* outidx, const SegTab& sg, uint32_t* seg_cnt, unsigned long long* cells,
+                       hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_walk, dim3((nqs + 255) / 256), dim3(256), 0, st, round, q0, nqs, both, spec_thr,
                      top_seqno, top_count, ntop, lens, res, acc_tab, rank_tab, ws, pq, pt, outidx,
-                     npairs, tsum);
+                     sg, seg_cnt, cells);
   return hipGetLastError();
 }
 
@@ -1684,34 +1715,41 @@ __device__ __forceinline__ bool peer_relevant(const WalkState& w, uint32_t count
   return walk_open(w) || cand_key_dev(count, len, seqno) < w.lastkey;
 }
 
-__global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* __restrict__ lens,
-                             const WalkState* __restrict__ ws, const uint16_t* __restrict__ peer_id,
-                             const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
-                             uint32_t* __restrict__ pq, uint32_t* __restrict__ pt, uint32_t* __restrict__ outidx,
-                             uint32_t* __restrict__ npairs, uint32_t* __restrict__ tsum,
-                             uint32_t* __restrict__ nstat, uint32_t out0, const uint8_t* __restrict__ strong,
-                             unsigned long long* __restrict__ aligned, int32_t emit) {
-  // one thread per (query, strand): the slot allocation is one (wave-combined) atomic per wave
-  // instead of one per row of kPeerCap lanes (same-address atomics saturate near 90 per us)
+__global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both,
+                                                    const uint8_t* __restrict__ lens, const WalkState* __restrict__ ws,
+                                                    const uint16_t* __restrict__ peer_id,
+                                                    const uint8_t* __restrict__ peer_count, const uint8_t* __restrict__ npeer,
+                                                    uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
+                                                    uint32_t* __restrict__ outidx, SegTab sg, uint32_t* __restrict__ seg_cnt,
+                                                    unsigned long long* __restrict__ cells, uint32_t* __restrict__ nstat,
+                                                    uint32_t out0, const uint8_t* __restrict__ strong,
+                                                    unsigned long long* __restrict__ aligned, int32_t emit) {
+  // one thread per (query, strand); the slots come from a wave-aggregated allocation per query length (seg_alloc)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
-  if (qs >= nqs) return;
-  const int np = npeer[qs];
-  aligned[qs] = 0ull;
-  if (np == 255 || np == 0 || !emit) return;
-  const WalkState w = ws[qs];
+  const bool live = qs < nqs;  // every lane stays to the slot allocation
+  const int np = live ? npeer[qs] : 0;
+  if (live) aligned[qs] = 0ull;
   unsigned long long rel = 0;
-  for (int x = 0; x < np; x++) {
-    const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
-    // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
-    if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
-        !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])))
-      rel |= 1ull << x;
+  if (live && np != 255 && np != 0 && emit) {
+    const WalkState w = ws[qs];
+    for (int x = 0; x < np; x++) {
+      const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
+      // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
+      if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
+          !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])))
+        rel |= 1ull << x;
+    }
+    aligned[qs] = rel;
   }
-  aligned[qs] = rel;
-  if (!rel) return;
-  uint32_t k = atomicAdd(npairs, (uint32_t)__builtin_popcountll(rel));
-  atomicAdd(nstat, (uint32_t)__builtin_popcountll(rel));
-  const uint32_t qv = ((uint32_t)(q0 + qs / both) << 1) | (uint32_t)(qs % both);
+  const int32_t q = q0 + (live ? qs : 0) / both;
+  const int ql = lens[q];
+  const uint32_t n = (uint32_t)__builtin_popcountll(rel);
+  const uint32_t si = (uint32_t)(sg.lmax - ql);
+  const uint32_t k0 = seg_alloc(n, si, seg_cnt);
+  if (!n) return;
+  atomicAdd(nstat, n);
+  uint32_t k = sg.base[si] + k0;
+  const uint32_t qv = ((uint32_t)q << 1) | (uint32_t)(qs % both);
   uint32_t tl = 0;
   for (int x = 0; x < np; x++)
     if ((rel >> x) & 1ull) {
@@ -1722,17 +1760,17 @@ __global__ void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
       tl += lens[t];
       k++;
     }
-  atomicAdd(tsum, tl);
+  atomicAdd(cells, (unsigned long long)ql * tl);
 }
 
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
-                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
-                             unsigned long long* aligned, int32_t emit, hipStream_t st) {
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, const SegTab& sg,
+                             uint32_t* seg_cnt, unsigned long long* cells, uint32_t* nstat, uint32_t out0,
+                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, npairs, tsum, nstat, out0, strong, aligned, emit);
+                     peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, strong, aligned, emit);
   return hipGetLastError();
 }
 

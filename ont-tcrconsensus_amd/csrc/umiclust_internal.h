@@ -102,7 +102,10 @@ constexpr int kPostSpread = 32;
 constexpr int kPartCand = 64;  // candidates a (query-strand, part) passes to the merge
 // pass counters: [0..15] stats and pair counts, the postings partial sums, the overflowed-unit count
 constexpr int kUnitsSlot = 16 + kPostSpread * 32;
-constexpr int kCountersLen = kUnitsSlot + 32;
+// per-length pair counters of the three walk rounds (SegTab), kSegLens each
+constexpr int kSegLens = 32;  // query lengths one greedy block may span
+constexpr int kSegSlot = kUnitsSlot + 32;
+constexpr int kCountersLen = kSegSlot + 3 * kSegLens;
 constexpr int kFKmers = 32;  // frequent k-mers of a load eligible for deferral (PrefilterArgs::fkmer)
 struct PrefilterArgs {
   DevSeqs seqs;
@@ -207,17 +210,27 @@ struct WalkState {
 // round r >= 0 evaluates every batch whose results exist and, if the walk goes on, emits all of its
 // remaining candidates (up to kWalk): a pass has two dependent alignment launches, not five.
 // Speculation changes which alignments are computed, never the walk: batches are evaluated in order.
+// A block may hold several query lengths (the aligner is compiled per length): the walk and the peer pairs append
+// their pairs to per-length segments, segment i = query length lmax - i at pair index base[i] (its capacity is the
+// block's query-strands of that length x the pairs one can emit), counted in seg_cnt[i]; one alignment launch per
+// segment.  Blocks span at most kSegLens lengths.
+struct SegTab {
+  int32_t lmax;
+  int32_t nseg;
+  uint32_t base[kSegLens];
+};
 hipError_t launch_walk(int32_t round, int32_t q0, int32_t nqs, int32_t both, int32_t spec_thr,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint8_t* ntop,
                        const uint8_t* lens, const uint32_t* res, const uint8_t* acc_tab,
                        const uint16_t* rank_tab, WalkState* ws, uint32_t* pq, uint32_t* pt,
-                       uint32_t* outidx, uint32_t* npairs, uint32_t* tsum, hipStream_t st);
-// tsum accumulates the target lengths of the pairs emitted (cells computed = qlen * sum)
+                       uint32_t* outidx, const SegTab& sg, uint32_t* seg_cnt, unsigned long long* cells,
+                       hipStream_t st);
+// cells accumulates qlen x tlen of the pairs emitted (the cells the device computes for them)
 hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, const uint8_t* lens,
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
-                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, uint32_t* npairs,
-                             uint32_t* tsum, uint32_t* nstat, uint32_t out0, const uint8_t* strong,
-                             unsigned long long* aligned, int32_t emit, hipStream_t st);
+                             const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, const SegTab& sg,
+                             uint32_t* seg_cnt, unsigned long long* cells, uint32_t* nstat, uint32_t out0,
+                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, hipStream_t st);
 // per query-strand outcome of the device walk, as the host reads it (pinned host memory)
 constexpr int kInlineRel = 6;  // relevant peers listed in HostQs itself
 struct HostQs {

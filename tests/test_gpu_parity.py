@@ -266,6 +266,36 @@ def test_kmer_deferral(defer, split, monkeypatch):
     assert sd["kmer_postings"] + sd["kmer_postings_deferred"] >= s0["kmer_postings"]
 
 
+def _ragged_lengths(seed, n_mol=40, max_reads=3000):
+    """Long high-error UMIs cut to random lengths 40..112: bins whose blocks span many query lengths."""
+    u = synth.make_umis(n_mol, seed=seed, max_reads=max_reads, orient_mix=0.2, mean_reads=80.0, error_rate=0.05,
+                        split=(0.0, 0.5, 0.5), max_edits=3, pattern_fwd=synth.UMI_FWD_LONG, pattern_rev=synth.UMI_REV_LONG)
+    rng = np.random.default_rng(seed)
+    return [x[:int(rng.integers(40, min(len(x), 112) + 1))] if len(x) > 40 else x for x in u.as_list()]
+
+
+@pytest.mark.parametrize("mix", ["0", "1"])
+@pytest.mark.parametrize("block,split", [("default", "default"), ("300", "0"), ("300", "1"), ("97", "1")])
+def test_mixed_length_blocks(mix, block, split, monkeypatch):
+    """Greedy blocks across query-length changes (UMICLUST_MIXLEN, default on): the walk and the peer pairs append to
+    per-length pair segments, one alignment launch per length and round, round B per run of one length, blocks of
+    at most kSegLens (32) lengths -- here 40..112 nt in one bin; equal to the oracle with and without mixing."""
+    seqs = _ragged_lengths(41)
+    monkeypatch.setenv("UMICLUST_MIXLEN", mix)
+    if block != "default":
+        monkeypatch.setenv("UMICLUST_BLOCK", block)
+    if split != "default":
+        monkeypatch.setenv("UMICLUST_SPLIT", split)
+    p = (1, 0.85, 32, _lib.MAX_LEN)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(*p), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(*p), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+
+
 @pytest.mark.parametrize("split", ["0", "1", "2"])
 def test_pipeline_modes_deep_clusters(split, monkeypatch):
     """Config-5 style deep clusters (long UMIs, 15 % indels) with small blocks: peer lists overflow, blocks

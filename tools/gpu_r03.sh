@@ -45,6 +45,14 @@ for st in "$@"; do
     c3trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c3trace" -o run -- \
              python3 bench.py --config 3 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c3trace.log" 2>&1; rc=$?
              rm -f "$out/c3trace/run_kernel_trace.csv" ;;  # ~10^5 dispatches: the stats file is what is kept
+    envab) # ENVAB="NAME1=a,NAME2=b;NAME1=c" CFG=3: one bench line per env set (2 steps, 1 warmup)
+          i=0; IFS=';' read -ra sets <<< "$ENVAB"
+          for es in "${sets[@]}"; do
+            i=$((i+1)); IFS=',' read -ra kv <<< "$es"
+            env "${kv[@]}" timeout -k 10 500 python3 -u bench.py --config ${CFG:-3} --steps 2 --warmup 1 --no-cpu-baseline \
+              --no-e2e $EXTRA > "$out/envab$i.json" 2> "$out/envab$i.err" || { rc=$?; break; }
+            echo "$es" > "$out/envab$i.env"
+          done ;;
     c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
     c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
