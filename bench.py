@@ -222,6 +222,8 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help="skip the file leg (config 2, N = 1)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="configs 3/4: bins clustered concurrently per GPU (one device context per lane)")
+    ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "0")),
+                    help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -294,7 +296,8 @@ def main() -> None:
         def step():
             return [ctx.cluster()]
     else:
-        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens, lanes=args.lanes, device=local_rank)
+        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens, lanes=args.lanes, device=local_rank,
+                              pack_reads=args.pack_reads)
         runners.append(r1)
         if args.config == 4:
             # round-2 inputs come from the round-1 results (deterministic): built once, resident like round 1
@@ -302,7 +305,7 @@ def main() -> None:
             bins2 = binset.round2_binset(bins, r1.results())
             ctx2 = _lib.Context(local_rank)
             runners.append(binset.BinRunner(ctx2, bins2, binset.ROUND2["preset"], binset.ROUND2["identity"], *lens,
-                                            lanes=args.lanes, device=local_rank))
+                                            lanes=args.lanes, device=local_rank, pack_reads=args.pack_reads))
 
         def step():
             out = []
@@ -377,8 +380,9 @@ def main() -> None:
             # per-bin wall times of the last step, measured while `lanes` bins share the GPU (so they do not
             # add up to the step): the largest bin bounds any split of these bins over GPUs
             per_bin = [s["t_total_s"] for s in last]
-            out["largest_bin_s"] = max(per_bin) if per_bin else 0.0
+            out["largest_bin_s"] = max(per_bin) if per_bin else 0.0  # (the largest pack, with packing)
             out["bins_timed"] = len(per_bin)
+            out["pack_reads"] = args.pack_reads
             out["lanes"] = args.lanes
         cpu = None
         if not args.no_cpu_baseline and world == 1:

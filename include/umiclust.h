@@ -206,6 +206,12 @@ int32_t umiclust_load_bins(umiclust_ctx *ctx, const umiclust_params *p, const ch
                            const int64_t *offsets, int64_t n, const int64_t *bin_start, int32_t nbins);
 /* cluster one bin of the load; returns its number of clusters */
 int64_t umiclust_cluster_bin(umiclust_ctx *ctx, int32_t bin, umiclust_stats *stats);
+/* cluster the bins [first, first + nbins) of the load as one pack: the bins' queries in one greedy order (each bin
+ * sorted on its own, the bins one after another), so small bins share the GPU passes of the bins around them.  Every
+ * bin's result is exactly its own vsearch run's (tcr_consensus.py:231-245 runs one vsearch per bin); fetch each with
+ * umiclust_fetch_bin.  Stats cover the whole pack; returns the pack's number of clusters.  Needs the sequential
+ * policy (policy_threads = 0). */
+int64_t umiclust_cluster_pack(umiclust_ctx *ctx, int32_t first, int32_t nbins, umiclust_stats *stats);
 /* umiclust_fetch for one clustered bin: arrays over the bin's input records (bin-local index) */
 int64_t umiclust_fetch_bin(umiclust_ctx *ctx, int32_t bin, int32_t *cluster, uint8_t *strand,
                            uint8_t *centroid, char *cons, int64_t cons_cap, int64_t *cons_off);

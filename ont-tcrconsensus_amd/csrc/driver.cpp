@@ -168,6 +168,7 @@ struct Pass {
   DevBuf<uint32_t> d_ppost;  // postings touched per (query-strand, part), summed by k_pf_merge
   DevBuf<uint32_t> d_pdef;   // postings of deferred lists per (query-strand, part) (frequent-k-mer deferral)
   DevBuf<uint32_t> d_pdm;    // deferred k-mer bits of each (query-strand, part)'s candidates (k_pf_merge)
+  DevBuf<uint32_t> d_pftab;  // k_pf_table's list tables of the counting launch (UMICLUST_PFTAB=0: none)
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
@@ -328,6 +329,12 @@ struct umiclust_ctx {
   // of them; UMICLUST_DEFER = the most k-mers a query-strand defers (default 0: off -- on config 2 deferring 2-4
   // k-mers streams 14-22 % fewer postings but the counting kernel's launch time is unchanged within noise:
   // 1.575 ms off, 1.589-1.600 ms at 2-4, profiles/r03/defer_ab.json)
+  // packs (umiclust_cluster_pack, multi-bin loads): sorted seqno -> load bin, each bin's first seqno and its first
+  // centroid ordinal in the pack being clustered (INT32_MAX until indexed), the per-bin k-mer XOR masks
+  std::vector<int32_t> hqbin;
+  DevBuf<int32_t> d_qbin, d_bin_seq0, d_bin_ord0;
+  PinBuf<int32_t> h_bin_ord0;
+  bool pack_on = false;            // the current cluster_all call clusters a pack of several bins
   DevBuf<uint32_t> d_fmask;
   DevBuf<uint32_t> d_cent_fm;     // ordinal -> fmask of its + strand (PrefilterArgs::fmask_ord)
   uint16_t fkmer[kFKmers] = {};
@@ -426,6 +433,11 @@ struct umiclust_ctx {
   int32_t block_min = 2048;       // UMICLUST_BLOCK_MIN: the smallest default block (bins of < 16 x this)
   // UMICLUST_MIXLEN=0: blocks end at every query-length change (one alignment launch per round); =1: a block spans
   // up to kSegLens lengths (one launch per length and round): a small bin is then a few passes, not one per length
+  // UMICLUST_PFTAB=1: the list tables of the counting launch are built ahead by k_pf_table (one wave per unit, no
+  // barriers); the counting workgroups then spend 5.2k instead of 15.6k cycles on the table, but the launch is not
+  // faster (1.62 -> 1.76 ms per count + table on config 2: the counting is bound by the LDS array, ~73 % busy, 60 %
+  // of it bank-conflict replays; profiles/r03/pftab_ab.json), so off by default
+  bool pf_tab = false;
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
@@ -718,12 +730,36 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
 // threshold, and one download of the walk states, top lists, walked results and peer results.
 // The peer window is [prev->base, q0+nq) with prev = the previous block's tile, or the block
 // alone (prev == nullptr).
+// the longest / shortest query of a block (sorted within a bin, but a pack's lengths restart at every bin)
+int32_t block_maxlen(const umiclust_ctx* c, int32_t q0, int32_t nq) {
+  int32_t m = 0;
+  for (int32_t q = q0; q < q0 + nq; q++) m = std::max<int32_t>(m, c->hlen[q]);
+  return m;
+}
+int32_t block_minlen(const umiclust_ctx* c, int32_t q0, int32_t nq) {
+  int32_t m = kMaxLen;
+  for (int32_t q = q0; q < q0 + nq; q++) m = std::min<int32_t>(m, c->hlen[q]);
+  return m;
+}
+
 // the frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask)
-void set_defer(const umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
+void set_defer(umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
+  a.qbin = c->pack_on ? c->d_qbin.p : nullptr;
+  a.bin_seq0 = c->d_bin_seq0.p;
+  a.bin_ord0 = c->d_bin_ord0.p;
+  a.cent_len = c->pack_on ? c->d_cent_len.p : nullptr;
   a.fmask = c->d_fmask.p;
   a.fmask_ord = c->d_cent_fm.p;
   a.pdef = P.d_pdef.p;
   a.pdm = P.d_pdm.p;
+  a.pftab = nullptr;
+  if (c->pf_tab && a.nlist_cap > 0) {
+    // sized by this launch (the table stride follows nlist_cap); grown only between passes of this buffer set,
+    // whose previous counting launch has completed (its events were waited on before the set is reused)
+    const size_t need = (size_t)a.nq * a.both * kParts * pf_table_stride(a.nlist_cap);
+    if (need > P.d_pftab.n) c->hip(P.d_pftab.ensure(need + need / 4), "alloc list tables");
+    a.pftab = P.d_pftab.p;
+  }
   a.defer_max = c->nfk > 0 ? c->defer_max : 0;
   a.defer_min_thr = c->defer_min_thr;
   for (int i = 0; i < kFKmers; i++) a.fkmer[i] = c->fkmer[i];
@@ -745,7 +781,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   own.prebuilt = false;
   own.base = q0;
   own.seg = region;
-  own.len = c->hlen[q0];  // the block's longest query
+  own.len = block_maxlen(c, q0, nq);  // the block's longest query
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -816,7 +852,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     a.peer_id_add = a.peer_shift;
   }
   // list table of the lean kernel: every k-mer of the block's length in every tile it reads
-  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, c->hlen[q0] - 7) *
+  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, block_maxlen(c, q0, nq) - 7) *
                                               ((a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0) + kPeerTiles));
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
@@ -862,7 +898,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   st = c->st_al;
   DevSeqs ds = dev_seqs(c);
   // the block's query lengths (sorted, non-increasing): one pair segment and one alignment launch per length
-  const int32_t lmax = c->hlen[q0], nsg = lmax - c->hlen[q0 + nq - 1] + 1;
+  const int32_t lmax = block_maxlen(c, q0, nq), nsg = lmax - block_minlen(c, q0, nq) + 1;
   if (nsg > kSegLens) c->fail(UMICLUST_EINVAL, "block spans %d query lengths (> %d)", nsg, kSegLens);
   int32_t nql[kSegLens] = {};
   for (int32_t q = q0; q < q0 + nq; q++) nql[lmax - c->hlen[q]]++;
@@ -1000,7 +1036,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   a.pncand = P.d_pncand.p;
   a.units = P.d_units.p;
   a.nunits = P.d_anunits.p;
-  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, c->hlen[q0] - 7) * (nv + kPeerTiles));
+  a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, block_maxlen(c, q0, nq) - 7) * (nv + kPeerTiles));
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;
@@ -1620,6 +1656,23 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
                             st),
              "h2d seq2ord");
   }
+  if (c->pack_on) {
+    // a bin's first query is always a centroid (nothing of its bin precedes it): its ordinal opens the bin's range
+    // (the bins starting inside this append are consecutive: one copy)
+    int32_t blo = INT32_MAX, bhi = -1;
+    for (size_t i = 0; i < new_cents.size(); i++) {
+      const int32_t q = new_cents[i], b = c->hqbin[q];
+      if (q == c->bin_s[b]) {
+        c->h_bin_ord0.p[b] = ord0 + (int32_t)i;
+        blo = std::min(blo, b);
+        bhi = std::max(bhi, b);
+      }
+    }
+    if (bhi >= blo)
+      c->hip(hipMemcpyAsync(c->d_bin_ord0.p + blo, c->h_bin_ord0.p + blo, (size_t)(bhi - blo + 1) * 4,
+                            hipMemcpyHostToDevice, st),
+             "h2d bin ord0");
+  }
   memcpy(c->h_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4);
   memcpy(c->h_cent_len.p + ord0, c->cent_len.data() + ord0, new_cents.size());
   c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->h_cent.p + ord0, new_cents.size() * 4, hipMemcpyHostToDevice, st),
@@ -1677,11 +1730,18 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   }
 }
 
-void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
+// Cluster bin `bin` -- or, npk > 1, the pack of bins [bin, bin + npk) in one greedy order (each bin's queries in
+// its own sorted order, the bins one after another: bins never interact, so this is every bin's own vsearch run):
+// blocks then span bin boundaries and small bins share passes; the prefilter keeps only a query's own bin
+// (PrefilterArgs::qbin) and the results are split per bin.
+void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
   const double t0 = now_s();
-  if (bin < 0 || bin + 1 >= (int32_t)c->bin_s.size()) c->fail(UMICLUST_EINVAL, "bin %d out of range", bin);
-  // one bin = the sorted seqnos [s0, s1); seqnos stay absolute everywhere
-  const int32_t s0 = c->bin_s[bin], s1 = c->bin_s[bin + 1];
+  if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
+    c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
+  if (npk > 1 && c->o4_T) c->fail(UMICLUST_EINVAL, "packs of bins need the sequential policy (policy_threads = 0)");
+  c->pack_on = npk > 1;
+  // one bin (or pack) = the sorted seqnos [s0, s1); seqnos stay absolute everywhere
+  const int32_t s0 = c->bin_s[bin], s1 = c->bin_s[bin + npk];
   const int32_t n = s1 - s0;
   c->cur_bin = bin;
   std::fill(c->cno.begin() + s0, c->cno.begin() + s1, -1);
@@ -1703,7 +1763,12 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   c->index_end = 0;
   c->nix = 0;
   c->stats = umiclust_stats{};
-  c->stats.n_input = c->bin_in[bin + 1] - c->bin_in[bin];
+  c->stats.n_input = c->bin_in[bin + npk] - c->bin_in[bin];
+  if (c->pack_on) {
+    for (int32_t b = bin; b < bin + npk; b++) c->h_bin_ord0.p[b] = INT32_MAX;  // no centroid of the bin indexed yet
+    c->hip(hipMemcpyAsync(c->d_bin_ord0.p + bin, c->h_bin_ord0.p + bin, (size_t)npk * 4, hipMemcpyHostToDevice, c->st),
+           "h2d bin ord0");
+  }
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
@@ -1747,18 +1812,26 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   std::vector<std::pair<int32_t, int32_t>> blocks;
   // blocks across length changes: bins below the full block size (config 3: 4.15 vs 3.61 M UMIs/s; a 2M-read bin
   // gains nothing, its length runs are many blocks long: profiles/r03/mixlen_ab.json)
-  const bool mix = c->mix_len > 0 || (c->mix_len < 0 && B < kMaxBlock);
+  const bool mix = c->mix_len > 0 || (c->mix_len < 0 && (B < kMaxBlock || c->pack_on));
   // the blocks from query `from` on, at most `bmax` queries (of one length each unless mix)
   auto split_blocks = [&](int32_t from, int32_t bmax) {
+    // packs: bmax (a deep cluster's halved size) holds until the end of `from`'s bin, the next bins start at B
+    const int32_t until = c->pack_on ? c->bin_s[c->hqbin[from] + 1] : s1;
     for (int32_t q0 = from; q0 < s1;) {
       int32_t same = 1;
+      const int32_t bcap = q0 < until ? bmax : B;
       if (mix && !c->o4_T) {  // across length changes, at most kSegLens lengths (one pair segment each);
                                      // O4 batched rounds keep one length per block (mixed blocks there: 21 more
                                      // alignments than the oracle on test_batched_rounds_deep_clusters, unresolved)
-        const int32_t lim = std::min<int32_t>(bmax, s1 - q0);
-        while (same < lim && c->hlen[q0] - c->hlen[q0 + same] < kSegLens) same++;
+        const int32_t lim = std::min<int32_t>(bcap, s1 - q0);
+        int32_t lo = c->hlen[q0], hi = lo;  // (a pack's lengths restart at every bin)
+        while (same < lim && std::max<int32_t>(hi, c->hlen[q0 + same]) - std::min<int32_t>(lo, c->hlen[q0 + same]) < kSegLens) {
+          lo = std::min<int32_t>(lo, c->hlen[q0 + same]);
+          hi = std::max<int32_t>(hi, c->hlen[q0 + same]);
+          same++;
+        }
       } else {
-        while (q0 + same < s1 && same < bmax && c->hlen[q0 + same] == c->hlen[q0]) same++;
+        while (q0 + same < s1 && same < bcap && c->hlen[q0 + same] == c->hlen[q0]) same++;
       }
       blocks.push_back({q0, same});
       q0 += same;
@@ -1797,7 +1870,17 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     sync_index(std::min(wnom, rs));
   };
   // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
-  int32_t b_eff = std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
+  int32_t b_eff = c->pack_on ? B : std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
+  int32_t eff_bin = -1;  // packs: the bin b_eff was last halved in (a deep cluster of one bin does not shrink the next)
+  auto halve = [&](int32_t q) -> bool {  // false: already at the smallest block
+    if (c->pack_on && c->hqbin[q] != eff_bin) {
+      eff_bin = c->hqbin[q];
+      b_eff = B;
+    }
+    if (b_eff <= 256) return false;
+    b_eff /= 2;
+    return true;
+  };
   split_blocks(s0, b_eff);
   int32_t nb = (int32_t)blocks.size();
   std::vector<int32_t> new_cents;
@@ -1915,8 +1998,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
           c->hip(hipMemsetAsync(Q.d_anunits.p, 0, 4, c->st), "memset");
         }
         run_alone(blocks[k].first, blocks[k].second);
-        if (b_eff > 256 && k + 1 < nb) {
-          b_eff /= 2;
+        if (k + 1 < nb && halve(blocks[k].first)) {
           const int32_t from = blocks[k].first + blocks[k].second;
           blocks.resize((size_t)k + 1);
           split_blocks(from, b_eff);
@@ -1959,8 +2041,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
       run_alone(blocks[k].first, blocks[k].second);
       // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
       // same-molecule peers), so the overflow re-runs do not repeat block after block
-      if (b_eff > 256 && k + 1 < nb) {
-        b_eff /= 2;
+      if (k + 1 < nb && halve(blocks[k].first)) {
         const int32_t from = blocks[k].first + blocks[k].second;
         blocks.resize((size_t)k + 1);
         split_blocks(from, b_eff);
@@ -2002,8 +2083,13 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
   for (int32_t s = s0; s < s1; s++) size[c->cno[s]]++;
   std::vector<int32_t> order(K);
   for (int32_t k = 0; k < K; k++) order[k] = k;
+  // (a pack's clusters stay grouped by bin -- creation order already is -- and are sorted within their bin)
+  auto cbin = [&](int32_t k) { return c->pack_on ? c->hqbin[c->cent[k]] : 0; };
   if (c->p.clusterout_sort)
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return size[a] > size[b]; });
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      const int32_t ba = cbin(a), bb = cbin(b);
+      return ba != bb ? ba < bb : size[a] > size[b];
+    });
   c->rank_of.assign(K, 0);
   for (int32_t k = 0; k < K; k++) c->rank_of[order[k]] = k;
   c->ostart.assign((size_t)K + 1, 0);
@@ -2095,11 +2181,28 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false) {
     for (int32_t k = 0; k < K; k++)
       memcpy(c->cons.data() + c->cons_off[k], craw.data() + (size_t)k * kConsCap, clen[k]);
   }
-  auto& bo = c->bout[bin];
-  bo.done = true;
-  bo.K = K;
-  bo.cons = c->cons;
-  bo.cons_off = c->cons_off;
+  if (!c->pack_on) {
+    auto& bo = c->bout[bin];
+    bo.done = true;
+    bo.K = K;
+    bo.cons = c->cons;
+    bo.cons_off = c->cons_off;
+  } else {
+    // per bin: its output clusters are the consecutive output numbers [k0, k1); numbers within the bin
+    int32_t k0 = 0;
+    for (int32_t b = bin; b < bin + npk; b++) {
+      int32_t k1 = k0;
+      while (k1 < K && cbin(order[k1]) == b) k1++;
+      auto& bo = c->bout[b];
+      bo.done = true;
+      bo.K = k1 - k0;
+      bo.cons_off.assign((size_t)bo.K + 1, 0);
+      for (int32_t k = 0; k <= bo.K; k++) bo.cons_off[k] = c->cons_off[k0 + k] - c->cons_off[k0];
+      bo.cons.assign(c->cons.begin() + c->cons_off[k0], c->cons.begin() + c->cons_off[k1]);
+      for (int32_t s = c->bin_s[b]; s < c->bin_s[b + 1]; s++) c->ocl[s] -= k0;
+      k0 = k1;
+    }
+  }
   c->stats.n_clusters = K;
   c->stats.t_prefilter_s = t_pf;
   c->stats.t_align_s = t_al;
@@ -2256,6 +2359,34 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
     c->hip(hipStreamSynchronize(c->st), "sync load");
   }
   c->ambig = amb != 0;
+  c->hqbin.clear();
+  if (nbins > 1 && c->n > 0) {
+    // packs: per-bin XOR masks on the k-mers (a bijection within a bin: counts within a bin are unchanged; other
+    // bins' structured k-mers land on unrelated lists), sorted seqno -> bin, each bin's first seqno
+    c->hqbin.resize(c->n);
+    std::vector<uint16_t> xm(nbins);
+    for (int32_t b = 0; b < nbins; b++) {
+      for (int32_t s = c->bin_s[b]; s < c->bin_s[b + 1]; s++) c->hqbin[s] = b;
+      uint32_t h = (uint32_t)b * 0x9E3779B1u + 0x7F4A7C15u;  // murmur3 finaliser
+      h ^= h >> 16;
+      h *= 0x85EBCA6Bu;
+      h ^= h >> 13;
+      h *= 0xC2B2AE35u;
+      h ^= h >> 16;
+      xm[b] = (uint16_t)(h ^ (h >> 16));
+    }
+    c->hip(c->d_qbin.ensure(c->n), "alloc");
+    c->hip(c->d_bin_seq0.ensure(nbins), "alloc");
+    c->hip(c->d_bin_ord0.ensure(nbins), "alloc");
+    c->hip(c->h_bin_ord0.ensure(nbins), "pin");
+    DevBuf<uint16_t> d_xm;
+    c->hip(d_xm.ensure(nbins), "alloc");
+    c->hip(hipMemcpyAsync(c->d_qbin.p, c->hqbin.data(), (size_t)c->n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(c->d_bin_seq0.p, c->bin_s.data(), (size_t)nbins * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(d_xm.p, xm.data(), (size_t)nbins * 2, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(launch_kmer_xor(c->d_kmers.p, c->d_nk.p, c->n, c->d_qbin.p, d_xm.p, c->st), "k-mer masks");
+    c->hip(hipStreamSynchronize(c->st), "sync load");
+  }
   {
     const int64_t sampled = c->n > 0 ? ((int64_t)c->n + stride - 1) / stride : 0;
     const double min_count = std::max(1.0, c->defer_freq * (double)sampled);
@@ -2415,6 +2546,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
@@ -2606,6 +2738,16 @@ int64_t umiclust_cluster_bin(umiclust_ctx* c, int32_t bin, umiclust_stats* stats
     if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster_bin before umiclust_load_bins");
     L3Pin pin(c);  // only with one live context (a bin-set runner's lanes each own one: then it stays off)
     cluster_all(c, bin, true);
+    if (stats) *stats = c->stats;
+    return c->nclusters;
+  });
+}
+
+int64_t umiclust_cluster_pack(umiclust_ctx* c, int32_t first, int32_t nbins, umiclust_stats* stats) {
+  UC_GUARD(c, {
+    if (!c->loaded) c->fail(UMICLUST_ESTATE, "umiclust_cluster_pack before umiclust_load_bins");
+    L3Pin pin(c);
+    cluster_all(c, first, true, nbins);
     if (stats) *stats = c->stats;
     return c->nclusters;
   });

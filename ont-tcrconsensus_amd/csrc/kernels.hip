@@ -399,7 +399,6 @@ static_assert(kPfLists < (1 << kListBits) && (uint64_t)kPfLists * (kTile / kPart
 constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
 constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
 
-constexpr int kPfWinBase = 128;   // windows whose base list and start mask are tabulated (the rest: search)
 constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors
 struct PfShared {
   union {
@@ -489,6 +488,31 @@ __device__ __forceinline__ TileView load_view(const TileView* p) {
     u32x4 a, b;
   } r{q[0], q[1]};
   return __builtin_bit_cast(TileView, r);
+}
+
+// packs: the bytes of a counter word from byte nb on (nb <= 0: all four, nb >= 4: none)
+__device__ __forceinline__ uint32_t keep_from(int nb) {
+  return nb <= 0 ? 0xffffffffu : nb >= 4 ? 0u : ~((1u << (8 * nb)) - 1u);
+}
+// packs: the query's bin bounds (PrefilterArgs::qbin): seq0 = its first seqno, ord0 = its first centroid ordinal
+__device__ __forceinline__ void pack_bounds(const PrefilterArgs& a, int32_t q, int32_t& seq0, int32_t& ord0) {
+  seq0 = 0;
+  ord0 = 0;
+  if (a.qbin) {
+    const int32_t qb = __builtin_amdgcn_readfirstlane(a.qbin[q]);
+    seq0 = __builtin_amdgcn_readfirstlane(a.bin_seq0[qb]);
+    ord0 = __builtin_amdgcn_readfirstlane(a.bin_ord0[qb]);
+  }
+}
+// first counter sub-id of a part whose ordinal (seg0 + (c << kPartShift) + part) is >= ord0
+__device__ __forceinline__ int32_t pack_cmin(int32_t ord0, int32_t seg0, int part, int32_t nsub) {
+  const int64_t d = (int64_t)ord0 - seg0 - part;
+  return d <= 0 ? 0 : (int32_t)min<int64_t>((int64_t)nsub, (d + kParts - 1) >> kPartShift);
+}
+// first peer byte index (4 x + b) of a peer tile whose seqno (base + ((4 x + b) << kPartShift) + part) is >= seq0
+__device__ __forceinline__ int32_t pack_pmin(int32_t seq0, int32_t base, int part) {
+  const int64_t d = (int64_t)seq0 - base - part;
+  return d <= 0 ? 0 : (int32_t)min<int64_t>(1 << 24, (d + kParts - 1) >> kPartShift);
 }
 
 // The u8 counters live at LDS byte kBase (k_pf_count: 0, k_pf_full: kPfSharedBytes).  Neither kernel has
@@ -837,6 +861,8 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
   }
   if (tid < kCge) S.cge[tid] = tid <= kMaxLen ? a.cnt_ge[tid] : 0;
   const int64_t pq_ = (int64_t)qs * kParts + part;
+  int32_t seq0, ord0;
+  pack_bounds(a, q, seq0, ord0);
   const int npass = a.nseg > 0 ? a.nseg : 1;
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
   for (int sg = 0; sg < npass; sg++) {
@@ -874,12 +900,15 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
     // scan: centroid counters >= thr (SWAR: bytes <= 65, so byte + 128 - thr sets bit 7 iff >= thr);
     // each wave sweeps 64 counter vectors per step and takes LDS slots with one atomic per step
     const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
+    const int32_t cmin = pack_cmin(ord0, seg0, part, nsubC);  // packs: earlier bins' centroids are never candidates
     if (thr > 0) {
       const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
       const uint4* c4 = cnt4 + kCentBase / 16;
-      for (int x0 = wv * 64; x0 < lim4; x0 += kPfThreads) {
+      for (int x0 = (cmin >> 4) + wv * 64; x0 < lim4; x0 += kPfThreads) {
         const int x = x0 + lane;
-        const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+        const int cb = cmin - x * 16;
+        if (cb > 0) v = make_uint4(v.x & keep_from(cb), v.y & keep_from(cb - 4), v.z & keep_from(cb - 8), v.w & keep_from(cb - 12));
         // most sweeps hold no candidate: one OR over the four words decides (no carries cross bytes)
         if (__ballot((((v.x + add) | (v.y + add) | (v.z + add) | (v.w + add)) & 0x80808080u) != 0u) == 0ull)
           continue;
@@ -910,9 +939,10 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
         const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
         const int nwords = (nsubP + 3) >> 2;
         const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
-        for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
+        const int32_t pmin = pack_pmin(seq0, pv.base, part);  // packs: earlier bins' queries are never peers
+        for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kPfThreads) {
           const int x = x0 + lane;
-          const uint32_t w = x < nwords ? pw[x] : 0u;
+          const uint32_t w = x < nwords ? pw[x] & keep_from(pmin - 4 * x) : 0u;
           const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
           uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
           if (__ballot(mk != 0u) == 0ull) continue;
@@ -941,7 +971,7 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
         __syncthreads();
         const int c0 = ch * kPfCand;
         const int c1 = min(nsubC, c0 + kPfCand);
-        for (int c = c0 + tid; c < c1; c += kPfThreads)
+        for (int c = max(c0, cmin) + tid; c < c1; c += kPfThreads)
           if ((int)cnt_get(cnt, (uint32_t)(kCentBase + c)) >= thr) S.cand[atomicAdd(&S.ncand, 1u)] = (uint32_t)c;
         __syncthreads();
       }
@@ -955,11 +985,15 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
         const uint32_t cntv = cnt_get(cnt, kCentBase + c);
         const int32_t ord = seg0 + (int32_t)(c << kPartShift) + part;
         uint32_t len = 0;
-        const int4* g4 = reinterpret_cast<const int4*>(S.cge);
+        if (a.cent_len) {
+          len = (uint32_t)a.cent_len[ord] + 1u;  // packs: lengths are not monotone in the ordinal across bins
+        } else {
+          const int4* g4 = reinterpret_cast<const int4*>(S.cge);
 #pragma unroll
-        for (int i = 0; i < kCge / 4; i++) {
-          const int4 g = g4[i];
-          len += (uint32_t)(g.x > ord) + (uint32_t)(g.y > ord) + (uint32_t)(g.z > ord) + (uint32_t)(g.w > ord);
+          for (int i = 0; i < kCge / 4; i++) {
+            const int4 g = g4[i];
+            len += (uint32_t)(g.x > ord) + (uint32_t)(g.y > ord) + (uint32_t)(g.z > ord) + (uint32_t)(g.w > ord);
+          }
         }
         S.cand[x] = ((127u - cntv) << 23) | ((len - 1u) << 16) | c;
       }
@@ -1078,6 +1112,122 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_pf_full(PrefilterArgs a, int 
   }
 }
 
+// The list table of k_pf_count, built ahead by k_pf_table into global memory: one wave per (query-strand, part)
+// unit, no barriers (a wave-level DPP scan lays the non-empty lists end to end), high occupancy (no counters in
+// LDS), so its latency chain -- tile views, list offsets, scan, writes -- overlaps across many units instead of
+// sitting inside every counting workgroup's lifetime between its barriers.  Unit image (u32 words, 16-B aligned):
+// [0] T (chunks), [1] nlc (lists), [2] deferred chunks, [3] -, then the k_pf_count LDS table image: wbase
+// (u16 x kPfWinBase), wlo, whi (u32 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap).
+__global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __restrict__ tab, int32_t nunits) {
+  __shared__ uint32_t wl[kPfWinBase], wh[kPfWinBase];
+  __shared__ uint16_t wb[kPfWinBase];
+  const int unit = (int)blockIdx.x;
+  if (unit >= nunits) return;
+  const int lane = (int)threadIdx.x;
+  const int part = unit & (kParts - 1);
+  const int qs = unit >> kPartShift;
+  const int strand = qs % a.both;
+  const int32_t q = a.q0 + qs / a.both;
+  const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
+  const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
+  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane < kKmerStride - 64 ? lane : 0)];
+  const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
+  const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
+  // frequent-k-mer deferral (PrefilterArgs::fmask): the lanes holding D's k-mers skip their centroid-tile lists
+  uint32_t dmask = 0u;
+  if (a.defer_max > 0 && thr > 0) {
+    uint32_t m = a.fmask[(int64_t)q * 2 + strand];
+    for (int i = 0; i < a.defer_max && m != 0u && thr - (i + 1) >= a.defer_min_thr; i++) {
+      dmask |= m & (0u - m);
+      m &= m - 1u;
+    }
+  }
+  dmask = (uint32_t)__builtin_amdgcn_readfirstlane((int)dmask);
+  bool skip0 = false, skip1 = false;
+  for (uint32_t m = dmask; m != 0u; m &= m - 1u) {
+    const uint32_t fk = a.fkmer[__builtin_ctz(m)];
+    skip0 |= lane < nk && km0 == fk;
+    skip1 |= lane + 64 < nk && km1 == fk;
+  }
+  const int nct = a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0;
+  const int ntl = nct + kPeerTiles;
+  const uint64_t pbase = a.seg_base[0];
+  // every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's, list 0 past nk)
+  u32x2 o0[kPfTiles], o1[kPfTiles];
+  uint32_t tb[kPfTiles];
+  bool lv[kPfTiles];
+#pragma unroll
+  for (int ti = 0; ti < kPfTiles; ti++) {
+    TileView tv;
+    if (ti < nct) tv = load_view(a.tiles + ti);
+    else if (ti < ntl) tv = a.peer[ti - nct];
+    else tv.n = 0;
+    lv[ti] = thr > 0 && ti < ntl && tv.n > 0;
+    const uint32_t* op = uniform_ptr((lv[ti] ? tv.off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
+    tb[ti] = lv[ti] ? (uint32_t)(tv.post_base - pbase) : 0u;
+    o0[ti] = ld_off2(op, km0);
+    o1[ti] = ld_off2(op, km1);
+  }
+  uint32_t sum_ch = 0, sum_ne = 0, dch = 0;
+#pragma unroll
+  for (int ti = 0; ti < kPfTiles; ti++) {
+    const bool cen = ti < nct;
+    const uint32_t c0 = (lv[ti] && lane < nk) ? (o0[ti].y - o0[ti].x) >> 3 : 0u;
+    const uint32_t c1 = (lv[ti] && lane + 64 < nk) ? (o1[ti].y - o1[ti].x) >> 3 : 0u;
+    const bool s0 = skip0 && cen, s1 = skip1 && cen;
+    dch += (s0 ? c0 : 0u) + (s1 ? c1 : 0u);
+    o0[ti].y = s0 ? 0u : c0;  // from here on: .x list offset, .y chunks
+    o1[ti].y = s1 ? 0u : c1;
+    sum_ch += o0[ti].y + o1[ti].y;
+    sum_ne += (o0[ti].y ? 1u : 0u) + (o1[ti].y ? 1u : 0u);
+  }
+  if (lane < kPfWinBase / 2) {
+    wl[lane] = wl[lane + 64] = 0u;
+    wh[lane] = wh[lane + 64] = 0u;
+  }
+  // wave scan of (chunks << kListBits | lists): the non-empty lists end to end, lane-major
+  const uint32_t packed = (sum_ch << kListBits) | sum_ne;
+  const uint32_t inc = wave_scan_dpp(packed, OpAdd());
+  const uint32_t tot = lane63(inc), ex = inc - packed;
+  const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
+  uint32_t* img = tab + (size_t)unit * pf_table_stride(a.nlist_cap);
+  uint32_t* lstart = img + 4 + kPfWinBase / 2 + 2 * kPfWinBase;
+  uint32_t* lbias = lstart + a.nlist_cap + 66;
+  uint32_t li = ex & kListMask, ci = ex >> kListBits;
+  auto put = [&](uint32_t nch, uint32_t bse) {
+    if (!nch) return;
+    lstart[li] = ci;
+    lbias[li] = bse - 8u * ci;
+    if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase) atomicOr(((ci & 32u) ? wh : wl) + (ci >> 6), 1u << (ci & 31u));
+    for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch && w < (uint32_t)kPfWinBase; w++) wb[w] = (uint16_t)li;
+    li++;
+    ci += nch;
+  };
+#pragma unroll
+  for (int ti = 0; ti < kPfTiles; ti++) {
+    put(o0[ti].y, tb[ti] + o0[ti].x);
+    put(o1[ti].y, tb[ti] + o1[ti].x);
+  }
+  if (lane < 66) lstart[nlc + lane] = T;
+  if (lane == 0) {
+    img[0] = T;
+    img[1] = nlc;
+    img[2] = 0u;
+  }
+  const uint32_t dsum = lane63(wave_scan_dpp(dch, OpAdd()));
+  if (lane == 0) img[2] = dsum;
+  // the window tables (LDS of this wave: its own writes are complete in order) to the image
+  const uint32_t nw = min((T + 63u) >> 6, (uint32_t)kPfWinBase);
+  uint16_t* gwb = reinterpret_cast<uint16_t*>(img + 4);
+  uint32_t* gwl = img + 4 + kPfWinBase / 2;
+  uint32_t* gwh = gwl + kPfWinBase;
+  for (uint32_t w = (uint32_t)lane; w < nw; w += 64) {
+    gwb[w] = wb[w];
+    gwl[w] = wl[w];
+    gwh[w] = wh[w];
+  }
+}
+
 // The lean counting kernel (one counter segment): list table, count, then every centroid counter >= the
 // threshold becomes a part candidate (count << 24 | ordinal, unsorted, at most kPartCand) and every earlier
 // window query over it a peer (unsorted); lengths, keys and the top-41 are the merge's.  Only what counting
@@ -1091,7 +1241,8 @@ __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
   return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 2 + 2 * kPfWinBase * 4 + (2 * nlist_cap + 66) * 4);
 }
 template <int CM>
-__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
+__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off,
+                                                            const uint32_t* __restrict__ gtab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
   uint16_t* wbase = reinterpret_cast<uint16_t*>(pf_smem + tab_off + sizeof(PfCountHdr));
@@ -1112,6 +1263,8 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
   const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
   const int64_t pq_ = (int64_t)qs * kParts + part;
+  int32_t seq0, ord0;
+  pack_bounds(a, q, seq0, ord0);
   // frequent-k-mer deferral (PrefilterArgs::fmask): D = the lowest set bits of the query-strand's F mask, at most
   // defer_max of them and thr - |D| >= defer_min_thr; the lanes holding D's k-mers skip their lists
   uint32_t dmask = 0u;
@@ -1155,11 +1308,25 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   }
   uint32_t T, nlc;
   PFC_MARK(0)
-  pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
-                km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof ? clk : nullptr);
-  if (prof) {
-    tsub[0] += clk[0] - tprev;
-    tsub[1] += clk[1] - clk[0];
+  if (gtab) {
+    // the table k_pf_table built for this unit: its image copied into LDS (16-byte vectors), one barrier
+    const uint32_t* img = gtab + (size_t)blockIdx.x * pf_table_stride(a.nlist_cap);
+    T = (uint32_t)__builtin_amdgcn_readfirstlane((int)img[0]);
+    nlc = (uint32_t)__builtin_amdgcn_readfirstlane((int)img[1]);
+    if (tid == 0) H.ndef = img[2];
+    const uint4* src = reinterpret_cast<const uint4*>(img + 4);
+    uint4* dst = reinterpret_cast<uint4*>(wbase);
+    const int nv4 = (int)((pf_table_img_words(a.nlist_cap) + 3u) >> 2);
+    for (int x = tid; x < nv4; x += kPfThreads) dst[x] = src[x];
+    __syncthreads();
+    if (prof) tsub[0] += __builtin_readcyclecounter() - tprev;
+  } else {
+    pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
+                  km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof ? clk : nullptr);
+    if (prof) {
+      tsub[0] += clk[0] - tprev;
+      tsub[1] += clk[1] - clk[0];
+    }
   }
   PFC_MARK(1)
   if (T > 0) {
@@ -1186,9 +1353,12 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   if (thr > 0) {
     const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
     const uint4* c4 = cnt4 + kCentBase / 16;
-    for (int x0 = wv * 64; x0 < lim4; x0 += kPfThreads) {
+    const int32_t cmin = pack_cmin(ord0, 0, part, nsubC);  // packs: earlier bins' centroids are never candidates
+    for (int x0 = (cmin >> 4) + wv * 64; x0 < lim4; x0 += kPfThreads) {
       const int x = x0 + lane;
-      const uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+      uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
+      const int cb = cmin - x * 16;
+      if (cb > 0) v = make_uint4(v.x & keep_from(cb), v.y & keep_from(cb - 4), v.z & keep_from(cb - 8), v.w & keep_from(cb - 12));
       if (__ballot((((v.x + cadd) | (v.y + cadd) | (v.z + cadd) | (v.w + cadd)) & 0x80808080u) != 0u) == 0ull) continue;
       const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
       uint32_t mk[4] = {(v.x + cadd) & 0x80808080u, (v.y + cadd) & 0x80808080u, (v.z + cadd) & 0x80808080u,
@@ -1219,9 +1389,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const int nsubP = lim > part ? (lim - part + kParts - 1) >> kPartShift : 0;
     const int nwords = (nsubP + 3) >> 2;
     const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
-    for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
+    const int32_t pmin = pack_pmin(seq0, pv.base, part);  // packs: earlier bins' queries are never peers
+    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kPfThreads) {
       const int x = x0 + lane;
-      const uint32_t w = x < nwords ? pw[x] : 0u;
+      const uint32_t w = x < nwords ? pw[x] & keep_from(pmin - 4 * x) : 0u;
       const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
       uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
       if (__ballot(mk != 0u) == 0ull) continue;
@@ -1244,9 +1415,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const int nsubP = pv.n > part ? (pv.n - part + kParts - 1) >> kPartShift : 0;
     const int nwords = (nsubP + 3) >> 2;
     const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
-    for (int x0 = wv * 64; x0 < nwords; x0 += kPfThreads) {
+    const int32_t pmin = pack_pmin(seq0, pv.base, part);
+    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kPfThreads) {
       const int x = x0 + lane;
-      const uint32_t w = x < nwords ? pw[x] : 0u;
+      const uint32_t w = x < nwords ? pw[x] & keep_from(pmin - 4 * x) : 0u;
       const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;
       uint32_t mk = (w + add) & 0x80808080u & (valid >= 4 ? 0xffffffffu : (1u << (8 * valid)) - 1u);
       if (__ballot(mk != 0u) == 0ull) continue;
@@ -1471,6 +1643,25 @@ __global__ __launch_bounds__(256) void k_fmask(const uint16_t* __restrict__ kmer
   v = wave_scan_dpp(v, OpOr());
   if (x == 63) fmask[ss] = v;
 }
+__global__ __launch_bounds__(256) void k_kmer_xor(uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
+                                                  int64_t n2, const int32_t* __restrict__ bin,
+                                                  const uint16_t* __restrict__ xmask) {
+  const int64_t ss = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // sequence * 2 + strand
+  const int x = threadIdx.x & 63;
+  if (ss >= n2) return;
+  const int m = nk[ss];
+  const uint16_t xm = xmask[bin[ss >> 1]];
+  uint16_t* k = kmers + ss * kKmerStride;
+  if (x < m) k[x] ^= xm;
+  if (x + 64 < m) k[x + 64] ^= xm;
+}
+hipError_t launch_kmer_xor(uint16_t* kmers, const uint8_t* nk, int32_t n, const int32_t* bin, const uint16_t* xmask,
+                           hipStream_t st) {
+  const int64_t n2 = (int64_t)n * 2;
+  if (n2 <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_kmer_xor, dim3((unsigned)((n2 + 3) / 4)), dim3(256), 0, st, kmers, nk, n2, bin, xmask);
+  return hipGetLastError();
+}
 __global__ __launch_bounds__(256) void k_fmask_ord(const uint32_t* __restrict__ fmask, const int32_t* __restrict__ cent,
                                                    int32_t n, uint32_t* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1500,7 +1691,7 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
   const int full_most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
-  const int count_most = kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists);
+  const int count_most = kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists) + 16;
   if (!attr_set_on_device(k_attr_prefilter)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
     if (e == hipSuccess)
@@ -1522,12 +1713,16 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     // UMICLUST_PFCOUNT: 0 (default) the paired loop, 1 addresses computed a round ahead (pf_count_stream_pre:
     // measured slower on config 2, 2.13 vs 1.55 ms per launch, profiles/r03/pfcount_ab.json)
     static const int cm = getenv("UMICLUST_PFCOUNT") ? atoi(getenv("UMICLUST_PFCOUNT")) : 0;
+    // the list tables first (k_pf_table, one wave per unit) when the pass has a table buffer
+    if (a.pftab)
+      hipLaunchKernelGGL(k_pf_table, dim3(nqs * kParts), dim3(64), 0, st, a, a.pftab, nqs * kParts);
+    const size_t lds = tab_off + pf_count_table_bytes(a.nlist_cap) + 16;  // (+16: the table copy's last vector)
     if (cm == 1)
-      hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
-                         st, a, tab_off);
+      hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
+                         (const uint32_t*)a.pftab);
     else
-      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), tab_off + pf_count_table_bytes(a.nlist_cap),
-                         st, a, tab_off);
+      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
+                         (const uint32_t*)a.pftab);
     if (mode == 1) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {

@@ -81,6 +81,9 @@ hipError_t launch_kmer_hist(const uint16_t* kmers, const uint8_t* nk, int32_t n,
                             hipStream_t st);
 hipError_t launch_fmask(const uint16_t* kmers, const uint8_t* nk, int32_t n, const uint8_t* lut, uint32_t* fmask,
                         hipStream_t st);
+// XOR every k-mer of sequence s (both strands) with xmask[bin[s]] (packs: a bijection per bin)
+hipError_t launch_kmer_xor(uint16_t* kmers, const uint8_t* nk, int32_t n, const int32_t* bin, const uint16_t* xmask,
+                           hipStream_t st);
 // out[i] = fmask[cent[i] * 2] (the + strand masks of centroid ordinals, PrefilterArgs::fmask_ord)
 hipError_t launch_fmask_ord(const uint32_t* fmask, const int32_t* cent, int32_t n, uint32_t* out, hipStream_t st);
 // index tile build over sequences c in [0, count) with seqno map[first + c] and ordinal
@@ -106,6 +109,15 @@ constexpr int kUnitsSlot = 16 + kPostSpread * 32;
 constexpr int kSegLens = 32;  // query lengths one greedy block may span
 constexpr int kSegSlot = kUnitsSlot + 32;
 constexpr int kCountersLen = kSegSlot + 3 * kSegLens;
+constexpr int kPfWinBase = 128;   // k_pf_count: windows whose base list and start mask are tabulated (the rest: search)
+// k_pf_table's per-unit image of k_pf_count's LDS list table (kernels.hip): header (4 words), then wbase (u16 x
+// kPfWinBase), wlo, whi (u32 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap)
+__host__ __device__ constexpr uint32_t pf_table_img_words(int nlist_cap) {
+  return (uint32_t)(kPfWinBase / 2 + 2 * kPfWinBase + 2 * nlist_cap + 66);
+}
+__host__ __device__ constexpr uint32_t pf_table_stride(int nlist_cap) {
+  return (4u + pf_table_img_words(nlist_cap) + 3u) & ~3u;
+}
 constexpr int kFKmers = 32;  // frequent k-mers of a load eligible for deferral (PrefilterArgs::fkmer)
 struct PrefilterArgs {
   DevSeqs seqs;
@@ -169,6 +181,16 @@ struct PrefilterArgs {
   // in the centroid tiles are not streamed, so a centroid counter misses at most |D| and the counters >= thr - |D|
   // are the only possible candidates; the merge adds popcount(fmask_ord[ordinal] & D) to each and drops the ones
   // still < thr.  defer_max = 0 turns it off; thr - |D| stays >= defer_min_thr.
+  // Packs (umiclust_cluster_pack: several bins in one greedy order, their k-mers XOR-scrambled per bin so other
+  // bins' postings are sparse noise): query q of load bin qbin[q] takes centroid candidates only from ordinals >=
+  // bin_ord0[bin] (INT32_MAX until the bin's first centroid is indexed) and peers / flagged hits only from
+  // seqnos >= bin_seq0[bin]; k_pf_full keys centroids by cent_len (lengths are not monotone in the ordinal across
+  // bins).  qbin == nullptr: one bin.
+  uint32_t* pftab;  // [nqs*kParts x pf_table_stride(nlist_cap)] k_pf_table's list tables (null: k_pf_count builds its own)
+  const int32_t* qbin;
+  const int32_t* bin_seq0;
+  const int32_t* bin_ord0;
+  const uint8_t* cent_len;
   const uint32_t* fmask;
   const uint32_t* fmask_ord;  // [ordinal] fmask of centroid ordinal's + strand (fmask[cent_seqno[o] * 2])
   uint32_t* pdef;            // [nqs*kParts] postings of the deferred lists (chunks x 8, incl. list padding)

@@ -107,7 +107,7 @@ class ParseResult(C.Structure):
 EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
-    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin",
+    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
     "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
 ]
@@ -157,6 +157,8 @@ def lib() -> C.CDLL:
                                      C.c_int32]
     L.umiclust_cluster_bin.restype = C.c_int64
     L.umiclust_cluster_bin.argtypes = [C.c_void_p, C.c_int32, P(Stats)]
+    L.umiclust_cluster_pack.restype = C.c_int64
+    L.umiclust_cluster_pack.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(Stats)]
     L.umiclust_fetch_bin.restype = C.c_int64
     L.umiclust_fetch_bin.argtypes = [C.c_void_p, C.c_int32, P(C.c_int32), P(C.c_uint8), P(C.c_uint8), C.c_void_p,
                                      C.c_int64, P(C.c_int64)]
@@ -302,6 +304,12 @@ class Context:
                                              len(bs) - 1), "load_bins")
         self._n = n
         self._bins = bs
+
+    def cluster_pack(self, first: int, nbins: int) -> dict:
+        """Bins [first, first + nbins) of the load in one greedy order (umiclust_cluster_pack); stats of the pack."""
+        st = Stats()
+        self._check(lib().umiclust_cluster_pack(self._h, first, nbins, C.byref(st)), "cluster_pack")
+        return st.as_dict()
 
     def cluster_bin(self, b: int) -> dict:
         st = Stats()

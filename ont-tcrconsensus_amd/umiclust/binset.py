@@ -49,9 +49,12 @@ class BinRunner:
     their own; lanes keep the GPU fed.  Results do not depend on the lane count."""
 
     def __init__(self, ctx, binset: synth.BinSet, preset: int, identity: float, minlen: int = 58,
-                 maxlen: int = 68, lanes: int = 1, device: int = 0):
+                 maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0):
+        """pack_reads > 0: a lane clusters its bins in packs (umiclust_cluster_pack) of consecutive bins holding up
+        to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack."""
         from .shard import bin_cost, lpt_assign
         self.binset = binset
+        self.pack_reads = pack_reads
         self.params = _lib.params(preset, identity, minlen, maxlen)
         nb = len(binset.bins)
         lanes = max(1, min(lanes, nb)) if nb else 1
@@ -73,13 +76,32 @@ class BinRunner:
     def nbins(self) -> int:
         return len(self.binset.bins)
 
+    def packs(self, lane: int) -> list:
+        """(first, count) runs of the lane's load bins clustered together."""
+        idx = self.plan[lane]
+        if self.pack_reads <= 0:
+            return [(j, 1) for j in range(len(idx))]
+        out, j = [], 0
+        while j < len(idx):
+            k, reads = j, 0
+            while k < len(idx) and (k == j or reads + self.binset.bins[idx[k]].umis.n <= self.pack_reads):
+                reads += self.binset.bins[idx[k]].umis.n
+                k += 1
+            out.append((j, k - j))
+            j = k
+        return out
+
     def cluster_all(self) -> list:
-        """Cluster every bin; per-bin stats in bin order."""
+        """Cluster every bin; stats per bin in bin order (per pack with packing: in lane order)."""
         out = [None] * self.nbins
+        packed = [[] for _ in self.ctxs]
 
         def run(lane):
-            for j, b in enumerate(self.plan[lane]):
-                out[b] = self.ctxs[lane].cluster_bin(j)
+            for j, m in self.packs(lane):
+                if m == 1:
+                    out[self.plan[lane][j]] = self.ctxs[lane].cluster_bin(j)
+                else:
+                    packed[lane].append(self.ctxs[lane].cluster_pack(j, m))
 
         if len(self.ctxs) == 1:
             run(0)
@@ -87,7 +109,7 @@ class BinRunner:
             import concurrent.futures as cf
             with cf.ThreadPoolExecutor(len(self.ctxs)) as ex:
                 list(ex.map(run, range(len(self.ctxs))))
-        return out
+        return [x for x in out if x is not None] + [x for p in packed for x in p]
 
     def results(self) -> list:
         return [self.ctxs[self.where[b][0]].fetch_bin(self.where[b][1]) for b in range(self.nbins)]

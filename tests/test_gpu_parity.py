@@ -542,10 +542,12 @@ def _multibin_cases():
 
 
 @pytest.mark.parametrize("name,gold", _multibin_cases(), ids=[n for n, _ in _multibin_cases()])
-@pytest.mark.parametrize("split", ["default", "1"])
-def test_multibin_vs_oracle_golden(name, gold, split, monkeypatch):
+@pytest.mark.parametrize("split,pack", [("default", 0), ("1", 0), ("default", 3000), ("1", 20000), ("0", 1 << 30)])
+def test_multibin_vs_oracle_golden(name, gold, split, pack, monkeypatch):
     """BASELINE configs 3 (24 barcodes x 40 Zipf bins) and 4 (both rounds, round 2 on the round-1 consensus
-    UMIs) at reduced scale: every bin resident in one load, clustered bin by bin; the checksum of the per-bin
+    UMIs) at reduced scale: every bin resident in one load, clustered bin by bin or in packs of consecutive bins
+    (umiclust_cluster_pack: one greedy order over the pack, blocks across bin boundaries, the prefilter keeping a
+    query's own bin; up to 3k / 20k reads per pack, or the whole set as one pack); the checksum of the per-bin
     digests (membership, strands, centroids, consensus) and every bin's cluster count equal the oracle's."""
     from umiclust import binset, synth
     if split != "default":  # multi-bin sets run whole passes unless UMICLUST_SPLIT says otherwise
@@ -556,7 +558,8 @@ def test_multibin_vs_oracle_golden(name, gold, split, monkeypatch):
     for rname, prm in rounds:
         g = gold[rname]
         with _lib.Context(0) as ctx:
-            run = binset.BinRunner(ctx, bs, prm["preset"], prm["identity"], gold["minlen"], gold["maxlen"])
+            run = binset.BinRunner(ctx, bs, prm["preset"], prm["identity"], gold["minlen"], gold["maxlen"],
+                                   pack_reads=pack)
             st = run.cluster_all()
             res = run.results()
         assert bs.n == g["n_reads"]
