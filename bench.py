@@ -220,8 +220,9 @@ def main() -> None:
     ap.add_argument("--cpu-sample", type=int, default=40000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the file leg (config 2, N = 1)")
-    ap.add_argument("--lanes", type=int, default=4,
-                    help="configs 3/4: bins clustered concurrently per GPU (one device context per lane)")
+    ap.add_argument("--lanes", type=int, default=8,
+                    help="configs 3/4: bins clustered concurrently per GPU (one device context per lane; 8 measured "
+                         "best on config 3 with blocks across length changes: profiles/r03/mixlen_ab.json)")
     ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "0")),
                     help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
