@@ -373,7 +373,8 @@ struct umiclust_ctx {
                                    // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json);
                                    // off by default when LOCAL_WORLD_SIZE > 1
   bool pin_forced = false;         // UMICLUST_PIN=1: pinned even beside other contexts / ranks
-  bool pre_resolve = true;          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
+  bool pre_resolve = true;
+  bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
                                    // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
@@ -1134,9 +1135,21 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
   const uint32_t* recs = P.h_rec.p;
   static const bool rec_copy = !(getenv("UMICLUST_RECCOPY") && atoi(getenv("UMICLUST_RECCOPY")) == 0);
+  if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
   if (rec_copy) {
     const double tc1 = now_s();
-    P.rec_copy.assign(P.h_rec.p, P.h_rec.p + *P.h_reccount.p);
+    // on the resolve threads: one core's streaming read of pinned memory is the limit (0.05 s per config-2 step)
+    const size_t nw = *P.h_reccount.p;
+    if (P.rec_copy.size() < nw) P.rec_copy.resize(nw + nw / 4);
+    const int TC = nw < (1u << 18) ? 1 : c->pool->size();
+    if (TC == 1) {
+      memcpy(P.rec_copy.data(), P.h_rec.p, nw * 4);
+    } else {
+      c->pool->run([&](int t) {
+        const size_t lo = nw * (size_t)t / (size_t)TC, hi = nw * (size_t)(t + 1) / (size_t)TC;
+        memcpy(P.rec_copy.data() + lo, P.h_rec.p + lo, (hi - lo) * 4);
+      });
+    }
     recs = P.rec_copy.data();
     c->stats.t_sync_s += now_s() - tc1;
     c->dbg_t[2] += now_s() - tc1;
@@ -1173,8 +1186,9 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // seq: the in-order phase (debug counters, merged-walk timer); otherwise a classify thread resolving a strand
   // whose peers' states are all final, with its own scratch
   auto strand_outcome_s = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert, Scratch& scr,
-                              bool seq) -> int {
-    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed
+                              bool seq, uint32_t ib_lim = UINT32_MAX) -> int {
+    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed; peers with a window id
+    // >= ib_lim are taken as non-centroids (the classify phase's speculative resolution, kind 5)
     auto& cp = scr.cp;
     auto& L = scr.L;
     const HostQs& h = hq[qs];
@@ -1187,6 +1201,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     if (h.nrel <= (uint32_t)kInlineRel) {
       bool cent = false;
       for (uint32_t i = 0; i < h.nrel; i++) {
+        if (h.rel[i] >= ib_lim) continue;
         const uint8_t st = state[(uint32_t)w0 + h.rel[i]];
         if (st == ST_UNDET) {
           cert = cert_device(h);
@@ -1205,6 +1220,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     bool affects = false, undet = false;
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
+      if ((pw & 0xffffu) >= ib_lim) continue;
       const uint8_t st = state[(uint32_t)w0 + (pw & 0xffffu)];
       if ((pw >> 24) & 1u) {
         if (st == ST_UNDET) {
@@ -1241,6 +1257,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     cx.clear();
     for (int y = 0; y < R.np; y++) {
       const uint32_t pw = R.peer[y];
+      if ((pw & 0xffffu) >= ib_lim) continue;
       const uint32_t ps = (uint32_t)w0 + (pw & 0xffffu);
       if (state[ps] == ST_CENT) (ps < rb ? cp : cx).push_back({cand_key((pw >> 16) & 0xffu, c->hlen[ps], ps), y});
     }
@@ -1442,14 +1459,27 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     P.ndeps[qs] = (uint8_t)nd;
     if (kd == 2 && c->pre_resolve) {
       const Rec R = rec_of(h);
-      bool early = true;
-      for (int y = 0; y < R.np && early; y++) early = (R.peer[y] & 0xffffu) < inb;
-      if (early) {
+      int nib = 0;  // in-block peers (any relevance)
+      for (int y = 0; y < R.np; y++) nib += (R.peer[y] & 0xffffu) >= inb;
+      if (nib == 0) {
         bool cert = false;
         const int r = strand_outcome_s(qs, q0 + qs / both, false, P.pre[qs], cert, scr, false);
         if (r != 1) {
           kd = r == 0 ? 3 : 4;
           P.pre_cert[qs] = cert;
+        }
+      } else if (nib <= kDeps && c->pre_spec) {
+        // kind 5: resolved here as if no in-block peer were a centroid (earlier-block peers are final); phase 2
+        // keeps this outcome if every in-block peer -- relevant or not: once a centroid peer joins the walk, any
+        // peer can -- turns out a member, and otherwise runs the full resolution
+        bool cert = false;
+        const int r = strand_outcome_s(qs, q0 + qs / both, false, P.pre[qs], cert, scr, false, inb);
+        if (r == 0) {
+          kd = 5;
+          nd = 0;
+          for (int y = 0; y < R.np; y++)
+            if ((R.peer[y] & 0xffffu) >= inb) d[nd++] = (uint16_t)(R.peer[y] & 0xffffu);
+          P.ndeps[qs] = (uint8_t)nd;
         }
       }
     }
@@ -1496,7 +1526,6 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       P.done[ql] = 2;
     }
   };
-  if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
   const int T = nqs < 2048 ? 1 : c->pool->size();
   std::vector<Scratch> scr_t((size_t)T);
   std::vector<Acc> acc_t((size_t)T);
@@ -1530,6 +1559,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     if (P.kind[qs] == 4) {
       cert = P.pre_cert[qs] != 0;
       return 2;
+    }
+    if (P.kind[qs] == 5) {
+      const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
+      bool member_peers = true;
+      for (int i = 0; i < P.ndeps[qs] && member_peers; i++) member_peers = state[(uint32_t)w0 + d[i]] == ST_MEMBER;
+      if (member_peers) {
+        o = P.pre[qs];
+        return 0;
+      }
+      return strand_outcome(qs, q, false, o, cert);
     }
     if (P.kind[qs] == 1) {
       const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
@@ -2547,6 +2586,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
