@@ -704,7 +704,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_outidx.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_res.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_hq.ensure(nqs), "alloc");
-  c->hip(P.d_paligned.ensure(nqs), "alloc");
+  c->hip(P.d_paligned.ensure((size_t)nqs * 2), "alloc");  // two 64-bit masks per query-strand (kPeerCap 128)
   c->hip(P.d_ws.ensure(nqs), "alloc");
   c->hip(P.d_reccount.ensure(1), "alloc");
   c->hip(P.h_hq.ensure(nqs), "pin");
@@ -748,7 +748,7 @@ void set_defer(umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
   a.qbin = c->pack_on ? c->d_qbin.p : nullptr;
   a.bin_seq0 = c->d_bin_seq0.p;
   a.bin_ord0 = c->d_bin_ord0.p;
-  a.cent_len = c->pack_on ? c->d_cent_len.p : nullptr;
+  a.cent_len = c->d_cent_len.p;
   a.fmask = c->d_fmask.p;
   a.fmask_ord = c->d_cent_fm.p;
   a.pdef = P.d_pdef.p;

@@ -977,25 +977,15 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
       }
       const int nc = (int)min(S.ncand, (uint32_t)kPfCand);
       // keys: (127-count) << 23 | len << 16 | sub-id   (30 bits, unique within the part of a segment;
-      // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc));
-      // the length is the largest L with cnt_ge[L] > ordinal = #{L >= 1 : cnt_ge[L] > ordinal}
-      // (broadcast 16-byte LDS reads, no HBM read)
+      // sub-id order is ordinal = seqno order, so key order is (count desc, length asc, seqno asc))
       for (int x = tid; x < nc; x += kPfThreads) {
         const uint32_t c = S.cand[x];
         const uint32_t cntv = cnt_get(cnt, kCentBase + c);
         const int32_t ord = seg0 + (int32_t)(c << kPartShift) + part;
-        uint32_t len = 0;
-        if (a.cent_len) {
-          len = (uint32_t)a.cent_len[ord] + 1u;  // packs: lengths are not monotone in the ordinal across bins
-        } else {
-          const int4* g4 = reinterpret_cast<const int4*>(S.cge);
-#pragma unroll
-          for (int i = 0; i < kCge / 4; i++) {
-            const int4 g = g4[i];
-            len += (uint32_t)(g.x > ord) + (uint32_t)(g.y > ord) + (uint32_t)(g.z > ord) + (uint32_t)(g.w > ord);
-          }
-        }
-        S.cand[x] = ((127u - cntv) << 23) | ((len - 1u) << 16) | c;
+        // the centroid's length from the ordinal table (a packs' lengths are not monotone in the ordinal across bins,
+        // so the cnt_ge count of round 2 no longer applies; one L2 read per candidate on this rare path)
+        const uint32_t len = (uint32_t)a.cent_len[ord];
+        S.cand[x] = ((127u - cntv) << 23) | (len << 16) | c;
       }
       __syncthreads();
       // best 41 of the segment part in key order: by rank (all-pairs count, broadcast LDS reads)
@@ -1596,21 +1586,29 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   for (int l = 0; l < kParts; l++) {
     const int n = __shfl(np_l, l, 64), o = __shfl(po_l, l, 64);
     if (n == 0) continue;
-    uint32_t key = 0xffffffffu;
-    if (lane < n) {
-      const uint32_t id = a.ppeer_id[(p0 + l) * kPeerCap + lane] - (uint32_t)a.peer_shift;  // peer_base-relative
-      const uint32_t cv = a.ppeer_count[(p0 + l) * kPeerCap + lane];
-      key = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[a.peer_base + (int32_t)id] << 16) | id;
-      P[lane] = key;
+    uint32_t key[kPeerCap / 64];
+#pragma unroll
+    for (int hh = 0; hh < kPeerCap / 64; hh++) {
+      const int x = lane + 64 * hh;
+      key[hh] = 0xffffffffu;
+      if (x < n) {
+        const uint32_t id = a.ppeer_id[(p0 + l) * kPeerCap + x] - (uint32_t)a.peer_shift;  // peer_base-relative
+        const uint32_t cv = a.ppeer_count[(p0 + l) * kPeerCap + x];
+        key[hh] = ((127u - cv) << 23) | ((uint32_t)a.seqs.lens[a.peer_base + (int32_t)id] << 16) | id;
+        P[x] = key[hh];
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < n) {
-      int r = 0;
-      for (int y = 0; y < n; y++) r += P[y] < key;
-      a.peer_id[(int64_t)qs * kPeerCap + o + r] = (uint16_t)(key & 0xffffu);
-      a.peer_count[(int64_t)qs * kPeerCap + o + r] = (uint8_t)(127u - (key >> 23));
+#pragma unroll
+    for (int hh = 0; hh < kPeerCap / 64; hh++) {
+      if (lane + 64 * hh < n) {
+        int r = 0;
+        for (int y = 0; y < n; y++) r += P[y] < key[hh];
+        a.peer_id[(int64_t)qs * kPeerCap + o + r] = (uint16_t)(key[hh] & 0xffffu);
+        a.peer_count[(int64_t)qs * kPeerCap + o + r] = (uint8_t)(127u - (key[hh] >> 23));
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1923,8 +1921,8 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = qs < nqs;  // every lane stays to the slot allocation
   const int np = live ? npeer[qs] : 0;
-  if (live) aligned[qs] = 0ull;
-  unsigned long long rel = 0;
+  if (live) aligned[(int64_t)qs * 2] = aligned[(int64_t)qs * 2 + 1] = 0ull;
+  unsigned long long rel[2] = {0ull, 0ull};  // peers 0..63, 64..127 (kPeerCap)
   if (live && np != 255 && np != 0 && emit) {
     const WalkState w = ws[qs];
     for (int x = 0; x < np; x++) {
@@ -1932,13 +1930,14 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
       // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
       if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
           !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])))
-        rel |= 1ull << x;
+        rel[x >> 6] |= 1ull << (x & 63);
     }
-    aligned[qs] = rel;
+    aligned[(int64_t)qs * 2] = rel[0];
+    aligned[(int64_t)qs * 2 + 1] = rel[1];
   }
   const int32_t q = q0 + (live ? qs : 0) / both;
   const int ql = lens[q];
-  const uint32_t n = (uint32_t)__builtin_popcountll(rel);
+  const uint32_t n = (uint32_t)(__builtin_popcountll(rel[0]) + __builtin_popcountll(rel[1]));
   const uint32_t si = (uint32_t)(sg.lmax - ql);
   const uint32_t k0 = seg_alloc(n, si, seg_cnt);
   if (!n) return;
@@ -1947,7 +1946,7 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
   const uint32_t qv = ((uint32_t)q << 1) | (uint32_t)(qs % both);
   uint32_t tl = 0;
   for (int x = 0; x < np; x++)
-    if ((rel >> x) & 1ull) {
+    if ((rel[x >> 6] >> (x & 63)) & 1ull) {
       const uint32_t t = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       pq[k] = qv;
       pt[k] = t;
@@ -2008,18 +2007,27 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
   const bool live = qs < nqs;
   const WalkState w = ws[live ? qs : 0];
   const int np = live ? npeer[qs] : 0;
-  bool rel = false, al = false;
-  uint32_t pw = 0;
-  if (live && np != 255 && lane < np) {
-    const uint32_t id = peer_id[(int64_t)qs * kPeerCap + lane];
-    const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + lane];
-    const uint32_t ps = (uint32_t)w0 + id;
-    rel = peer_relevant(w, cnt, lens[ps], ps);
-    al = (aligned[qs] >> lane) & 1ull;
-    pw = id | (cnt << 16) | (rel ? 1u << 24 : 0u) | (al ? 1u << 25 : 0u);
+  constexpr int kH = kPeerCap / 64;  // peers lane, lane + 64, ...
+  bool rel[kH], al[kH];
+  uint32_t pw[kH];
+  bool anyrel = false;
+#pragma unroll
+  for (int hh = 0; hh < kH; hh++) {
+    const int x = lane + 64 * hh;
+    rel[hh] = al[hh] = false;
+    pw[hh] = 0;
+    if (live && np != 255 && x < np) {
+      const uint32_t id = peer_id[(int64_t)qs * kPeerCap + x];
+      const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + x];
+      const uint32_t ps = (uint32_t)w0 + id;
+      rel[hh] = peer_relevant(w, cnt, lens[ps], ps);
+      al[hh] = (aligned[(int64_t)qs * 2 + hh] >> lane) & 1ull;
+      pw[hh] = id | (cnt << 16) | (rel[hh] ? 1u << 24 : 0u) | (al[hh] ? 1u << 25 : 0u);
+    }
+    anyrel |= rel[hh];
   }
   uint32_t base = 0xffffffffu;
-  const bool has_rec = __any(rel);
+  const bool has_rec = __any(anyrel);
   const int nt = live ? min((int)ntop[qs], kWalk) : 0;
   const int ncw = (nt + 3) >> 2;
   // record space: the workgroup's sizes scanned in LDS, one atomic
@@ -2052,22 +2060,36 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
         if (4 * lane + e < nt) cw |= (uint32_t)top_count[(int64_t)qs * kTopHits + 4 * lane + e] << (8 * e);
       r[1 + 2 * nt + lane] = cw;
     }
-    if (lane < np) {
-      r[1 + 2 * nt + ncw + lane] = pw;
-      r[1 + 2 * nt + ncw + np + lane] = al ? peer_res[(int64_t)qs * kPeerCap + lane] : 0u;
+#pragma unroll
+    for (int hh = 0; hh < kH; hh++) {
+      const int x = lane + 64 * hh;
+      if (x < np) {
+        r[1 + 2 * nt + ncw + x] = pw[hh];
+        r[1 + 2 * nt + ncw + np + x] = al[hh] ? peer_res[(int64_t)qs * kPeerCap + x] : 0u;
+      }
     }
   }
-  // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform mask)
-  unsigned long long rm = __ballot(rel);
-  const uint32_t nrel = (uint32_t)__builtin_popcountll(rm);
+  // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform masks, peer order)
+  unsigned long long rm[kH];
+  uint32_t nrel = 0;
+#pragma unroll
+  for (int hh = 0; hh < kH; hh++) {
+    rm[hh] = __ballot(rel[hh]);
+    nrel += (uint32_t)__builtin_popcountll(rm[hh]);
+  }
   uint16_t ids[kInlineRel];
+  int hcur = 0;
 #pragma unroll
   for (int i = 0; i < kInlineRel; i++) {
     uint32_t id = 0;
-    if (rm) {
-      const int l = __builtin_ctzll(rm);
-      rm &= rm - 1ull;
-      id = (uint32_t)__builtin_amdgcn_readlane((int)(pw & 0xffffu), l);
+    while (hcur < kH && !rm[hcur]) hcur++;
+    if (hcur < kH) {
+      const int l = __builtin_ctzll(rm[hcur]);
+      rm[hcur] &= rm[hcur] - 1ull;
+      uint32_t v = pw[0];
+#pragma unroll
+      for (int hh = 1; hh < kH; hh++) v = hh == hcur ? pw[hh] : v;
+      id = (uint32_t)__builtin_amdgcn_readlane((int)(v & 0xffffu), l);
     }
     ids[i] = (uint16_t)id;
   }

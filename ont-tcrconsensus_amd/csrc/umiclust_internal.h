@@ -43,7 +43,9 @@ constexpr int kMaxSegs = 16;
 constexpr int kTopHits = 41;        // maxaccepts + maxrejects + MAXDELAYED (searchcore.cc)
 constexpr int kBatch = 8;           // MAXDELAYED: alignment batch of search_onequery
 constexpr int kWalk = 32;           // maxaccepts + maxrejects - 1: most candidates ever aligned
-constexpr int kPeerCap = 64;        // in-block peer candidates kept per query-strand
+constexpr int kPeerCap = 128;       // in-window peer candidates kept per query-strand (a multiple of 64; <= 254:
+                                    // u8 counts, 255 = overflow)
+static_assert(kPeerCap % 64 == 0 && kPeerCap <= 254, "peer cap");
 constexpr int kOpsStride = 2 * kMaxLen;  // alignment ops per member (<= qlen + tlen)
 constexpr int kConsCap = 2 * kMaxLen;    // consensus bytes reserved per cluster
 constexpr int kMsaCols = 2048;      // LDS profile columns of the consensus kernel
