@@ -223,8 +223,9 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=8,
                     help="configs 3/4: bins clustered concurrently per GPU (one device context per lane; 8 measured "
                          "best on config 3 with blocks across length changes: profiles/r03/mixlen_ab.json)")
-    ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "0")),
-                    help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack)")
+    ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "100000")),
+                    help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack; "
+                         "0: one bin per call; 100k measured best on config 3: profiles/r03/pack_ab.json)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
