@@ -8,7 +8,7 @@ shift
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e"
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT"
 SQ2="SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"
 rc=0
