@@ -591,6 +591,41 @@ def test_config_vs_oracle_golden(gpu_ctx, name, gold):
         assert d[k] == gold[k], k
 
 
+@pytest.mark.parametrize("packs", [[(0, 7)], [(0, 3), (3, 4)], [(2, 3), (0, 2), (5, 2)]])
+def test_pack_edge_cases(gpu_ctx, packs):
+    """umiclust_cluster_pack over the same edge-case bins (empty, fully length-filtered, one-record and ordinary bins)
+    as the whole load, two packs, or packs clustered out of order: every bin equals the oracle run on it alone."""
+    base = "TTTCGTTCCGCTTGGCATTCCAGTTAGCGTTTAAACGGGAATGCTAACGGCAAGCGTAATGAAA"
+    groups = [[], ["ACGT", "ACGTACGT"], [base], synth.make_umis(40, seed=61, max_reads=500, orient_mix=0.2).as_list(),
+              [], synth.make_umis(25, seed=62, max_reads=300).as_list(), [base[:57], base + "A" * 5]]
+    buf, off = _lib._pack([s for g in groups for s in g])
+    starts = np.cumsum([0] + [len(g) for g in groups])
+    op = orc.params(1, 0.93, 58, 68)
+    gpu_ctx.load_bins(_lib.params(1, 0.93, 58, 68), buf, off, starts)
+    for first, m in packs:
+        gpu_ctx.cluster_pack(first, m)
+    for b, g in enumerate(groups):
+        got = gpu_ctx.fetch_bin(b)
+        want = orc.cluster(op, g) if g else dict(n_clusters=0, cluster=np.zeros(0, np.int32), strand=np.zeros(0, np.uint8),
+                                                centroid=np.zeros(0, np.uint8), consensus=[])
+        _cmp_cluster(got, want)
+
+
+def test_pack_errors(gpu_ctx):
+    """A pack past the load's bins, an empty pack and a pack under the batched O4 policy fail with EINVAL."""
+    seqs = synth.make_umis(20, seed=63, max_reads=200).as_list()
+    buf, off = _lib._pack(seqs + seqs)
+    gpu_ctx.load_bins(_lib.params(1, 0.93, 58, 68), buf, off, [0, len(seqs), 2 * len(seqs)])
+    for first, m in [(1, 2), (0, 0), (-1, 2)]:
+        with pytest.raises(_lib.UmiclustError):
+            gpu_ctx.cluster_pack(first, m)
+    p = _lib.params(1, 0.93, 58, 68)
+    p.threads, p.policy_threads = 25, 1
+    gpu_ctx.load_bins(p, buf, off, [0, len(seqs), 2 * len(seqs)])
+    with pytest.raises(_lib.UmiclustError):
+        gpu_ctx.cluster_pack(0, 2)
+
+
 def test_load_bins_edge_cases(gpu_ctx):
     """umiclust_load_bins: empty bins, bins whose every record is length-filtered, one-record bins and
     ordinary bins in one load; each bin equals the oracle run on that bin alone, in any clustering order."""
