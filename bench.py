@@ -162,9 +162,13 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
     g_alg = cells / t_al / 1e9 if t_al else 0.0
     g_cmp = cells_c / t_al / 1e9 if t_al else 0.0
     ceiling = VALU_LANE_OPS / ALIGN_VALU_PER_CELL / 1e9
+    # against SURVEY §8d's nominal 12 int16 ops per affine cell with stats carry (not reachable with vsearch's path
+    # statistics: DESIGN.md §6 "The aligner's instruction count" -- 15.4 VALU per cell in the ISA)
+    ceiling12 = VALU_LANE_OPS / 12.0 / 1e9
     align = dict(kernel="k_align_pk", bound="valu", seconds_total=t_al, cells=cells, cells_computed=cells_c,
                  gcups_kernel=g_alg, gcups_computed=g_cmp, valu_per_cell=ALIGN_VALU_PER_CELL,
                  ceiling_gcups=ceiling, frac=g_alg / ceiling, frac_computed=g_cmp / ceiling,
+                 ceiling_gcups_12ops=ceiling12, frac_12ops=g_alg / ceiling12,
                  speculative_ratio=cells_c / cells if cells else None)
     return roof, align
 
