@@ -389,7 +389,9 @@ struct umiclust_ctx {
   hipStream_t ix_st = nullptr;     // null: the main stream
   hipEvent_t ix_done = nullptr, last_r_ev = nullptr;
   std::unique_ptr<WorkPool> pool;  // host threads of resolve_pass (UMICLUST_RESOLVE_THREADS)
-  int32_t resolve_threads = 4;
+  // host threads of resolve_pass (caller included); 0: 8 while this is the process's only context (config 2: host
+  // resolve 0.22 -> 0.14 s per step, profiles/r03/resolve_threads_ab.json), 4 beside other contexts (bin-set lanes)
+  int32_t resolve_threads = 0;
   DevBuf<uint16_t> arena;         // postings of every tile (one buffer, one descriptor per pass)
   uint64_t sealed_slot0 = 0;      // arena index of sealed tile 0's slot
   int32_t index_end = 0;          // centroid ordinals [0, index_end) are indexed
@@ -483,6 +485,10 @@ namespace {
 // is the process's one live context and the process is its node's only rank (LOCAL_WORLD_SIZE <= 1): several
 // contexts (bin-set lanes) or ranks pinned by where their callers happen to run could all land on one CCD.
 // UMICLUST_PIN=0 turns it off, UMICLUST_PIN=1 forces it on.
+int pool_threads(const umiclust_ctx* c) {
+  return c->resolve_threads > 0 ? c->resolve_threads : (g_live_ctx.load() > 1 ? 4 : 8);
+}
+
 struct L3Pin {
   cpu_set_t saved;
   bool on = false;
@@ -492,7 +498,7 @@ struct L3Pin {
       return;
     // the pool is created with the caller's own mask before the caller is narrowed, so restoring `saved` on
     // both undoes the call's pinning completely
-    if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
+    if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
     const int cpu = sched_getcpu();
     char path[96], buf[256];
     snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
@@ -1135,7 +1141,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
   const uint32_t* recs = P.h_rec.p;
   static const bool rec_copy = !(getenv("UMICLUST_RECCOPY") && atoi(getenv("UMICLUST_RECCOPY")) == 0);
-  if (!c->pool) c->pool.reset(new WorkPool(c->resolve_threads));
+  if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
   if (rec_copy) {
     const double tc1 = now_s();
     // on the resolve threads: one core's streaming read of pinned memory is the limit (0.05 s per config-2 step)
