@@ -441,6 +441,7 @@ struct umiclust_ctx {
   // faster (1.62 -> 1.76 ms per count + table on config 2: the counting is bound by the LDS array, ~73 % busy, 60 %
   // of it bank-conflict replays; profiles/r03/pftab_ab.json), so off by default
   bool pf_tab = false;
+  bool rec_direct = true;          // UMICLUST_RECDIRECT=0: k_pack's outcomes and records by DMA from device buffers
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
@@ -956,15 +957,20 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   // what the host needs goes straight to pinned host memory; the pass that next reuses these
   // buffers is enqueued only after the host has waited for ev[4]
   c->hip(hipMemsetAsync(P.d_reccount.p, 0, 4, st), "memset");
+  // rec_direct: k_pack writes the outcomes and records straight into the pinned host buffers (no DMA copies on the
+  // chain the host waits for: a 3 MB record copy was 0.14 ms per config-2 block); otherwise device buffers + copies
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
                      P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_paligned.p, P.d_reccount.p,
-                     P.d_hq.p,
-                     P.d_rec.p, P.d_counters.p, P.h_counters.p, st),
+                     c->rec_direct ? P.h_hq.p : P.d_hq.p,
+                     c->rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, st),
          "pack");
-  c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
+  if (!c->rec_direct)
+    c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
   c->hip(hipMemcpyAsync(P.h_reccount.p, P.d_reccount.p, 4, hipMemcpyDeviceToHost, st), "d2h record count");
-  const size_t est = std::min<size_t>(P.rec_est, P.d_rec.n);
-  c->hip(hipMemcpyAsync(P.h_rec.p, P.d_rec.p, est * 4, hipMemcpyDeviceToHost, st), "d2h records");
+  if (!c->rec_direct) {
+    const size_t est = std::min<size_t>(P.rec_est, P.d_rec.n);
+    c->hip(hipMemcpyAsync(P.h_rec.p, P.d_rec.p, est * 4, hipMemcpyDeviceToHost, st), "d2h records");
+  }
   c->hip(hipEventRecord(P.ev[4], st), "event");
 }
 
@@ -1099,7 +1105,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   {
     // records past the DMA'd prefix (a pass that used more than the estimate): fetch the rest now
     const size_t used = *P.h_reccount.p, est = std::min<size_t>(P.rec_est, P.d_rec.n);
-    if (used > est) {
+    if (used > est && !c->rec_direct) {
       c->hip(hipMemcpyAsync(P.h_rec.p + est, P.d_rec.p + est, (used - est) * 4, hipMemcpyDeviceToHost, c->st_copy),
              "d2h records");
       c->hip(hipStreamSynchronize(c->st_copy), "sync");
@@ -2593,6 +2599,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
