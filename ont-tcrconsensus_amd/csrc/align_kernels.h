@@ -186,6 +186,47 @@ __device__ __forceinline__ uint32_t gt_mask(v2s b, v2s a) {
   return d;
 }
 
+// Cheaper cells than a literal restatement of the recurrences (24 VALU ops per packed cell pair):
+//  * row potential: the kernel works on H'(i,j) = H(i,j) - X (i+1) with X the mismatch score (E and
+//    F shifted alike).  Every comparison is between states of one cell, so the offset changes no
+//    decision; a diagonal step becomes H'd + e DELTA (no mismatch add) and a vertical step costs
+//    X more (folded into the F gap constants).  The end score adds X QL back.
+//  * summaries count matches m (bits 0-7) and u + 1 (bits 8-15), with u = the boundary index the
+//    path starts from (row r of column -1, or column c of row -1; the corner is u = -1) plus its
+//    diagonal moves.  Moves into real cells are a = i + j + 2 - (u + 1): a gap move changes
+//    neither field, a diagonal move adds e + 0x100, so the summaries need no per-cell increments.
+//  * the trailing-D-run tracker (the D run length of the F state; H inherits it when it takes F)
+//    only matters in the end cell's column, i.e. in the last two steps; the main loop runs without it.
+//  * each row's diagonal candidate is formed from the previous row's old H / S_H before that row
+//    overwrites them, so the register rotation needs no copies.
+//  * the boundary initialisation is an inlined function, not a lambda captured by the step lambda
+//    (that closure kept the row arrays in scratch).
+// k_align_pk's boundary column -1: H'(i,-1) = -(GO_TL + (i+1) GE_TL) - X (i+1), E'(i,0) opened
+// from it; summaries u + 1 = i + 1, no matches; keep_mask selects the halves to (re)initialise
+template <int QL, int TOP>
+__device__ __forceinline__ void pk_init_rows(v2s (&H)[TOP], v2s (&E)[TOP], uint32_t (&SH)[TOP],
+                                             uint32_t (&SE)[TOP], uint32_t keep_mask,
+                                             const Scoring& sc, int X, int QRqi, int QRqr) {
+  int vz;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
+#pragma unroll
+  for (int kk = 0; kk < TOP; kk++) {
+    const int i0 = kk, i1 = TOP + kk;
+    const int h0 = vz - sc.go[1] - (i0 + 1) * (sc.ge[1] + X);
+    const int h1 = vz - sc.go[1] - (i1 + 1) * (sc.ge[1] + X);
+    const int q1 = (i1 == QL - 1) ? QRqr : QRqi;
+    const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
+    const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
+    const uint32_t s01 = pk2((i0 + 1) << 8, (i1 + 1) << 8);
+    H[kk] = as_v2(bfi(keep_mask, pk2(h0, h1), as_u(H[kk])));
+    E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
+    SH[kk] = bfi(keep_mask, s01, SH[kk]);
+    SE[kk] = bfi(keep_mask, s01, SE[kk]);
+  }
+}
+
+template <bool B> struct BTag { static constexpr bool value = B; };
+
 template <int QL>
 __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __restrict__ pq,
                                                  const uint32_t* __restrict__ pt, int32_t npairs,
@@ -221,45 +262,28 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
     }
   }
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int X = sc.mismatch;
+  const int QRti = sc.go[3] + sc.ge[3] + X, Rti = sc.ge[3] + X;  // vertical gaps: + X (potential)
+  const int QRtr = sc.go[5] + sc.ge[5] + X, Rtr = sc.ge[5] + X;
   const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
   const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  const v2s MM = as_v2(pk2(sc.mismatch, sc.mismatch));
   const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
   v2s H[TOP], E[TOP];
-  uint32_t SH[TOP], SE[TOP];  // summaries; SH stored +1 (every consumer adds the move)
-  auto init_rows = [&](uint32_t keep_mask) {
-    // boundary column -1: H(i,-1) = -(GO_TL + (i+1) GE_TL), E(i,0) opened from it, S_H = 0,
-    // S_E = one real move; keep_mask selects the halves to (re)initialise
-    int vz;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-#pragma unroll
-    for (int kk = 0; kk < TOP; kk++) {
-      const int i0 = kk, i1 = TOP + kk;
-      const int h0 = vz - sc.go[1] - (i0 + 1) * sc.ge[1];
-      const int h1 = vz - sc.go[1] - (i1 + 1) * sc.ge[1];
-      const int q1 = (i1 == QL - 1) ? QRqr : QRqi;
-      const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
-      const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
-      H[kk] = as_v2(bfi(keep_mask, pk2(h0, h1), as_u(H[kk])));
-      E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
-      SH[kk] = bfi(keep_mask, 0x00010001u, SH[kk]);
-      SE[kk] = bfi(keep_mask, 0x00010001u, SE[kk]);
-    }
-  };
+  uint32_t SH[TOP], SE[TOP];
 #pragma unroll
   for (int kk = 0; kk < TOP; kk++) {
     H[kk] = as_v2(0u);
     E[kk] = as_v2(0u);
     SH[kk] = SE[kk] = 0;
   }
-  init_rows(0xffffffffu);
+  pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffffffffu, sc, X, QRqi, QRqr);
   // carries of the top half's last row, consumed by the bottom half in the next step
-  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDF = 0;
+  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDL = 0;
   int Lext = 0, trail = 0;
   uint32_t tword = 0, tprev = 1;
-  for (int j = 0; j <= tl; j++) {
+  // one step: top half at column j, bottom half at column j-1; LAST: one of the end cell's two steps
+  auto step = [&](int j, auto last_tag) __attribute__((always_inline)) {
+    constexpr bool LAST = decltype(last_tag)::value;
     if ((j & 7) == 0) tword = tcp[j >> 3];
     const uint32_t tcode = tword & 15u;
     tword >>= 4;
@@ -269,22 +293,34 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
 #pragma unroll
     for (int g = 0; g < NG; g++)
       M[g] = ((uint32_t)(MT[g] >> (16 * bl)) & 0xffffu) | ((uint32_t)(MB[g] >> (16 * bh)) << 16);
-    const bool lc0 = (j == tl - 1), lc1 = (j == tl);
-    const uint32_t QRt = pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti);
-    const uint32_t Rt = pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti);
-    // row -1 (top half, column j) | carry (bottom half, column j-1)
+    const bool lc0 = LAST && (j == tl - 1), lc1 = LAST && (j == tl);
+    const uint32_t QRt = LAST ? pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti) : pk2(QRti, QRti);
+    const uint32_t Rt = LAST ? pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti) : pk2(Rti, Rti);
+    // row -1 (top half, column j: potential 0) | carry (bottom half, column j-1)
     const int hd0 = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
     const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
     v2s Hd = as_v2(pk2(hd0, (int)cHd));
-    uint32_t SHd = pk2(1, (int)cSHd);
+    uint32_t SHd = pk2(j << 8, (int)cSHd);  // H(-1, j-1): u = j - 1
     v2s F = as_v2(pk2(f0, (int)cF));
-    uint32_t SF = pk2(1, (int)cSF);
-    uint32_t DF = pk2(-1, (int)cDF);  // row the current D run opened from (-1: boundary)
+    uint32_t SF = pk2((j + 1) << 8, (int)cSF);  // F(0, j) opened from H(-1, j): u = j
+    uint32_t DL = pk2(1, (int)cDL);             // D run of the F state (F(0, j): one move)
+    // each row's diagonal candidate is formed from the previous row's old H / S_H before that row
+    // overwrites them (no register copies for the rotation)
+    uint32_t e = M[0] & 0x00010001u;
+    v2s hn = as_v2(e) * DELTA + Hd;
+    uint32_t shn = SHd + e + 0x01000100u;
 #pragma unroll
     for (int kk = 0; kk < TOP; kk++) {
-      const uint32_t e = (M[kk >> 4] >> (kk & 15)) & 0x00010001u;
-      v2s h = Hd + MM + as_v2(e) * DELTA;
-      uint32_t sh = SHd + (e << 8);
+      v2s h = hn;
+      uint32_t sh = shn;
+      if (kk + 1 < TOP) {
+        e = (M[(kk + 1) >> 4] >> ((kk + 1) & 15)) & 0x00010001u;
+        hn = as_v2(e) * DELTA + H[kk];
+        shn = SH[kk] + e + 0x01000100u;
+      } else {
+        Hd = H[kk];
+        SHd = SH[kk];
+      }
       const uint32_t mF = gt_mask(F, h);
       h = __builtin_elementwise_max(h, F);
       sh = bfi(mF, SF, sh);
@@ -292,20 +328,23 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
       const uint32_t mE = gt_mask(Ec, h);
       h = __builtin_elementwise_max(h, Ec);
       sh = bfi(mE, SE[kk], sh);
-      const uint32_t sh1 = sh + 0x00010001u;
       int dr_last = 0;
       bool eb_last = false;
       if (kk == KL) {
-        // last row (high half): D run of the chosen F = rows since it opened (before DF moves on)
         eb_last = (mE >> 31) != 0;
-        dr_last = (mF >> 31) != 0 ? (QL - 1) - (int)(short)(DF >> 16) : 0;
+        // last row (high half): D run of the chosen F = rows since it opened (before DF moves on)
+        if (LAST) dr_last = (mF >> 31) != 0 ? (int)(DL >> 16) : 0;
       }
       const v2s fo = h - as_v2(QRt), fe = F - as_v2(Rt);
       const uint32_t mfx = gt_mask(fe, fo);
       F = __builtin_elementwise_max(fo, fe);
       // a new D run opened from H continues H's own D run when H took F
-      DF = bfi(mfx | (mF & ~mE), DF, pk2(kk, TOP + kk));
-      SF = bfi(mfx, SF + 0x00010001u, sh1);
+      if (LAST) {
+        const uint32_t dlh = DL & mF & ~mE;  // H's own D run (0 unless H took F)
+        DL = bfi(mfx, DL, dlh) + 0x00010001u;
+        asm volatile("" : "+v"(DL));  // keep the tracker in its row (sinking it keeps 3 masks per row live)
+      }
+      SF = bfi(mfx, SF, sh);
       const uint32_t qrq = pk2(QRqi, (TOP + kk == QL - 1) ? QRqr : QRqi);
       const uint32_t rq = pk2(Rqi, (TOP + kk == QL - 1) ? Rqr : Rqi);
       const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
@@ -315,32 +354,43 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
         // end cell's (vsearch align_trim's trailing run)
         const bool ex = (mex >> 31) != 0;
         const int lh = eb_last ? 1 + Lext : 0;
-        trail = eb_last ? lh : dr_last;
+        if (LAST) trail = eb_last ? lh : dr_last;
         Lext = ex ? 1 + Lext : lh;
       }
       E[kk] = __builtin_elementwise_max(eo, ee);
-      SE[kk] = bfi(mex, SE[kk] + 0x00010001u, sh1);
-      Hd = H[kk];
-      SHd = SH[kk];
+      SE[kk] = bfi(mex, SE[kk], sh);
       H[kk] = h;
-      SH[kk] = sh1;
+      SH[kk] = sh;
     }
     // carry the top half's outputs into the bottom half of the next step
     cHd = as_u(Hd) & 0xffffu;
     cSHd = SHd & 0xffffu;
     cF = as_u(F) & 0xffffu;
     cSF = SF & 0xffffu;
-    cDF = DF & 0xffffu;
+    if (LAST) cDL = DL & 0xffffu;
+  };
+  // the bottom half processes column -1 in step 0: the boundary column is restored after it
+  int j = 0;
+  for (; j < tl - 1; j++) {
+    step(j, BTag<false>{});
     if (j == 0) {
-      // the bottom half processed column -1 in this step: restore the boundary column
-      init_rows(0xffff0000u);
+      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X, QRqi, QRqr);
       Lext = 0;
       trail = 0;
     }
   }
-  const int Hend = (int)(short)(as_u(H[KL]) >> 16);
-  const uint32_t S = ((SH[KL] >> 16) - 1u) & 0xffffu;
-  const uint32_t m = S >> 8, acols = S & 0xffu;
+  for (; j <= tl; j++) {
+    step(j, BTag<true>{});
+    if (j == 0) {
+      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X, QRqi, QRqr);
+      Lext = 0;
+      trail = 0;
+    }
+  }
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + X * QL;
+  const uint32_t S = (SH[KL] >> 16) & 0xffffu;
+  const uint32_t m = S & 0xffu;
+  const uint32_t acols = (uint32_t)(QL + tl) - (S >> 8);
   const uint32_t internal = acols - (uint32_t)trail;
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
 }
