@@ -44,9 +44,14 @@ L2_GATHER_GBS = 18800.0    # MI355X_MICROARCH.md "Indexed rows: gather into LDS"
 # integer VALU issue ceiling: 256 CUs x 4 SIMDs x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md
 # "v_fma_f32 (wave64) 2 cyc (SIMD-32)"); lane-instructions per second
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
-# VALU wave-instructions per alignment cell of k_align_pk, measured: SQ_INSTS_VALU x 64 / cells computed
-# (profiles/r02/pmc_c2.json: SQ_INSTS_VALU of every k_align_pk x 64 / cells_computed of the step)
-ALIGN_VALU_PER_CELL = 17.9
+# VALU lane-instructions per alignment cell of k_align_pk, measured: SQ_INSTS_VALU x 64 / cells computed
+# (profiles/r03/pmc_align_valu.json, a rocprofv3 --pmc pass over the config-2 bench; round 2: 17.9)
+def _align_valu_per_cell() -> float:
+    p = os.path.join(ROOT, "profiles", "r03", "pmc_align_valu.json")
+    return json.load(open(p))["valu_lane_instrs_per_computed_cell"] if os.path.exists(p) else 17.9
+
+
+ALIGN_VALU_PER_CELL = _align_valu_per_cell()
 
 
 def cpu_baseline_bins(bins, identity: float, lens, budget_s: float = 20.0, preset: int = 1) -> dict:

@@ -261,6 +261,17 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
       else MB[(i - TOP) >> 4] |= 1ull << (16 * b + ((i - TOP) & 15));
     }
   }
+  // the per-base row masks move to LDS (lane-private, [base][group][half][lane] u16): two 16-bit reads
+  // per group and column instead of 4 NG live VGPRs and the 64-bit shifts
+  __shared__ uint16_t sM[4 * NG * 2 * 64];
+  uint16_t* const pM = sM + threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      pM[((b * NG + g) * 2 + 0) * 64] = (uint16_t)(MT[g] >> (16 * b));
+      pM[((b * NG + g) * 2 + 1) * 64] = (uint16_t)(MB[g] >> (16 * b));
+    }
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
   const int X = sc.mismatch;
   const int QRti = sc.go[3] + sc.ge[3] + X, Rti = sc.ge[3] + X;  // vertical gaps: + X (potential)
@@ -292,7 +303,7 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
     uint32_t M[NG];
 #pragma unroll
     for (int g = 0; g < NG; g++)
-      M[g] = ((uint32_t)(MT[g] >> (16 * bl)) & 0xffffu) | ((uint32_t)(MB[g] >> (16 * bh)) << 16);
+      M[g] = (uint32_t)pM[((bl * NG + g) * 2 + 0) * 64] | ((uint32_t)pM[((bh * NG + g) * 2 + 1) * 64] << 16);
     const bool lc0 = LAST && (j == tl - 1), lc1 = LAST && (j == tl);
     const uint32_t QRt = LAST ? pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti) : pk2(QRti, QRti);
     const uint32_t Rt = LAST ? pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti) : pk2(Rti, Rti);
