@@ -368,16 +368,17 @@ struct umiclust_ctx {
   // split passes (depth 2, UMICLUST_SPLIT=0 turns them off): a block's counting runs against the index
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
-  int32_t split_env = -1;
+  int32_t split_env = -1;         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
   bool pin = true;                 // UMICLUST_PIN=0: host resolve threads not kept in the caller's L3 domain (L3Pin;
                                    // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json);
                                    // off by default when LOCAL_WORLD_SIZE > 1
   bool pin_forced = false;         // UMICLUST_PIN=1: pinned even beside other contexts / ranks
-  bool pre_resolve = true;
-  bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)          // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
-  int32_t band_pairs = 70000;      // UMICLUST_BAND: alignment launches of at most this many pairs (launch bound)
-                                   // run banded: ~1,100 one-lane waves would not cover the 1,024 SIMDs
-  bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)         // UMICLUST_SPLIT (-1: single-bin loads split, multi-bin sets do not)
+  bool pre_resolve = true;         // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
+  bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)
+  int32_t band_pairs = 140000;     // UMICLUST_BAND: alignment launches of at most this many pairs run banded
+                                   // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
+                                   // k_align_pk (profiles/r03/band_ab.json)
+  bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
   DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
