@@ -351,8 +351,8 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
       F = __builtin_elementwise_max(fo, fe);
       // a new D run opened from H continues H's own D run when H took F
       if (LAST) {
-        const uint32_t dlh = DL & mF & ~mE;  // H's own D run (0 unless H took F)
-        DL = bfi(mfx, DL, dlh) + 0x00010001u;
+        // extended, or opened from an H that took F (continuing H's run): one more; else a new run of 1
+        DL = bfi(mfx | (mF & ~mE), DL + 0x00010001u, 0x00010001u);
         asm volatile("" : "+v"(DL));  // keep the tracker in its row (sinking it keeps 3 masks per row live)
       }
       SF = bfi(mfx, SF, sh);
@@ -467,26 +467,31 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     }
   }
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
-  const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
+  const int X = sc.mismatch;  // k_align_pk's row potential: H' = H - X (global row + 1)
+  const int QRti = sc.go[3] + sc.ge[3] + X, Rti = sc.ge[3] + X;
+  const int QRtr = sc.go[5] + sc.ge[5] + X, Rtr = sc.ge[5] + X;
   const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
   const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
-  const v2s MM = as_v2(pk2(sc.mismatch, sc.mismatch));
   const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
-  const v2s R0 = as_v2(pk2(r0, r0));
   const uint32_t qrqL = pk2(QRqi, last ? QRqr : QRqi), rqL = pk2(Rqi, last ? Rqr : Rqi);
   v2s H[TOP], E[TOP];
-  uint32_t SH[TOP], SE[TOP];  // summaries; SH stored +1 (every consumer adds the move)
+  // summaries: k_align_pk's m | (u + 1) << 8 with u biased by kSB (> the virtual rows' depth P - 1, so the
+  // virtual rows' start values are not negative either)
+  constexpr int kSB = 8;
+  static_assert(P <= kSB, "summary bias");
+  uint32_t SH[TOP], SE[TOP];
   auto init_rows = [&](uint32_t keep_mask) {
-    // boundary column -1 (k_align_pk's init_rows at global rows); lane 0's row -1 stand-in holds H(-1,-1) = 0.
-    // The opaque zero keeps the loop-invariant row values from being hoisted into 2 TOP live VGPRs.
+    // boundary column -1 (k_align_pk's pk_init_rows at global rows); lane 0's row -1 stand-in holds
+    // H(-1,-1) = 0 and the corner's summary (u + 1 = 0).  The opaque zero keeps the loop-invariant row
+    // values from being hoisted into 2 TOP live VGPRs.
     int vz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-    const int hbase = vz - sc.go[1] - (r0 + 1) * sc.ge[1];
+    const int hbase = vz - sc.go[1] - (r0 + 1) * (sc.ge[1] + X);
+    const uint32_t sbase = (uint32_t)vz + pk2((r0 + 1 + kSB) << 8, (r0 + TOP + 1 + kSB) << 8);
 #pragma unroll
     for (int kk = 0; kk < TOP; kk++) {
-      const int h0 = hbase - kk * sc.ge[1];
-      const int h1 = hbase - (TOP + kk) * sc.ge[1];
+      const int h0 = hbase - kk * (sc.ge[1] + X);
+      const int h1 = hbase - (TOP + kk) * (sc.ge[1] + X);
       const int q1 = (kk == KL && last) ? QRqr : QRqi;
       const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
       const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
@@ -495,8 +500,9 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
         if (kk == VK) hp &= ~(VM & fm);
       H[kk] = as_v2(bfi(keep_mask, hp, as_u(H[kk])));
       E[kk] = as_v2(bfi(keep_mask, pk2(e0, e1), as_u(E[kk])));
-      SH[kk] = bfi(keep_mask, 0x00010001u, SH[kk]);
-      SE[kk] = bfi(keep_mask, 0x00010001u, SE[kk]);
+      const uint32_t s01 = sbase + (uint32_t)kk * 0x01000100u;
+      SH[kk] = bfi(keep_mask, s01, SH[kk]);
+      SE[kk] = bfi(keep_mask, s01, SE[kk]);
     }
   };
 #pragma unroll
@@ -506,14 +512,14 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     SH[kk] = SE[kk] = 0;
   }
   init_rows(0xffffffffu);
-  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDF = 0;  // top half's last row -> bottom half (next step)
-  uint32_t xHF = 0, xSS = 0, xDF = 0;                    // last row (Hd | F, SHd | SF, DF) -> lane g+1
+  uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDL = 0;  // top half's last row -> bottom half (next step)
+  uint32_t xHF = 0, xSS = 0, xDL = 0;                    // last row (Hd | F, SHd | SF, DL) -> lane g+1
   int Lext = 0, trail = 0;
   uint32_t tword = 0, tprev = 1;
   const int nsteps = tl + 2 * G - 1;
   for (int st = 0; st < nsteps; st++) {
     const int j = st - 2 * g;  // top half's column; the bottom half's is j - 1
-    const uint32_t rHF = row_shr1(xHF), rSS = row_shr1(xSS), rDF = row_shr1(xDF);
+    const uint32_t rHF = row_shr1(xHF), rSS = row_shr1(xSS), rDL = row_shr1(xDL);
     uint32_t tcode = 0;
     if (j >= 0 && j <= tl) {
       if ((j & 7) == 0) tword = tcp[j >> 3];
@@ -532,16 +538,30 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     // the row above the top half: the boundary row -1 (lane 0) or lane g-1's last row | carry (bottom half)
     const int hd0 = (j <= 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
     const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
+    // boundary row -1 for lane 0: H(-1, j-1) (u = j - 1), F(0, j) (u = j, one D move)
+    const int jb = (j < 0 ? 0 : j) + kSB;
     v2s Hd = as_v2(bfi(fm, (uint32_t)hd0 & 0xffffu, rHF & 0xffffu) | (cHd << 16));
-    uint32_t SHd = bfi(fm, 1u, rSS & 0xffffu) | (cSHd << 16);
+    uint32_t SHd = bfi(fm, (uint32_t)jb << 8, rSS & 0xffffu) | (cSHd << 16);
     v2s F = as_v2(bfi(fm, (uint32_t)f0 & 0xffffu, rHF >> 16) | (cF << 16));
-    uint32_t SF = bfi(fm, 1u, rSS >> 16) | (cSF << 16);
-    uint32_t DF = bfi(fm, 0xffffu, rDF & 0xffffu) | (cDF << 16);  // row the current D run opened from
+    uint32_t SF = bfi(fm, (uint32_t)(jb + 1) << 8, rSS >> 16) | (cSF << 16);
+    uint32_t DL = bfi(fm, 1u, rDL & 0xffffu) | (cDL << 16);  // D run of the F state
+    // each row's diagonal candidate is formed before the row above overwrites its H / S_H (k_align_pk)
+    uint32_t e = M[0] & 0x00010001u;
+    v2s hn = as_v2(e) * DELTA + Hd;
+    uint32_t shn = SHd + e + 0x01000100u;
 #pragma unroll
     for (int kk = 0; kk < TOP; kk++) {
-      const uint32_t e = (M[kk >> 4] >> (kk & 15)) & 0x00010001u;
-      v2s h = Hd + MM + as_v2(e) * DELTA;
-      uint32_t sh = SHd + (e << 8);
+      v2s h = hn;
+      uint32_t sh = shn;
+      const uint32_t oldH = as_u(H[kk]), oldS = SH[kk];  // (the last row's carry for lane g+1)
+      if (kk + 1 < TOP) {
+        e = (M[(kk + 1) >> 4] >> ((kk + 1) & 15)) & 0x00010001u;
+        hn = as_v2(e) * DELTA + H[kk];
+        shn = SH[kk] + e + 0x01000100u;
+      } else {
+        Hd = H[kk];
+        SHd = SH[kk];
+      }
       const uint32_t mF = gt_mask(F, h);
       h = __builtin_elementwise_max(h, F);
       sh = bfi(mF, SF, sh);
@@ -549,18 +569,18 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
       const uint32_t mE = gt_mask(Ec, h);
       h = __builtin_elementwise_max(h, Ec);
       sh = bfi(mE, SE[kk], sh);
-      const uint32_t sh1 = sh + 0x00010001u;
       int dr_last = 0;
       bool eb_last = false;
       if (kk == KL) {
         eb_last = (mE >> 31) != 0;
-        dr_last = (mF >> 31) != 0 ? (QL - 1) - (int)(short)(DF >> 16) : 0;
+        dr_last = (mF >> 31) != 0 ? (int)(DL >> 16) : 0;
       }
       const v2s fo = h - as_v2(QRt), fe = F - as_v2(Rt);
       const uint32_t mfx = gt_mask(fe, fo);
       F = __builtin_elementwise_max(fo, fe);
-      DF = bfi(mfx | (mF & ~mE), DF, as_u(as_v2(pk2(kk, TOP + kk)) + R0));
-      SF = bfi(mfx, SF + 0x00010001u, sh1);
+      // extended, or opened from an H that took F (continuing H's run): one more; else a new run of 1
+      DL = bfi(mfx | (mF & ~mE), DL + 0x00010001u, 0x00010001u);
+      SF = bfi(mfx, SF, sh);
       const uint32_t qrq = kk == KL ? qrqL : pk2(QRqi, QRqi);
       const uint32_t rq = kk == KL ? rqL : pk2(Rqi, Rqi);
       const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
@@ -572,37 +592,36 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
         Lext = ex ? 1 + Lext : lh;
       }
       E[kk] = __builtin_elementwise_max(eo, ee);
-      SE[kk] = bfi(mex, SE[kk] + 0x00010001u, sh1);
-      Hd = H[kk];
-      SHd = SH[kk];
+      SE[kk] = bfi(mex, SE[kk], sh);
       H[kk] = h;
-      SH[kk] = sh1;
+      SH[kk] = sh;
       if constexpr (P > 0) {
         if (kk == VK) {
           // lane 0's stand-in row leaves exactly what the boundary row -1 gives the row below it
           const int cv = VR < TOP ? j : j - 1;
           const int hb = cv < 0 ? 0 : -(sc.go[0] + (cv + 1) * sc.ge[0]);
           const int fb = sc.boundary_open ? hb - (cv == tl - 1 ? QRtr : QRti) : kNegInf;
+          const int sb = (cv < -1 ? -1 : cv) + 1 + kSB;  // H(-1, cv) and F(0, cv): u = cv
           const uint32_t vm = VM & fm;
           H[kk] = as_v2(bfi(vm, pk2(hb, hb), as_u(H[kk])));
-          SH[kk] = bfi(vm, 0x00010001u, SH[kk]);
+          SH[kk] = bfi(vm, pk2(sb << 8, sb << 8), SH[kk]);
           F = as_v2(bfi(vm, pk2(fb, fb), as_u(F)));
-          SF = bfi(vm, 0x00010001u, SF);
-          DF |= vm;
+          SF = bfi(vm, pk2(sb << 8, sb << 8), SF);
+          DL = bfi(vm, 0x00010001u, DL);
         }
       }
       if (kk == KL) {
-        // carries for lane g+1: H(last, j-2) and S_H before this step's update, F / S_F / DF out of it
-        xHF = (as_u(Hd) >> 16) | (as_u(F) & 0xffff0000u);
-        xSS = (SHd >> 16) | (SF & 0xffff0000u);
-        xDF = DF >> 16;
+        // carries for lane g+1: H(last, j-2) and S_H before this step's update, F / S_F / DL out of it
+        xHF = (oldH >> 16) | (as_u(F) & 0xffff0000u);
+        xSS = (oldS >> 16) | (SF & 0xffff0000u);
+        xDL = DL >> 16;
       }
     }
     cHd = as_u(Hd) & 0xffffu;
     cSHd = SHd & 0xffffu;
     cF = as_u(F) & 0xffffu;
     cSF = SF & 0xffffu;
-    cDF = DF & 0xffffu;
+    cDL = DL & 0xffffu;
     if (j <= 0) {
       // columns before 0 (this lane has not started) and the bottom half's column -1: restore
       init_rows(j < 0 ? 0xffffffffu : 0xffff0000u);
@@ -611,9 +630,10 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     }
   }
   if (!last) return;
-  const int Hend = (int)(short)(as_u(H[KL]) >> 16);
-  const uint32_t S = ((SH[KL] >> 16) - 1u) & 0xffffu;
-  const uint32_t m = S >> 8, acols = S & 0xffu;
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + X * QL;
+  const uint32_t S = (SH[KL] >> 16) & 0xffffu;
+  const uint32_t m = S & 0xffu;
+  const uint32_t acols = (uint32_t)(QL + tl + kSB) - (S >> 8);
   const uint32_t internal = acols - (uint32_t)trail;
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
 }
