@@ -1689,7 +1689,8 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
   const int full_most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
-  const int count_most = kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists) + 16;
+  // (at least 64 KB: UMICLUST_PFWG pads the counting workgroups' LDS)
+  const int count_most = std::max(65536, kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists) + 16);
   if (!attr_set_on_device(k_attr_prefilter)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
     if (e == hipSuccess)
@@ -1714,7 +1715,15 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     // the list tables first (k_pf_table, one wave per unit) when the pass has a table buffer
     if (a.pftab)
       hipLaunchKernelGGL(k_pf_table, dim3(nqs * kParts), dim3(64), 0, st, a, a.pftab, nqs * kParts);
-    const size_t lds = tab_off + pf_count_table_bytes(a.nlist_cap) + 16;  // (+16: the table copy's last vector)
+    size_t lds = tab_off + pf_count_table_bytes(a.nlist_cap) + 16;  // (+16: the table copy's last vector)
+    // UMICLUST_PFWG=k: pad the workgroup's LDS so that at most k counting workgroups share a CU and the
+    // rest of the CU's LDS (UMICLUST_PFWG_RESERVE bytes, default 16 KB) stays free for alignment waves
+    static const int pfwg = getenv("UMICLUST_PFWG") ? atoi(getenv("UMICLUST_PFWG")) : 0;
+    static const int pfres = getenv("UMICLUST_PFWG_RESERVE") ? atoi(getenv("UMICLUST_PFWG_RESERVE")) : 16384;
+    if (pfwg > 0) {
+      const size_t pad = ((size_t)(160 * 1024 - pfres) / (size_t)pfwg) & ~(size_t)255;
+      if (pad > lds && pad <= 65536) lds = pad;
+    }
     if (cm == 1)
       hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
                          (const uint32_t*)a.pftab);
