@@ -379,6 +379,7 @@ struct umiclust_ctx {
                                    // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
                                    // k_align_pk (profiles/r03/band_ab.json)
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)
+  bool r_on_al = false;            // UMICLUST_RAL=1: second halves' prefilter on the align stream (split passes)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
   DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
@@ -785,12 +786,20 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   P.nq = nq;
   P.w0 = w0;
   P.live = true;
-  if (!(own.prebuilt && own.base == q0 && own.n == nq && own.seg == region))
-    build_tile(c, own, c->d_iota.p, q0, nq, 0, region * kPeerRegion, 1 << 30);
+  const bool built_now = !(own.prebuilt && own.base == q0 && own.n == nq && own.seg == region);
+  if (built_now) build_tile(c, own, c->d_iota.p, q0, nq, 0, region * kPeerRegion, 1 << 30);
   own.prebuilt = false;
   own.base = q0;
   own.seg = region;
   own.len = block_maxlen(c, q0, nq);  // the block's longest query
+  const bool second_half = after_count && P.a_live && P.a_q0 == q0;
+  // r_on_al: a second half's prefilter (full kernel + merge) runs on the align stream ahead of its walk, so the
+  // main stream's next counting half does not queue behind it.  It needs its counting half (a_ev) and the
+  // index / tiles (ix_done; index appends on the side stream wait for the latest second half, last_r_ev)
+  if (second_half && c->r_on_al && c->ix_st && !built_now) {
+    st = c->st_al;
+    if (c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");
+  }
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
   if (need > P.h_tiles.n) {
@@ -852,7 +861,6 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.peer_shift = 0;
   a.peer_id_add = 0;
   a.seq2ord = c->d_seq2ord.p - c->bin_s[c->cur_bin];
-  const bool second_half = after_count && P.a_live && P.a_q0 == q0;
   if (second_half) {
     // the counting half ran with the window one block wider (oldest first): its peer ids are relative to
     // that window's start
@@ -1004,6 +1012,9 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
     st = c->st_pf;
     c->hip(hipStreamWaitEvent(st, c->a_ev[slot][2], 0), "wait");
   }
+  // this buffer set's last second half (full kernel + merge on the align stream under r_on_al) has read what
+  // the counting half overwrites
+  if (c->r_on_al && c->ix_st) c->hip(hipStreamWaitEvent(st, P.ev[1], 0), "wait");
   c->hip(hipEventSynchronize(P.ev_a), "sync");  // the last upload from h_tiles_a is done
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
@@ -2596,6 +2607,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_RAL")) c->r_on_al = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
