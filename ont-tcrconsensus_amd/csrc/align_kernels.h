@@ -170,7 +170,8 @@ __global__ __launch_bounds__(64) void k_align(DevSeqs s, const uint32_t* __restr
 // Branch-free selection: for |values| well inside int16, (a - b) >> 15 (arithmetic, per half) is
 // the mask of "b > a", which drives v_bfi for the summaries and v_pk_max for the scores.
 // Substitution: per 16-row group a match bit-mask of the column's target base, selected per step
-// from per-base masks built once per pair (non-ambiguous sequences only: one-hot codes).
+// from per-base masks built once per pair (non-ambiguous sequences only: one-hot codes; k_align_pk
+// keeps them in lane-private LDS, k_align_band in VGPRs).
 typedef short v2s __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ v2s as_v2(uint32_t x) { return __builtin_bit_cast(v2s, x); }
@@ -201,6 +202,7 @@ __device__ __forceinline__ uint32_t gt_mask(v2s b, v2s a) {
 //    overwrites them, so the register rotation needs no copies.
 //  * the boundary initialisation is an inlined function, not a lambda captured by the step lambda
 //    (that closure kept the row arrays in scratch).
+
 // k_align_pk's boundary column -1: H'(i,-1) = -(GO_TL + (i+1) GE_TL) - X (i+1), E'(i,0) opened
 // from it; summaries u + 1 = i + 1, no matches; keep_mask selects the halves to (re)initialise
 template <int QL, int TOP>
