@@ -2048,7 +2048,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     prime(0);
     for (int32_t k = 0; k < nb; k++) {
       Pass& P = c->pass[k % 2];
+      const double tb0 = now_s();
       if (k + 3 < nb) build_peer(k + 3, true);  // queries only: built while the host resolves block k
+      c->dbg_t[5] += now_s() - tb0;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
         // drain everything queued (its windows include block k) and restart the pipeline after block k
         c->hip(hipStreamSynchronize(c->st_al), "sync");
@@ -2071,12 +2073,16 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
         prime(k + 1);
         continue;
       }
+      const double ta0 = now_s();
       append_centroids(c, new_cents);
+      const double ta1 = now_s();
       c->stats.n_blocks++;
       lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
       c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
       if (k + 2 < nb) second_half(k + 2, k + 1, true);
       if (k + 3 < nb) count_half(k + 3, k + 1, 0);
+      c->dbg_t[7] += ta1 - ta0;           // UMICLUST_DEBUG: index appends (host side)
+      c->dbg_t[5] += now_s() - ta1;       // and the next passes' enqueue
     }
   } else {
   for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
@@ -2301,6 +2307,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     fprintf(stderr, "bin %d: resolve wait %.3f hq-copy %.3f rec-copy %.3f classify %.3f in-order %.3f total %.3f s "
             "(round B and the rest %.3f)\n", bin, c->dbg_t[0], c->dbg_t[1], c->dbg_t[2], c->dbg_t[3], c->dbg_t[4],
             c->dbg_t[6], c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[3] - c->dbg_t[4]);
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: split-pass host: appends %.3f enqueue %.3f s\n", bin, c->dbg_t[7], c->dbg_t[5]);
   for (double& x : c->dbg_t) x = 0;
   c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
   c->dbg_p[0] = c->dbg_p[1] = c->dbg_p[2] = c->dbg_p[3] = 0;
