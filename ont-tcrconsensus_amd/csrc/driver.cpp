@@ -454,6 +454,10 @@ struct umiclust_ctx {
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
   int64_t dbg_q[4] = {0, 0, 0, 0};
+  // UMICLUST_WALK_DUMP=<file>: per sorted seqno of the bin, the alignments each strand's walk counted and the
+  // path that resolved it (0 device, 1 classify thread, 2 in order, 3 round B) -- a parity-debugging aid
+  const char* walk_dump = getenv("UMICLUST_WALK_DUMP");
+  std::vector<int16_t> wd;
   double dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // UMICLUST_DEBUG: resolve_pass phases (s): event wait, outcome copy,
                                                // record copy, classify, in-order resolve, round B + rest, total
   int64_t dbg_p[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: strands on the inline path / with > kInlineRel relevant
@@ -687,6 +691,15 @@ struct StateView {
   int32_t s0 = 0;
   uint8_t& operator[](int64_t i) const { return p[i - s0]; }
 };
+
+// Policy O4 (batched rounds of o4_T queries): the first query of q's round.  Rounds are counted from the first
+// sorted query of q's own bin -- in a pack of bins (one greedy order over several bins) from the bin's first
+// seqno, so every bin's rounds are the ones its own vsearch run would have.  Sequential policy: q itself.
+inline int32_t round_start(const umiclust_ctx* c, int32_t s0, int32_t q) {
+  if (!c->o4_T) return q;
+  const int32_t b0 = c->pack_on ? c->bin_s[c->hqbin[q]] : s0;
+  return b0 + (q - b0) / c->o4_T * c->o4_T;
+}
 
 void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   const size_t nqs = (size_t)B * c->both;
@@ -1275,7 +1288,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     const int32_t row = allow_extra ? extra_row[qs] : -1;
     // O4 batched rounds: centroids created before q's round join its search (the merged walk); those of its
     // own round are the extras of the re-check below.  Sequential: every centroid peer joins the walk.
-    const uint32_t rb = c->o4_T ? (uint32_t)(state.s0 + (q - state.s0) / c->o4_T * c->o4_T) : UINT32_MAX;
+    const uint32_t rb = c->o4_T ? (uint32_t)round_start(c, state.s0, q) : UINT32_MAX;
     auto& cx = scr.cx;
     cp.clear();
     cx.clear();
@@ -1405,6 +1418,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     for (int s = 0; s < both; s++) {
       c->stats.n_alignments += os[s].walked;
       c->stats.cells += os[s].cells;
+      if (!c->wd.empty()) {
+        c->wd[(size_t)(q - state.s0) * 4 + s] = (int16_t)os[s].walked;
+        c->wd[(size_t)(q - state.s0) * 4 + 2 + s] = allow_extra ? 3 : 2;
+      }
       if (better(os[s], best)) {
         best = os[s];
         bs = s;
@@ -1534,6 +1551,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       else os[s] = P.pre[qs];
       acc.aln += os[s].walked;
       acc.cells += os[s].cells;
+      if (!c->wd.empty()) {
+        c->wd[(size_t)(q0 + ql - state.s0) * 4 + s] = (int16_t)os[s].walked;
+        c->wd[(size_t)(q0 + ql - state.s0) * 4 + 2 + s] = P.kind[qs] == 0 ? 0 : 1;
+      }
       if (better(os[s], best)) {
         best = os[s];
         bs = s;
@@ -1801,7 +1822,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   const double t0 = now_s();
   if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
     c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
-  if (npk > 1 && c->o4_T) c->fail(UMICLUST_EINVAL, "packs of bins need the sequential policy (policy_threads = 0)");
   c->pack_on = npk > 1;
   // one bin (or pack) = the sorted seqnos [s0, s1); seqnos stay absolute everywhere
   const int32_t s0 = c->bin_s[bin], s1 = c->bin_s[bin + npk];
@@ -1844,6 +1864,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   c->hip(hipMemsetAsync(c->d_seq2ord.p, 0xff, (size_t)n * 4, c->st), "memset");
   std::vector<uint8_t> state_buf((size_t)n, ST_UNDET);
   StateView state{state_buf.data(), s0};
+  if (c->walk_dump) c->wd.assign((size_t)n * 4, -1);
   double t_pf = 0, t_al = 0, t_host = 0;
   // blocks of at most B queries of one length (the aligner is compiled per query length); a block's
   // peer tile fills one kPeerRegion of the prefilter counters, so B <= kMaxBlock
@@ -1883,9 +1904,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     for (int32_t q0 = from; q0 < s1;) {
       int32_t same = 1;
       const int32_t bcap = q0 < until ? bmax : B;
-      if (mix && !c->o4_T) {  // across length changes, at most kSegLens lengths (one pair segment each);
-                                     // O4 batched rounds keep one length per block (mixed blocks there: 21 more
-                                     // alignments than the oracle on test_batched_rounds_deep_clusters, unresolved)
+      if (mix) {  // across length changes, at most kSegLens lengths (one pair segment each)
         const int32_t lim = std::min<int32_t>(bcap, s1 - q0);
         int32_t lo = c->hlen[q0], hi = lo;  // (a pack's lengths restart at every bin)
         while (same < lim && std::max<int32_t>(hi, c->hlen[q0 + same]) - std::min<int32_t>(lo, c->hlen[q0 + same]) < kSegLens) {
@@ -1900,14 +1919,14 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       q0 += same;
     }
   };
-  // Policy O4 batched rounds (c->o4_T queries each, counted from the bin's first sorted query): query q's search
+  // Policy O4 batched rounds (c->o4_T queries each, counted from the first sorted query of q's bin): query q's search
   // sees only the centroids before its round start rstart(q), and the centroids of its round before it are the
   // re-check's extras -- both must be in its pass's peer window, and the index must hold nothing from the round.
   // So a pass's window starts at min(nominal window start, round start of its first query) (a round tile over
   // [round start, block start) replaces the nominal previous tiles when the round began earlier), and resolved
   // centroids wait in `pending` until every later pass's window starts after them.
   const int32_t T4 = c->o4_T;
-  auto rstart = [&](int32_t q) { return T4 ? s0 + (q - s0) / T4 * T4 : q; };
+  auto rstart = [&](int32_t q) { return round_start(c, s0, q); };
   std::vector<int32_t> pending;
   auto sync_index = [&](int32_t X) {  // the index gets the pending centroids before seqno X
     size_t m = 0;
@@ -2294,6 +2313,13 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   }
   c->stats.t_total_s = now_s() - t0;
   c->clustered = true;
+  if (c->walk_dump && !c->wd.empty()) {
+    if (FILE* f = fopen(c->walk_dump, "wb")) {
+      fwrite(c->wd.data(), 2, c->wd.size(), f);
+      fclose(f);
+    }
+    c->wd.clear();
+  }
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: n %d mispredicted %lld saved(seen) %lld blocked %lld deferred %lld\n", bin, n,
             (long long)c->dbg[0], (long long)c->dbg[1], (long long)c->dbg[2], (long long)c->stats.n_deferred);
@@ -3299,7 +3325,7 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
     // the reference raises KeyError at the first record whose region is unknown, after the records before it
     int64_t stop = n;
     for (int64_t r = 0; r < n && stop == n; r++)
-      if (cls[r] == kBamNoRegion || cls[r] == kBamNoCluster || cls[r] == kBamNoCigar) stop = r;
+      if (cls[r] == kBamNoRegion || cls[r] == kBamNoCluster) stop = r;
     int32_t ncl = 0;
     for (int64_t r = 0; r < stop; r++)
       if (cls[r] == kBamKept) ncl = std::max(ncl, clu[r] + 1);
@@ -3361,8 +3387,6 @@ int64_t umiclust_region_split(umiclust_ctx* c, const char* bam_file, int32_t nre
       }
     }
     for (int x = 0; x < 4; x++) counts[x] = cnt[x];
-    if (stop < n && cls[stop] == kBamNoCigar)
-      c->fail(UMICLUST_EFORMAT, "TypeError: '<' not supported between instances of 'NoneType' and 'float'");
     if (stop < n) {
       const int32_t ref = rd_i32(raw.data() + roff[stop] + 4);
       const std::string nm = ref >= 0 && ref < nref ? refname[ref] : std::string("None");

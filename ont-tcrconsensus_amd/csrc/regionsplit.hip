@@ -43,8 +43,6 @@ __global__ void k_bam_classify(const uint8_t* __restrict__ raw, const int64_t* _
     c = kBamSecondary;
   } else if (ref < 0 || ref >= nref || ref_len[ref] < 0) {
     c = kBamNoRegion;  // region_length_dict[entry.reference_name] raises
-  } else if (ncig == 0) {
-    c = kBamNoCigar;  // pysam's reference_length is None without a CIGAR: `None < float` raises TypeError (:261)
   } else {
     const uint8_t* cg = p + 32 + lrn;
     int64_t rl = 0;
@@ -52,6 +50,9 @@ __global__ void k_bam_classify(const uint8_t* __restrict__ raw, const int64_t* _
       const uint32_t v = ld_u32(cg + 4 * x), op = v & 15u;
       if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += v >> 4;
     }
+    // pysam's reference_length = bam_endpos - pos, and htslib's bam_endpos counts a zero reference span (no CIGAR,
+    // or only I/S/H/P ops) as 1: such a record is 1 base long and drops as short (:261-263)
+    if (rl == 0) rl = 1;
     const double L = (double)ref_len[ref];
     if ((double)rl < L * minov) {
       c = kBamShort;

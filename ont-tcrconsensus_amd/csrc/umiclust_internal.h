@@ -338,7 +338,7 @@ hipError_t launch_extract_win(const char* win, const uint8_t* wlen, int64_t n, i
 
 // ---- region binning of BAM records (regionsplit.hip) ----
 enum : int8_t { kBamUnmapped = 0, kBamSecondary = 1, kBamShort = 2, kBamLong = 3, kBamKept = 4, kBamNoRegion = 5,
-                kBamNoCluster = 6, kBamNoCigar = 7 };
+                kBamNoCluster = 6 };
 // raw: uncompressed BAM, roff[r]: offset of record r's block_size field; ref_len / ref_cluster per BAM reference
 // (-1: not in the reference FASTA / not in the cluster dict)
 hipError_t launch_bam_classify(const uint8_t* raw, const int64_t* roff, int64_t n, int32_t nref, const int64_t* ref_len,

@@ -69,9 +69,9 @@ class AlignedSegment:
     def reference_length(self):
         if self.is_unmapped:
             return None
-        if not self.cigartuples:  # pysam: reference_end (hence reference_length) is None without a CIGAR
-            return None
-        return sum(ln for op, ln in self.cigartuples if op in (0, 2, 3, 7, 8))
+        # pysam: bam_endpos(b) - pos, and htslib's bam_endpos turns a zero reference span (no CIGAR) into 1
+        # (reference_end, not reference_length, is the one that is None without a CIGAR)
+        return sum(ln for op, ln in (self.cigartuples or ()) if op in (0, 2, 3, 7, 8)) or 1
 
     def get_forward_sequence(self):
         s = self.query_sequence

@@ -10,8 +10,8 @@ records read by oracle/bam.py (pysam is not installed):
   - a kept record goes to region_cluster<k>.fasta as `>{query_name};strand={+|-}` and its forward sequence
     (`None` when the record stores none, as print() writes it) (:271-283);
   - the region-length and cluster lookups raise KeyError for a reference missing from them (:261, :271);
-  - a mapped primary record without a CIGAR has no reference_length (pysam: None) and the comparison at :261
-    raises TypeError, after the records before it.
+  - a mapped primary record without a CIGAR has reference_length 1 (pysam's bam_endpos - pos; htslib's
+    bam_endpos counts a zero reference span as 1), so it drops as short.
 Pinned by tests/golden/region_split/*.json, the reference's own outputs (tests/test_region_split_cpu.py).
 With `out_dir` the records are appended one open() per record, as the reference does (:273-280): the
 CPU baseline of bench_rows.py times exactly that loop.

@@ -633,6 +633,9 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
   hit_t *hm = (hit_t *)malloc(sizeof(hit_t) * (size_t)tophits);
   char *rcq = (char *)malloc((size_t)maxl + 2);
   int32_t clusters = 0;
+  /* ORC_WALK_DUMP=<file>: alignments per sorted seqno and strand (search + O4 re-check), a parity-debugging aid */
+  const char *walk_dump = getenv("ORC_WALK_DUMP");
+  int16_t *wd = walk_dump ? (int16_t *)calloc((size_t)nk * 2 + 2, sizeof(int16_t)) : NULL;
   /* assign s from its hits: search_findbest2_byid (accepted hit with max id; tie -> lower target; plus
    * first), then a member of that centroid's cluster or a new centroid */
   #define ASSIGN(s, hp, np, hm, nm) do {                                                            \
@@ -666,12 +669,16 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
   if (T == 1) {
     /* cluster_core_serial (cluster.cc) */
     for (int32_t s = 0; s < nk; s++) {
+      int64_t a0 = c.alignments;
       int np = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, hp);
+      if (wd) wd[2 * s] = (int16_t)(c.alignments - a0);
+      a0 = c.alignments;
       int nm = 0;
       if (p->strand_both) {
         revcomp(rcq, c.seq[s], c.len[s]);
         nm = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, hm);
       }
+      if (wd) wd[2 * s + 1] = (int16_t)(c.alignments - a0);
       ASSIGN(s, hp, np, hm, nm);
     }
   } else {
@@ -692,12 +699,16 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
       const int32_t nb = (nk - b0 < T) ? nk - b0 : T;
       for (int32_t i = 0; i < nb; i++) {
         const int32_t s = b0 + i;
+        int64_t a0 = c.alignments;
         bn[2 * i] = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, bh + (size_t)(2 * i) * cap);
+        if (wd) wd[2 * s] = (int16_t)(c.alignments - a0);
+        a0 = c.alignments;
         bn[2 * i + 1] = 0;
         if (p->strand_both) {
           revcomp(rcq, c.seq[s], c.len[s]);
           bn[2 * i + 1] = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, bh + (size_t)(2 * i + 1) * cap);
         }
+        if (wd) wd[2 * s + 1] = (int16_t)(c.alignments - a0);
       }
       int nextra = 0;
       for (int32_t i = 0; i < nb; i++) {
@@ -739,6 +750,7 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
           if (added) {
             int accepts = 0, rejects = 0;
             for (int t = 0; accepts < p->maxaccepts && rejects < p->maxrejects && t < *nh; t++) {
+              if (!h[t].aligned && wd) wd[2 * s + st]++;
               if (!h[t].aligned) align_hit(&c, p, qs, c.len[s], &h[t]);
               if (h[t].accepted) accepts++;
               else rejects++;
@@ -758,6 +770,14 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
     free(bh);
   }
   #undef ASSIGN
+  if (wd) {
+    FILE *wf = fopen(walk_dump, "wb");
+    if (wf) {
+      fwrite(wd, sizeof(int16_t), (size_t)nk * 2, wf);
+      fclose(wf);
+    }
+    free(wd);
+  }
   /* cluster sizes and output numbering (--clusterout_sort: size desc, creation order) */
   csz_t *cs = (csz_t *)calloc((size_t)clusters + 1, sizeof(csz_t));
   for (int32_t k = 0; k < clusters; k++) cs[k].cno = k;

@@ -70,7 +70,7 @@ def make_case(rng, name, n_regions, n_reads, minimal_region_overlap=0.95, s5=73,
             seq = ""  # secondary without a stored sequence
         records.append(dict(name=f"read{i:05d}", flag=flag, ref=ref if not flag & 4 or rng.random() < 0.5 else -1,
                             pos=rng.randint(0, 20), cigar=cigar, seq=seq))
-        if i == no_cigar_at:  # a mapped primary record without a CIGAR: pysam's reference_length is None
+        if i == no_cigar_at:  # a mapped primary record without a CIGAR: reference_length 1 (htslib bam_endpos)
             records[-1].update(flag=16, ref=0, cigar=[])
     pre = {}
     if pre_existing:  # the reference appends to region_cluster<k>.fasta

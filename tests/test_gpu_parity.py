@@ -612,18 +612,14 @@ def test_pack_edge_cases(gpu_ctx, packs):
 
 
 def test_pack_errors(gpu_ctx):
-    """A pack past the load's bins, an empty pack and a pack under the batched O4 policy fail with EINVAL."""
+    """A pack past the load's bins and an empty pack fail with EINVAL (packs under the batched O4 policy are
+    tests/test_gpu_o4.py's)."""
     seqs = synth.make_umis(20, seed=63, max_reads=200).as_list()
     buf, off = _lib._pack(seqs + seqs)
     gpu_ctx.load_bins(_lib.params(1, 0.93, 58, 68), buf, off, [0, len(seqs), 2 * len(seqs)])
     for first, m in [(1, 2), (0, 0), (-1, 2)]:
         with pytest.raises(_lib.UmiclustError):
             gpu_ctx.cluster_pack(first, m)
-    p = _lib.params(1, 0.93, 58, 68)
-    p.threads, p.policy_threads = 25, 1
-    gpu_ctx.load_bins(p, buf, off, [0, len(seqs), 2 * len(seqs)])
-    with pytest.raises(_lib.UmiclustError):
-        gpu_ctx.cluster_pack(0, 2)
 
 
 def test_load_bins_edge_cases(gpu_ctx):

@@ -31,7 +31,7 @@ def test_region_split_vs_reference_fixtures(tmp_path, case):
     kw = dict(minimal_region_overlap=case["minimal_region_overlap"], max_softclip_5_end=case["max_softclip_5_end"],
               max_softclip_3_end=case["max_softclip_3_end"])
     if case["error"]:
-        exc = KeyError if case["error"].startswith("KeyError") else TypeError  # no CIGAR: pysam's None
+        exc = KeyError
         with pytest.raises(exc) as e:
             rs.filter_and_split_reads_by_region_cluster(bam_path, js, ref_fa, logs, out, **kw)
         assert f"{exc.__name__}: {e.value}" == case["error"]
