@@ -9,13 +9,15 @@ Workloads (BASELINE.json configs):
   --config 4: 70M reads, 24 barcodes x 40 Zipf bins, both rounds: round 1 on every bin, round 2 (default
       scoring, --id 0.97) on the round-1 consensus UMIs of every bin (tcr_consensus.py:190-267, :376-446).
   --config 5: the long-UMI high-error stress bin (300k ~96-nt UMIs, 15 % indels, >1k-member clusters).
-A step = one full pass of the hot path over the rank's bins with the sequences already resident in HBM:
-K1 prep/DUST/k-mers, greedy blocks of K2 prefilter + K3 walk alignment + host resolution, K3T traceback
-for members, K4 consensus, and the result download.  Config 2 (N = 1) also runs the file leg (`e2e`, on by
-default, --no-e2e skips it): the same bin written as a FASTA with 1,500-nt `seq=` reads, then read FASTA ->
-cluster -> files written (umiclust_run_fasta, the reference's boundary: vsearch_umi_cluster.py:17-56) and the
-fused drop-in (umiclust_run_fasta_parse), each beside a write probe of the same file count and bytes on the same
-filesystem (tools/io_probe.c), so the writers' share of the disk's rate is a measured fraction.
+A step = one full pass of the hot path over the rank's bins, the raw records staged in HBM beforehand
+(umiclust_stage, untimed): vsearch's load-time work (umiclust_prepare: length filter and stable length sort, K1
+DUST / 4-bit codes / unique 8-mers of both strands), greedy blocks of K2 prefilter + K3 walk alignment + host
+resolution, K3T traceback for members, K4 consensus, and the result download.  Config 2 (N = 1) also runs the
+file leg (`e2e`, on by default, --no-e2e skips it): the same bin written as a FASTA with 1,500-nt `seq=` reads,
+then read FASTA -> cluster -> files written (umiclust_run_fasta, the reference's boundary:
+vsearch_umi_cluster.py:17-56) and the fused drop-in (umiclust_run_fasta_parse); each writer is followed by a
+replay of its own system calls (the same files, sizes and thread split, no formatting: tools/io_probe.c
+io_probe_replay), the bound the writer cannot beat on that filesystem, so write_frac = replay / writer <= 1.
 
     python bench.py --gpus N --steps K --warmup W [--config 2|3|4|5] [--no-e2e]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -302,10 +304,15 @@ def main() -> None:
     runners = []
     if umis is not None:
         params = _lib.params(_lib.PRESET_ROUND1, args.identity, *lens)
-        ctx.load(params, buf=umis.seq, off=umis.off)
+        ctx.stage(umis.seq, umis.off)  # the raw records resident in HBM (untimed)
 
         def step():
-            return [ctx.cluster()]
+            t0 = time.perf_counter()
+            ctx.prepare(params)  # A3: length filter, sort, DUST, codes, k-mers -- inside the step
+            t_prep = time.perf_counter() - t0
+            st = ctx.cluster()
+            st["t_prepare_s"] = t_prep
+            return [st]
     else:
         r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, args.identity, *lens, lanes=args.lanes, device=local_rank,
                               pack_reads=args.pack_reads)
@@ -321,7 +328,13 @@ def main() -> None:
         def step():
             out = []
             for r in runners:
-                out += r.cluster_all()
+                t0 = time.perf_counter()
+                r.prepare()  # A3 on every lane's staged bins -- inside the step
+                t_prep = time.perf_counter() - t0
+                st = r.cluster_all()
+                if st:
+                    st[0]["t_prepare_s"] = st[0].get("t_prepare_s", 0.0) + t_prep
+                out += st
             return out
 
     def barrier():
@@ -361,6 +374,7 @@ def main() -> None:
         roof, align = roofline(flat, args.config, args.traffic_json)
         # per-step averages for the breakdown
         bd = {k: v / args.steps for k, v in breakdown(flat).items()}
+        bd["t_prepare_s"] = sum(s.get("t_prepare_s", 0.0) for s in flat) / args.steps
         bd["wall"] = t_max / args.steps
         cfg = {"workload": workload, "parallelism": (f"{world} independent bins (1 per GPU), no data-path collective"
                                                       if args.config in (2, 5) else
@@ -407,6 +421,9 @@ def main() -> None:
         out["cpu_baseline"] = cpu
         if not args.no_e2e and args.config == 2 and world == 1:
             out["e2e"] = e2e_leg(ctx, umis, args.identity, lens)
+            # SURVEY §8d's UMIs/s (FASTA in -> files written) beside the HBM-resident value
+            out["e2e_umis_per_s"] = out["e2e"]["umis_per_s"]
+            out["e2e_fused_umis_per_s"] = out["e2e"]["fused_parse"]["umis_per_s"]
         print(json.dumps(out), flush=True)
     ctx.close()
     if ctx2 is not None:
@@ -424,45 +441,44 @@ def _tree_bytes(d: str) -> tuple[int, int]:
     return n, b
 
 
-def write_probe_mmap(d: str, nbytes: int, threads: int) -> dict:
-    """tools/io_probe.c io_probe_mmap: nbytes into one file through a shared mapping from `threads` threads."""
-    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libioprobe.so"))
-    lib.io_probe_mmap.restype = ctypes.c_double
-    lib.io_probe_mmap.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int]
-    pd = os.path.join(d, "probe")
-    os.mkdir(pd)
-    t = lib.io_probe_mmap(pd.encode(), nbytes, threads)
-    os.rmdir(pd)
-    if t < 0:
-        raise RuntimeError("io_probe_mmap failed")
-    return dict(files=1, bytes=nbytes, threads=threads, seconds=t, gbps=nbytes / t / 1e9 if t > 0 else None)
+def _numbered_sizes(d: str, prefix: str, suffix: str = "") -> list:
+    """Sizes of d/<prefix><N><suffix> in N order."""
+    out = []
+    for f in os.listdir(d):
+        if f.startswith(prefix) and f.endswith(suffix) and f[len(prefix):len(f) - len(suffix)].isdigit():
+            out.append((int(f[len(prefix):len(f) - len(suffix)]), os.path.getsize(os.path.join(d, f))))
+    return [sz for _, sz in sorted(out)]
 
 
-def write_probe(d: str, nfiles: int, nbytes: int, threads: int, fsync: bool = False) -> dict:
-    """tools/io_probe.c: nbytes into nfiles equal files (or slices of one file) from `threads` threads on the
-    filesystem of d, the shape the writers use; seconds, GB/s (and the fsync'd commit rate when asked)."""
+def replay_probe(d: str, sizes: list, one_bytes: int, threads: int) -> dict:
+    """tools/io_probe.c io_probe_replay: the writer's own create / write / close sequence (the same file sizes, the
+    same contiguous split over `threads`, one_bytes streamed into one more file as the fused writer streams
+    smolecule_clusters.fa) with no formatting -- the bound the writer cannot beat on this filesystem."""
+    import numpy as np
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libioprobe.so"))
-    lib.io_probe.restype = ctypes.c_double
-    lib.io_probe.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-    pd = os.path.join(d, "probe")
+    lib.io_probe_replay.restype = ctypes.c_double
+    lib.io_probe_replay.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                    ctypes.c_int64]
+    pd = os.path.join(d, "replay")
     os.mkdir(pd)
-    fs = ctypes.c_double(0.0)
-    t = lib.io_probe(pd.encode(), max(1, nfiles), nbytes, threads, ctypes.byref(fs) if fsync else None)
+    sz = np.ascontiguousarray(sizes, np.int64)
+    t = lib.io_probe_replay(pd.encode(), len(sz), sz.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), threads,
+                            int(one_bytes))
     os.rmdir(pd)
     if t < 0:
-        raise RuntimeError("io_probe failed")
-    out = dict(files=nfiles, bytes=nbytes, threads=threads, seconds=t, gbps=nbytes / t / 1e9 if t > 0 else None)
-    if fsync:
-        out.update(fsync_s=fs.value, committed_gbps=nbytes / (t + fs.value) / 1e9)
-    return out
+        raise RuntimeError("io_probe_replay failed")
+    tot = int(sz.sum()) + int(one_bytes)
+    return dict(files=len(sz) + (1 if one_bytes else 0), bytes=tot, threads=threads, seconds=t,
+                gbps=tot / t / 1e9 if t > 0 else None)
 
 
 def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
     """§8d's UMIs/s at the drop-in's file boundary (vsearch_umi_cluster.py:17-56: FASTA in, cluster<N> files +
     consout out; umiclust_run_fasta) and for the fused drop-in (umiclust_run_fasta_parse:
     clustering + parse_umi_clusters' outputs, no cluster<N> files), on the same bin written with 1,500-nt `seq=`
-    reads.  Each writer is followed by a write probe of its own file count and bytes on the same filesystem, so
-    write_frac = probe seconds / writer seconds is the writer's share of what the disk takes for that shape."""
+    reads.  Each writer is followed by a replay of its own system calls (same files, sizes and threads, no
+    formatting), so write_frac = replay seconds / writer seconds is the writer's fraction of what the filesystem
+    allows for exactly its output."""
     import shutil
     import tempfile
     from umiclust import _lib, synth
@@ -484,9 +500,11 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
                            os.path.join(out, "vsearch_cluster.log"))
         t_run = time.perf_counter() - t0
         nf, nb = _tree_bytes(out)
+        sizes = _numbered_sizes(out, "cluster")
+        cons_bytes = os.path.getsize(os.path.join(out, "umi_clusters_consensus.fasta"))
         shutil.rmtree(out, ignore_errors=True)
         os.sync()
-        probe = write_probe(d, nf, nb, io_t)
+        bound = replay_probe(d, sizes, cons_bytes, io_t)
         os.sync()
         # the fused drop-in (run_config.json:17-19 defaults: >= 4 reads, <= 60 per cluster, no strand balancing)
         work = os.path.join(d, "work")
@@ -497,37 +515,30 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
                                       os.path.join(work, "vsearch_cluster.log"), pp, work)
         t_fused = time.perf_counter() - t0
         nf2, nb2 = _tree_bytes(os.path.join(work, "clusters_fa"))
+        sizes2 = _numbered_sizes(os.path.join(work, "clusters_fa"), "cluster", ".fasta")
         smol = os.path.getsize(os.path.join(work, "smolecule_clusters.fa"))
         _, nb_all = _tree_bytes(work)
         shutil.rmtree(work, ignore_errors=True)
         os.sync()
-        probe_f = write_probe(d, nf2, nb2, io_t)
-        os.sync()
-        probe_s = write_probe(d, 1, smol, io_t)
-        os.sync()
-        probe_s_mmap = write_probe_mmap(d, smol, io_t)
-        os.sync()
-        disk = write_probe(d, 1, 2 << 30, io_t, fsync=True)
-        fused_probe_s = probe_f["seconds"] + probe_s["seconds"]
+        bound_f = replay_probe(d, sizes2, smol, io_t)
         return dict(
             umis_per_s=st["n_kept"] / t_run, seconds=t_run, fasta_bytes=size, n_kept=st["n_kept"],
             clusters=st["n_clusters"], t_read_s=st.get("t_read_s"), t_cluster_s=st["t_total_s"],
             t_write_s=st.get("t_write_s"), files_written=nf, bytes_written=nb,
             write_gbps=nb / st["t_write_s"] / 1e9 if st.get("t_write_s") else None,
-            probe=probe, write_frac=probe["seconds"] / st["t_write_s"] if st.get("t_write_s") else None,
+            write_bound=bound, write_frac=bound["seconds"] / st["t_write_s"] if st.get("t_write_s") else None,
             fasta_write_s=t_gen,
             fused_parse=dict(umis_per_s=st2["n_kept"] / t_fused, seconds=t_fused, t_read_s=st2.get("t_read_s"),
                              t_cluster_s=st2["t_total_s"], t_write_s=st2.get("t_write_s"),
                              clusters_written=pr["n_written"], cluster_files=nf2, cluster_file_bytes=nb2,
                              smolecule_bytes=smol, bytes_written=nb_all,
                              write_gbps=nb_all / st2["t_write_s"] / 1e9 if st2.get("t_write_s") else None,
-                             probe_files=probe_f, probe_smolecule=probe_s, probe_smolecule_mmap=probe_s_mmap,
-                             write_frac=fused_probe_s / st2["t_write_s"] if st2.get("t_write_s") else None),
-            disk_commit=disk,
+                             write_bound=bound_f,
+                             write_frac=bound_f["seconds"] / st2["t_write_s"] if st2.get("t_write_s") else None),
             note="page-cache-warm input; outputs on the box's local disk ($TMPDIR); every timed write (writers and "
-                 "probes) starts after an untimed sync; write_frac = seconds of the write probe (same files and bytes, "
-                 "same threads, no fsync, as the writers) / the writer's seconds; probe_smolecule_mmap = the one-file "
-                 "probe through a shared mapping instead of pwrite; disk_commit = a 2 GiB file written and fsync'd")
+                 "replays) starts after an untimed sync; write_bound = io_probe_replay of the writer's own files "
+                 "(sizes, contiguous thread split, the one streamed file) with no formatting; write_frac = "
+                 "write_bound seconds / the writer's seconds")
     finally:
         shutil.rmtree(d, ignore_errors=True)
 

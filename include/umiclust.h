@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 5
+#define UMICLUST_ABI_VERSION 6
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -181,9 +181,18 @@ int64_t umiclust_run_fasta_parse(umiclust_ctx *ctx, const umiclust_params *p, co
 
 /* ---- session API (in-memory, inputs resident in HBM) ---- */
 /* Stage n sequences (concatenated ASCII `seqs`, record i at [offsets[i], offsets[i+1])) into
- * device memory.  Length-filters, sorts and encodes on the device side of the boundary. */
+ * device memory, then prepare them (umiclust_prepare).  = umiclust_stage + umiclust_prepare. */
 int32_t umiclust_load(umiclust_ctx *ctx, const umiclust_params *p, const char *seqs,
                       const int64_t *offsets, int64_t n);
+/* The two halves of umiclust_load (ABI 6).  umiclust_stage copies the raw records into HBM (bin_start as in
+ * umiclust_load_bins; NULL = one bin) and keeps them resident.  umiclust_prepare does vsearch's load-time work on
+ * the staged records (the length filter, DUST soft-masking and the stable length sort that
+ * `vsearch --cluster_fast` runs before clustering; vsearch_umi_cluster.py:21-54 starts it): the length
+ * filter and sort on the host, DUST, 4-bit codes and unique 8-mers on the device.  It may be called again with
+ * other parameters (or the same, benchmarking: the headline times umiclust_prepare + umiclust_cluster). */
+int32_t umiclust_stage(umiclust_ctx *ctx, const char *seqs, const int64_t *offsets, int64_t n,
+                       const int64_t *bin_start, int32_t nbins);
+int32_t umiclust_prepare(umiclust_ctx *ctx, const umiclust_params *p);
 /* Run the hot path on the loaded sequences (prefilter, alignment, greedy, consensus).
  * Returns number of clusters. May be called repeatedly (benchmarking). */
 int64_t umiclust_cluster(umiclust_ctx *ctx, umiclust_stats *stats);
@@ -209,8 +218,8 @@ int64_t umiclust_cluster_bin(umiclust_ctx *ctx, int32_t bin, umiclust_stats *sta
 /* cluster the bins [first, first + nbins) of the load as one pack: the bins' queries in one greedy order (each bin
  * sorted on its own, the bins one after another), so small bins share the GPU passes of the bins around them.  Every
  * bin's result is exactly its own vsearch run's (tcr_consensus.py:231-245 runs one vsearch per bin); fetch each with
- * umiclust_fetch_bin.  Stats cover the whole pack; returns the pack's number of clusters.  Needs the sequential
- * policy (policy_threads = 0). */
+ * umiclust_fetch_bin.  Stats cover the whole pack; returns the pack's number of clusters.  Under the batched O4
+ * policy every bin's rounds are counted from its own first sorted query. */
 int64_t umiclust_cluster_pack(umiclust_ctx *ctx, int32_t first, int32_t nbins, umiclust_stats *stats);
 /* umiclust_fetch for one clustered bin: arrays over the bin's input records (bin-local index) */
 int64_t umiclust_fetch_bin(umiclust_ctx *ctx, int32_t bin, int32_t *cluster, uint8_t *strand,

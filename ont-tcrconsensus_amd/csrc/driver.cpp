@@ -324,6 +324,15 @@ struct umiclust_ctx {
   DevBuf<uint8_t> d_strong;       // [seqno * 2 + strand] prefilter's near-identical-peer flags (speculation)
   DevBuf<char> d_masked;
   DevBuf<int32_t> d_iota;
+  size_t iota_n = 0;               // d_iota holds 0 .. iota_n - 1
+  // staged raw records (umiclust_stage): ASCII + offsets in HBM (d_ascii, d_offs), lengths on the host
+  bool staged = false;
+  std::vector<uint32_t> rec_len;
+  PinBuf<int32_t> h_perm;          // the sorted order's pinned mirror (perm upload)
+  DevBuf<uint32_t> d_amb;
+  PinBuf<uint32_t> h_amb;
+  PinBuf<uint16_t> h_xm;
+  DevBuf<uint16_t> d_xm;
   // frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask; exact): the load's most frequent
   // + strand k-mers (>= defer_freq of the sampled sequences, at most kFKmers) and every (sequence, strand)'s mask
   // of them; UMICLUST_DEFER = the most k-mers a query-strand defers (default 0: off -- on config 2 deferring 2-4
@@ -2343,17 +2352,15 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
 
 // ---------------------------------------------------------------- load
 // bin_in: nbins + 1 input record boundaries (NULL: one bin of all n records)
-void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs, int64_t n,
-               const int64_t* bin_in = nullptr, int32_t nbins = 1) {
-  if (!p || (!seqs && n > 0) || !offs || n < 0 || nbins < 1) c->fail(UMICLUST_EINVAL, "null argument");
-  validate(c, *p);
+// Stage the raw records of a load in HBM (umiclust_stage): the ASCII bytes and record offsets, and the record lengths
+// and bin boundaries on the host.  Nothing of A3 (length filter, sort, DUST, k-mers) happens here: that is
+// prepare_impl's, from these resident records.
+void stage_impl(umiclust_ctx* c, const char* seqs, const int64_t* offs, int64_t n, const int64_t* bin_in = nullptr,
+                int32_t nbins = 1) {
+  if ((!seqs && n > 0) || !offs || n < 0 || nbins < 1) c->fail(UMICLUST_EINVAL, "null argument");
+  c->staged = false;
   c->loaded = false;
   c->clustered = false;
-  c->p = *p;
-  c->sc = to_scoring(*p);
-  c->both = p->strand_both ? 2 : 1;
-  c->o4_T = (p->policy_threads && p->threads > 1) ? p->threads : 0;
-  build_tables(c);
   c->n_input = n;
   c->bin_in.assign((size_t)nbins + 1, 0);
   if (bin_in) {
@@ -2364,31 +2371,66 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
   } else {
     c->bin_in[1] = n;
   }
+  c->rec_len.resize((size_t)n);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t L = offs[i + 1] - offs[i];
+    if (L < 0) c->fail(UMICLUST_EINVAL, "record offsets must not decrease");
+    c->rec_len[i] = (uint32_t)std::min<int64_t>(L, UINT32_MAX);
+  }
+  const int64_t bytes = n > 0 ? offs[n] - offs[0] : 0;
+  c->hip(c->d_ascii.ensure((size_t)bytes + 1), "alloc ascii");
+  c->hip(c->d_offs.ensure((size_t)n + 1), "alloc offs");
+  std::vector<int64_t> rel((size_t)n + 1);
+  for (int64_t i = 0; i <= n; i++) rel[i] = offs[i] - offs[0];
+  if (bytes > 0)
+    c->hip(hipMemcpyAsync(c->d_ascii.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipMemcpyAsync(c->d_offs.p, rel.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(hipStreamSynchronize(c->st), "sync stage");  // `rel` goes out of scope
+  c->staged = true;
+}
+
+// vsearch's load, length filter, DUST and length sort over the staged records
+// (umiclust_prepare): the stable counting sort by length on the host (perm, hlen: the host's resolve and writers
+// use them), then K1 k_prep on the device (DUST, 4-bit codes, unique 8-mers of both strands) from the resident
+// ASCII.  One stream synchronisation at the end.
+void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
+  if (!p) c->fail(UMICLUST_EINVAL, "null argument");
+  if (!c->staged) c->fail(UMICLUST_ESTATE, "umiclust_prepare before umiclust_stage");
+  validate(c, *p);
+  c->loaded = false;
+  c->clustered = false;
+  c->p = *p;
+  c->sc = to_scoring(*p);
+  c->both = p->strand_both ? 2 : 1;
+  c->o4_T = (p->policy_threads && p->threads > 1) ? p->threads : 0;
+  build_tables(c);
+  const int64_t n = c->n_input;
+  const int32_t nbins = (int32_t)c->bin_in.size() - 1;
+  const uint32_t* rl = c->rec_len.data();
   // length filter + stable sort by length desc within every bin (db_sortbylength; ties keep input
   // order, O1): one counting sort per bin, bins laid out one after another
   const int64_t maxlen = std::min<int64_t>(p->maxseqlength, kMaxLen);
-  for (int64_t i = 0; i < n; i++) {
-    const int64_t L = offs[i + 1] - offs[i];
-    if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
-  }
   int64_t kept = 0;
   for (int64_t i = 0; i < n; i++) {
-    const int64_t L = offs[i + 1] - offs[i];
+    const int64_t L = rl[i];
+    if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
     kept += (L >= p->minseqlength && L <= maxlen) ? 1 : 0;
   }
   if (kept > (int64_t)INT32_MAX / 2) c->fail(UMICLUST_ERANGE, "too many sequences in one load");
   c->n = (int32_t)kept;
-  c->perm.assign(c->n, 0);
+  const size_t ns = (size_t)c->n + 1;
+  c->hip(c->h_perm.ensure(ns), "pin perm");
   c->hlen.assign(c->n, 0);
   c->bin_s.assign((size_t)nbins + 1, 0);
   {
+    int32_t* perm = c->h_perm.p;
     std::vector<int64_t> cnt(kMaxLen + 2, 0);
     int64_t acc = 0;
     for (int32_t b = 0; b < nbins; b++) {
       c->bin_s[b] = (int32_t)acc;
       std::fill(cnt.begin(), cnt.end(), 0);
       for (int64_t i = c->bin_in[b]; i < c->bin_in[b + 1]; i++) {
-        const int64_t L = offs[i + 1] - offs[i];
+        const int64_t L = rl[i];
         if (L >= p->minseqlength && L <= maxlen) cnt[kMaxLen - L]++;
       }
       for (int L = 0; L <= kMaxLen; L++) {
@@ -2397,34 +2439,28 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
         acc += t;
       }
       for (int64_t i = c->bin_in[b]; i < c->bin_in[b + 1]; i++) {
-        const int64_t L = offs[i + 1] - offs[i];
+        const int64_t L = rl[i];
         if (L >= p->minseqlength && L <= maxlen) {
           const int64_t s = cnt[kMaxLen - L]++;
-          c->perm[s] = (int32_t)i;
+          perm[s] = (int32_t)i;
           c->hlen[s] = (uint8_t)L;
         }
       }
     }
     c->bin_s[nbins] = (int32_t)acc;
   }
+  for (int32_t s = 0; s < c->n; s++)
+    if (c->hlen[s] < kMinTplLen) c->fail(UMICLUST_ERANGE, "sequence shorter than %d (minseqlength)", kMinTplLen);
+  c->perm.assign(c->h_perm.p, c->h_perm.p + c->n);
   c->cno.assign(c->n, -1);
   c->strand.assign(c->n, 0);
   c->target.assign(c->n, -1);
   c->ocl.assign(c->n, -1);
   c->bout.assign(nbins, umiclust_ctx::BinOut());
   c->cur_bin = -1;
-  const int64_t bytes = n > 0 ? offs[n] - offs[0] : 0;
-  c->hip(c->d_ascii.ensure((size_t)bytes + 1), "alloc ascii");
-  c->hip(c->d_offs.ensure((size_t)n + 1), "alloc offs");
-  c->hip(c->d_perm.ensure((size_t)c->n + 1), "alloc perm");
-  std::vector<int64_t> rel((size_t)n + 1);
-  for (int64_t i = 0; i <= n; i++) rel[i] = offs[i] - offs[0];
-  if (bytes > 0)
-    c->hip(hipMemcpyAsync(c->d_ascii.p, seqs + offs[0], (size_t)bytes, hipMemcpyHostToDevice, c->st), "h2d");
-  c->hip(hipMemcpyAsync(c->d_offs.p, rel.data(), ((size_t)n + 1) * 8, hipMemcpyHostToDevice, c->st), "h2d");
+  c->hip(c->d_perm.ensure(ns), "alloc perm");
   if (c->n > 0)
-    c->hip(hipMemcpyAsync(c->d_perm.p, c->perm.data(), (size_t)c->n * 4, hipMemcpyHostToDevice, c->st), "h2d");
-  const size_t ns = (size_t)c->n + 1;
+    c->hip(hipMemcpyAsync(c->d_perm.p, c->h_perm.p, (size_t)c->n * 4, hipMemcpyHostToDevice, c->st), "h2d");
   c->hip(c->d_codes.ensure(ns * 2 * kCodeWords), "alloc");
   c->hip(c->d_lens.ensure(ns), "alloc");
   c->hip(c->d_kmers.ensure(ns * 2 * kKmerStride), "alloc");
@@ -2432,36 +2468,24 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
   c->hip(c->d_strong.ensure(ns * 2), "alloc");
   c->hip(hipMemsetAsync(c->d_strong.p, 0, ns * 2, c->st), "memset");
   c->hip(c->d_masked.ensure(ns * kMaxLen), "alloc");
-  c->hip(c->d_iota.ensure(ns), "alloc");
-  std::vector<int32_t> iota(ns);
-  for (size_t i = 0; i < ns; i++) iota[i] = (int32_t)i;
-  c->hip(hipMemcpyAsync(c->d_iota.p, iota.data(), ns * 4, hipMemcpyHostToDevice, c->st), "h2d");
-  DevBuf<uint32_t> d_amb;
-  c->hip(d_amb.ensure(1), "alloc");
-  c->hip(hipMemsetAsync(d_amb.p, 0, 4, c->st), "memset");
-  c->hip(launch_prep(c->d_ascii.p, c->d_offs.p, c->d_perm.p, c->n, p->qmask_dust, c->d_codes.p,
-                     c->d_lens.p, c->d_kmers.p, c->d_nk.p, c->d_masked.p, d_amb.p, c->st),
-         "prep");
-  uint32_t amb = 0;
-  c->hip(hipMemcpyAsync(&amb, d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
-  // frequent k-mers (the lean counting kernel's deferral): + strand counts over <= 2^18 sampled sequences
-  const int32_t stride = std::max<int32_t>(1, c->n >> 18);
-  std::vector<uint32_t> hist(kBins / kParts);
-  {
-    DevBuf<uint32_t> d_hist;
-    c->hip(d_hist.ensure(hist.size()), "alloc");
-    c->hip(hipMemsetAsync(d_hist.p, 0, hist.size() * 4, c->st), "memset");
-    c->hip(launch_kmer_hist(c->d_kmers.p, c->d_nk.p, c->n, stride, d_hist.p, c->st), "k-mer counts");
-    c->hip(hipMemcpyAsync(hist.data(), d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, c->st), "d2h");
-    c->hip(hipStreamSynchronize(c->st), "sync load");
+  if (c->iota_n < ns) {  // 0, 1, 2, ... (peer tiles index sequences by seqno); the same for every load
+    c->hip(c->d_iota.ensure(ns), "alloc");
+    c->hip(launch_iota(c->d_iota.p, (int32_t)ns, c->st), "iota");
+    c->iota_n = ns;
   }
-  c->ambig = amb != 0;
+  c->hip(c->d_amb.ensure(1), "alloc");
+  c->hip(c->h_amb.ensure(1), "pin");
+  c->hip(hipMemsetAsync(c->d_amb.p, 0, 4, c->st), "memset");
+  c->hip(launch_prep(c->d_ascii.p, c->d_offs.p, c->d_perm.p, c->n, p->qmask_dust, c->d_codes.p,
+                     c->d_lens.p, c->d_kmers.p, c->d_nk.p, c->d_masked.p, c->d_amb.p, c->st),
+         "prep");
+  c->hip(hipMemcpyAsync(c->h_amb.p, c->d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
   c->hqbin.clear();
   if (nbins > 1 && c->n > 0) {
     // packs: per-bin XOR masks on the k-mers (a bijection within a bin: counts within a bin are unchanged; other
     // bins' structured k-mers land on unrelated lists), sorted seqno -> bin, each bin's first seqno
     c->hqbin.resize(c->n);
-    std::vector<uint16_t> xm(nbins);
+    c->hip(c->h_xm.ensure((size_t)nbins), "pin");
     for (int32_t b = 0; b < nbins; b++) {
       for (int32_t s = c->bin_s[b]; s < c->bin_s[b + 1]; s++) c->hqbin[s] = b;
       uint32_t h = (uint32_t)b * 0x9E3779B1u + 0x7F4A7C15u;  // murmur3 finaliser
@@ -2470,22 +2494,32 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
       h ^= h >> 13;
       h *= 0xC2B2AE35u;
       h ^= h >> 16;
-      xm[b] = (uint16_t)(h ^ (h >> 16));
+      c->h_xm.p[b] = (uint16_t)(h ^ (h >> 16));
     }
     c->hip(c->d_qbin.ensure(c->n), "alloc");
     c->hip(c->d_bin_seq0.ensure(nbins), "alloc");
     c->hip(c->d_bin_ord0.ensure(nbins), "alloc");
     c->hip(c->h_bin_ord0.ensure(nbins), "pin");
-    DevBuf<uint16_t> d_xm;
-    c->hip(d_xm.ensure(nbins), "alloc");
+    c->hip(c->d_xm.ensure(nbins), "alloc");
     c->hip(hipMemcpyAsync(c->d_qbin.p, c->hqbin.data(), (size_t)c->n * 4, hipMemcpyHostToDevice, c->st), "h2d");
     c->hip(hipMemcpyAsync(c->d_bin_seq0.p, c->bin_s.data(), (size_t)nbins * 4, hipMemcpyHostToDevice, c->st), "h2d");
-    c->hip(hipMemcpyAsync(d_xm.p, xm.data(), (size_t)nbins * 2, hipMemcpyHostToDevice, c->st), "h2d");
-    c->hip(launch_kmer_xor(c->d_kmers.p, c->d_nk.p, c->n, c->d_qbin.p, d_xm.p, c->st), "k-mer masks");
-    c->hip(hipStreamSynchronize(c->st), "sync load");
+    c->hip(hipMemcpyAsync(c->d_xm.p, c->h_xm.p, (size_t)nbins * 2, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(launch_kmer_xor(c->d_kmers.p, c->d_nk.p, c->n, c->d_qbin.p, c->d_xm.p, c->st), "k-mer masks");
   }
-  {
-    const int64_t sampled = c->n > 0 ? ((int64_t)c->n + stride - 1) / stride : 0;
+  c->hip(c->d_fmask.ensure(ns * 2), "alloc");
+  c->nfk = 0;
+  if (c->defer_max > 0 && c->n > 0) {
+    // frequent k-mers (the lean counting kernel's deferral, UMICLUST_DEFER; off by default): + strand counts over
+    // <= 2^18 sampled sequences, after the per-bin XOR (the lut and the masks are in the k-mers' final space)
+    const int32_t stride = std::max<int32_t>(1, c->n >> 18);
+    std::vector<uint32_t> hist(kBins / kParts);
+    DevBuf<uint32_t> d_hist;
+    c->hip(d_hist.ensure(hist.size()), "alloc");
+    c->hip(hipMemsetAsync(d_hist.p, 0, hist.size() * 4, c->st), "memset");
+    c->hip(launch_kmer_hist(c->d_kmers.p, c->d_nk.p, c->n, stride, d_hist.p, c->st), "k-mer counts");
+    c->hip(hipMemcpyAsync(hist.data(), d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipStreamSynchronize(c->st), "sync load");
+    const int64_t sampled = ((int64_t)c->n + stride - 1) / stride;
     const double min_count = std::max(1.0, c->defer_freq * (double)sampled);
     std::vector<uint32_t> order;
     for (uint32_t k = 0; k < (uint32_t)hist.size(); k++)
@@ -2497,19 +2531,26 @@ void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, cons
       c->fkmer[i] = i < c->nfk ? (uint16_t)order[i] : 0;
       if (i < c->nfk) lut[order[i]] = (uint8_t)i;
     }
-    c->hip(c->d_fmask.ensure(ns * 2), "alloc");
-    if (c->nfk > 0 && c->n > 0) {
+    if (c->nfk > 0) {
       DevBuf<uint8_t> d_lut;
       c->hip(d_lut.ensure(lut.size()), "alloc");
       c->hip(hipMemcpyAsync(d_lut.p, lut.data(), lut.size(), hipMemcpyHostToDevice, c->st), "h2d");
       c->hip(launch_fmask(c->d_kmers.p, c->d_nk.p, c->n, d_lut.p, c->d_fmask.p, c->st), "k-mer masks");
-      c->hip(hipStreamSynchronize(c->st), "sync load");
+      c->hip(hipStreamSynchronize(c->st), "sync load");  // d_lut goes out of scope
     }
   }
-  for (int32_t s = 0; s < c->n; s++)
-    if (c->hlen[s] < kMinTplLen) c->fail(UMICLUST_ERANGE, "sequence shorter than %d (minseqlength)", kMinTplLen);
+  c->hip(hipStreamSynchronize(c->st), "sync load");
+  c->ambig = *c->h_amb.p != 0;
   c->loaded = true;
   c->clustered = false;
+}
+
+void load_impl(umiclust_ctx* c, const umiclust_params* p, const char* seqs, const int64_t* offs, int64_t n,
+               const int64_t* bin_in = nullptr, int32_t nbins = 1) {
+  if (!p) c->fail(UMICLUST_EINVAL, "null argument");
+  validate(c, *p);
+  stage_impl(c, seqs, offs, n, bin_in, nbins);
+  prepare_impl(c, p);
 }
 
 int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in_fasta,
@@ -2821,6 +2862,21 @@ int64_t umiclust_fetch_bin(umiclust_ctx* c, int32_t bin, int32_t* cluster, uint8
       memcpy(cons, bo.cons.data(), bo.cons.size());
     }
     return K;
+  });
+}
+
+int32_t umiclust_stage(umiclust_ctx* c, const char* seqs, const int64_t* offs, int64_t n, const int64_t* bin_start,
+                       int32_t nbins) {
+  UC_GUARD(c, {
+    stage_impl(c, seqs, offs, n, bin_start, bin_start ? nbins : 1);
+    return UMICLUST_OK;
+  });
+}
+
+int32_t umiclust_prepare(umiclust_ctx* c, const umiclust_params* p) {
+  UC_GUARD(c, {
+    prepare_impl(c, p);
+    return UMICLUST_OK;
   });
 }
 

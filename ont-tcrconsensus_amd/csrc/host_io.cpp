@@ -359,12 +359,17 @@ bool split1(Sv s, const char* sep, Sv& out) {
 
 static void split_fields(Sv name, std::vector<Sv>& f) {  // name.split(";")
   f.clear();
-  size_t st = 0;
-  for (size_t i = 0; i <= name.n; i++)
-    if (i == name.n || name.p[i] == ';') {
-      f.push_back(Sv{name.p + st, i - st});
-      st = i + 1;
+  const char* p = name.p;
+  const char* const e = name.p + name.n;
+  for (;;) {  // memchr: the headers are ~1.6 KB, nearly all of it the last field's read
+    const char* q = (const char*)memchr(p, ';', (size_t)(e - p));
+    if (!q) {
+      f.push_back(Sv{p, (size_t)(e - p)});
+      return;
     }
+    f.push_back(Sv{p, (size_t)(q - p)});
+    p = q + 1;
+  }
 }
 
 // ---------------------------------------------------------------- vsearch writers (--consout, --clusters)
@@ -454,11 +459,18 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     std::vector<std::pair<Sv, int32_t>> kept[2];  // insertion-ordered dict read id -> record (:61-65)
     std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position)
   };
+  // an entry written: its read id (`cols[0]`) and read (`cols[6].split("seq=")[1]`), kept from the analysis so the
+  // write phase never splits a header again
+  struct Ent {
+    const char* rid;
+    const char* read;
+    uint32_t rid_n, read_n;
+  };
   auto entry = [&](const PClus& r, const Scratch& sc, int64_t y) -> int32_t {
     return (y < r.w_fwd ? sc.kept[0][y] : sc.kept[1][y - r.w_fwd]).second;
   };
-  // one cluster's counts (and its kept records in sc.kept); false on the first error
-  auto analyze = [&](int32_t k, PClus& r, Scratch& sc) -> bool {
+  // one cluster's counts (and the entries it writes, appended to ents); false on the first error
+  auto analyze = [&](int32_t k, PClus& r, Scratch& sc, std::vector<Ent>& ents) -> bool {
     sc.kept[0].clear();
     sc.kept[1].clear();
     sc.index.clear();
@@ -541,10 +553,11 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
         Sv read;
         if (!split1(sc.fields[6], "seq=", read)) {
           r.err = UMICLUST_EFORMAT;
-          r.noseq_at = y;
+          r.noseq_at = y;  // the entries before it are written (and kept in ents)
           r.msg = "IndexError: no seq= field in " + Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}.str();
           return false;
         }
+        ents.push_back(Ent{sc.fields[0].p, read.p, (uint32_t)sc.fields[0].n, (uint32_t)read.n});
         r.smol_bytes += head + (int64_t)read.n;
       }
     }
@@ -553,9 +566,17 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   const int T = K < 256 ? 1 : io_threads();
   const std::vector<int32_t> cut = cluster_slices(cv.ostart, K, T);
   std::vector<PClus> res((size_t)K);
+  std::vector<std::vector<Ent>> ents_t((size_t)T);
+  std::vector<int64_t> ent_beg((size_t)K + 1, 0);  // cluster k's entries: ents_t[thread of k][ent_beg[k] ..)
+  std::vector<int32_t> ent_thr((size_t)K, 0);
   parallel_for(T, [&](int t) {
     Scratch sc;
-    for (int32_t k = cut[t]; k < cut[t + 1]; k++) analyze(k, res[k], sc);
+    std::vector<Ent>& ents = ents_t[(size_t)t];
+    for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
+      ent_beg[k] = (int64_t)ents.size();
+      ent_thr[k] = t;
+      analyze(k, res[k], sc, ents);
+    }
   });
   // the reference's loop in order: its first error, its early exit
   int64_t n_written = 0, reads_found = 0, reads_written = 0;
@@ -576,28 +597,16 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       break;
     }
   }
-  // a missing seq= field interrupts cluster kerr after its first noseq_at entries: written like the others
+  // a missing seq= field interrupts cluster kerr after its first noseq_at entries: written like the others (its
+  // smol_bytes and entries stop before the failing one)
   const bool partial = kerr >= 0 && res[kerr].noseq_at >= 0;
   const int32_t kwrite = partial ? kerr + 1 : kend;
-  if (partial) {  // the bytes of its first noseq_at entries (analyze stopped counting at the failing one)
-    const int64_t head = 3 + (int64_t)std::to_string(kerr).size();
-    PClus r;
-    Scratch sc;
-    analyze(kerr, r, sc);
-    res[kerr].smol_bytes = 0;
-    for (int64_t y = 0; y < res[kerr].noseq_at; y++) {
-      const int32_t i = entry(r, sc, y);
-      split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
-      Sv read;
-      split1(sc.fields[6], "seq=", read);
-      res[kerr].smol_bytes += head + (int64_t)read.n;
-    }
-  }
   // smolecule_clusters.fa: every read written once more (GBs at production depth).  Its records are laid out
-  // by cluster in advance (offsets from the counts above), and each writing thread pwrites its clusters' records
-  // at their offset as soon as its range is done, beside the other threads' cluster files.  (A shared mapping of
-  // the file was measured 5x slower than pwrite on the GPU box's filesystem: 2.2 vs 10.4 GB/s,
-  // profiles/r03/e2e_probes.json.)
+  // by cluster in advance (offsets from the counts above); each writing thread streams its clusters' records to
+  // their offsets in chunks of kSmolChunk bytes while it creates its cluster files, so the one file's writes (which
+  // serialise on its inode) overlap the other threads' file creation.  (A shared mapping of the file was measured
+  // 5x slower than pwrite on the GPU box's filesystem: 2.2 vs 10.4 GB/s, profiles/r03/e2e_probes.json.)
+  constexpr size_t kSmolChunk = 8u << 20;
   std::vector<int64_t> smol_off((size_t)kwrite + 1, 0);
   for (int32_t k = 0; k < kwrite; k++) smol_off[k + 1] = smol_off[k] + res[k].smol_bytes;
   const std::string smol_path = pjoin(work_dir, "smolecule_clusters.fa");
@@ -610,8 +619,8 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   std::vector<int32_t> bad(T, -1);
   std::vector<uint8_t> wrote((size_t)kwrite, 0), smol_bad(T, 0);
   parallel_for(T, [&](int t) {
-    Scratch sc;
     std::string lines, smol, &log = log_p[t], &stats_out = stats_p[t];
+    smol.reserve(kSmolChunk + (1u << 16));
     // this thread's records, contiguous in the file from its first cluster's offset (also on an early return:
     // the clusters before a failing one keep their records, as the reference's buffered file does)
     struct Flush {
@@ -619,41 +628,45 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       int fd;
       off_t at;
       uint8_t& bad;
-      ~Flush() {
+      void run() {
         size_t o = 0;
         while (o < s.size()) {
           const ssize_t w = pwrite(fd, s.data() + o, s.size() - o, at + (off_t)o);
           if (w < 0) {
             if (errno == EINTR) continue;
             bad = 1;
-            return;
+            break;
           }
           o += (size_t)w;
         }
+        at += (off_t)s.size();
+        s.clear();
       }
+      ~Flush() { run(); }
     } flush{smol, smol_fd, (off_t)smol_off[wcut[t]], smol_bad[t]};
+    std::string fname;
     for (int32_t k = wcut[t]; k < wcut[t + 1]; k++) {
       stats_beg[k] = stats_out.size();
-      PClus r;
-      analyze(k, r, sc);
-      const int64_t nw = (partial && k == kerr) ? res[k].noseq_at : r.w_all;
-      const std::string out_fasta = pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta");  // :34
+      const PClus& r = res[k];
+      const int64_t nw = (partial && k == kerr) ? r.noseq_at : r.w_all;
+      const std::string kstr = std::to_string(k);
+      fname = "cluster" + kstr + ".fasta";
+      const std::string out_fasta = pjoin(fa_dir, fname);  // :34
       log += "Cluster: " + out_fasta + " has " + std::to_string(r.n_fwd) + "/" + std::to_string(r.max_fwd) +
              " fwd and " + std::to_string(r.n_rev) + "/" + std::to_string(r.max_rev) + " rev reads\n";
       if (r.written) {
         lines.clear();
+        const Ent* e = ents_t[(size_t)ent_thr[k]].data() + ent_beg[k];
         for (int64_t y = 0; y < nw; y++) {
-          const int32_t i = entry(r, sc, y);
-          split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
-          Sv read;
-          split1(sc.fields[6], "seq=", read);
           lines.push_back('>');
-          lines.append(sc.fields[0].p, sc.fields[0].n);
+          lines.append(e[y].rid, e[y].rid_n);
           lines.push_back('\n');
-          lines.append(read.p, read.n);
+          lines.append(e[y].read, e[y].read_n);
           lines.push_back('\n');
-          smol += ">" + std::to_string(k) + "\n";
-          smol.append(read.p, read.n);
+          smol.push_back('>');
+          smol += kstr;
+          smol.push_back('\n');
+          smol.append(e[y].read, e[y].read_n);
           smol.push_back('\n');
         }
         if (!write_file(out_fasta, lines)) {
@@ -661,13 +674,14 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
           return;
         }
         wrote[k] = 1;
+        if (smol.size() >= kSmolChunk) flush.run();
       } else {
-        log += "Cluster " + std::to_string(k) + " skipped\n";
+        log += "Cluster " + kstr + " skipped\n";
       }
       if (partial && k == kerr) break;  // the exception: no log or stats line for it
       log += "Cluster: " + out_fasta + " has " + std::to_string(r.w_all) + " reads written: " + std::to_string(r.w_fwd) +
              " fwd - " + std::to_string(r.w_rev) + " rev\n";
-      stats_out += "cluster" + std::to_string(k) + "\t" + std::to_string(r.n_fwd) + "\t" + std::to_string(r.n_rev) +
+      stats_out += "cluster" + kstr + "\t" + std::to_string(r.n_fwd) + "\t" + std::to_string(r.n_rev) +
                    "\t" + std::to_string(r.w_fwd) + "\t" + std::to_string(r.w_rev) + "\t" + std::to_string(r.found) +
                    "\t" + std::to_string(r.w_all) + "\t" + std::to_string(r.written) + "\n";
     }

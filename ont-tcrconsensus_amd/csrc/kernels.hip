@@ -227,6 +227,17 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ 
   }
 }
 
+__global__ __launch_bounds__(256) void k_iota(int32_t* __restrict__ out, int32_t n) {
+  const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+  if (i < n) out[i] = i;
+}
+
+hipError_t launch_iota(int32_t* out, int32_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
                        char* masked, uint32_t* ambig, hipStream_t st) {

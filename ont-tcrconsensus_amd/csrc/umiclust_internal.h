@@ -74,6 +74,7 @@ struct DevSeqs {
 };
 
 // ---- kernel launchers (kernels.hip) ----
+hipError_t launch_iota(int32_t* out, int32_t n, hipStream_t st);
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
                        char* masked, uint32_t* ambig, hipStream_t st);

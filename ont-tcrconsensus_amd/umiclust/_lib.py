@@ -107,7 +107,7 @@ class ParseResult(C.Structure):
 EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
-    "umiclust_load", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
+    "umiclust_load", "umiclust_stage", "umiclust_prepare", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
     "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
 ]
@@ -147,6 +147,10 @@ def lib() -> C.CDLL:
     L.umiclust_run_argv.argtypes = [C.c_void_p, C.c_int32, P(C.c_char_p), P(Stats)]
     L.umiclust_load.restype = C.c_int32
     L.umiclust_load.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_int64]
+    L.umiclust_stage.restype = C.c_int32
+    L.umiclust_stage.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64), C.c_int32]
+    L.umiclust_prepare.restype = C.c_int32
+    L.umiclust_prepare.argtypes = [C.c_void_p, P(Params)]
     L.umiclust_cluster.restype = C.c_int64
     L.umiclust_cluster.argtypes = [C.c_void_p, P(Stats)]
     L.umiclust_fetch.restype = C.c_int64
@@ -287,6 +291,19 @@ class Context:
         self._check(lib().umiclust_load(self._h, C.byref(p), buf.ctypes.data, _i64(off), n), "load")
         self._n = n
         self._bins = None
+
+    def stage(self, buf: np.ndarray, off: np.ndarray, bin_start=None) -> None:
+        """umiclust_stage: the raw records into HBM (one bin, or bins [bin_start[b], bin_start[b+1]))."""
+        n = len(off) - 1
+        bs = None if bin_start is None else np.ascontiguousarray(bin_start, np.int64)
+        self._check(lib().umiclust_stage(self._h, buf.ctypes.data, _i64(off), n, None if bs is None else _i64(bs),
+                                         0 if bs is None else len(bs) - 1), "stage")
+        self._n = n
+        self._bins = bs
+
+    def prepare(self, p: Params) -> None:
+        """umiclust_prepare: length filter, sort, DUST, codes and k-mers of the staged records."""
+        self._check(lib().umiclust_prepare(self._h, C.byref(p)), "prepare")
 
     def cluster(self) -> dict:
         st = Stats()

@@ -40,6 +40,16 @@ def cluster_sizes(res: dict) -> np.ndarray:
     return np.bincount(cl[cl >= 0], minlength=int(res["n_clusters"]))
 
 
+class RunStats(list):
+    """BinRunner.cluster_all's result: the stats of every call unit (bins clustered alone, then packs).  per_bin[b] is
+    bin b's stats or None (clustered in a pack); packs lists the packs' stats, each with its "bins"."""
+
+    def __init__(self, units, per_bin, packs):
+        super().__init__(units)
+        self.per_bin = per_bin
+        self.packs = packs
+
+
 class BinRunner:
     """One rank's bins of one round, resident on one device.
 
@@ -70,7 +80,20 @@ class BinRunner:
                 self.plan = [idx]
             for j, b in enumerate(idx):
                 self.where[b] = (lane, j)
-            self.ctxs[lane].load_bins(self.params, sub.seq, sub.off, sub.bin_start)
+            self.ctxs[lane].stage(sub.seq, sub.off, sub.bin_start)
+        self.prepare()
+
+    def _each_lane(self, fn) -> list:
+        if len(self.ctxs) == 1:
+            return [fn(0)]
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(len(self.ctxs)) as ex:
+            return list(ex.map(fn, range(len(self.ctxs))))
+
+    def prepare(self) -> None:
+        """umiclust_prepare on every lane: vsearch's load-time work (length filter, DUST, sort, k-mers) of the staged
+        bins (bench.py times it inside each step)."""
+        self._each_lane(lambda lane: self.ctxs[lane].prepare(self.params))
 
     @property
     def nbins(self) -> int:
@@ -91,8 +114,11 @@ class BinRunner:
             j = k
         return out
 
-    def cluster_all(self) -> list:
-        """Cluster every bin; stats per bin in bin order (per pack with packing: in lane order)."""
+    def cluster_all(self) -> "RunStats":
+        """Cluster every bin.  Returns the stats of every call unit -- each bin clustered alone, then each pack (stats
+        cover the pack's bins together) -- as a RunStats list, so sums over it are totals; `.per_bin[b]` holds bin b's
+        own stats (None for a bin clustered inside a pack) and `.packs` the packs' (with their bins).  The list is NOT
+        indexed by bin."""
         out = [None] * self.nbins
         packed = [[] for _ in self.ctxs]
 
@@ -101,15 +127,13 @@ class BinRunner:
                 if m == 1:
                     out[self.plan[lane][j]] = self.ctxs[lane].cluster_bin(j)
                 else:
-                    packed[lane].append(self.ctxs[lane].cluster_pack(j, m))
+                    st = self.ctxs[lane].cluster_pack(j, m)
+                    st["bins"] = [self.plan[lane][x] for x in range(j, j + m)]
+                    packed[lane].append(st)
 
-        if len(self.ctxs) == 1:
-            run(0)
-        else:
-            import concurrent.futures as cf
-            with cf.ThreadPoolExecutor(len(self.ctxs)) as ex:
-                list(ex.map(run, range(len(self.ctxs))))
-        return [x for x in out if x is not None] + [x for p in packed for x in p]
+        self._each_lane(run)
+        packs = [x for p in packed for x in p]
+        return RunStats([x for x in out if x is not None] + packs, out, packs)
 
     def results(self) -> list:
         return [self.ctxs[self.where[b][0]].fetch_bin(self.where[b][1]) for b in range(self.nbins)]

@@ -639,3 +639,31 @@ def test_load_bins_edge_cases(gpu_ctx):
         want = orc.cluster(op, g) if g else dict(n_clusters=0, cluster=np.zeros(0, np.int32), strand=np.zeros(0, np.uint8),
                                                 centroid=np.zeros(0, np.uint8), consensus=[])
         _cmp_cluster(got, want)
+
+
+def test_stage_prepare_equals_load():
+    """umiclust_stage + umiclust_prepare (ABI 6; bench.py times prepare + cluster per step) equal umiclust_load:
+    preparing the same staged records again, or with other parameters, gives the oracle's result each time; a
+    multi-bin staging prepares every bin."""
+    seqs = synth.make_umis(300, seed=77, max_reads=6000, error_rate=0.03, orient_mix=0.2).as_list()
+    seqs += ["ACGT" * 5, "T" * 80]  # length-filtered at either end
+    buf, off = _lib._pack(seqs)
+    with _lib.Context(0) as ctx:
+        ctx.stage(buf, off)
+        for idn, lens in [(0.93, (58, 68)), (0.93, (58, 68)), (0.97, (60, 68))]:
+            p = _lib.params(1, idn, *lens)
+            ctx.prepare(p)
+            st = ctx.cluster()
+            o = orc.cluster(orc.params(1, idn, *lens), seqs)
+            _cmp_cluster(ctx.fetch(), o)
+            assert st["n_alignments"] == o["stats"]["alignments"] and st["n_kept"] == o["stats"]["kept"]
+        starts = [0, 2000, 2000, len(seqs)]
+        ctx.stage(buf, off, starts)
+        ctx.prepare(_lib.params(1, 0.93, 58, 68))
+        for b in range(3):
+            ctx.cluster_bin(b)
+            g = seqs[starts[b]:starts[b + 1]]
+            if g:
+                _cmp_cluster(ctx.fetch_bin(b), orc.cluster(orc.params(1, 0.93, 58, 68), g))
+    with _lib.Context(0) as ctx, pytest.raises(_lib.UmiclustError):
+        ctx.prepare(_lib.params(1, 0.93, 58, 68))  # nothing staged

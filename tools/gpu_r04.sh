@@ -1,0 +1,72 @@
+#!/bin/bash
+# Round-4 GPU session: parity tests, the default bench line (config 2 + e2e), PMC calibration and the
+# k_pf_count busy pass, kernel trace.  Every GPU step has its own time limit; the first failure ends the call.
+# Usage: bash tools/gpu_r04.sh <tag> <steps...>   steps: tests | solo | bench | defer (DEFERS="0 3") | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5 | c5trace
+set -o pipefail
+tag=${1:-r04}
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
+SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT"
+SQ2="SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"
+rc=0
+for st in "$@"; do
+  echo "== $st $(date +%T)"
+  case $st in
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             > "$out/tests.log" 2>&1; rc=$?; tail -3 "$out/tests.log" ;;
+    bench) timeout -k 10 600 python3 -u bench.py --steps 5 --warmup 1 > "$out/bench.json" 2> "$out/bench.err"; rc=$? ;;
+    calib) timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d "$out/calib" -o run -- tools/pmc_calib \
+             > "$out/calib.log" 2>&1; rc=$? ;;
+    busy) timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d "$out/busy" -o run -- python3 $B \
+             > "$out/busy.log" 2>&1; rc=$? ;;
+    busy2) timeout -s KILL 300 rocprofv3 --pmc $SQ2 --output-format csv -d "$out/busy2" -o run -- python3 $B \
+             > "$out/busy2.log" 2>&1; rc=$? ;;
+    fetch) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B \
+             > "$out/fetch.log" 2>&1; rc=$? ;;
+    write) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B \
+             > "$out/write.log" 2>&1; rc=$? ;;
+    pfprof) UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof.json" 2> "$out/pfprof.err"; rc=$? ;;
+    pfab) for cm in 0 1; do
+            UMICLUST_PFCOUNT=$cm timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+              > "$out/pfab$cm.json" 2> "$out/pfab$cm.err" || { rc=$?; break; }
+            UMICLUST_PFCOUNT=$cm UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof$cm.json" \
+              2> "$out/pfprof$cm.err" || { rc=$?; break; }
+          done ;;
+    defer) for dm in ${DEFERS:-0 3}; do
+            UMICLUST_DEFER=$dm timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+              > "$out/defer$dm.json" 2> "$out/defer$dm.err" || { rc=$?; break; }
+          done ;;
+    solo) # PMC collection serialises the dispatches: the kernel trace of this run holds every kernel's solo duration
+          timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv -d "$out/solo" -o run -- \
+             python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/solo.log" 2>&1; rc=$?
+          rm -f "$out/solo/run_kernel_trace.csv" "$out/solo/run_counter_collection.csv" ;;
+    trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
+             python3 $B > "$out/trace.log" 2>&1; rc=$? ;;
+    c3) timeout -k 10 500 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
+    c3trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c3trace" -o run -- \
+             python3 bench.py --config 3 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c3trace.log" 2>&1; rc=$?
+             rm -f "$out/c3trace/run_kernel_trace.csv" ;;  # ~10^5 dispatches: the stats file is what is kept
+    envab) # ENVAB="NAME1=a,NAME2=b;NAME1=c" CFG=3: one bench line per env set (2 steps, 1 warmup)
+          i=0; IFS=';' read -ra sets <<< "$ENVAB"
+          for es in "${sets[@]}"; do
+            i=$((i+1)); IFS=',' read -ra kv <<< "$es"
+            env "${kv[@]}" timeout -k 10 500 python3 -u bench.py --config ${CFG:-3} --steps 2 --warmup 1 --no-cpu-baseline \
+              --no-e2e $EXTRA > "$out/envab$i.json" 2> "$out/envab$i.err" || { rc=$?; break; }
+            echo "$es" > "$out/envab$i.env"
+          done ;;
+    c5trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c5trace" -o run -- \
+             python3 bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c5trace.log" 2>&1; rc=$?
+             rm -f "$out/c5trace/run_kernel_trace.csv" ;;
+    c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
+    c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
+    *) echo "unknown step $st"; rc=2 ;;
+  esac
+  echo "== $st rc=$rc $(date +%T)"
+  [ $rc -ne 0 ] && break
+done
+du -sh "$out"
+for f in "$out"/*.json; do [ -f "$f" ] && { echo "--- $f"; cut -c1-400 "$f"; }; done
+exit $rc

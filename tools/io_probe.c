@@ -197,3 +197,113 @@ double io_probe_mmap(const char *dir, int64_t total, int threads) {
   free(buf);
   return err ? -1.0 : dt;
 }
+
+/* io_probe_replay: the writers' own system-call sequence with no formatting -- the bound a writer cannot beat on
+ * the same filesystem.  nfiles files named <dir>/cluster<i>.fasta of the given sizes, split over `threads` threads
+ * in contiguous ranges of about equal bytes (the writers' cluster_slices), each file one open / write / close from a
+ * prepared buffer; with one_bytes > 0 one more file <dir>/one is written beside them as the fused writer writes
+ * smolecule_clusters.fa: pre-created, every thread pwrite-ing its share (proportional to its files' bytes) at its
+ * offset in chunks of 8 MiB as its files accumulate it.  Returns seconds (files removed afterwards, untimed). */
+typedef struct {
+  const char *dir;
+  const int64_t *sizes;
+  int64_t f0, f1;          /* files [f0, f1) */
+  int one_fd;
+  int64_t one_at, one_n;   /* this thread's slice of the one file */
+  int64_t files_bytes;     /* bytes of its files (the slice is streamed in proportion) */
+  const char *buf;
+  int64_t bufsz;
+  int err;
+} rjob_t;
+
+static void *replay_worker(void *arg) {
+  rjob_t *j = (rjob_t *)arg;
+  char path[4096];
+  const int64_t chunk = 8 << 20;
+  int64_t done = 0, sent = 0;
+  for (int64_t i = j->f0; i < j->f1 && !j->err; i++) {
+    snprintf(path, sizeof path, "%s/cluster%lld.fasta", j->dir, (long long)i);
+    int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (fd < 0) { j->err = errno; break; }
+    int64_t left = j->sizes[i];
+    while (left > 0 && !j->err) {
+      int64_t n = left < j->bufsz ? left : j->bufsz;
+      if (write_all(fd, j->buf, n, 0, 0)) j->err = errno;
+      left -= n;
+    }
+    if (close(fd)) j->err = errno;
+    done += j->sizes[i];
+    if (j->one_fd >= 0 && j->one_n > 0) {
+      const int64_t due = j->files_bytes > 0 ? (int64_t)((double)j->one_n * (double)done / (double)j->files_bytes) : j->one_n;
+      while (due - sent >= chunk && !j->err) {
+        int64_t n = chunk;
+        for (int64_t o = 0; o < n && !j->err; o += j->bufsz) {
+          int64_t m = n - o < j->bufsz ? n - o : j->bufsz;
+          if (write_all(j->one_fd, j->buf, m, j->one_at + sent + o, 1)) j->err = errno;
+        }
+        sent += n;
+      }
+    }
+  }
+  while (j->one_fd >= 0 && sent < j->one_n && !j->err) {
+    int64_t m = j->one_n - sent < j->bufsz ? j->one_n - sent : j->bufsz;
+    if (write_all(j->one_fd, j->buf, m, j->one_at + sent, 1)) j->err = errno;
+    sent += m;
+  }
+  return NULL;
+}
+
+double io_probe_replay(const char *dir, int64_t nfiles, const int64_t *sizes, int threads, int64_t one_bytes) {
+  if (!dir || nfiles < 0 || (nfiles > 0 && !sizes) || threads < 1 || one_bytes < 0) return -1.0;
+  int64_t maxsz = 1 << 20, tot = 0;
+  for (int64_t i = 0; i < nfiles; i++) {
+    tot += sizes[i];
+    if (sizes[i] > maxsz) maxsz = sizes[i];
+  }
+  const int64_t bufsz = maxsz < (8 << 20) ? maxsz : (8 << 20);
+  char *buf = (char *)malloc((size_t)bufsz);
+  if (!buf) return -1.0;
+  for (int64_t i = 0; i < bufsz; i++) buf[i] = "ACGT\n"[i % 5];
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  rjob_t *jobs = (rjob_t *)calloc((size_t)threads, sizeof(rjob_t));
+  char path[4096];
+  snprintf(path, sizeof path, "%s/one", dir);
+  const double t0 = now_s();
+  int one_fd = -1, err = 0;
+  if (one_bytes > 0) {
+    one_fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (one_fd < 0) err = errno;
+  }
+  int64_t f = 0, acc = 0, one_at = 0;
+  for (int t = 0; t < threads; t++) {
+    const int64_t want = tot * (t + 1) / threads;
+    const int64_t f0 = f;
+    int64_t fb = 0;
+    while (f < nfiles && (t == threads - 1 || acc < want)) {
+      acc += sizes[f];
+      fb += sizes[f];
+      f++;
+    }
+    const int64_t share = tot > 0 ? (int64_t)((double)one_bytes * (double)acc / (double)tot) - one_at
+                                  : (t == threads - 1 ? one_bytes : 0);
+    jobs[t] = (rjob_t){dir, sizes, f0, f, one_fd, one_at, t == threads - 1 ? one_bytes - one_at : share, fb, buf, bufsz, 0};
+    one_at += jobs[t].one_n;
+  }
+  for (int t = 0; t < threads && !err; t++) pthread_create(&th[t], NULL, replay_worker, &jobs[t]);
+  for (int t = 0; t < threads && !err; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].err) err = jobs[t].err;
+  }
+  if (one_fd >= 0 && close(one_fd)) err = errno;
+  const double dt = now_s() - t0;
+  for (int64_t i = 0; i < nfiles; i++) {
+    char p2[4096];
+    snprintf(p2, sizeof p2, "%s/cluster%lld.fasta", dir, (long long)i);
+    unlink(p2);
+  }
+  if (one_bytes > 0) unlink(path);
+  free(jobs);
+  free(th);
+  free(buf);
+  return err ? -1.0 : dt;
+}
