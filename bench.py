@@ -237,6 +237,14 @@ def main() -> None:
     ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "100000")),
                     help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack; "
                          "0: one bin per call; 100k measured best on config 3: profiles/r03/pack_ab.json)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="configs 3/4, one GPU: cluster only the LPT share --shard of a --shard-of-GPU node (the bins that "
+                         "rank would get); timing every share this way bounds the node's makespan")
+    ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--largest-bin", action="store_true", help="configs 3/4: the largest bin alone")
+    ap.add_argument("--shard-sweep", type=int, default=0,
+                    help="configs 3/4, one GPU: time every LPT share of an N-GPU node one after another (plus the largest "
+                         "bin alone) in one process; the largest share time is the measured N-GPU makespan bound")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -256,13 +264,23 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     from umiclust import _lib, binset, shard, synth
+    if args.shard_sweep:
+        return shard_sweep(args)
     # multi-bin inputs are generated before anything touches the GPU (spawned workers)
     bins = None
     if args.config in (3, 4):
         all_bins = synth.config_bins(args.config, args.scale, workers=min(16, os.cpu_count() or 4))
         costs = [shard.bin_cost(b.umis.n) for b in all_bins]
-        plan = shard.lpt_assign(costs, world)
-        bins = synth.concat_bins([all_bins[i] for i in plan[rank]])
+        if args.largest_bin:
+            sel = [max(range(len(costs)), key=lambda i: (costs[i], -i))]
+        elif args.shard_of > 0:
+            if world != 1 or not 0 <= args.shard < args.shard_of:
+                raise SystemExit("--shard-of N --shard R: one process, 0 <= R < N")
+            sel = shard.lpt_assign(costs, args.shard_of)[args.shard]
+        else:
+            sel = shard.lpt_assign(costs, world)[rank]
+        bins = synth.concat_bins([all_bins[i] for i in sel])
+        share_cost = sum(costs[i] for i in sel) / max(1e-9, sum(costs))
     import torch
     dist = None
     if world > 1:
@@ -384,7 +402,12 @@ def main() -> None:
                        clusters=int(last[0]["n_clusters"]))
         else:
             cfg.update(bins_rank0=sum(r.nbins for r in runners), reads_rank0=int(sum(r.binset.n for r in runners)),
-                       umis_kept_rank0=int(my_umis), clusters_rank0=int(sum(s["n_clusters"] for s in last)))
+                       umis_kept_rank0=int(my_umis), clusters_rank0=int(sum(s["n_clusters"] for s in last)),
+                       cost_share=share_cost)
+            if args.largest_bin:
+                cfg["selection"] = "the largest bin alone"
+            elif args.shard_of > 0:
+                cfg["selection"] = f"LPT share {args.shard} of {args.shard_of} (the bins rank {args.shard} of a {args.shard_of}-GPU run clusters)"
         out = {
             "metric": METRIC, "value": value, "unit": "UMIs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
@@ -430,6 +453,72 @@ def main() -> None:
         ctx2.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def shard_sweep(args) -> None:
+    """8-GPU readiness measured on one GPU (configs 3/4): the node's bins are LPT-assigned to N ranks exactly as a
+    `--gpus N` run assigns them (shard.lpt_assign), and each rank's share is clustered alone on this GPU, one after
+    another, each timed over one full step (stage untimed; prepare + cluster of every round timed), after an untimed
+    warm-up of the first share.  The largest share time is the makespan bound of an N-GPU node (each rank runs its
+    share on its own GPU, no collective); the largest bin alone bounds any split of the bins."""
+    import torch
+    from umiclust import _lib, binset, shard, synth
+    if args.config not in (3, 4):
+        raise SystemExit("--shard-sweep: configs 3 and 4")
+    N = args.shard_sweep
+    ident = args.identity if args.identity is not None else 0.93
+    lens = synth.CONFIG_LENGTHS[args.config]
+    all_bins = synth.config_bins(args.config, args.scale, workers=min(16, os.cpu_count() or 4))
+    costs = [shard.bin_cost(b.umis.n) for b in all_bins]
+    plan = shard.lpt_assign(costs, N)
+    largest = max(range(len(costs)), key=lambda i: (costs[i], -i))
+    torch.cuda.set_device(0)
+    ctx = _lib.Context(0)
+    ctx2 = _lib.Context(0) if args.config == 4 else None
+
+    def run(sel):
+        bins = synth.concat_bins([all_bins[i] for i in sel])
+        r1 = binset.BinRunner(ctx, bins, _lib.PRESET_ROUND1, ident, *lens, lanes=args.lanes, pack_reads=args.pack_reads)
+        runners = [r1]
+        if args.config == 4:
+            r1.cluster_all()
+            b2 = binset.round2_binset(bins, r1.results())
+            runners.append(binset.BinRunner(ctx2, b2, binset.ROUND2["preset"], binset.ROUND2["identity"], *lens,
+                                            lanes=args.lanes, pack_reads=args.pack_reads))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = []
+        for r in runners:
+            r.prepare()
+            st += r.cluster_all()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        kept = sum(x["n_kept"] for x in st)
+        for r in runners:
+            r.close()
+        return dict(bins=len(sel), reads=int(bins.n), umis_kept=int(kept), seconds=dt, umis_per_s=kept / dt,
+                    cost_share=sum(costs[i] for i in sel) / sum(costs),
+                    largest_pack_s=max((x["t_total_s"] for x in st), default=0.0))
+
+    run(plan[0])  # warm-up (untimed): allocations, code objects
+    shares = [run(p) for p in plan]
+    big = run([largest])
+    tmax = max(x["seconds"] for x in shares)
+    node_umis = sum(x["umis_kept"] for x in shares)
+    out = {"metric": METRIC, "value": node_umis / tmax, "unit": "UMIs/s", "n_gpus": N, "steps": 1, "warmup": 1,
+           "ms_per_step": 1e3 * tmax, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "int16/int32", "data": "synthetic",
+           "config": {"workload": f"BASELINE config {args.config} at scale {args.scale}: every LPT share of an {N}-GPU "
+                                  "node clustered alone on one MI355X, one after another",
+                      "parallelism": f"{N} shares (shard.lpt_assign), each timed alone; value = the node's UMIs / the "
+                                     "largest share's time (the makespan of N GPUs running their shares at once)",
+                      "lanes": args.lanes, "pack_reads": args.pack_reads},
+           "shares": shares, "makespan_s": tmax, "sum_s": sum(x["seconds"] for x in shares),
+           "largest_bin": dict(big, bin=largest), "measured_on": "one GPU"}
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    if ctx2 is not None:
+        ctx2.close()
 
 
 def _tree_bytes(d: str) -> tuple[int, int]:
@@ -483,7 +572,18 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
     import tempfile
     from umiclust import _lib, synth
     io_t = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)))
-    d = tempfile.mkdtemp(prefix="umiclust_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    # RAM-backed (/dev/shm) when it has room: on the GPU box's disk-backed overlay every create / delete cycle of
+    # ~10^5 files leaves the next one slower (the same replay: 2.0 s fresh, 7.6 s after one delete, 25 s after three:
+    # profiles/r04/io_order_probe.txt), so later writers would be timed against the filesystem's history
+    base = os.environ.get("UMICLUST_E2E_DIR")
+    if not base:
+        try:
+            st_ = os.statvfs("/dev/shm")
+            base = "/dev/shm" if os.access("/dev/shm", os.W_OK) and st_.f_bavail * st_.f_frsize > (64 << 30) else None
+        except OSError:
+            base = None
+    base = base or os.environ.get("TMPDIR", "/tmp")
+    d = tempfile.mkdtemp(prefix="umiclust_e2e_", dir=base)
     try:
         fa = os.path.join(d, "region_cluster0_detected_umis.fasta")
         t0 = time.perf_counter()
@@ -535,7 +635,8 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500) -> dict:
                              write_gbps=nb_all / st2["t_write_s"] / 1e9 if st2.get("t_write_s") else None,
                              write_bound=bound_f,
                              write_frac=bound_f["seconds"] / st2["t_write_s"] if st2.get("t_write_s") else None),
-            note="page-cache-warm input; outputs on the box's local disk ($TMPDIR); every timed write (writers and "
+            output_dir=base,
+            note="page-cache-warm input; outputs under output_dir (RAM-backed /dev/shm when it has room); every timed write (writers and "
                  "replays) starts after an untimed sync; write_bound = io_probe_replay of the writer's own files "
                  "(sizes, contiguous thread split, the one streamed file) with no formatting; write_frac = "
                  "write_bound seconds / the writer's seconds")

@@ -51,6 +51,7 @@
 
 #include "../../include/umiclust.h"
 #include "host_io.h"
+#include "resolve.h"
 #include "umiclust_internal.h"
 
 using namespace uc;
@@ -147,15 +148,6 @@ struct Fail {
 
 // One greedy block in flight: its own peer tile, device outputs and pinned mirrors, so the device
 // runs block k+1 while the host resolves block k.
-// Outcome of one strand's walk.
-struct Outcome {
-  bool acc = false;
-  uint16_t rank = 0;
-  uint32_t t = 0xffffffffu;
-  int walked = 0;
-  int64_t cells = 0;
-};
-
 struct Pass {
   int32_t q0 = 0, nq = 0, w0 = 0;  // block [q0, q0+nq), peer window [w0, q0+nq)
   bool live = false;
@@ -187,12 +179,7 @@ struct Pass {
   PinBuf<uint32_t> h_rec, h_counters, h_reccount;
   std::vector<HostQs> hq_copy;
   std::vector<uint32_t> rec_copy;
-  // parallel classification of the pass's query-strands (resolve_pass): 0 the device outcome is final,
-  // 1 final unless one of its in-block relevant peers (deps) turns out a centroid or is undetermined,
-  // 2 resolved sequentially in full
-  std::vector<uint8_t> kind, ndeps, pre_cert, done;
-  std::vector<uint16_t> deps;
-  std::vector<Outcome> pre;  // outcomes the classify threads resolved (kind 3) or found needing round B (kind 4)
+  ResolveScratch rsx;  // resolve_block's classification scratch (resolve.h)
   hipEvent_t ev[5] = {};  // prefilter begin/end, align begin/end, results in host memory
   // split passes: the counting half (enqueue_count) of the block this buffer set serves next
   PinBuf<TileView> h_tiles_a;
@@ -210,70 +197,6 @@ struct Pass {
     for (hipEvent_t e : ev_c)
       if (e) (void)hipEventDestroy(e);
   }
-};
-
-// A small persistent worker pool: run(T, f) calls f(t) for t in [0, T) on the workers and the caller (t = 0).
-class WorkPool {
- public:
-  explicit WorkPool(int n) {
-    for (int i = 1; i < n; i++) th_.emplace_back([this, i] { loop(i); });
-  }
-  ~WorkPool() {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int size() const { return (int)th_.size() + 1; }
-  void set_affinity(const cpu_set_t& set) {
-    for (auto& t : th_) pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
-  }
-  void run(const std::function<void(int)>& f) {
-    if (th_.empty()) {
-      f(0);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &f;
-      pending_ = (int)th_.size();
-      gen_++;
-    }
-    cv_.notify_all();
-    f(0);
-    std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [this] { return pending_ == 0; });
-    job_ = nullptr;
-  }
-
- private:
-  void loop(int i) {
-    uint64_t seen = 0;
-    for (;;) {
-      const std::function<void(int)>* f;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-        f = job_;
-      }
-      (*f)(i);
-      {
-        std::lock_guard<std::mutex> g(m_);
-        if (--pending_ == 0) done_.notify_one();
-      }
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex m_;
-  std::condition_variable cv_, done_;
-  const std::function<void(int)>* job_ = nullptr;
-  uint64_t gen_ = 0;
-  int pending_ = 0;
-  bool stop_ = false;
 };
 
 }  // namespace
@@ -388,6 +311,7 @@ struct umiclust_ctx {
                                    // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
                                    // k_align_pk (profiles/r03/band_ab.json)
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)
+  bool rb_on_b = false;            // UMICLUST_RB_STREAM=b: round B on st_b (behind the index appends) instead of st_copy
   bool r_on_al = false;            // UMICLUST_RAL=1: second halves' prefilter on the align stream (split passes)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
@@ -456,6 +380,7 @@ struct umiclust_ctx {
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
+  bool peer_cert = true;          // UMICLUST_PEER_CERT=0: align relevant peers even when certain to become members
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
   int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
@@ -466,6 +391,22 @@ struct umiclust_ctx {
   // UMICLUST_WALK_DUMP=<file>: per sorted seqno of the bin, the alignments each strand's walk counted and the
   // path that resolved it (0 device, 1 classify thread, 2 in order, 3 round B) -- a parity-debugging aid
   const char* walk_dump = getenv("UMICLUST_WALK_DUMP");
+  // UMICLUST_RESOLVE_DUMP=<prefix>[:i,j,...]: record resolve_block's inputs and outputs of the i-th, j-th, ... passes
+  // of the context (default 10, 40, 80) to <prefix>.<i>.bin (single-bin clustering only)
+  const char* resolve_dump = getenv("UMICLUST_RESOLVE_DUMP");
+  int64_t n_resolved = 0;
+  bool dump_want(int64_t k) const {
+    const char* c = strchr(resolve_dump, ':');
+    if (!c) return k == 10 || k == 40 || k == 80;
+    for (const char* p = c + 1; *p;) {
+      char* e;
+      const long v = strtol(p, &e, 10);
+      if (e == p) break;
+      if (v == k) return true;
+      p = *e == ',' ? e + 1 : e;
+    }
+    return false;
+  }
   std::vector<int16_t> wd;
   double dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // UMICLUST_DEBUG: resolve_pass phases (s): event wait, outcome copy,
                                                // record copy, classify, in-order resolve, round B + rest, total
@@ -645,69 +586,8 @@ TileView view_of(const Tile& t) {
   return v;
 }
 
-inline unsigned long long cand_key(uint32_t count, uint32_t len, uint32_t seqno) {
-  return ((unsigned long long)(127u - count) << 56) | ((unsigned long long)len << 48) | seqno;
-}
-
-// One candidate of a merged walk.
-struct MCand {
-  unsigned long long key;
-  uint32_t seqno;
-  uint32_t res;  // alignment result (matches | internal << 8), valid if have
-  bool have;
-};
-
-// vsearch search_onequery over a merged, sorted candidate list (maxaccepts 1, maxrejects 32).
-// Returns false if an alignment result is missing.
-bool merged_walk(const umiclust_ctx* c, std::vector<MCand>& L, int ql, Outcome& o) {
-  const int n = std::min<int>((int)L.size(), kTopHits);
-  int w = 0;
-  o = Outcome();
-  while (w < n && w < kWalk && !o.acc) {
-    const int b1 = std::min(std::min(n, w + kBatch), kWalk);
-    for (int x = w; x < b1; x++) {
-      if (!L[x].have) return false;
-      const uint32_t m = L[x].res & 0xffu, Li = (L[x].res >> 8) & 0xffu;
-      o.cells += (int64_t)ql * c->hlen[L[x].seqno];
-      if (c->h_acc[(size_t)Li * kTabM + m]) {
-        const uint16_t rk = c->h_rank[(size_t)Li * kTabM + m];
-        if (!o.acc || rk > o.rank || (rk == o.rank && L[x].seqno < o.t)) {
-          o.rank = rk;
-          o.t = L[x].seqno;
-        }
-        o.acc = true;
-      }
-    }
-    w = b1;
-  }
-  o.walked = w;
-  return true;
-}
-
-// search_findbest2_byid: max id, then lower target seqno, plus strand first.
-inline bool better(const Outcome& a, const Outcome& b) {
-  if (!a.acc) return false;
-  if (!b.acc) return true;
-  if (a.rank != b.rank) return a.rank > b.rank;
-  return a.t < b.t;
-}
-
-enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
-
-// greedy state of the sorted seqnos [s0, s0 + n) of the bin being clustered, indexed by absolute seqno
-struct StateView {
-  uint8_t* p = nullptr;
-  int32_t s0 = 0;
-  uint8_t& operator[](int64_t i) const { return p[i - s0]; }
-};
-
-// Policy O4 (batched rounds of o4_T queries): the first query of q's round.  Rounds are counted from the first
-// sorted query of q's own bin -- in a pack of bins (one greedy order over several bins) from the bin's first
-// seqno, so every bin's rounds are the ones its own vsearch run would have.  Sequential policy: q itself.
 inline int32_t round_start(const umiclust_ctx* c, int32_t s0, int32_t q) {
-  if (!c->o4_T) return q;
-  const int32_t b0 = c->pack_on ? c->bin_s[c->hqbin[q]] : s0;
-  return b0 + (q - b0) / c->o4_T * c->o4_T;
+  return o4_round_start(c->o4_T, c->pack_on ? c->hqbin.data() : nullptr, c->bin_s.data(), s0, q);
 }
 
 void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
@@ -974,10 +854,17 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
                      P.d_res.p, c->d_acc.p, c->d_rank.p, P.d_ws.p, P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1, segc + kSegLens,
                      cells_w, st),
          "walk 0");
+  // the previous block's pass (its walk states are final and stay until that buffer set's next walk, which is
+  // queued after this one on the align stream): peers there whose device walk accepted are certain members
+  const Pass* prev = nullptr;
+  if (c->peer_cert)
+    for (const Pass& Q : c->pass)
+      if (&Q != &P && Q.nq > 0 && Q.q0 + Q.nq == q0) prev = &Q;
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
                            P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1, segc + kSegLens, cells_p, P.d_counters.p + 8,
                            peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, lazy_peers ? 0 : 1,
-                           st),
+                           prev ? prev->d_ws.p : nullptr, prev ? prev->d_npeer.p : nullptr, prev ? prev->q0 : 0,
+                           prev ? prev->nq : 0, st),
          "peer pairs");
   align_round(sg1, kWalk + kPeerCap, segc + kSegLens, "align 1");
   c->hip(launch_walk(1, q0, nqs, both, c->spec_thr, P.d_top_seqno.p, P.d_top_count.p, P.d_ntop.p, c->d_lens.p,
@@ -1100,16 +987,53 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   P.a_slot = slot;
 }
 
-// Wait for a pass and resolve its block on the host in sorted order.  Returns false if a peer
-// list overflowed (the caller re-runs the block in smaller pieces).  Every query of the peer
-// window before the block is already resolved, so peers are final or earlier in this block.
-//
-// A (query, strand) without a record (no relevant peer: k_pack) takes the device walk.  With one,
-// its outcome depends on the peers' states: a relevant peer still undetermined blocks it; a
-// relevant peer that is a centroid makes the host run the exact merged walk over T_old u (peers
-// that are centroids) -- every such peer now matters, so an undetermined one blocks too.  A merged
-// walk that needs an alignment the pass did not compute (a T_old entry past the device walk, or a
-// peer that was not relevant) is deferred to round B, and so are queries blocked by deferred ones.
+// One resolve_block call, replayable without a GPU (format read by tools/resolve_tsan_main.cpp): little-endian,
+// "UCRD" v1, the parameters, hlen of the bin up to the block's end, the acceptance / rank tables, the window's states
+// before, the pass's HostQs and records, round B's pairs and results, then the outputs (the block's states, targets
+// and strands, the new centroids, alignments and cells).
+void write_resolve_dump(const umiclust_ctx* c, const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0,
+                        const StateView& state, const std::vector<uint8_t>& state_in, const HostQs* hq,
+                        const uint32_t* recs, uint32_t nrec, const std::vector<uint32_t>& bpq,
+                        const std::vector<uint32_t>& bpt, const std::vector<uint32_t>& bres,
+                        const std::vector<int32_t>& new_cents, const ResolveStats& rs) {
+  const std::string path = std::string(c->resolve_dump, strcspn(c->resolve_dump, ":")) + "." +
+                           std::to_string(c->n_resolved - 1) + ".bin";
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) return;
+  auto w = [&](const void* p, size_t n) { fwrite(p, 1, n, f); };
+  auto wi = [&](int64_t v) { w(&v, 8); };
+  w("UCRD", 4);
+  const int32_t s0 = state.s0;
+  const int32_t hdr[12] = {1, q0, nq, w0, env.both, env.o4_T, env.maxaccepts, env.maxrejects, env.pre_resolve ? 1 : 0,
+                           env.pre_spec ? 1 : 0, s0, 0};
+  w(hdr, sizeof hdr);
+  wi(q0 + nq - s0);
+  w(env.hlen + s0, (size_t)(q0 + nq - s0));
+  w(env.acc, (size_t)kTabL * kTabM);
+  w(env.rank, (size_t)kTabL * kTabM * 2);
+  wi((int64_t)state_in.size());
+  w(state_in.data(), state_in.size());
+  const int64_t nqs = (int64_t)nq * env.both;
+  wi(nqs);
+  w(hq, (size_t)nqs * sizeof(HostQs));
+  wi(nrec);
+  w(recs, (size_t)nrec * 4);
+  wi((int64_t)bpq.size());
+  w(bpq.data(), bpq.size() * 4);
+  w(bpt.data(), bpt.size() * 4);
+  w(bres.data(), bres.size() * 4);
+  w(&state[q0], (size_t)nq);
+  w(env.target + q0, (size_t)nq * 4);
+  w(env.strand + q0, (size_t)nq);
+  wi((int64_t)new_cents.size());
+  w(new_cents.data(), new_cents.size() * 4);
+  wi(rs.n_alignments);
+  wi(rs.cells);
+  fclose(f);
+}
+
+// Wait for a pass and resolve its block on the host in sorted order (resolve.cpp resolve_block).  Returns false if a
+// peer list overflowed (the caller re-runs the block in smaller pieces).
 bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<int32_t>& new_cents,
                   double& t_pf, double& t_al, double& t_host) {
   const int both = c->both;
@@ -1163,25 +1087,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   c->stats.t_sync_s += now_s() - tc0;
   c->dbg_t[1] += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
-  for (int32_t qs = 0; qs < nqs; qs++)
-    if (hq[qs].flags & 2u) return false;
-  new_cents.clear();
-  const double th0 = now_s();
-  constexpr int kSlots = kWalk + kPeerCap;  // round-B result slots per query-strand: T_old, peers
-  std::vector<int32_t> deferred;
-  std::vector<uint32_t> extra_res;   // [row*kSlots + slot] results of round B (valid if flag)
-  std::vector<uint8_t> extra_have;
-  std::vector<int32_t> extra_row;    // qs -> row of the round-B arrays (-1: none)
-  struct Rec {
-    int nt, np;
-    const uint32_t *seq, *res, *cw, *peer, *pres;
-    uint32_t count(int x) const { return (cw[x >> 2] >> ((x & 3) * 8)) & 0xffu; }
-  };
+  if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
   // the records are copied into pageable memory first (one streaming read; scattered reads of the DMA'd
   // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
   const uint32_t* recs = P.h_rec.p;
   static const bool rec_copy = !(getenv("UMICLUST_RECCOPY") && atoi(getenv("UMICLUST_RECCOPY")) == 0);
-  if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
   if (rec_copy) {
     const double tc1 = now_s();
     // on the resolve threads: one core's streaming read of pinned memory is the limit (0.05 s per config-2 step)
@@ -1200,530 +1110,89 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     c->stats.t_sync_s += now_s() - tc1;
     c->dbg_t[2] += now_s() - tc1;
   }
-  auto rec_of = [&](const HostQs& h) {
-    const uint32_t* r = recs + h.rec;
-    Rec R;
-    R.nt = (int)(r[0] & 0xffu);
-    R.np = (int)((r[0] >> 8) & 0xffu);
-    R.seq = r + 1;
-    R.res = R.seq + R.nt;
-    R.cw = R.res + R.nt;
-    R.peer = R.cw + ((R.nt + 3) >> 2);
-    R.pres = R.peer + R.np;
-    return R;
-  };
-  auto device_outcome = [](const HostQs& h, Outcome& o) {
-    o.acc = (h.flags & 1u) != 0;
-    o.rank = h.best_rank;
-    o.t = h.best_t;
-    o.walked = h.w;
-    o.cells = h.cells;
-  };
-  // Membership can be certain while the walk's outcome is not: a device walk that accepted within its first w
-  // candidates still accepts when at most nrel relevant peers are inserted before them (w + nrel <= kWalk).
-  // Such a query is a member whichever centroid it ends up joining, so later queries that only need to
-  // know "centroid or not" are not held up by it.
-  auto cert_device = [](const HostQs& h) { return (h.flags & 1u) && (int)h.w + (int)h.nrel <= kWalk; };
-  struct Scratch {
-    std::vector<std::pair<unsigned long long, int>> cp, cx;
-    std::vector<MCand> L;
-    int64_t merged = 0;
-  };
-  // seq: the in-order phase (debug counters, merged-walk timer); otherwise a classify thread resolving a strand
-  // whose peers' states are all final, with its own scratch
-  auto strand_outcome_s = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert, Scratch& scr,
-                              bool seq, uint32_t ib_lim = UINT32_MAX) -> int {
-    // returns 0 resolved, 1 blocked by an undetermined peer, 2 needs alignments not computed; peers with a window id
-    // >= ib_lim are taken as non-centroids (the classify phase's speculative resolution, kind 5)
-    auto& cp = scr.cp;
-    auto& L = scr.L;
-    const HostQs& h = hq[qs];
-    cert = false;
-    if (h.rec == 0xffffffffu) {
-      device_outcome(h, o);
-      return 0;
-    }
-    if (seq && c->debug) c->dbg_p[h.nrel <= (uint32_t)kInlineRel ? 0 : 1]++;
-    if (h.nrel <= (uint32_t)kInlineRel) {
-      bool cent = false;
-      for (uint32_t i = 0; i < h.nrel; i++) {
-        if (h.rel[i] >= ib_lim) continue;
-        const uint8_t st = state[(uint32_t)w0 + h.rel[i]];
-        if (st == ST_UNDET) {
-          cert = cert_device(h);
-          return 1;
-        }
-        cent |= st == ST_CENT;
-      }
-      if (!cent) {
-        device_outcome(h, o);
-        return 0;
-      }
-    }
-    if (seq && c->debug) c->dbg_p[2]++;
-    const Rec R = rec_of(h);
-    if (seq && c->debug) c->dbg_p[3] += R.np;
-    bool affects = false, undet = false;
-    for (int y = 0; y < R.np; y++) {
-      const uint32_t pw = R.peer[y];
-      if ((pw & 0xffffu) >= ib_lim) continue;
-      const uint8_t st = state[(uint32_t)w0 + (pw & 0xffffu)];
-      if ((pw >> 24) & 1u) {
-        if (st == ST_UNDET) {
-          if (seq) c->dbg[2]++;
-          cert = cert_device(h);
-          return 1;
-        }
-        affects |= st == ST_CENT;
-        if (seq && !((pw >> 25) & 1u)) c->dbg[st == ST_CENT ? 0 : 1]++;  // mispredicted / saved
-      } else {
-        undet |= st == ST_UNDET;
-      }
-    }
-    if (!affects) {
-      device_outcome(h, o);
-      return 0;
-    }
-    if (undet) {
-      cert = cert_device(h);
-      return 1;
-    }
-    scr.merged++;
-    double t_unused = 0;
-    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{seq ? &c->stats.t_merged_s : &t_unused,
-                                                                               now_s()};
-    // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
-    // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
-    const int32_t row = allow_extra ? extra_row[qs] : -1;
-    // O4 batched rounds: centroids created before q's round join its search (the merged walk); those of its
-    // own round are the extras of the re-check below.  Sequential: every centroid peer joins the walk.
-    const uint32_t rb = c->o4_T ? (uint32_t)round_start(c, state.s0, q) : UINT32_MAX;
-    auto& cx = scr.cx;
-    cp.clear();
-    cx.clear();
-    for (int y = 0; y < R.np; y++) {
-      const uint32_t pw = R.peer[y];
-      if ((pw & 0xffffu) >= ib_lim) continue;
-      const uint32_t ps = (uint32_t)w0 + (pw & 0xffffu);
-      if (state[ps] == ST_CENT) (ps < rb ? cp : cx).push_back({cand_key((pw >> 16) & 0xffu, c->hlen[ps], ps), y});
-    }
-    std::sort(cp.begin(), cp.end());
-    L.clear();
-    int i = 0;
-    size_t x = 0;
-    while ((int)L.size() < kWalk && (i < R.nt || x < cp.size())) {
-      const unsigned long long kt = (i < R.nt) ? cand_key(R.count(i), c->hlen[R.seq[i]], R.seq[i]) : ~0ull;
-      const unsigned long long kp = (x < cp.size()) ? cp[x].first : ~0ull;
-      MCand m;
-      if (kt < kp) {
-        m.key = kt;
-        m.seqno = R.seq[i];
-        if (i < h.e) {
-          m.res = R.res[i];
-          m.have = true;
-        } else if (row >= 0 && extra_have[(size_t)row * kSlots + i]) {
-          m.res = extra_res[(size_t)row * kSlots + i];
-          m.have = true;
-        } else {
-          m.res = 0;
-          m.have = false;
-        }
-        i++;
-      } else {
-        const int y = cp[x].second;
-        m.key = kp;
-        m.seqno = (uint32_t)w0 + (R.peer[y] & 0xffffu);
-        if ((R.peer[y] >> 25) & 1u) {  // aligned by the pass
-          m.res = R.pres[y];
-          m.have = true;
-        } else if (row >= 0 && extra_have[(size_t)row * kSlots + kWalk + y]) {
-          m.res = extra_res[(size_t)row * kSlots + kWalk + y];
-          m.have = true;
-        } else {
-          m.res = 0;
-          m.have = false;
-        }
-        x++;
-      }
-      L.push_back(m);
-    }
-    if (merged_walk(c, L, c->hlen[q], o)) {
-      if (cx.empty()) return 0;
-      // cluster_core_parallel's re-check (policy O4): the round's new centroids over the k-mer threshold are
-      // inserted into the hit list (the walked candidates, all aligned) by (count desc, shorter first, then
-      // seqno), and the list is walked again one alignment at a time from the top until an accept or
-      // maxrejects rejects; the best hit is then the best accepted one of every aligned hit
-      std::sort(cx.begin(), cx.end());
-      int acc = 0, rej = 0;
-      size_t a = 0, b = 0;
-      const size_t w = (size_t)o.walked;
-      while (acc < c->p.maxaccepts && rej < c->p.maxrejects && (a < w || b < cx.size())) {
-        uint32_t res, t;
-        if (a < w && (b >= cx.size() || L[a].key < cx[b].first)) {
-          res = L[a].res;
-          t = L[a].seqno;
-          a++;
-        } else {
-          const int y = cx[b].second;
-          t = (uint32_t)w0 + (R.peer[y] & 0xffffu);
-          if ((R.peer[y] >> 25) & 1u) {
-            res = R.pres[y];
-          } else if (row >= 0 && extra_have[(size_t)row * kSlots + kWalk + y]) {
-            res = extra_res[(size_t)row * kSlots + kWalk + y];
-          } else {
-            cert = o.acc;  // an accepted hit of the search stays a candidate whatever the re-check finds
-            return 2;
-          }
-          b++;
-          o.walked++;
-          o.cells += (int64_t)c->hlen[q] * c->hlen[t];
-        }
-        const uint32_t m = res & 0xffu, Li = (res >> 8) & 0xffu;
-        if (c->h_acc[(size_t)Li * kTabM + m]) {
-          acc++;
-          const uint16_t rk = c->h_rank[(size_t)Li * kTabM + m];
-          if (!o.acc || rk > o.rank || (rk == o.rank && t < o.t)) {
-            o.rank = rk;
-            o.t = t;
-          }
-          o.acc = true;
-        } else {
-          rej++;
-        }
-      }
-      return 0;
-    }
-    // an accept already known within the first kWalk candidates ends the walk by its batch at the latest
-    for (int x = 0; x < std::min<int>((int)L.size(), kWalk) && !cert; x++)
-      if (L[x].have) {
-        const uint32_t m = L[x].res & 0xffu, Li = (L[x].res >> 8) & 0xffu;
-        cert = c->h_acc[(size_t)Li * kTabM + m] != 0;
-      }
-    return 2;
-  };
-  Scratch scr0;
-  auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert) -> int {
-    return strand_outcome_s(qs, q, allow_extra, o, cert, scr0, true);
-  };
-  auto resolve = [&](int32_t ql, bool allow_extra, auto&& strand_fn) -> bool {
-    const int32_t q = q0 + ql;
-    Outcome best, os[2];
-    int bs = 0;
-    bool open = false, member = false;
-    for (int s = 0; s < both; s++) {
-      bool cert = false;
-      if (strand_fn(ql * both + s, q, allow_extra, os[s], cert) != 0) {
-        open = true;
-        member |= cert;
-      } else {
-        member |= os[s].acc;
-      }
-    }
-    if (open) {
-      // deferred; a certain member is marked so already (its centroid is settled in round B)
-      if (member) state[q] = ST_MEMBER;
-      return false;
-    }
-    for (int s = 0; s < both; s++) {
-      c->stats.n_alignments += os[s].walked;
-      c->stats.cells += os[s].cells;
-      if (!c->wd.empty()) {
-        c->wd[(size_t)(q - state.s0) * 4 + s] = (int16_t)os[s].walked;
-        c->wd[(size_t)(q - state.s0) * 4 + 2 + s] = allow_extra ? 3 : 2;
-      }
-      if (better(os[s], best)) {
-        best = os[s];
-        bs = s;
-      }
-    }
-    if (best.acc) {
-      state[q] = ST_MEMBER;
-      c->target[q] = (int32_t)best.t;
-      c->strand[q] = (uint8_t)bs;
-    } else {
-      state[q] = ST_CENT;
-      new_cents.push_back(q);
-    }
-    return true;
-  };
-  if (c->debug && getenv("UMICLUST_DEBUG_CLASSES")) {
-    const uint32_t inb = (uint32_t)(q0 - w0);
-    for (int32_t ql = 0; ql < nq; ql++) {
-      int cls = 0;
-      for (int s = 0; s < both; s++) {
-        const HostQs& h = hq[ql * both + s];
-        if (h.rec == 0xffffffffu) continue;
-        cls = std::max(cls, 1);
-        const Rec R = rec_of(h);
-        for (int y = 0; y < R.np; y++)
-          if (((R.peer[y] >> 24) & 1u) && (R.peer[y] & 0xffffu) >= inb) cls = 2;
-      }
-      c->dbg_q[cls]++;
-    }
-  }
-  const double tp0 = now_s();
-  // Phase 1 (host threads): classify every query-strand.  Peers in earlier blocks are final, so a strand
-  // whose relevant peers there include a centroid needs the full (sequential) resolution, and one whose
-  // relevant peers are all earlier-block members and in-block peers keeps its device outcome unless one of
-  // those in-block peers becomes a centroid or is deferred -- checked in order in phase 2.
-  constexpr int kDeps = 8;
-  const uint32_t inb = (uint32_t)(q0 - w0);
-  P.kind.resize((size_t)nqs);
-  P.ndeps.resize((size_t)nqs);
-  P.deps.resize((size_t)nqs * kDeps);
-  P.pre.resize((size_t)nqs);
-  P.pre_cert.resize((size_t)nqs);
-  // kind 0: the device outcome is final; 1: final unless an in-block dependency becomes a centroid or is
-  // deferred; 2: full resolution in order; 3 / 4: every peer lies in an earlier (resolved) block, so the
-  // full resolution needs no in-order state and ran here: resolved (3) or needing round B (4)
-  auto classify = [&](int32_t qs, Scratch& scr) {
-    const HostQs& h = hq[qs];
-    uint8_t& kd = P.kind[qs];
-    if (h.rec == 0xffffffffu) {
-      kd = 0;
-      return;
-    }
-    if (c->o4_T) {  // O4 batched rounds: every strand with a record resolves in order (strand_outcome_s)
-      kd = 2;
-      return;
-    }
-    int nd = 0;
-    uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
-    auto rel_peer = [&](uint32_t id) -> bool {  // false: needs the full resolution
-      if (id >= inb) {
-        if (nd == kDeps) return false;
-        d[nd++] = (uint16_t)id;
-        return true;
-      }
-      return state[(uint32_t)w0 + id] != ST_CENT;
-    };
-    bool ok = true;
-    if (h.nrel <= (uint32_t)kInlineRel) {
-      for (uint32_t i = 0; i < h.nrel && ok; i++) ok = rel_peer(h.rel[i]);
-    } else {
-      const Rec R = rec_of(h);
-      for (int y = 0; y < R.np && ok; y++)
-        if ((R.peer[y] >> 24) & 1u) ok = rel_peer(R.peer[y] & 0xffffu);
-    }
-    kd = !ok ? 2 : nd ? 1 : 0;
-    P.ndeps[qs] = (uint8_t)nd;
-    if (kd == 2 && c->pre_resolve) {
-      const Rec R = rec_of(h);
-      int nib = 0;  // in-block peers (any relevance)
-      for (int y = 0; y < R.np; y++) nib += (R.peer[y] & 0xffffu) >= inb;
-      if (nib == 0) {
-        bool cert = false;
-        const int r = strand_outcome_s(qs, q0 + qs / both, false, P.pre[qs], cert, scr, false);
-        if (r != 1) {
-          kd = r == 0 ? 3 : 4;
-          P.pre_cert[qs] = cert;
-        }
-      } else if (nib <= kDeps && c->pre_spec) {
-        // kind 5: resolved here as if no in-block peer were a centroid (earlier-block peers are final); phase 2
-        // keeps this outcome if every in-block peer -- relevant or not: once a centroid peer joins the walk, any
-        // peer can -- turns out a member, and otherwise runs the full resolution
-        bool cert = false;
-        const int r = strand_outcome_s(qs, q0 + qs / both, false, P.pre[qs], cert, scr, false, inb);
-        if (r == 0) {
-          kd = 5;
-          nd = 0;
-          for (int y = 0; y < R.np; y++)
-            if ((R.peer[y] & 0xffffu) >= inb) d[nd++] = (uint16_t)(R.peer[y] & 0xffffu);
-          P.ndeps[qs] = (uint8_t)nd;
-        }
-      }
-    }
-  };
-  // A query whose strands are all final here (kinds 0 and 3: no in-block dependency) is resolved here too: its
-  // outcome needs no in-order state, and only in-block queries ever read its state, in phase 2, after this
-  // phase.  P.done: 0 pending (phase 2), 1 member, 2 centroid.
-  P.done.resize((size_t)nq);
-  struct Acc {
-    int64_t aln = 0, cells = 0;
-  };
-  auto classify_query = [&](int32_t ql, Scratch& scr, Acc& acc) {
-    bool det = true;
-    for (int s = 0; s < both; s++) {
-      const int32_t qs = ql * both + s;
-      classify(qs, scr);
-      det &= P.kind[qs] == 0 || P.kind[qs] == 3;
-    }
-    if (!det) {
-      P.done[ql] = 0;
-      return;
-    }
-    Outcome best, os[2];
-    int bs = 0;
-    for (int s = 0; s < both; s++) {
-      const int32_t qs = ql * both + s;
-      if (P.kind[qs] == 0) device_outcome(hq[qs], os[s]);
-      else os[s] = P.pre[qs];
-      acc.aln += os[s].walked;
-      acc.cells += os[s].cells;
-      if (!c->wd.empty()) {
-        c->wd[(size_t)(q0 + ql - state.s0) * 4 + s] = (int16_t)os[s].walked;
-        c->wd[(size_t)(q0 + ql - state.s0) * 4 + 2 + s] = P.kind[qs] == 0 ? 0 : 1;
-      }
-      if (better(os[s], best)) {
-        best = os[s];
-        bs = s;
-      }
-    }
-    const int32_t q = q0 + ql;
-    if (best.acc) {
-      state[q] = ST_MEMBER;
-      c->target[q] = (int32_t)best.t;
-      c->strand[q] = (uint8_t)bs;
-      P.done[ql] = 1;
-    } else {
-      state[q] = ST_CENT;
-      P.done[ql] = 2;
-    }
-  };
-  const int T = nqs < 2048 ? 1 : c->pool->size();
-  std::vector<Scratch> scr_t((size_t)T);
-  std::vector<Acc> acc_t((size_t)T);
-  if (T == 1) {
-    for (int32_t ql = 0; ql < nq; ql++) classify_query(ql, scr_t[0], acc_t[0]);
-  } else {
-    c->pool->run([&](int t) {
-      const int32_t lo = (int32_t)((int64_t)nq * t / T), hi = (int32_t)((int64_t)nq * (t + 1) / T);
-      for (int32_t ql = lo; ql < hi; ql++) classify_query(ql, scr_t[(size_t)t], acc_t[(size_t)t]);
-    });
-  }
-  for (const Scratch& x : scr_t) c->stats.n_merged_walks += x.merged;
-  for (const Acc& x : acc_t) {
-    c->stats.n_alignments += x.aln;
-    c->stats.cells += x.cells;
-  }
-  const double tp1 = now_s();
-  c->dbg_t[3] += tp1 - tp0;
-  // Phase 2 (sequential, sorted order): confirm the device outcomes against the in-block peers' states
-  auto strand_fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
-    const HostQs& h = hq[qs];
-    cert = false;
-    if (P.kind[qs] == 0) {
-      device_outcome(h, o);
-      return 0;
-    }
-    if (P.kind[qs] == 3) {
-      o = P.pre[qs];
-      return 0;
-    }
-    if (P.kind[qs] == 4) {
-      cert = P.pre_cert[qs] != 0;
-      return 2;
-    }
-    if (P.kind[qs] == 5) {
-      const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
-      bool member_peers = true;
-      for (int i = 0; i < P.ndeps[qs] && member_peers; i++) member_peers = state[(uint32_t)w0 + d[i]] == ST_MEMBER;
-      if (member_peers) {
-        o = P.pre[qs];
-        return 0;
-      }
-      return strand_outcome(qs, q, false, o, cert);
-    }
-    if (P.kind[qs] == 1) {
-      const uint16_t* d = P.deps.data() + (size_t)qs * kDeps;
-      bool cent = false;
-      for (int i = 0; i < P.ndeps[qs]; i++) {
-        const uint8_t st = state[(uint32_t)w0 + d[i]];
-        if (st == ST_UNDET) {
-          cert = cert_device(h);
-          return 1;
-        }
-        cent |= st == ST_CENT;
-      }
-      if (!cent) {
-        device_outcome(h, o);
-        return 0;
-      }
-    }
-    return strand_outcome(qs, q, false, o, cert);
-  };
-  for (int32_t ql = 0; ql < nq; ql++) {
-    const uint8_t d = P.done[ql];
-    if (d == 2) new_cents.push_back(q0 + ql);
-    else if (d == 0 && !resolve(ql, false, strand_fast)) deferred.push_back(ql);
-  }
-  c->dbg_q[3] += (int64_t)((now_s() - tp0) * 1e9);
-  c->dbg_t[4] += now_s() - tp1;
-  t_host += now_s() - th0;
-  c->stats.t_host_pass1_s += now_s() - th0;
-  c->stats.n_deferred += (int64_t)deferred.size();
-  // --- round B (side stream, so the queued pass keeps the device busy): align every T_old entry and
-  // every peer a deferred query could still need, then resolve the deferred queries in order
-  if (!deferred.empty()) {
-    const double th1 = now_s();
-    std::vector<uint32_t> bpq, bpt, bidx;
-    for (int32_t ql : deferred)
-      for (int s = 0; s < both; s++) {
-        const int32_t qs = ql * both + s;
-        const HostQs& h = hq[qs];
-        if (h.rec == 0xffffffffu) continue;
-        const Rec R = rec_of(h);
-        const uint32_t qv = ((uint32_t)(q0 + ql) << 1) | (uint32_t)s;
-        for (int x = h.e; x < R.nt; x++) {
-          bpq.push_back(qv);
-          bpt.push_back(R.seq[x]);
-          bidx.push_back((uint32_t)(qs * kSlots + x));
-        }
-        for (int y = 0; y < R.np; y++)
-          // a peer that is a member never enters the merged walk (only centroids are candidates)
-          if (!((R.peer[y] >> 25) & 1u) && state[(uint32_t)w0 + (R.peer[y] & 0xffffu)] != ST_MEMBER) {
-            bpq.push_back(qv);
-            bpt.push_back((uint32_t)w0 + (R.peer[y] & 0xffffu));
-            bidx.push_back((uint32_t)(qs * kSlots + kWalk + y));
-          }
-      }
-    t_host += now_s() - th1;
+  ResolveEnv env;
+  env.hlen = c->hlen.data();
+  env.acc = c->h_acc.data();
+  env.rank = c->h_rank.data();
+  env.both = both;
+  env.o4_T = c->o4_T;
+  env.maxaccepts = c->p.maxaccepts;
+  env.maxrejects = c->p.maxrejects;
+  env.hqbin = c->pack_on ? c->hqbin.data() : nullptr;
+  env.bin_s = c->bin_s.data();
+  env.pre_resolve = c->pre_resolve;
+  env.pre_spec = c->pre_spec;
+  env.debug = c->debug;
+  env.target = c->target.data();
+  env.strand = c->strand.data();
+  env.walk_dump = c->wd.empty() ? nullptr : c->wd.data();
+  // round B on the copy stream (a hardware queue of its own, otherwise idle): on st_b it queued behind the split
+  // passes' index appends and peer-tile builds, which wait for the next counting half -- about one counting launch of
+  // latency on the host's critical path per block with deferred queries (UMICLUST_RB_STREAM=b: st_b)
+  auto round_b = [&](const std::vector<uint32_t>& bpq, const std::vector<uint32_t>& bpt, std::vector<uint32_t>& bres) {
     const int32_t nb = (int32_t)bpq.size();
-    c->stats.pairs_round_b += nb;
-    for (int32_t x = 0; x < nb; x++) c->stats.cells_computed += (int64_t)c->hlen[bpq[x] >> 1] * c->hlen[bpt[x]];
-    std::vector<uint32_t> bres(nb);
-    if (nb > 0) {
-      hipStream_t sb = c->st_b;
-      c->hip(c->d_bpq.ensure(nb), "alloc");
-      c->hip(c->d_bpt.ensure(nb), "alloc");
-      c->hip(c->d_bres.ensure(nb), "alloc");
-      c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
-      c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
-      c->hip(hipEventRecord(c->evb[0], sb), "event");
-      // the pairs are in query order: one launch per run of one query length
-      for (int32_t x0 = 0; x0 < nb;) {
-        const int32_t L = c->hlen[bpq[x0] >> 1];
-        int32_t x1 = x0 + 1;
-        while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
-        c->hip(launch_align(dev_seqs(c), L, c->ambig, c->d_bpq.p + x0, c->d_bpt.p + x0, x1 - x0, nullptr, nullptr, c->sc,
-                            c->d_bres.p + x0, sb, c->band_pairs),
-               "align B");
-        x0 = x1;
-      }
-      c->hip(hipEventRecord(c->evb[1], sb), "event");
-      c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
-      c->hip(hipStreamSynchronize(sb), "sync");
-      c->hip(hipEventElapsedTime(&ms, c->evb[0], c->evb[1]), "elapsed");
-      t_al += ms * 1e-3;
+    hipStream_t sb = c->rb_on_b ? c->st_b : c->st_copy;
+    c->hip(c->d_bpq.ensure(nb), "alloc");
+    c->hip(c->d_bpt.ensure(nb), "alloc");
+    c->hip(c->d_bres.ensure(nb), "alloc");
+    c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+    c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+    c->hip(hipEventRecord(c->evb[0], sb), "event");
+    // the pairs are in query order: one launch per run of one query length
+    for (int32_t x0 = 0; x0 < nb;) {
+      const int32_t L = c->hlen[bpq[x0] >> 1];
+      int32_t x1 = x0 + 1;
+      while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
+      c->hip(launch_align(dev_seqs(c), L, c->ambig, c->d_bpq.p + x0, c->d_bpt.p + x0, x1 - x0, nullptr, nullptr, c->sc,
+                          c->d_bres.p + x0, sb, c->band_pairs),
+             "align B");
+      x0 = x1;
     }
-    const double th2 = now_s();
-    extra_row.assign((size_t)nqs, -1);
-    for (size_t r = 0; r < deferred.size(); r++)
-      for (int s = 0; s < both; s++) extra_row[(size_t)deferred[r] * both + s] = (int32_t)(r * both + s);
-    extra_res.assign(deferred.size() * both * kSlots, 0);
-    extra_have.assign(deferred.size() * both * kSlots, 0);
-    for (int32_t x = 0; x < nb; x++) {
-      const int32_t qs = (int32_t)(bidx[x] / kSlots), e = (int32_t)(bidx[x] % kSlots);
-      extra_res[(size_t)extra_row[qs] * kSlots + e] = bres[x];
-      extra_have[(size_t)extra_row[qs] * kSlots + e] = 1;
-    }
-    for (int32_t ql : deferred)
-      if (!resolve(ql, true, strand_outcome))
-        c->fail(UMICLUST_EDEVICE, "internal: deferred query %d still unresolved", q0 + ql);
-    t_host += now_s() - th2;
-    std::sort(new_cents.begin(), new_cents.end());
+    c->hip(hipEventRecord(c->evb[1], sb), "event");
+    c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
+    c->hip(hipStreamSynchronize(sb), "sync");
+    float bms = 0;
+    c->hip(hipEventElapsedTime(&bms, c->evb[0], c->evb[1]), "elapsed");
+    t_al += bms * 1e-3;
+  };
+  // UMICLUST_RESOLVE_DUMP: the pass's inputs, round-B pairs / results and outputs, for the host-only replay
+  // (tools/resolve_tsan_main.cpp: the ThreadSanitizer harness of the CPU suite)
+  const bool dump = c->resolve_dump && !c->pack_on && c->dump_want(c->n_resolved);
+  c->n_resolved++;
+  std::vector<uint32_t> dpq, dpt, dres;
+  std::vector<uint8_t> state_in;
+  if (dump) state_in.assign(&state[w0], &state[w0] + (q0 + nq - w0));
+  RoundB round_b_rec = [&](const std::vector<uint32_t>& bpq, const std::vector<uint32_t>& bpt, std::vector<uint32_t>& bres) {
+    round_b(bpq, bpt, bres);
+    dpq.insert(dpq.end(), bpq.begin(), bpq.end());
+    dpt.insert(dpt.end(), bpt.begin(), bpt.end());
+    dres.insert(dres.end(), bres.begin(), bres.end());
+  };
+  ResolveStats rs;
+  const double th0 = now_s();
+  const int r = resolve_block(env, q0, nq, w0, hq, recs, state, P.rsx, *c->pool, new_cents, rs,
+                              dump ? round_b_rec : RoundB(round_b));
+  const double th = now_s() - th0;
+  if (r == kResolveOverflow) return false;
+  if (r == kResolveStuck) c->fail(UMICLUST_EDEVICE, "internal: a deferred query of block %d is still unresolved", q0);
+  if (dump)
+    write_resolve_dump(c, env, q0, nq, w0, state, state_in, hq, recs, *P.h_reccount.p, dpq, dpt, dres, new_cents, rs);
+  t_host += th - rs.t_round_b_s;
+  c->stats.t_host_pass1_s += rs.t_classify_s + rs.t_inorder_s;
+  c->dbg_t[3] += rs.t_classify_s;
+  c->dbg_t[4] += rs.t_inorder_s;
+  c->stats.n_alignments += rs.n_alignments;
+  c->stats.cells += rs.cells;
+  c->stats.n_merged_walks += rs.n_merged_walks;
+  c->stats.t_merged_s += rs.t_merged_s;
+  c->stats.n_deferred += rs.n_deferred;
+  c->stats.pairs_round_b += rs.pairs_round_b;
+  c->stats.cells_computed += rs.cells_round_b;
+  for (int i = 0; i < 4; i++) {
+    c->dbg[i] += rs.dbg[i];
+    c->dbg_p[i] += rs.dbg_p[i];
+    c->dbg_q[i] += rs.dbg_q[i];
   }
-  c->stats.n_merged_walks += scr0.merged;
   return true;
 }
 
@@ -2681,6 +2150,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   }
   if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
   if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_RB_STREAM")) c->rb_on_b = e[0] == 'b';
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_RAL")) c->r_on_al = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
@@ -2708,6 +2178,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* b = getenv("UMICLUST_BLOCK_DIV")) c->block_div = std::max(0, atoi(b));
   if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PEER_CERT")) c->peer_cert = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {

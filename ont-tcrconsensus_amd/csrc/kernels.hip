@@ -227,6 +227,180 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ 
   }
 }
 
+// K1, wave form (the default; UMICLUST_PREP=thread selects k_prep above): one wave per sorted sequence, lane x
+// holding residue positions x and x + 64.  DUST (mask.cc dust() / wo()): per 64-nt window (every 32 nt) lane i runs
+// wo()'s inner loop for start i over its own triplet counts (a lane-private LDS row); wo()'s result is the
+// lexicographically first (i, j) with the largest floor(10 sum / j) -- its strict `v > bestv` update never replaces
+// an equal value -- so the window's best is the lanes' (v desc, i asc) maximum with the winner's own first j.
+// Codes: 14 lanes pack 8 nibbles each.  Unique 8-mers (unique.cc): each lane builds the k-mers ending at its two
+// positions (masked windows and short prefixes become distinct sentinels above every code), a bitonic sort of the
+// 128 keys across the wave, then neighbour comparison and a ballot compaction -- ascending, as the thread form.
+constexpr int kDustRow = 17;  // dwords per lane-private count row (64 u8 counters + 1: rotates the banks per lane)
+
+__global__ __launch_bounds__(64) void k_prep_wave(const char* __restrict__ ascii, const int64_t* __restrict__ offs,
+                                                  const int32_t* __restrict__ perm, int32_t n, int dust,
+                                                  uint32_t* __restrict__ codes, uint8_t* __restrict__ lens,
+                                                  uint16_t* __restrict__ kmers, uint8_t* __restrict__ nk,
+                                                  char* __restrict__ masked, uint32_t* __restrict__ ambig) {
+  __shared__ uint8_t s_c2[2][kMaxLen + 8];   // 2-bit bases of the + strand and of its reverse complement
+  __shared__ uint8_t s_c4[kMaxLen + 8];      // 4-bit codes of the output characters
+  __shared__ uint8_t s_w[64];                // the DUST window's triplet words
+  __shared__ uint32_t s_cnt[64 * kDustRow];  // lane-private triplet counts
+  const int lane = (int)threadIdx.x;
+  const int s = (int)blockIdx.x;
+  if (s >= n) return;
+  const int r = perm ? perm[s] : s;
+  const int64_t b = offs[r];
+  const int len = (int)(offs[r + 1] - b);
+  const bool in0 = lane < len, in1 = lane + 64 < len;
+  const uint8_t ch0 = in0 ? (uint8_t)ascii[b + lane] : (uint8_t)0, ch1 = in1 ? (uint8_t)ascii[b + 64 + lane] : (uint8_t)0;
+  const uint32_t a0 = c_map4[ch0], a1 = c_map4[ch1];  // 0 past the sequence
+  if (in0) {
+    s_c2[0][lane] = (uint8_t)code2_of4(a0);
+    s_c2[1][len - 1 - lane] = (uint8_t)code2_of4(comp4(a0));
+  }
+  if (in1) {
+    s_c2[0][lane + 64] = (uint8_t)code2_of4(a1);
+    s_c2[1][len - 65 - lane] = (uint8_t)code2_of4(comp4(a1));
+  }
+  __syncthreads();
+  bool m0 = false, m1 = false;  // DUST-masked at positions lane, lane + 64
+  if (dust) {
+    for (int i0 = 0; i0 < len; i0 += 32) {
+      const int l = len - i0 < 64 ? len - i0 : 64;
+      const int l1 = l - 3 + 1 - 5;  // wo(): smallest region 8
+      if (l1 < 0) continue;         // wo() returns 0: nothing masked
+      if (lane < l) {
+        uint32_t w = s_c2[0][i0 + lane];
+        if (lane >= 1) w |= (uint32_t)s_c2[0][i0 + lane - 1] << 2;
+        if (lane >= 2) w |= (uint32_t)s_c2[0][i0 + lane - 2] << 4;
+        s_w[lane] = (uint8_t)(w & 63u);
+      }
+      __syncthreads();
+      int bv = 0, bj = 0;
+      if (lane < l1) {
+        uint32_t* row = s_cnt + lane * kDustRow;
+#pragma unroll
+        for (int x = 0; x < 16; x++) row[x] = 0u;
+        uint8_t* cnt = reinterpret_cast<uint8_t*>(row);
+        int sum = 0;
+        for (int j = 2; j < l - lane; j++) {
+          const int x = s_w[lane + j];
+          const int c = cnt[x];
+          if (c) {
+            sum += c;
+            // v = 10*sum/j (integer); v > bv  <=>  10*sum >= (bv+1)*j
+            if (10 * sum >= (bv + 1) * j) {
+              bv = (10 * sum) / j;
+              bj = j;
+            }
+          }
+          cnt[x] = (uint8_t)(c + 1);
+        }
+      }
+      uint32_t key = lane < l1 ? ((uint32_t)bv << 8) | (uint32_t)(63 - lane) : 0u;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) key = max(key, (uint32_t)__shfl_xor((int)key, d, 64));
+      const int bestv = (int)(key >> 8), besti = 63 - (int)(key & 255u);
+      const int bestj = __shfl(bj, besti, 64);
+      if (bestv > 20) {
+        const int lo = i0 + besti, hi = i0 + besti + bestj;
+        m0 = m0 || (lane >= lo && lane <= hi);
+        m1 = m1 || (lane + 64 >= lo && lane + 64 <= hi);
+      }
+      __syncthreads();  // s_w is rewritten by the next window
+    }
+  }
+  // output characters: dust() upper-cases the sequence and lower-cases the masked intervals
+  auto fin = [&](uint8_t c, bool m) -> uint8_t {
+    const uint8_t up = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+    return dust ? (m ? (uint8_t)(up | 0x20) : up) : c;
+  };
+  const uint8_t f0 = fin(ch0, m0), f1 = fin(ch1, m1);
+  if (masked) {
+    if (in0) masked[(int64_t)s * kMaxLen + lane] = (char)f0;
+    if (in1) masked[(int64_t)s * kMaxLen + 64 + lane] = (char)f1;
+  }
+  const uint32_t c40 = c_map4[f0], c41 = c_map4[f1];
+  auto amb = [](uint32_t c4) { return c4 != 1u && c4 != 2u && c4 != 4u && c4 != 8u; };
+  const unsigned long long anyamb = __ballot((in0 && amb(c40)) || (in1 && amb(c41)));
+  if (lane == 0) {
+    lens[s] = (uint8_t)len;
+    if (anyamb && ambig) atomicOr(ambig, 1u);
+  }
+  if (in0) s_c4[lane] = (uint8_t)c40;
+  if (in1) s_c4[lane + 64] = (uint8_t)c41;
+  const unsigned long long mlo = __ballot(m0), mhi = __ballot(m1);
+  __syncthreads();
+  if (lane < kCodeWords) {
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const int p = lane * 8 + t;
+      if (p < len) {
+        w0 |= (uint32_t)s_c4[p] << (4 * t);
+        w1 |= comp4(s_c4[len - 1 - p]) << (4 * t);
+      }
+    }
+    codes[((int64_t)s * 2 + 0) * kCodeWords + lane] = w0;
+    codes[((int64_t)s * 2 + 1) * kCodeWords + lane] = w1;
+  }
+  // any masked original position in [p, p + 8)
+  auto win8 = [&](int p) -> bool {
+    unsigned long long v;
+    if (p >= 64) v = mhi >> (p - 64);
+    else v = (mlo >> p) | (p > 0 ? (mhi << (64 - p)) : 0ull);
+    return (v & 0xffull) != 0ull;
+  };
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int st = 0; st < 2; st++) {
+    uint32_t k[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int y = lane + 64 * h;  // the k-mer ending at strand position y
+      bool ok = y < len && y >= 7;
+      if (ok) ok = !win8(st ? len - 1 - y : y - 7);
+      uint32_t km = 0;
+      if (ok)
+#pragma unroll
+        for (int t = 0; t < 8; t++) km = (km << 2) | s_c2[st][y - 7 + t];
+      k[h] = ok ? km : (0x10000u | (uint32_t)y);
+    }
+    // bitonic sort of the 128 keys (element e = lane + 64 h), ascending
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1)
+#pragma unroll
+      for (int d = size >> 1; d > 0; d >>= 1) {
+        if (d == 64) {
+          const uint32_t lo = min(k[0], k[1]), hi = max(k[0], k[1]);
+          k[0] = lo;
+          k[1] = hi;
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int e = lane + 64 * h;
+            const uint32_t o = (uint32_t)__shfl_xor((int)k[h], d, 64);
+            const bool asc = (e & size) == 0, lower = (e & d) == 0;
+            k[h] = (lower == asc) ? min(k[h], o) : max(k[h], o);
+          }
+        }
+      }
+    // neighbours (every lane takes part in every shuffle: a shuffle from a lane outside EXEC reads nothing useful)
+    const uint32_t p0 = (uint32_t)__shfl_up((int)k[0], 1, 64);
+    const uint32_t k063 = (uint32_t)__shfl((int)k[0], 63, 64);
+    const uint32_t k1up = (uint32_t)__shfl_up((int)k[1], 1, 64);
+    const uint32_t p1 = lane == 0 ? k063 : k1up;
+    const bool u0 = k[0] < 0x10000u && (lane == 0 || k[0] != p0);
+    const bool u1 = k[1] < 0x10000u && k[1] != p1;
+    const unsigned long long b0 = __ballot(u0), b1 = __ballot(u1);
+    const int n0 = __builtin_popcountll(b0);
+    uint16_t* dst = kmers + ((int64_t)s * 2 + st) * kKmerStride;
+    if (u0) dst[__builtin_popcountll(b0 & lt)] = (uint16_t)k[0];
+    if (u1) dst[n0 + __builtin_popcountll(b1 & lt)] = (uint16_t)k[1];
+    if (lane == 0) nk[(int64_t)s * 2 + st] = (uint8_t)(n0 + __builtin_popcountll(b1));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_iota(int32_t* __restrict__ out, int32_t n) {
   const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
   if (i < n) out[i] = i;
@@ -244,8 +418,14 @@ hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* pe
   hipError_t e = ensure_maps(st);
   if (e != hipSuccess) return e;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prep, dim3((n + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0, st,
-                     ascii, offs, perm, n, dust, codes, lens, kmers, nk, masked, ambig);
+  // UMICLUST_PREP=thread: the one-thread-per-sequence form (A/B and cross-checks)
+  static const bool per_thread = getenv("UMICLUST_PREP") && getenv("UMICLUST_PREP")[0] == 't';
+  if (per_thread)
+    hipLaunchKernelGGL(k_prep, dim3((n + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0, st,
+                       ascii, offs, perm, n, dust, codes, lens, kmers, nk, masked, ambig);
+  else
+    hipLaunchKernelGGL(k_prep_wave, dim3((unsigned)n), dim3(64), 0, st, ascii, offs, perm, n, dust, codes, lens, kmers,
+                       nk, masked, ambig);
   return hipGetLastError();
 }
 
@@ -1936,20 +2116,51 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
                                                     uint32_t* __restrict__ outidx, SegTab sg, uint32_t* __restrict__ seg_cnt,
                                                     unsigned long long* __restrict__ cells, uint32_t* __restrict__ nstat,
                                                     uint32_t out0, const uint8_t* __restrict__ strong,
-                                                    unsigned long long* __restrict__ aligned, int32_t emit) {
+                                                    unsigned long long* __restrict__ aligned, int32_t emit,
+                                                    const WalkState* __restrict__ ws_prev,
+                                                    const uint8_t* __restrict__ npeer_prev, int32_t q0_prev,
+                                                    int32_t nq_prev) {
   // one thread per (query, strand); the slots come from a wave-aggregated allocation per query length (seg_alloc)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = qs < nqs;  // every lane stays to the slot allocation
   const int np = live ? npeer[qs] : 0;
   if (live) aligned[(int64_t)qs * 2] = aligned[(int64_t)qs * 2 + 1] = 0ull;
   unsigned long long rel[2] = {0ull, 0ull};  // peers 0..63, 64..127 (kPeerCap)
+  // A peer whose own device walk has already accepted a hit -- within its first w candidates, with w plus its
+  // in-window peer count <= kWalk, so no merge can push that hit out of its walk -- is certain to become a member,
+  // and members never enter a query's merged walk: its alignment would never be read.  The peer's walk state is
+  // this pass's (an in-block peer, after round 0's evaluation) or the previous block's pass's (final).  (A peer
+  // judged wrongly would only cost a round-B alignment: the host aligns every needed peer the pass did not.)
+  const int32_t nqb = nqs / both;
+  auto certain_member = [&](uint32_t ps) -> bool {
+    const WalkState* W;
+    const uint8_t* NP;
+    int32_t base;
+    if ((int32_t)ps >= q0 && (int32_t)ps < q0 + nqb) {
+      W = ws;
+      NP = npeer;
+      base = q0;
+    } else if (ws_prev && (int32_t)ps >= q0_prev && (int32_t)ps < q0_prev + nq_prev) {
+      W = ws_prev;
+      NP = npeer_prev;
+      base = q0_prev;
+    } else {
+      return false;
+    }
+    for (int s = 0; s < both; s++) {
+      const int64_t i = (int64_t)((int32_t)ps - base) * both + s;
+      const uint32_t n = NP[i];
+      if (W[i].acc && n != 255u && (uint32_t)W[i].w + n <= (uint32_t)kWalk) return true;
+    }
+    return false;
+  };
   if (live && np != 255 && np != 0 && emit) {
     const WalkState w = ws[qs];
     for (int x = 0; x < np; x++) {
       const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
       if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
-          !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])))
+          !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])) && !certain_member(ps))
         rel[x >> 6] |= 1ull << (x & 63);
     }
     aligned[(int64_t)qs * 2] = rel[0];
@@ -1981,10 +2192,12 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, const SegTab& sg,
                              uint32_t* seg_cnt, unsigned long long* cells, uint32_t* nstat, uint32_t out0,
-                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, hipStream_t st) {
+                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
+                             const uint8_t* npeer_prev, int32_t q0_prev, int32_t nq_prev, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, strong, aligned, emit);
+                     peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, strong, aligned, emit, ws_prev,
+                     npeer_prev, q0_prev, nq_prev);
   return hipGetLastError();
 }
 
@@ -2202,6 +2415,27 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   // both sequences' code words in VGPRs (lane w holds word w): the backtrack reads them by v_readlane
   // instead of a global / LDS load per diagonal step
   const uint32_t qword = lane < kCodeWords ? qcp[lane] : 0u, tword = lane < kCodeWords ? tcp[lane] : 0u;
+  // identical sequences of one-hot codes (a member equal to its centroid: about (1 - error)^L of them): the all-M
+  // path is the only optimum -- any other path trades matches for gaps or mismatches -- so its ops, matches and
+  // internal length are known without the DP (codes past the length are 0 in both)
+  if (ql == tl) {
+    bool same = qword == tword;
+    if (same && lane < kCodeWords)
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const uint32_t c = (qword >> (4 * e)) & 15u;
+        same = same && (lane * 8 + e >= ql || (c != 0u && (c & (c - 1u)) == 0u));
+      }
+    if (__all(same)) {
+      uint8_t* o = ops + (int64_t)k * kOpsStride + (kOpsStride - ql);
+      for (int x = lane; x < ql; x += 64) o[x] = (uint8_t)'M';
+      if (lane == 0) {
+        nops[k] = (uint16_t)ql;
+        out[k] = (uint32_t)ql | ((uint32_t)ql << 8) | (((uint32_t)(ql * sc.match)) & 0xffffu) << 16;
+      }
+      return;
+    }
+  }
   const int QRti = sc.go[3] + sc.ge[3], Rti = sc.ge[3];
   const int QRtr = sc.go[5] + sc.ge[5], Rtr = sc.ge[5];
   const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];

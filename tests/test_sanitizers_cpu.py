@@ -233,3 +233,39 @@ def test_host_argv_under_asan(host_asan):
     assert host_asan("argv", "vsearch", "--gapopen", "4X", "--cluster_fast", "a").strip() == "rc -22"
     assert host_asan("argv", "vsearch", "--cluster_fast").strip() == "rc -22"
     assert host_asan("argv", "vsearch", "--cluster_fast", "x" * 300).strip() == "rc -22"  # longer than the buffer
+
+
+# ---- the host resolve (ont-tcrconsensus_amd/csrc/resolve.cpp) under ThreadSanitizer ----
+# resolve_block's classify phase runs on a worker pool over the window's states and the pass's records while the
+# in-order phase writes the block's states; tools/resolve_tsan_main.cpp replays resolve_block calls recorded from
+# GPU clustering runs (tests/golden/make_resolve_dumps.py: a config-2-like bin, lazy peers with round B, deep
+# clusters, batched O4 rounds) with 1, 3 and 8 threads and checks every output against the recorded one.
+RESOLVE_DUMPS = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "resolve", "*.bin.gz")))
+
+
+@pytest.fixture(scope="module")
+def resolve_tsan(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    out = str(tmp_path_factory.mktemp("resolve_tsan"))
+    exe = os.path.join(out, "resolve_tsan")
+    src = os.path.join(ROOT, "ont-tcrconsensus_amd", "csrc")
+    b = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-o", exe,
+                        os.path.join(ROOT, "tools", "resolve_tsan_main.cpp"), os.path.join(src, "resolve.cpp"),
+                        "-lpthread"], capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr
+    return exe, out
+
+
+@pytest.mark.skipif(not RESOLVE_DUMPS, reason="no recorded resolve dumps")
+@pytest.mark.parametrize("path", RESOLVE_DUMPS, ids=[os.path.basename(p)[:-7] for p in RESOLVE_DUMPS])
+def test_host_resolve_under_tsan(resolve_tsan, path):
+    exe, out = resolve_tsan
+    raw = os.path.join(out, os.path.basename(path)[:-3])
+    with gzip.open(path, "rb") as fi, open(raw, "wb") as fo:
+        fo.write(fi.read())
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, raw], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.stdout.count(": equal") == 3, r.stdout
