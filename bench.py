@@ -164,6 +164,25 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
                      "traffic is `traffic`); peak = L2-served gather rate, MI355X_MICROARCH.md (1,152-B rows). "
                      "What binds it is instruction issue, not bytes: VALU and LDS-atomic issue per posting "
                      "(profiles/r02/pmc_pf_count_c2.json)")
+    # against the LDS atomic ceiling (what binds it: LDS array busy 0.69, 60 % of it bank-conflict replays): one
+    # ds_add_u32 wave-instruction per 64 postings streamed, 4.32 cycles per wave-instruction per CU at best
+    # (tools/pmc_calib.hip, conflict-free), at the clock measured during the kernel (GRBM_GUI_ACTIVE / 8 / duration of
+    # its dispatches in a PMC run: tools/pmc_clock.py)
+    cal_p = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
+    clk_p = os.path.join(ROOT, "profiles", "r04", "pmc_clock_k_pf_count.json")
+    if os.path.exists(cal_p) and os.path.exists(clk_p) and n_cnt:
+        cal, clk = json.load(open(cal_p)), json.load(open(clk_p))
+        atom = streamed / 64.0 / n_cnt
+        ghz = clk["clock_ghz"]
+        ceil_ms = atom * cal["ds_add_u32_cycles_per_instr_per_cu"] / cal["cus"] / (ghz * 1e9) * 1e3
+        roof["lds"] = dict(bound="lds-atomic issue", atomic_wave_instrs_per_launch=atom,
+                           cycles_per_instr_per_cu=cal["ds_add_u32_cycles_per_instr_per_cu"], clock_ghz=ghz,
+                           clock_source=os.path.relpath(clk_p, ROOT), ceiling_ms=ceil_ms,
+                           frac=ceil_ms / roof["avg_launch_ms"], solo_launch_ms=clk.get("mean_us", 0) / 1e3 or None,
+                           frac_solo=(ceil_ms / (clk["mean_us"] / 1e3)) if clk.get("mean_us") else None,
+                           note="frac = the conflict-free atomic issue time of the launch's postings / its launch time "
+                                "in the step (shared with the alignment chain); frac_solo against its duration alone "
+                                "(PMC-serialised dispatches)")
     cells = sum(s["cells"] for s in stats)
     cells_c = sum(s["cells_computed"] for s in stats)
     g_alg = cells / t_al / 1e9 if t_al else 0.0
@@ -245,6 +264,13 @@ def main() -> None:
     ap.add_argument("--shard-sweep", type=int, default=0,
                     help="configs 3/4, one GPU: time every LPT share of an N-GPU node one after another (plus the largest "
                          "bin alone) in one process; the largest share time is the measured N-GPU makespan bound")
+    ap.add_argument("--e2e-files", action="store_true",
+                    help="config 4 at the file boundary: per-bin FASTA inputs, round 1 through the fused drop-in "
+                         "(clustering + parse outputs), round-2 FASTA from its consensus, round 2 to files, every bin "
+                         "on `lanes` concurrent contexts (tcr_consensus.py:231-267, :411-446)")
+    ap.add_argument("--read-len", type=int, default=32,
+                    help="--e2e-files: length of the synthetic full read in each header's seq= field (SURVEY §8d "
+                         "--short-read: 32 keeps 70M records at ~19 GB; production reads are ~1,500 nt)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -266,6 +292,8 @@ def main() -> None:
     from umiclust import _lib, binset, shard, synth
     if args.shard_sweep:
         return shard_sweep(args)
+    if args.e2e_files:
+        return e2e_files(args)
     # multi-bin inputs are generated before anything touches the GPU (spawned workers)
     bins = None
     if args.config in (3, 4):
@@ -453,6 +481,161 @@ def main() -> None:
         ctx2.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _write_bin_fastas(job):
+    """Worker (process pool): write the round's input FASTA of each (bin, path)."""
+    from umiclust import synth
+    out = []
+    for b, path, read_len in job:
+        synth.write_umi_fasta_fast(path, b.umis, seed=b.seed, read_len=read_len, chunk=16384)
+        out.append(os.path.getsize(path))
+    return out
+
+
+def _read_consout(path: str) -> tuple[list, list]:
+    """(consensus sequences, cluster sizes) of a consout FASTA (`>centroid=...;seqs=N;clusterid=K`), file order."""
+    cons, sizes = [], []
+    with open(path, "rb") as fh:
+        hdr = None
+        for line in fh:
+            line = line.rstrip(b"\n")
+            if line.startswith(b">"):
+                hdr = line
+                f = line.split(b";")
+                sizes.append(int(next(x for x in reversed(f) if x.startswith(b"seqs="))[5:]))
+                cons.append("")
+            elif hdr is not None:
+                cons[-1] += line.decode()
+    return cons, sizes
+
+
+def e2e_files(args) -> None:
+    """BASELINE config 4 at the drop-in's file boundary on one GPU (the rank share of --shard-of/--shard, or every
+    bin): round 1 = per bin `vsearch --cluster_fast` + parse_umi_clusters (tcr_consensus.py:231-267; here the fused
+    drop-in umiclust_run_fasta_parse: consout + clusters_fa/ + smolecule_clusters.fa + stats), round 2 = per bin the
+    consensus molecules' UMIs clustered to cluster<N> files + consout and parsed (:411-446).  Inputs (the per-bin
+    FASTA region_split / extract_umis would leave; round 2's stands in for medaka + extract_umis on the consensus
+    reads: synth.round2_bin) are written untimed; each round is timed from the first read to the last file written,
+    its bins on `lanes` concurrent device contexts (one vsearch process per bin in the reference)."""
+    import concurrent.futures as cf
+    import shutil
+    import tempfile
+    import torch
+    from umiclust import _lib, binset, shard, synth
+    if args.config != 4:
+        raise SystemExit("--e2e-files: config 4")
+    lens = synth.CONFIG_LENGTHS[4]
+    ident = args.identity if args.identity is not None else 0.93
+    workers = min(16, os.cpu_count() or 4)
+    all_bins = synth.config_bins(4, args.scale, workers=workers)
+    costs = [shard.bin_cost(b.umis.n) for b in all_bins]
+    sel = shard.lpt_assign(costs, args.shard_of)[args.shard] if args.shard_of > 0 else list(range(len(all_bins)))
+    bins = [all_bins[i] for i in sel]
+    base = os.environ.get("UMICLUST_E2E_DIR")
+    if not base:
+        try:
+            st_ = os.statvfs("/dev/shm")
+            base = "/dev/shm" if os.access("/dev/shm", os.W_OK) and st_.f_bavail * st_.f_frsize > (200 << 30) else None
+        except OSError:
+            base = None
+    base = base or os.environ.get("TMPDIR", "/tmp")
+    root = tempfile.mkdtemp(prefix="umiclust_c4e2e_", dir=base)
+    try:
+        dirs = [os.path.join(root, f"b{i:04d}") for i in range(len(bins))]
+        for d in dirs:
+            os.mkdir(d)
+        t0 = time.perf_counter()
+
+        def write_all(paths_bins):
+            jobs = [[] for _ in range(workers)]
+            order = sorted(range(len(paths_bins)), key=lambda i: -paths_bins[i][0].umis.n)
+            load = [0] * workers
+            for i in order:  # LPT over the writer processes
+                w = min(range(workers), key=lambda k: load[k])
+                jobs[w].append((paths_bins[i][0], paths_bins[i][1], args.read_len))
+                load[w] += paths_bins[i][0].umis.n
+            with cf.ProcessPoolExecutor(workers) as ex:
+                return sum(sum(x) for x in ex.map(_write_bin_fastas, jobs))
+        in1 = [os.path.join(d, "region_cluster_detected_umis.fasta") for d in dirs]
+        bytes1 = write_all(list(zip(bins, in1)))
+        t_gen1 = time.perf_counter() - t0
+        torch.cuda.set_device(0)
+        lanes = max(1, min(args.lanes, len(bins)))
+        ctxs = [_lib.Context(0) for _ in range(lanes)]
+        plan = shard.lpt_assign([shard.bin_cost(b.umis.n) for b in bins], lanes)
+        p1 = _lib.params(_lib.PRESET_ROUND1, ident, *lens)
+        p2 = _lib.params(binset.ROUND2["preset"], binset.ROUND2["identity"], *lens)
+        pp1 = _lib.ParseParams(min_reads_per_cluster=4, max_reads_per_cluster=60, balance_strands=0, max_clusters=0)
+        pp2 = _lib.ParseParams(min_reads_per_cluster=1, max_reads_per_cluster=60, balance_strands=0, max_clusters=0)
+        # warm-up (untimed): one small bin through both paths, so allocations and code objects are not timed
+        wi = min(range(len(bins)), key=lambda i: bins[i].umis.n)
+        wd = os.path.join(root, "warm")
+        os.mkdir(wd)
+        ctxs[0].run_fasta_parse(p1, in1[wi], None, os.path.join(wd, "c.fa"), None, pp1, wd)
+        shutil.rmtree(wd)
+
+        def run_round(rnd):
+            per = [None] * len(bins)
+
+            def lane(li):
+                for i in plan[li]:
+                    d = os.path.join(dirs[i], f"round{rnd}")
+                    os.mkdir(d)
+                    t = time.perf_counter()
+                    if rnd == 1:
+                        st, pr = ctxs[li].run_fasta_parse(p1, in1[i], None, os.path.join(d, "umi_clusters_consensus.fasta"),
+                                                          os.path.join(d, "vsearch_cluster.log"), pp1, d)
+                    else:
+                        st, pr = ctxs[li].run_fasta_parse(p2, in2[i], os.path.join(d, "cluster"),
+                                                          os.path.join(d, "umi_clusters_consensus.fasta"),
+                                                          os.path.join(d, "vsearch_cluster_consensus.log"), pp2, d)
+                    per[i] = dict(seconds=time.perf_counter() - t, kept=st["n_kept"], clusters=st["n_clusters"],
+                                  t_read_s=st["t_read_s"], t_cluster_s=st["t_total_s"], t_write_s=st["t_write_s"],
+                                  written=pr["n_written"])
+            t0_ = time.perf_counter()
+            with cf.ThreadPoolExecutor(lanes) as ex:
+                list(ex.map(lane, range(lanes)))
+            wall = time.perf_counter() - t0_
+            nf, nb = 0, 0
+            for d in dirs:
+                f, b = _tree_bytes(os.path.join(d, f"round{rnd}"))
+                nf += f
+                nb += b
+            tot = lambda k: sum(x[k] for x in per)  # noqa: E731
+            return dict(wall_s=wall, umis_kept=int(tot("kept")), umis_per_s=tot("kept") / wall, clusters=int(tot("clusters")),
+                        clusters_written=int(tot("written")), sum_read_s=tot("t_read_s"), sum_cluster_s=tot("t_cluster_s"),
+                        sum_write_s=tot("t_write_s"), largest_bin_s=max(x["seconds"] for x in per),
+                        files_written=nf, bytes_written=nb), per
+        r1, per1 = run_round(1)
+        # round-2 inputs from round 1's consout (untimed: medaka + extract_umis stand-in)
+        t0 = time.perf_counter()
+        b2 = []
+        for i, b in enumerate(bins):
+            cons, sizes = _read_consout(os.path.join(dirs[i], "round1", "umi_clusters_consensus.fasta"))
+            b2.append(synth.round2_bin(b, cons, sizes))
+        in2 = [os.path.join(d, "consensus_umis.fasta") for d in dirs]
+        bytes2 = write_all(list(zip(b2, in2)))
+        t_gen2 = time.perf_counter() - t0
+        r2, _ = run_round(2)
+        for c in ctxs:
+            c.close()
+        wall = r1["wall_s"] + r2["wall_s"]
+        kept = r1["umis_kept"] + r2["umis_kept"]
+        out = {"metric": METRIC, "value": kept / wall, "unit": "UMIs/s", "n_gpus": 1, "steps": 1, "warmup": 1,
+               "ms_per_step": 1e3 * wall, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "int16/int32", "data": "synthetic",
+               "config": {"workload": f"BASELINE config 4 at the file boundary, scale {args.scale}: "
+                                      f"{sum(b.umis.n for b in bins)} reads in {len(bins)} bins"
+                                      + (f" (LPT share {args.shard} of {args.shard_of})" if args.shard_of else "")
+                                      + f", both rounds, {args.read_len}-nt seq= reads",
+                          "parallelism": f"one MI355X, {lanes} concurrent per-bin contexts", "output_dir": base},
+               "round1": r1, "round2": r2, "input_bytes": [bytes1, bytes2], "input_write_s": [t_gen1, t_gen2],
+               "note": "value = UMIs of both rounds / (round-1 wall + round-2 wall), each from its first FASTA read to "
+                       "its last file; inputs written untimed; RAM-backed output_dir when /dev/shm has room"}
+        print(json.dumps(out), flush=True)
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
 
 
 def shard_sweep(args) -> None:

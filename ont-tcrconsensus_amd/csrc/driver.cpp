@@ -380,7 +380,9 @@ struct umiclust_ctx {
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
-  bool peer_cert = true;          // UMICLUST_PEER_CERT=0: align relevant peers even when certain to become members
+  bool peer_cert = true;
+  bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
+  DevBuf<uint32_t> d_probe;          // UMICLUST_PEER_CERT=0: align relevant peers even when certain to become members
   int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
   int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
@@ -677,6 +679,32 @@ void set_defer(umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
   for (int i = 0; i < kFKmers; i++) a.fkmer[i] = c->fkmer[i];
 }
 
+// UMICLUST_PFPROBE=1 (measurement only): after every counting launch, the same launch without its count loop
+// (k_pf_count<2>) into scratch outputs, so a kernel trace shows what the table, zeroing, scan and output phases cost
+// on their own beside the full kernel
+void launch_pf_probe(umiclust_ctx* c, const PrefilterArgs& a, hipStream_t st) {
+  const size_t U = (size_t)a.nq * a.both * kParts;
+  const size_t words = U * kPartCand + U * (kPeerCap / 2) + 8 * U + 16 + U * (kPeerCap / 4);
+  c->hip(c->d_probe.ensure(words), "alloc probe");
+  uint32_t* p = c->d_probe.p;
+  PrefilterArgs b = a;
+  b.pcand = p;
+  p += U * kPartCand;
+  b.ppeer_id = reinterpret_cast<uint16_t*>(p);
+  p += U * (kPeerCap / 2);
+  b.ppost = p;
+  b.pdef = p + U;
+  b.pdm = p + 2 * U;
+  b.units = p + 3 * U;
+  b.pncand = reinterpret_cast<uint8_t*>(p + 4 * U);
+  b.pnpeer = reinterpret_cast<uint8_t*>(p + 5 * U);
+  b.nunits = p + 7 * U + 8;
+  b.ppeer_count = reinterpret_cast<uint8_t*>(p + 8 * U + 16);  // U * kPeerCap bytes
+  b.prof = nullptr;
+  c->hip(hipMemsetAsync(b.nunits, 0, 4, st), "memset");
+  c->hip(launch_prefilter(b, st, 3), "prefilter probe");
+}
+
 void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* const* prevs, int nprev, Tile& own,
                   int32_t region, bool lazy_peers = false, bool after_count = false) {
   const int32_t w0 = nprev > 0 ? prevs[0]->base : q0;
@@ -800,6 +828,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     c->hip(hipEventRecord(P.ev_c[0], st), "event");
     c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
     c->hip(hipEventRecord(P.ev_c[1], st), "event");
+    if (c->pf_probe) launch_pf_probe(c, a, st);
     c->hip(launch_prefilter(a, st, 2), "prefilter");
     P.c_timed = true;
   } else {
@@ -980,6 +1009,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
   c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
   c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
+  if (c->pf_probe) launch_pf_probe(c, a, st);
   c->last_a_slot = slot;
   P.a_live = true;
   P.a_q0 = q0;

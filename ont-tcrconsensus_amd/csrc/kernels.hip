@@ -596,9 +596,8 @@ struct PfShared {
     struct {                        // list table (count phase)
       uint32_t lstart[kPfLists + 66];  // first chunk of each non-empty list, then the chunk total
       uint32_t lbias[kPfLists];        // posting index of chunk g of list L: lbias[L] + 8 g
-      uint16_t wbase[kPfWinBase];      // the list holding chunk 64 w
-      uint32_t wlo[kPfWinBase];        // bit b (b > 0): a list starts at chunk 64 w + b (b < 32) ...
-      uint32_t whi[kPfWinBase];        // ... (b >= 32)
+      uint4 wtab[kPfWinBase];          // per 64-chunk window: x the list holding chunk 64 w, y / z bit b (b > 0):
+                                       // a list starts at chunk 64 w + b (b < 32 / b >= 32); one b128 read
     };
     uint32_t cand[kPfCand];         // candidate sub-ids, then 30-bit keys (scan / select phases)
   };
@@ -811,8 +810,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
 // every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's offsets, a
 // k-mer slot past nk reads list 0) and masked afterwards.  A packed block scan lays the non-empty lists
 // end to end as one stream of T 16-byte chunks: lstart[L] = first chunk of list L (then T), lbias[L] =
-// posting index of chunk g of list L minus 8 g; per 64-chunk window w < kPfWinBase, wbase[w] = the list
-// holding chunk 64 w and wlo/whi[w] bit b = a list starts at chunk 64 w + b (b > 0).  Ends with a barrier.
+// posting index of chunk g of list L minus 8 g; per 64-chunk window w < kPfWinBase, wtab[w].x = the list
+// holding chunk 64 w and wtab[w].y / .z bit b = a list starts at chunk 64 w + b (b > 0).  Ends with a barrier.
 // a part candidate for the merge: count << 24 | ordinal (ordinals stay below kMaxSegs * kSegCentroids < 2^23)
 static_assert(kMaxSegs * kSegCentroids < (1 << 24), "ordinal field");
 __device__ __forceinline__ uint32_t cand_entry(unsigned long long key64) {
@@ -821,9 +820,7 @@ __device__ __forceinline__ uint32_t cand_entry(unsigned long long key64) {
 struct PfTable {
   uint32_t* lstart;
   uint32_t* lbias;
-  uint16_t* wbase;
-  uint32_t* wlo;
-  uint32_t* whi;
+  uint4* wtab;  // per window {base list, start bits 0-31, start bits 32-63, 0}
   uint32_t* wsum;
 };
 __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, int t0, int nct, int ntl,
@@ -870,8 +867,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
   }
   if (clk) clk[0] = __builtin_readcyclecounter();  // phase probe: the list offsets have arrived
   // window start masks (set below, after block_excl_scan's barriers)
-  if (tid < kPfWinBase) tb.wlo[tid] = 0u;
-  else if (tid < 2 * kPfWinBase) tb.whi[tid - kPfWinBase] = 0u;
+  if (tid < kPfWinBase) tb.wtab[tid] = make_uint4(0u, 0u, 0u, 0u);
   // packed scan: chunks << kListBits | lists (see kListBits)
   uint32_t tot;
   const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
@@ -886,10 +882,10 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
       tb.lstart[li] = ci;
       tb.lbias[li] = bse[j] - 8u * ci;
       if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase)
-        atomicOr(((ci & 32u) ? tb.whi : tb.wlo) + (ci >> 6), 1u << (ci & 31u));
+        atomicOr(reinterpret_cast<uint32_t*>(tb.wtab + (ci >> 6)) + ((ci & 32u) ? 2 : 1), 1u << (ci & 31u));
       // windows whose first chunk lies in this list
       for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch[j] && w < (uint32_t)kPfWinBase; w++)
-        tb.wbase[w] = (uint16_t)li;
+        tb.wtab[w].x = li;
       li++;
       ci += nch[j];
     }
@@ -908,8 +904,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
 template <uint32_t kBase>
 __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
                                                 const uint32_t* lstart, const uint32_t* lbias,
-                                                const uint16_t* wbase, const uint32_t* wlo, const uint32_t* whi,
-                                                int lane, int wv) {
+                                                const uint4* wtab, int lane, int wv) {
   const uint32_t nwin = (T + 63u) >> 6;
   const unsigned long long below = (2ull << lane) - 1ull;  // lanes <= this one
   const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
@@ -918,8 +913,8 @@ __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, ui
     if (w >= nwin) return 0xffffffffu;
     const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
     if (w < (uint32_t)kPfWinBase) {
-      const uint32_t L0 = wbase[w] + (uint32_t)__builtin_popcount(wlo[w] & below_lo) +
-                          (uint32_t)__builtin_popcount(whi[w] & below_hi);
+      const uint4 t = wtab[w];  // one uniform b128 read (was three)
+      const uint32_t L0 = t.x + (uint32_t)__builtin_popcount(t.y & below_lo) + (uint32_t)__builtin_popcount(t.z & below_hi);
       return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
     }
     int lo = 0, hi = (int)nlc - 1;
@@ -966,8 +961,7 @@ constexpr int kPfPre = 16, kPfAhead = 4;
 template <uint32_t kBase>
 __device__ __forceinline__ void pf_count_stream_pre(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
                                                     const uint32_t* lstart, const uint32_t* lbias,
-                                                    const uint16_t* wbase, const uint32_t* wlo, const uint32_t* whi,
-                                                    int lane, int wv) {
+                                                    const uint4* wtab, int lane, int wv) {
   const uint32_t nwin = (T + 63u) >> 6;
   const unsigned long long below = (2ull << lane) - 1ull;
   const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
@@ -976,8 +970,8 @@ __device__ __forceinline__ void pf_count_stream_pre(__amdgpu_buffer_rsrc_t arena
     if (w >= nwin) return 0xffffffffu;
     const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
     if (w < (uint32_t)kPfWinBase) {
-      const uint32_t L0 = wbase[w] + (uint32_t)__builtin_popcount(wlo[w] & below_lo) +
-                          (uint32_t)__builtin_popcount(whi[w] & below_hi);
+      const uint4 t = wtab[w];  // one uniform b128 read (was three)
+      const uint32_t L0 = t.x + (uint32_t)__builtin_popcount(t.y & below_lo) + (uint32_t)__builtin_popcount(t.z & below_hi);
       return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
     }
     int lo = 0, hi = (int)nlc - 1;
@@ -1075,10 +1069,10 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
       S.overflow = 0;
     }
     uint32_t T, nlc;
-    pf_list_table(a, PfTable{S.lstart, S.lbias, S.wbase, S.wlo, S.whi, S.wsum}, t0, nct, ntl, pbase, part, thr, nk,
+    pf_list_table(a, PfTable{S.lstart, S.lbias, S.wtab, S.wsum}, t0, nct, ntl, pbase, part, thr, nk,
                   km0, km1, wv, lane, tid, T, nlc);
     PF_MARK(0)
-    if (T > 0) pf_count_stream<kPfSharedBytes>(arena, T, nlc, S.lstart, S.lbias, S.wbase, S.wlo, S.whi, lane, wv);
+    if (T > 0) pf_count_stream<kPfSharedBytes>(arena, T, nlc, S.lstart, S.lbias, S.wtab, lane, wv);
     __syncthreads();
     PF_MARK(1)
     if (wave == 0) {
@@ -1297,11 +1291,10 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_pf_full(PrefilterArgs a, int 
 // unit, no barriers (a wave-level DPP scan lays the non-empty lists end to end), high occupancy (no counters in
 // LDS), so its latency chain -- tile views, list offsets, scan, writes -- overlaps across many units instead of
 // sitting inside every counting workgroup's lifetime between its barriers.  Unit image (u32 words, 16-B aligned):
-// [0] T (chunks), [1] nlc (lists), [2] deferred chunks, [3] -, then the k_pf_count LDS table image: wbase
-// (u16 x kPfWinBase), wlo, whi (u32 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap).
+// [0] T (chunks), [1] nlc (lists), [2] deferred chunks, [3] -, then the k_pf_count LDS table image: wtab
+// (uint4 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap).
 __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __restrict__ tab, int32_t nunits) {
-  __shared__ uint32_t wl[kPfWinBase], wh[kPfWinBase];
-  __shared__ uint16_t wb[kPfWinBase];
+  __shared__ uint32_t wl[kPfWinBase], wh[kPfWinBase], wb[kPfWinBase];
   const int unit = (int)blockIdx.x;
   if (unit >= nunits) return;
   const int lane = (int)threadIdx.x;
@@ -1372,7 +1365,7 @@ __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __re
   const uint32_t tot = lane63(inc), ex = inc - packed;
   const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
   uint32_t* img = tab + (size_t)unit * pf_table_stride(a.nlist_cap);
-  uint32_t* lstart = img + 4 + kPfWinBase / 2 + 2 * kPfWinBase;
+  uint32_t* lstart = img + 4 + 4 * kPfWinBase;
   uint32_t* lbias = lstart + a.nlist_cap + 66;
   uint32_t li = ex & kListMask, ci = ex >> kListBits;
   auto put = [&](uint32_t nch, uint32_t bse) {
@@ -1380,7 +1373,7 @@ __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __re
     lstart[li] = ci;
     lbias[li] = bse - 8u * ci;
     if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase) atomicOr(((ci & 32u) ? wh : wl) + (ci >> 6), 1u << (ci & 31u));
-    for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch && w < (uint32_t)kPfWinBase; w++) wb[w] = (uint16_t)li;
+    for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch && w < (uint32_t)kPfWinBase; w++) wb[w] = li;
     li++;
     ci += nch;
   };
@@ -1399,14 +1392,8 @@ __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __re
   if (lane == 0) img[2] = dsum;
   // the window tables (LDS of this wave: its own writes are complete in order) to the image
   const uint32_t nw = min((T + 63u) >> 6, (uint32_t)kPfWinBase);
-  uint16_t* gwb = reinterpret_cast<uint16_t*>(img + 4);
-  uint32_t* gwl = img + 4 + kPfWinBase / 2;
-  uint32_t* gwh = gwl + kPfWinBase;
-  for (uint32_t w = (uint32_t)lane; w < nw; w += 64) {
-    gwb[w] = wb[w];
-    gwl[w] = wl[w];
-    gwh[w] = wh[w];
-  }
+  uint4* gwt = reinterpret_cast<uint4*>(img + 4);
+  for (uint32_t w = (uint32_t)lane; w < nw; w += 64) gwt[w] = make_uint4(wb[w], wl[w], wh[w], 0u);
 }
 
 // The lean counting kernel (one counter segment): list table, count, then every centroid counter >= the
@@ -1419,17 +1406,15 @@ struct PfCountHdr {
   uint32_t ncand, npc, ndef, pad1;
 };
 __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
-  return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 2 + 2 * kPfWinBase * 4 + (2 * nlist_cap + 66) * 4);
+  return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 16 + (2 * nlist_cap + 66) * 4);
 }
 template <int CM>
 __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off,
                                                             const uint32_t* __restrict__ gtab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
-  uint16_t* wbase = reinterpret_cast<uint16_t*>(pf_smem + tab_off + sizeof(PfCountHdr));
-  uint32_t* wlo = reinterpret_cast<uint32_t*>(wbase + kPfWinBase);
-  uint32_t* whi = wlo + kPfWinBase;
-  uint32_t* lstart = whi + kPfWinBase;
+  uint4* wtab = reinterpret_cast<uint4*>(pf_smem + tab_off + sizeof(PfCountHdr));
+  uint32_t* lstart = reinterpret_cast<uint32_t*>(wtab + kPfWinBase);
   uint32_t* lbias = lstart + a.nlist_cap + 66;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(pf_smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1496,13 +1481,13 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     nlc = (uint32_t)__builtin_amdgcn_readfirstlane((int)img[1]);
     if (tid == 0) H.ndef = img[2];
     const uint4* src = reinterpret_cast<const uint4*>(img + 4);
-    uint4* dst = reinterpret_cast<uint4*>(wbase);
+    uint4* dst = wtab;
     const int nv4 = (int)((pf_table_img_words(a.nlist_cap) + 3u) >> 2);
     for (int x = tid; x < nv4; x += kPfThreads) dst[x] = src[x];
     __syncthreads();
     if (prof) tsub[0] += __builtin_readcyclecounter() - tprev;
   } else {
-    pf_list_table(a, PfTable{lstart, lbias, wbase, wlo, whi, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
+    pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
                   km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof ? clk : nullptr);
     if (prof) {
       tsub[0] += clk[0] - tprev;
@@ -1510,9 +1495,9 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     }
   }
   PFC_MARK(1)
-  if (T > 0) {
-    if (CM == 1) pf_count_stream_pre<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
-    else pf_count_stream<0>(arena, T, nlc, lstart, lbias, wbase, wlo, whi, lane, wv);
+  if (T > 0 && CM != 2) {  // CM 2: the timing probe without the count loop (UMICLUST_PFPROBE)
+    if (CM == 1) pf_count_stream_pre<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
+    else pf_count_stream<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
   }
   __syncthreads();
   PFC_MARK(2)
@@ -1888,6 +1873,8 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
       e = hipFuncSetAttribute((const void*)k_pf_count<0>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)k_pf_count<1>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_pf_count<2>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
     if (e != hipSuccess) return e;
     mark_attr_set(k_attr_prefilter);
   }
@@ -1896,7 +1883,7 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int segn = a.ncent < kSegCentroids ? a.ncent : kSegCentroids;
   const size_t sub = (size_t)(((segn + kParts - 1) >> kPartShift) + 15) & ~(size_t)15;
   const size_t smem_full = (size_t)kPfSharedBytes + kCentBase + sub;
-  if (mode == 1 || (mode == 0 && a.nseg <= 1)) {
+  if (mode == 1 || mode == 3 || (mode == 0 && a.nseg <= 1)) {
     // lean counting (one counter segment)
     if (a.nseg > 1 || a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
     const uint32_t tab_off = (uint32_t)(kCentBase + sub);
@@ -1915,13 +1902,16 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
       const size_t pad = ((size_t)(160 * 1024 - pfres) / (size_t)pfwg) & ~(size_t)255;
       if (pad > lds && pad <= 65536) lds = pad;
     }
-    if (cm == 1)
+    if (mode == 3)  // the timing probe: every phase but the count loop, into scratch outputs (UMICLUST_PFPROBE)
+      hipLaunchKernelGGL(k_pf_count<2>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
+                         (const uint32_t*)a.pftab);
+    else if (cm == 1)
       hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
                          (const uint32_t*)a.pftab);
     else
       hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
                          (const uint32_t*)a.pftab);
-    if (mode == 1) return hipGetLastError();
+    if (mode == 1 || mode == 3) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {
     // the full kernel over the units the lean kernel could not finish (exits at once when there are none)

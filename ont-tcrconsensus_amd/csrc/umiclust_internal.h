@@ -71,10 +71,10 @@ constexpr int kSegLens = 32;  // query lengths one greedy block may span
 constexpr int kSegSlot = kUnitsSlot + 32;
 constexpr int kCountersLen = kSegSlot + 3 * kSegLens;
 constexpr int kPfWinBase = 128;   // k_pf_count: windows whose base list and start mask are tabulated (the rest: search)
-// k_pf_table's per-unit image of k_pf_count's LDS list table (kernels.hip): header (4 words), then wbase (u16 x
-// kPfWinBase), wlo, whi (u32 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap)
+// k_pf_table's per-unit image of k_pf_count's LDS list table (kernels.hip): header (4 words), then wtab (uint4 x
+// kPfWinBase: base list, start bits 0-31, 32-63, 0), lstart (nlist_cap + 66), lbias (nlist_cap)
 __host__ __device__ constexpr uint32_t pf_table_img_words(int nlist_cap) {
-  return (uint32_t)(kPfWinBase / 2 + 2 * kPfWinBase + 2 * nlist_cap + 66);
+  return (uint32_t)(4 * kPfWinBase + 2 * nlist_cap + 66);
 }
 __host__ __device__ constexpr uint32_t pf_table_stride(int nlist_cap) {
   return (4u + pf_table_img_words(nlist_cap) + 3u) & ~3u;

@@ -43,6 +43,10 @@ for st in "$@"; do
           timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv -d "$out/solo" -o run -- \
              python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/solo.log" 2>&1; rc=$?
           rm -f "$out/solo/run_kernel_trace.csv" "$out/solo/run_counter_collection.csv" ;;
+    probe) # the counting kernel with and without its count loop, solo (PMC serialises the dispatches)
+          UMICLUST_PFPROBE=1 timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv \
+             -d "$out/probe" -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/probe.log" 2>&1; rc=$?
+          ;;
     trace) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
              python3 $B > "$out/trace.log" 2>&1; rc=$? ;;
     c3) timeout -k 10 500 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
