@@ -560,6 +560,7 @@ def e2e_files(args) -> None:
         in1 = [os.path.join(d, "region_cluster_detected_umis.fasta") for d in dirs]
         bytes1 = write_all(list(zip(bins, in1)))
         t_gen1 = time.perf_counter() - t0
+        _progress(f"e2e-files: {len(bins)} round-1 inputs written, {bytes1 / 1e9:.1f} GB in {t_gen1:.0f} s")
         torch.cuda.set_device(0)
         lanes = max(1, min(args.lanes, len(bins)))
         ctxs = [_lib.Context(0) for _ in range(lanes)]
@@ -608,6 +609,7 @@ def e2e_files(args) -> None:
                         sum_write_s=tot("t_write_s"), largest_bin_s=max(x["seconds"] for x in per),
                         files_written=nf, bytes_written=nb), per
         r1, per1 = run_round(1)
+        _progress(f"e2e-files: round 1 {r1['wall_s']:.1f} s, {r1['umis_per_s'] / 1e6:.2f} M UMIs/s")
         # round-2 inputs from round 1's consout (untimed: medaka + extract_umis stand-in)
         t0 = time.perf_counter()
         b2 = []
@@ -617,7 +619,9 @@ def e2e_files(args) -> None:
         in2 = [os.path.join(d, "consensus_umis.fasta") for d in dirs]
         bytes2 = write_all(list(zip(b2, in2)))
         t_gen2 = time.perf_counter() - t0
+        _progress(f"e2e-files: {len(bins)} round-2 inputs written, {bytes2 / 1e9:.1f} GB in {t_gen2:.0f} s")
         r2, _ = run_round(2)
+        _progress(f"e2e-files: round 2 {r2['wall_s']:.1f} s, {r2['umis_per_s'] / 1e6:.2f} M UMIs/s")
         for c in ctxs:
             c.close()
         wall = r1["wall_s"] + r2["wall_s"]
@@ -679,6 +683,7 @@ def shard_sweep(args) -> None:
         kept = sum(x["n_kept"] for x in st)
         for r in runners:
             r.close()
+        _progress(f"shard-sweep: {len(sel)} bins, {kept} UMIs in {dt:.2f} s")
         return dict(bins=len(sel), reads=int(bins.n), umis_kept=int(kept), seconds=dt, umis_per_s=kept / dt,
                     cost_share=sum(costs[i] for i in sel) / sum(costs),
                     largest_pack_s=max((x["t_total_s"] for x in st), default=0.0))
@@ -702,6 +707,10 @@ def shard_sweep(args) -> None:
     ctx.close()
     if ctx2 is not None:
         ctx2.close()
+
+
+def _progress(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def _tree_bytes(d: str) -> tuple[int, int]:

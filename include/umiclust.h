@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 6
+#define UMICLUST_ABI_VERSION 7
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -128,6 +128,11 @@ int32_t umiclust_params_from_argv(umiclust_params *p, int32_t argc, const char *
  * and sets *err = UMICLUST_EDEVICE). */
 umiclust_ctx *umiclust_create(int32_t device_id, int32_t *err);
 void umiclust_destroy(umiclust_ctx *ctx);
+/* ABI 7: the context's main (counting) stream at the device's greatest stream priority (level 1) or a plain
+ * stream (level 0, the default); its alignment stream is always prioritised.  Lets a caller running several
+ * bins at once on one GPU (BinRunner lanes; tcr_consensus.py:231-245 runs one vsearch per bin) put the bin that
+ * sets the makespan ahead of the others.  Synchronises the context first.  Results do not depend on it. */
+int32_t umiclust_set_priority(umiclust_ctx *ctx, int32_t level);
 /* human-readable message for the last error on this context */
 const char *umiclust_last_error(const umiclust_ctx *ctx);
 

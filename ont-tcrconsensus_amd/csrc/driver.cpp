@@ -2222,6 +2222,20 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   return c;
 }
 
+int32_t umiclust_set_priority(umiclust_ctx* c, int32_t level) {
+  if (!c || level < 0 || level > 1) return UMICLUST_EINVAL;
+  if (hipSetDevice(c->dev) != hipSuccess || hipStreamSynchronize(c->st) != hipSuccess) return UMICLUST_EDEVICE;
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return UMICLUST_EDEVICE;
+  hipStream_t s = nullptr;
+  if ((level ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi) : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) !=
+      hipSuccess)
+    return UMICLUST_EDEVICE;
+  (void)hipStreamDestroy(c->st);  // idle (synchronised above); nothing holds the stream itself
+  c->st = s;
+  return UMICLUST_OK;
+}
+
 void umiclust_destroy(umiclust_ctx* c) {
   if (!c) return;
   g_live_ctx--;

@@ -107,7 +107,7 @@ class ParseResult(C.Structure):
 EXPORTS = [
     "umiclust_abi_version", "umiclust_params_init", "umiclust_params_from_argv", "umiclust_create",
     "umiclust_destroy", "umiclust_last_error", "umiclust_run_fasta", "umiclust_run_argv", "umiclust_run_fasta_parse",
-    "umiclust_load", "umiclust_stage", "umiclust_prepare", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
+    "umiclust_load", "umiclust_stage", "umiclust_prepare", "umiclust_set_priority", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
     "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
 ]
@@ -151,6 +151,8 @@ def lib() -> C.CDLL:
     L.umiclust_stage.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int64), C.c_int64, P(C.c_int64), C.c_int32]
     L.umiclust_prepare.restype = C.c_int32
     L.umiclust_prepare.argtypes = [C.c_void_p, P(Params)]
+    L.umiclust_set_priority.restype = C.c_int32
+    L.umiclust_set_priority.argtypes = [C.c_void_p, C.c_int32]
     L.umiclust_cluster.restype = C.c_int64
     L.umiclust_cluster.argtypes = [C.c_void_p, P(Stats)]
     L.umiclust_fetch.restype = C.c_int64
@@ -304,6 +306,10 @@ class Context:
     def prepare(self, p: Params) -> None:
         """umiclust_prepare: length filter, sort, DUST, codes and k-mers of the staged records."""
         self._check(lib().umiclust_prepare(self._h, C.byref(p)), "prepare")
+
+    def set_priority(self, level: int) -> None:
+        """umiclust_set_priority: 1 = this context's counting stream at the greatest priority, 0 = plain."""
+        self._check(lib().umiclust_set_priority(self._h, int(level)), "set_priority")
 
     def cluster(self) -> dict:
         st = Stats()

@@ -11,6 +11,8 @@ from __future__ import annotations
 import hashlib
 import json
 
+import os
+
 import numpy as np
 
 from . import _lib, synth
@@ -59,9 +61,12 @@ class BinRunner:
     their own; lanes keep the GPU fed.  Results do not depend on the lane count."""
 
     def __init__(self, ctx, binset: synth.BinSet, preset: int, identity: float, minlen: int = 58,
-                 maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0):
+                 maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0, critical_priority=None):
         """pack_reads > 0: a lane clusters its bins in packs (umiclust_cluster_pack) of consecutive bins holding up
-        to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack."""
+        to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack.
+        critical_priority (default: UMICLUST_CRIT_PRIO, off): the lane holding the largest bin -- the bin that sets the
+        makespan when it is far above the rest -- counts on a stream of the greatest priority (umiclust_set_priority)
+        while the other lanes keep plain ones."""
         from .shard import bin_cost, lpt_assign
         self.binset = binset
         self.pack_reads = pack_reads
@@ -81,6 +86,14 @@ class BinRunner:
             for j, b in enumerate(idx):
                 self.where[b] = (lane, j)
             self.ctxs[lane].stage(sub.seq, sub.off, sub.bin_start)
+        if critical_priority is None:
+            critical_priority = os.environ.get("UMICLUST_CRIT_PRIO", "0") not in ("", "0")
+        self.critical_lane = None
+        if critical_priority and len(self.ctxs) > 1 and nb:
+            big = max(range(nb), key=lambda b: binset.bins[b].umis.n)
+            self.critical_lane = self.where[big][0]
+            for lane, c in enumerate(self.ctxs):
+                c.set_priority(1 if lane == self.critical_lane else 0)
         self.prepare()
 
     def _each_lane(self, fn) -> list:

@@ -543,7 +543,8 @@ def _multibin_cases():
 
 
 @pytest.mark.parametrize("name,gold", _multibin_cases(), ids=[n for n, _ in _multibin_cases()])
-@pytest.mark.parametrize("split,pack", [("default", 0), ("1", 0), ("default", 3000), ("1", 20000), ("0", 1 << 30)])
+@pytest.mark.parametrize("split,pack", [("default", 0), ("1", 0), ("default", 3000), ("1", 20000), ("0", 1 << 30),
+                                        ("lanes4prio", 3000)])
 def test_multibin_vs_oracle_golden(name, gold, split, pack, monkeypatch):
     """BASELINE configs 3 (24 barcodes x 40 Zipf bins) and 4 (both rounds, round 2 on the round-1 consensus
     UMIs) at reduced scale: every bin resident in one load, clustered bin by bin or in packs of consecutive bins
@@ -551,7 +552,8 @@ def test_multibin_vs_oracle_golden(name, gold, split, pack, monkeypatch):
     query's own bin; up to 3k / 20k reads per pack, or the whole set as one pack); the checksum of the per-bin
     digests (membership, strands, centroids, consensus) and every bin's cluster count equal the oracle's."""
     from umiclust import binset, synth
-    if split != "default":  # multi-bin sets run whole passes unless UMICLUST_SPLIT says otherwise
+    lanes, prio = (4, True) if split == "lanes4prio" else (1, False)  # 4 lanes, the largest bin's on the priority stream
+    if split not in ("default", "lanes4prio"):  # multi-bin sets run whole passes unless UMICLUST_SPLIT says otherwise
         monkeypatch.setenv("UMICLUST_SPLIT", split)
     bs = synth.concat_bins(synth.config_bins(gold["config"], gold["scale"], workers=4))
     assert len(bs.bins) == gold["n_bins"] and bs.n == gold["n_reads"]
@@ -560,9 +562,11 @@ def test_multibin_vs_oracle_golden(name, gold, split, pack, monkeypatch):
         g = gold[rname]
         with _lib.Context(0) as ctx:
             run = binset.BinRunner(ctx, bs, prm["preset"], prm["identity"], gold["minlen"], gold["maxlen"],
-                                   pack_reads=pack)
+                                   pack_reads=pack, lanes=lanes, critical_priority=prio)
+            assert (run.critical_lane is not None) == prio
             st = run.cluster_all()
             res = run.results()
+            run.close()
         assert bs.n == g["n_reads"]
         dg = [binset.digest(r) for r in res]
         assert [d["n_clusters"] for d in dg] == g["n_clusters"], rname

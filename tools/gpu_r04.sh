@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session: parity tests, the default bench line (config 2 + e2e), PMC calibration and the
 # k_pf_count busy pass, kernel trace.  Every GPU step has its own time limit; the first failure ends the call.
-# Usage: bash tools/gpu_r04.sh <tag> <steps...>   steps: tests | solo | sweep3 | sweep4 | bench | defer (DEFERS="0 3") | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5 | c5trace
+# Usage: bash tools/gpu_r04.sh <tag> <steps...>   steps: tests | solo | sweep3 | sweep4 | bench | defer (DEFERS="0 3") | calib | busy | busy2 | fetch | write | pfprof | pfab | trace | c3 | c3trace | c4 | c5 | c5trace | c4e2e (SCALE=)
 set -o pipefail
 tag=${1:-r04}
 shift
@@ -66,6 +66,7 @@ for st in "$@"; do
              rm -f "$out/c5trace/run_kernel_trace.csv" ;;
     c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
     sweep3) timeout -k 10 900 python3 -u bench.py --config 3 --shard-sweep 8 > "$out/sweep3.json" 2> "$out/sweep3.err"; rc=$? ;;
+    c4e2e) timeout -k 10 900 python3 -u bench.py --config 4 --e2e-files --scale "${SCALE:-1.0}" > "$out/c4e2e.json" 2> "$out/c4e2e.err"; rc=$? ;;
     sweep4) timeout -k 10 1000 python3 -u bench.py --config 4 --shard-sweep 8 > "$out/sweep4.json" 2> "$out/sweep4.err"; rc=$? ;;
     c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
