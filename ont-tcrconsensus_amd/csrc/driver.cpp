@@ -376,7 +376,8 @@ struct umiclust_ctx {
   // faster (1.62 -> 1.76 ms per count + table on config 2: the counting is bound by the LDS array, ~73 % busy, 60 %
   // of it bank-conflict replays; profiles/r03/pftab_ab.json), so off by default
   bool pf_tab = false;
-  bool rec_direct = true;          // UMICLUST_RECDIRECT=0: k_pack's outcomes and records by DMA from device buffers
+  bool rec_direct = false;         // UMICLUST_RECDIRECT=1: k_pack writes outcomes and records straight to pinned host
+                                   // memory (round 4: DMA copies 4.33-4.36 vs 4.21-4.22 M UMIs/s, r04k envab)
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
@@ -417,6 +418,13 @@ struct umiclust_ctx {
                                     // relevant peers / with an in-block relevant peer / host ns in pass 1
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
+  PinBuf<uint32_t> h_mpq, h_mpt;     // the member pairs' pinned staging (traceback launch)
+  PinBuf<int32_t> h_mseq, h_mops, h_cstart;
+  PinBuf<uint8_t> h_mstr;
+  PinBuf<uint16_t> h_clen;           // consensus lengths / sequences / overflow flag (pinned downloads)
+  PinBuf<char> h_craw;
+  PinBuf<int32_t> h_over;
+  std::vector<int32_t> t_opsidx;
   DevBuf<uint8_t> t_ops, t_mstrand;
   DevBuf<uint16_t> t_nops, t_conslen;
   DevBuf<int32_t> t_cstart, t_mseq, t_mops, t_over;
@@ -1668,6 +1676,47 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->hip(hipEventElapsedTime(&ms, c->ix_events[i].first, c->ix_events[i].second), "elapsed");
     c->stats.t_index_s += ms * 1e-3;
   }
+  // --- member tracebacks first: their pairs (sorted seqno order) need only the targets, so the launch goes out
+  // before the host numbers the clusters, which then overlaps the traceback (round 4: the numbering and the
+  // pageable pair uploads were ~16 ms of idle GPU before the traceback of a 2M-read bin)
+  std::vector<int32_t>& opsidx = c->t_opsidx;
+  opsidx.assign(n, -1);
+  int32_t nm = 0;
+  for (int32_t s = s0; s < s1; s++) nm += c->target[s] >= 0;
+  c->hip(c->h_mpq.ensure((size_t)std::max(nm, 1)), "pin");
+  c->hip(c->h_mpt.ensure((size_t)std::max(nm, 1)), "pin");
+  {
+    int32_t x = 0;
+    for (int32_t s = s0; s < s1; s++)
+      if (c->target[s] >= 0) {
+        opsidx[s - s0] = x;
+        c->h_mpq.p[x] = ((uint32_t)s << 1) | c->strand[s];
+        c->h_mpt.p[x] = (uint32_t)c->target[s];
+        x++;
+      }
+  }
+  c->hip(c->t_mpq.ensure(nm), "alloc");
+  c->hip(c->t_mpt.ensure(nm), "alloc");
+  c->hip(c->t_mout.ensure(nm), "alloc");
+  c->hip(c->t_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
+  c->hip(c->t_nops.ensure(nm), "alloc");
+  if (nm > 0) {
+    c->hip(hipMemcpyAsync(c->t_mpq.p, c->h_mpq.p, (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(c->t_mpt.p, c->h_mpt.p, (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
+  }
+  if (!c->tev[0]) {
+    c->hip(hipEventCreate(&c->tev[0]), "event");
+    c->hip(hipEventCreate(&c->tev[1]), "event");
+  }
+  c->hip(hipEventRecord(c->tev[0], c->st), "event");
+  DevSeqs ds = dev_seqs(c);
+  {
+    // every member's chosen hit in one launch (one wave per alignment, any query length)
+    // the bin's longest sequence bounds every pair's lengths (one pass over its lengths)
+    const int32_t maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
+    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl),
+           "traceback");
+  }
   // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's
   c->nclusters = (int32_t)c->cent.size();
   for (int32_t k = 0; k < c->nclusters; k++) c->cno[c->cent[k]] = k;
@@ -1699,47 +1748,21 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     std::vector<int32_t> fill(c->ostart.begin(), c->ostart.end() - 1);
     for (int32_t s = s0; s < s1; s++) c->omemb[fill[c->ocl[s]]++] = s;
   }
-  // --- traceback for members, then consensus
+  // --- consensus (behind the traceback on the same stream)
   double t_cons = 0;
   {
-    std::vector<uint32_t> mpq, mpt;
-    std::vector<int32_t> opsidx(n, -1);
-    for (int32_t s = s0; s < s1; s++)
-      if (c->target[s] >= 0) {
-        opsidx[s - s0] = (int32_t)mpq.size();
-        mpq.push_back(((uint32_t)s << 1) | c->strand[s]);
-        mpt.push_back((uint32_t)c->target[s]);
-      }
-    const int32_t nm = (int32_t)mpq.size();
-    c->hip(c->t_mpq.ensure(nm), "alloc");
-    c->hip(c->t_mpt.ensure(nm), "alloc");
-    c->hip(c->t_mout.ensure(nm), "alloc");
-    c->hip(c->t_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
-    c->hip(c->t_nops.ensure(nm), "alloc");
-    if (nm > 0) {
-      c->hip(hipMemcpyAsync(c->t_mpq.p, mpq.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(c->t_mpt.p, mpt.data(), (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
-    }
-    if (!c->tev[0]) {
-      c->hip(hipEventCreate(&c->tev[0]), "event");
-      c->hip(hipEventCreate(&c->tev[1]), "event");
-    }
-    c->hip(hipEventRecord(c->tev[0], c->st), "event");
-    DevSeqs ds = dev_seqs(c);
-    // every member's chosen hit in one launch (one wave per alignment, any query length)
-    // the bin's longest sequence bounds every pair's lengths (one pass over its lengths)
-    const int32_t maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
-    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl),
-           "traceback");
-    // consensus inputs in output-cluster order
-    std::vector<int32_t> mseq(n), mops(n);
-    std::vector<uint8_t> mstr(n);
+    // consensus inputs in output-cluster order (pinned: the uploads are queued, not staged)
+    c->hip(c->h_mseq.ensure((size_t)std::max(n, 1)), "pin");
+    c->hip(c->h_mops.ensure((size_t)std::max(n, 1)), "pin");
+    c->hip(c->h_mstr.ensure((size_t)std::max(n, 1)), "pin");
+    c->hip(c->h_cstart.ensure((size_t)K + 1), "pin");
     for (int32_t x = 0; x < n; x++) {
       const int32_t s = c->omemb[x];
-      mseq[x] = s;
-      mops[x] = opsidx[s - s0];
-      mstr[x] = c->strand[s];
+      c->h_mseq.p[x] = s;
+      c->h_mops.p[x] = opsidx[s - s0];
+      c->h_mstr.p[x] = c->strand[s];
     }
+    std::copy(c->ostart.begin(), c->ostart.end(), c->h_cstart.p);
     c->hip(c->t_cstart.ensure((size_t)K + 1), "alloc");
     c->hip(c->t_mseq.ensure(n), "alloc");
     c->hip(c->t_mops.ensure(n), "alloc");
@@ -1748,25 +1771,35 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->hip(c->t_conslen.ensure((size_t)std::max(K, 1)), "alloc");
     c->hip(c->t_over.ensure(1), "alloc");
     c->hip(hipMemsetAsync(c->t_over.p, 0, 4, c->st), "memset");
-    c->hip(hipMemcpyAsync(c->t_cstart.p, c->ostart.data(), ((size_t)K + 1) * 4, hipMemcpyHostToDevice, c->st), "h2d");
+    c->hip(hipMemcpyAsync(c->t_cstart.p, c->h_cstart.p, ((size_t)K + 1) * 4, hipMemcpyHostToDevice, c->st), "h2d");
     if (n > 0) {
-      c->hip(hipMemcpyAsync(c->t_mseq.p, mseq.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(c->t_mops.p, mops.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(hipMemcpyAsync(c->t_mstrand.p, mstr.data(), (size_t)n, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mseq.p, c->h_mseq.p, (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mops.p, c->h_mops.p, (size_t)n * 4, hipMemcpyHostToDevice, c->st), "h2d");
+      c->hip(hipMemcpyAsync(c->t_mstrand.p, c->h_mstr.p, (size_t)n, hipMemcpyHostToDevice, c->st), "h2d");
     }
     c->hip(launch_consensus(ds, c->t_cstart.p, K, c->t_mseq.p, c->t_mops.p, c->t_mstrand.p, c->t_ops.p, c->t_nops.p,
                             c->t_cons.p, c->t_conslen.p, c->t_over.p, c->st),
            "consensus");
     c->hip(hipEventRecord(c->tev[1], c->st), "event");
-    std::vector<uint16_t> clen(K);
-    std::vector<char> craw((size_t)K * kConsCap);
-    int32_t over = 0;
+    c->hip(c->h_clen.ensure((size_t)std::max(K, 1)), "pin");
+    c->hip(c->h_craw.ensure((size_t)std::max(K, 1) * kConsCap), "pin");
+    c->hip(c->h_over.ensure(1), "pin");
+    const uint16_t* clen = c->h_clen.p;
+    const char* craw = c->h_craw.p;
     if (K > 0) {
-      c->hip(hipMemcpyAsync(clen.data(), c->t_conslen.p, (size_t)K * 2, hipMemcpyDeviceToHost, c->st), "d2h");
-      c->hip(hipMemcpyAsync(craw.data(), c->t_cons.p, (size_t)K * kConsCap, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(c->h_clen.p, c->t_conslen.p, (size_t)K * 2, hipMemcpyDeviceToHost, c->st), "d2h");
+      c->hip(hipMemcpyAsync(c->h_craw.p, c->t_cons.p, (size_t)K * kConsCap, hipMemcpyDeviceToHost, c->st), "d2h");
     }
-    c->hip(hipMemcpyAsync(&over, c->t_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+    c->hip(hipMemcpyAsync(c->h_over.p, c->t_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
     c->hip(hipStreamSynchronize(c->st), "sync");
+    const int32_t over = *c->h_over.p;
+    if (getenv("UMICLUST_TWPROF")) {
+      unsigned long long tw[4];
+      c->hip(traceback_profile(tw, true), "twprof");
+      const double nw = tw[3] ? (double)tw[3] : 1.0;
+      fprintf(stderr, "traceback phase clocks per sampled wave (%llu): setup %.0f sweep %.0f backtrack %.0f\n", tw[3],
+              tw[0] / nw, tw[1] / nw, tw[2] / nw);
+    }
     float ms = 0;
     c->hip(hipEventElapsedTime(&ms, c->tev[0], c->tev[1]), "elapsed");
     t_cons = ms * 1e-3;
@@ -1775,7 +1808,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     for (int32_t k = 0; k < K; k++) c->cons_off[k + 1] = c->cons_off[k] + clen[k];
     c->cons.resize((size_t)c->cons_off[K]);
     for (int32_t k = 0; k < K; k++)
-      memcpy(c->cons.data() + c->cons_off[k], craw.data() + (size_t)k * kConsCap, clen[k]);
+      memcpy(c->cons.data() + c->cons_off[k], craw + (size_t)k * kConsCap, clen[k]);
   }
   if (!c->pack_on) {
     auto& bo = c->bout[bin];

@@ -17,6 +17,8 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 #include <mutex>
 
 #include "align_kernels.h"
@@ -2195,12 +2197,13 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
 // query-strand the device walk's outcome (HostQs), and -- only for query-strands with a relevant
 // peer, whose outcome depends on which peers turn out to be centroids -- a record with the walk's
 // candidate list (seqno, k-mer count, result of the walked ones) and every peer (window id, count,
-// relevant flag, result of the aligned ones).  One wave per query-strand, lanes writing consecutive
-// words.  Record layout (u32 words): nt | np << 8, seqno[nt], res[nt], counts[(nt+3)/4] (u8 x4),
+// relevant flag, result of the aligned ones).  One wave per kPackQ consecutive query-strands, lanes writing
+// consecutive words.  Record layout (u32 words): nt | np << 8, seqno[nt], res[nt], counts[(nt+3)/4] (u8 x4),
 // peer[np] (id | count << 16 | relevant << 24 | aligned << 25), peer_res[np] (valid if aligned).  Record
-// space is taken with one atomic per workgroup of kPackWaves query-strands (a same-address atomic per
-// query-strand serialises in the L2).
-constexpr int kPackWaves = 4;
+// space is taken with one device-scope atomic per workgroup of kPackWaves x kPackQ query-strands: a returning
+// atomic on one word saturates at ~88 per us on MI355X (MI355X_MICROARCH.md, "dequeue"), so one per 4
+// query-strands held a 16k-query-strand pack at ~46 us of atomics alone (115-131 us per launch measured).
+constexpr int kPackWaves = 4, kPackQ = 4;
 __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w0, const uint8_t* __restrict__ lens,
                                               const WalkState* __restrict__ ws, const uint8_t* __restrict__ ntop,
                                               const uint32_t* __restrict__ top_seqno,
@@ -2212,9 +2215,9 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
                                               uint32_t* __restrict__ reccount,
                                               HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
                                               const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
-  __shared__ uint32_t wsize[kPackWaves];
+  __shared__ uint32_t wsize[kPackWaves * kPackQ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int qs = (int)blockIdx.x * kPackWaves + wave;
+  const int qs0 = ((int)blockIdx.x * kPackWaves + wave) * kPackQ;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // counters[0] = the postings partial sums (k_pf_merge spreads its atomics over kPostSpread lines)
     // counters[11] = the deferred postings' partial sums (the next word of each line)
@@ -2227,109 +2230,125 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
     }
     if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : threadIdx.x == 11 ? vd : counters[threadIdx.x];
   }
-  const bool live = qs < nqs;
-  const WalkState w = ws[live ? qs : 0];
-  const int np = live ? npeer[qs] : 0;
   constexpr int kH = kPeerCap / 64;  // peers lane, lane + 64, ...
-  bool rel[kH], al[kH];
-  uint32_t pw[kH];
-  bool anyrel = false;
+  static_assert(kPackQ * kH <= 32, "relevant / aligned bits per lane");
+  // phase 1: every query-strand's peer words and record size (the lane's relevant / aligned peers as bits
+  // i * kH + hh)
+  uint32_t pw[kPackQ][kH], relb = 0u, alb = 0u;
 #pragma unroll
-  for (int hh = 0; hh < kH; hh++) {
-    const int x = lane + 64 * hh;
-    rel[hh] = al[hh] = false;
-    pw[hh] = 0;
-    if (live && np != 255 && x < np) {
-      const uint32_t id = peer_id[(int64_t)qs * kPeerCap + x];
-      const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + x];
-      const uint32_t ps = (uint32_t)w0 + id;
-      rel[hh] = peer_relevant(w, cnt, lens[ps], ps);
-      al[hh] = (aligned[(int64_t)qs * 2 + hh] >> lane) & 1ull;
-      pw[hh] = id | (cnt << 16) | (rel[hh] ? 1u << 24 : 0u) | (al[hh] ? 1u << 25 : 0u);
-    }
-    anyrel |= rel[hh];
-  }
-  uint32_t base = 0xffffffffu;
-  const bool has_rec = __any(anyrel);
-  const int nt = live ? min((int)ntop[qs], kWalk) : 0;
-  const int ncw = (nt + 3) >> 2;
-  // record space: the workgroup's sizes scanned in LDS, one atomic
-  if (lane == 0) wsize[wave] = has_rec ? (uint32_t)(1 + 2 * nt + ncw + 2 * np) : 0u;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (int i = 0; i < kPackWaves; i++) {
-      const uint32_t x = wsize[i];
-      wsize[i] = tot;
-      tot += x;
-    }
-    const uint32_t b0 = tot ? atomicAdd(reccount, tot) : 0u;
-    for (int i = 0; i < kPackWaves; i++) wsize[i] += b0;
-  }
-  __syncthreads();
-  if (!live) return;
-  if (has_rec) {
-    base = wsize[wave];
-    uint32_t* r = rec + base;
-    if (lane == 0) r[0] = (uint32_t)nt | ((uint32_t)np << 8);
-    if (lane < nt) {
-      r[1 + lane] = top_seqno[(int64_t)qs * kTopHits + lane];
-      r[1 + nt + lane] = lane < w.e ? res[(int64_t)qs * kWalk + lane] : 0u;
-    }
-    if (lane < ncw) {
-      uint32_t cw = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (4 * lane + e < nt) cw |= (uint32_t)top_count[(int64_t)qs * kTopHits + 4 * lane + e] << (8 * e);
-      r[1 + 2 * nt + lane] = cw;
-    }
+  for (int i = 0; i < kPackQ; i++) {
+    const int qs = qs0 + i;
+    const bool live = qs < nqs;
+    const WalkState w = ws[live ? qs : 0];
+    const int np = live ? npeer[qs] : 0;
+    bool anyrel = false;
 #pragma unroll
     for (int hh = 0; hh < kH; hh++) {
       const int x = lane + 64 * hh;
-      if (x < np) {
-        r[1 + 2 * nt + ncw + x] = pw[hh];
-        r[1 + 2 * nt + ncw + np + x] = al[hh] ? peer_res[(int64_t)qs * kPeerCap + x] : 0u;
+      pw[i][hh] = 0;
+      if (live && np != 255 && x < np) {
+        const uint32_t id = peer_id[(int64_t)qs * kPeerCap + x];
+        const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + x];
+        const uint32_t ps = (uint32_t)w0 + id;
+        const bool rel = peer_relevant(w, cnt, lens[ps], ps);
+        const bool al = (aligned[(int64_t)qs * 2 + hh] >> lane) & 1ull;
+        pw[i][hh] = id | (cnt << 16) | (rel ? 1u << 24 : 0u) | (al ? 1u << 25 : 0u);
+        relb |= rel ? 1u << (i * kH + hh) : 0u;
+        alb |= al ? 1u << (i * kH + hh) : 0u;
+        anyrel |= rel;
       }
     }
+    const bool has_rec = __any(anyrel);
+    const int nt = live ? min((int)ntop[qs], kWalk) : 0;
+    if (lane == 0) wsize[wave * kPackQ + i] = has_rec ? (uint32_t)(1 + 2 * nt + ((nt + 3) >> 2) + 2 * np) : 0u;
   }
-  // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform masks, peer order)
-  unsigned long long rm[kH];
-  uint32_t nrel = 0;
-#pragma unroll
-  for (int hh = 0; hh < kH; hh++) {
-    rm[hh] = __ballot(rel[hh]);
-    nrel += (uint32_t)__builtin_popcountll(rm[hh]);
-  }
-  uint16_t ids[kInlineRel];
-  int hcur = 0;
-#pragma unroll
-  for (int i = 0; i < kInlineRel; i++) {
-    uint32_t id = 0;
-    while (hcur < kH && !rm[hcur]) hcur++;
-    if (hcur < kH) {
-      const int l = __builtin_ctzll(rm[hcur]);
-      rm[hcur] &= rm[hcur] - 1ull;
-      uint32_t v = pw[0];
-#pragma unroll
-      for (int hh = 1; hh < kH; hh++) v = hh == hcur ? pw[hh] : v;
-      id = (uint32_t)__builtin_amdgcn_readlane((int)(v & 0xffffu), l);
+  // record space: the workgroup's sizes scanned in LDS, one atomic
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int i = 0; i < kPackWaves * kPackQ; i++) {
+      const uint32_t x = wsize[i];
+      wsize[i] = x ? tot : 0xffffffffu;
+      tot += x;
     }
-    ids[i] = (uint16_t)id;
+    const uint32_t b0 = tot ? atomicAdd(reccount, tot) : 0u;
+    for (int i = 0; i < kPackWaves * kPackQ; i++)
+      if (wsize[i] != 0xffffffffu) wsize[i] += b0;
   }
-  if (lane == 0) {
-    HostQs h;
-    h.best_t = w.best_t;
-    h.cells = w.cells;
-    h.rec = base;
-    h.best_rank = w.best_rank;
-    h.w = w.w;
-    h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
-    h.nrel = (uint16_t)nrel;
-    h.e = w.e;
-    h.pad = 0;
+  __syncthreads();
+  // phase 2: records and outcomes
 #pragma unroll
-    for (int i = 0; i < kInlineRel; i++) h.rel[i] = ids[i];
-    hq[qs] = h;
+  for (int i = 0; i < kPackQ; i++) {
+    const int qs = qs0 + i;
+    if (qs >= nqs) break;  // wave-uniform
+    const WalkState w = ws[qs];
+    const int np = npeer[qs];
+    const int nt = min((int)ntop[qs], kWalk);
+    const int ncw = (nt + 3) >> 2;
+    const uint32_t base = wsize[wave * kPackQ + i];
+    if (base != 0xffffffffu) {
+      uint32_t* r = rec + base;
+      if (lane == 0) r[0] = (uint32_t)nt | ((uint32_t)np << 8);
+      if (lane < nt) {
+        r[1 + lane] = top_seqno[(int64_t)qs * kTopHits + lane];
+        r[1 + nt + lane] = lane < w.e ? res[(int64_t)qs * kWalk + lane] : 0u;
+      }
+      if (lane < ncw) {
+        uint32_t cw = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if (4 * lane + e < nt) cw |= (uint32_t)top_count[(int64_t)qs * kTopHits + 4 * lane + e] << (8 * e);
+        r[1 + 2 * nt + lane] = cw;
+      }
+#pragma unroll
+      for (int hh = 0; hh < kH; hh++) {
+        const int x = lane + 64 * hh;
+        if (x < np) {
+          const bool al = (alb >> (i * kH + hh)) & 1u;
+          r[1 + 2 * nt + ncw + x] = pw[i][hh];
+          r[1 + 2 * nt + ncw + np + x] = al ? peer_res[(int64_t)qs * kPeerCap + x] : 0u;
+        }
+      }
+    }
+    // the first kInlineRel relevant peers' ids, gathered from their lanes (wave-uniform masks, peer order)
+    unsigned long long rm[kH];
+    uint32_t nrel = 0;
+#pragma unroll
+    for (int hh = 0; hh < kH; hh++) {
+      rm[hh] = __ballot((relb >> (i * kH + hh)) & 1u);
+      nrel += (uint32_t)__builtin_popcountll(rm[hh]);
+    }
+    uint16_t ids[kInlineRel];
+    int hcur = 0;
+#pragma unroll
+    for (int j = 0; j < kInlineRel; j++) {
+      uint32_t id = 0;
+      while (hcur < kH && !rm[hcur]) hcur++;
+      if (hcur < kH) {
+        const int l = __builtin_ctzll(rm[hcur]);
+        rm[hcur] &= rm[hcur] - 1ull;
+        uint32_t v = pw[i][0];
+#pragma unroll
+        for (int hh = 1; hh < kH; hh++) v = hh == hcur ? pw[i][hh] : v;
+        id = (uint32_t)__builtin_amdgcn_readlane((int)(v & 0xffffu), l);
+      }
+      ids[j] = (uint16_t)id;
+    }
+    if (lane == 0) {
+      HostQs h;
+      h.best_t = w.best_t;
+      h.cells = w.cells;
+      h.rec = base;
+      h.best_rank = w.best_rank;
+      h.w = w.w;
+      h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
+      h.nrel = (uint16_t)nrel;
+      h.e = w.e;
+      h.pad = 0;
+#pragma unroll
+      for (int j = 0; j < kInlineRel; j++) h.rel[j] = ids[j];
+      hq[qs] = h;
+    }
   }
 }
 
@@ -2339,7 +2358,8 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
                        uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pack, dim3((nqs + kPackWaves - 1) / kPackWaves), dim3(64 * kPackWaves), 0, st, nqs, w0, lens,
+  constexpr int per = kPackWaves * kPackQ;
+  hipLaunchKernelGGL(k_pack, dim3((nqs + per - 1) / per), dim3(64 * kPackWaves), 0, st, nqs, w0, lens,
                      ws, ntop, top_seqno, top_count,
                      res, npeer, peer_id, peer_count, peer_res, aligned, reccount, hq, rec, counters, hcounters);
   return hipGetLastError();
@@ -2365,7 +2385,7 @@ struct TwLayout {
   __host__ __device__ explicit TwLayout(int maxl) {
     words = (maxl + 63 + 7) / 8;
     dir_u32 = ((maxl + 63) / 64) * words * 64;
-    wave_bytes = (dir_u32 * 4 + 2 * maxl * 4 + 4 + maxl + 64 + 15) & ~15;
+    wave_bytes = (dir_u32 * 4 + 2 * maxl * 4 + 4 + maxl + 72 + 15) & ~15;  // tcode: maxl + 64 + 8 (whole 8-step groups)
   }
 };
 
@@ -2373,15 +2393,21 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
 
+// UMICLUST_TWPROF: sampled waves' shader-clock phase totals (setup, sweep, backtrack) and their count
+__device__ unsigned long long g_twprof[4];
+template <bool kGrouped>
 __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const uint32_t* __restrict__ pq,
                                                               const uint32_t* __restrict__ pt, int32_t npairs,
                                                               Scoring sc, uint8_t* __restrict__ ops,
                                                               uint16_t* __restrict__ nops, uint32_t* __restrict__ out,
-                                                              int32_t maxl) {
+                                                              int32_t maxl, int32_t prof) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tw_smem[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave-uniform by construction (readfirstlane), so the pair's lengths, the sweep bounds and the backtrack are
+  // scalar
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int k = (int)blockIdx.x * kTwWaves + wave;
   if (k >= npairs) return;  // wave-uniform
+  const unsigned long long c0 = prof ? __builtin_readcyclecounter() : 0ull;
   const TwLayout lay(maxl);
   struct {
     uint32_t* dir;
@@ -2401,7 +2427,11 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const int tl = s.lens[t], ql = s.lens[q];
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
   const uint32_t* qcp = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
-  for (int j = lane; j < tl + 64; j += 64) S.tcode[j] = j < tl ? (uint8_t)((tcp[j >> 3] >> ((j & 7) * 4)) & 15u) : 0;
+  // kGrouped: the target codes staged one-hot (0 = ambiguous or past the end), so the substitution score is two tests
+  for (int j = lane; j < tl + 72; j += 64) {
+    const uint32_t c = j < tl ? (tcp[j >> 3] >> ((j & 7) * 4)) & 15u : 0u;
+    S.tcode[j] = (uint8_t)(kGrouped ? ((c & (c - 1u)) == 0u ? c : 0u) : c);
+  }
   // both sequences' code words in VGPRs (lane w holds word w): the backtrack reads them by v_readlane
   // instead of a global / LDS load per diagonal step
   const uint32_t qword = lane < kCodeWords ? qcp[lane] : 0u, tword = lane < kCodeWords ? tcp[lane] : 0u;
@@ -2432,114 +2462,263 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+  const bool pw = prof && (k & 63) == 0;
+  const unsigned long long c1 = pw ? __builtin_readcyclecounter() : 0ull;
   const int nstripe = (ql + 63) >> 6;
-  for (int st = 0; st < nstripe; st++) {
-    const int i = st * 64 + lane;
-    const int rows = min(64, ql - st * 64);  // live lanes of the stripe
-    const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
-    const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-    const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
-    int Hl = -(sc.go[1] + (i + 1) * sc.ge[1]);  // H(i, -1)
-    int E = sc.boundary_open ? Hl - qrq : kNegInf;
-    int Hd = 0;                                 // H(i-1, j-1) for the next cell
-    int hout = 0, fout = 0;                     // this lane's last cell: H(i, j), F(i+1, j)
-    uint32_t tc = 0, dword = 0;
-    const int nsteps = tl + rows - 1;
-    for (int tt = 0; tt < nsteps; tt++) {
-      const int j = tt - lane;
-      // row above at column tt for lane 0: the top boundary (stripe 0) or the previous stripe's bottom row
-      int hb, fb;
-      if (st == 0) {
-        hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
-        const int qrt = (tt == tl - 1) ? QRtr : QRti;
-        fb = sc.boundary_open ? hb - qrt : kNegInf;
-      } else {
-        hb = tt < tl ? S.botH[tt] : 0;
-        fb = tt < tl ? S.botF[tt] : 0;
+  int hend = 0;
+  if constexpr (kGrouped) {
+    // The sweep in groups of 8 steps (one direction word per group, no per-step store test), the diagonal's
+    // column -1 and H(ql - 1, tl - 1) without per-step tests: a lane's H starts as H(i, -1), which the lane below
+    // reads as its diagonal at column 0, and H(ql - 1, tl - 1) is the last H lane (ql - 1) % 64 of the last stripe
+    // kept.  Steps past the stripe's end (to the group's end) touch no live cell.
+    // one sweep per stripe, specialised on the top boundary (stripe 0: computed; later stripes: the previous
+    // stripe's bottom row from LDS) and on whether a stripe follows (lane 63 then stores its row)
+    auto sweep = [&](int st, auto top_c, auto bot_c) {
+      constexpr bool kTop = decltype(top_c)::value, kBot = decltype(bot_c)::value;
+      const int i = st * 64 + lane;
+      const int rows = min(64, ql - st * 64);
+      const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
+      const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+      const uint32_t qm = qamb ? 0u : qcode;
+      const int Mq = qamb ? 0 : sc.match, Xq = qamb ? 0 : sc.mismatch;
+      const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
+      const uint32_t tle = i < ql ? (uint32_t)tl : 0u;  // live columns of this lane
+      int hout = -(sc.go[1] + (i + 1) * sc.ge[1]);      // H(i, -1)
+      int E = sc.boundary_open ? hout - qrq : kNegInf;
+      int Hd = i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1]);  // H(i - 1, -1)
+      int fout = 0;
+      uint32_t tc = 0;
+      const int nsteps = tl + rows - 1;
+      for (int t8 = 0; t8 < nsteps; t8 += 8) {
+        uint32_t dword = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int tt = t8 + u;
+          int hb, fb;
+          if constexpr (kTop) {
+            hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
+            fb = sc.boundary_open ? hb - ((tt == tl - 1) ? QRtr : QRti) : kNegInf;
+          } else {
+            hb = tt < tl ? S.botH[tt] : 0;
+            fb = tt < tl ? S.botF[tt] : 0;
+          }
+          const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
+          tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
+          const int Hup = sx16(recv), Fin = (int)recv >> 16;
+          const int j = tt - lane;
+          const bool live = (uint32_t)j < tle;
+          const bool lc = j == tl - 1;
+          const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
+          const int sub = (qm & tc) ? Mq : (tc ? Xq : 0);
+          const int diag = Hd + sub;
+          const int m1 = max(diag, Fin);
+          const int h = max(m1, E);
+          const int fo = h - QRt, fe = Fin - Rt;
+          const int eo = h - qrq, ee = E - rq;
+          const uint32_t d = (Fin > diag ? 1u : 0u) | (E > m1 ? 2u : 0u) | (fe > fo ? 4u : 0u) | (ee > eo ? 8u : 0u);
+          E = live ? max(eo, ee) : E;
+          hout = live ? h : hout;
+          fout = live ? max(fo, fe) : fout;
+          if constexpr (kBot) {
+            if (live && lane == 63) {
+              S.botH[j] = hout;
+              S.botF[j] = fout;
+            }
+          }
+          Hd = Hup;
+          dword |= d << (4 * u);
+        }
+        S.dir[(st * TW + (t8 >> 3)) * 64 + lane] = dword;
       }
-      const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
-      tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
-      const int Hup = sx16(recv), Fin = (int)recv >> 16;
-      const bool live = j >= 0 && j < tl && i < ql;
-      const int hd = (j == 0) ? (i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1])) : Hd;
-      const bool lc = (j == tl - 1);
-      const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
-      const bool tamb = (tc & (tc - 1u)) != 0u || tc == 0u;
-      const int sub = (tamb || qamb) ? 0 : (qcode == tc ? sc.match : sc.mismatch);
-      int h = hd + sub;
-      uint32_t d = 0;
-      if (Fin > h) { h = Fin; d |= 1u; }
-      if (E > h) { h = E; d |= 2u; }
-      const int fo = h - QRt, fe = Fin - Rt;
-      int Fn = fo;
-      if (fe > fo) { Fn = fe; d |= 4u; }
-      const int eo = h - qrq, ee = E - rq;
-      int En = eo;
-      if (ee > eo) { En = ee; d |= 8u; }
-      if (live) {
-        Hl = h;
-        E = En;
-        hout = h;
-        fout = Fn;
-        if (i == ql - 1 && j == tl - 1) *S.hendp = h;
-        if (lane == 63 && st + 1 < nstripe) {
-          S.botH[j] = h;
-          S.botF[j] = Fn;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      return hout;
+    };
+    using T1 = std::integral_constant<bool, true>;
+    using T0 = std::integral_constant<bool, false>;
+    int hlast;
+    if (nstripe == 1) {
+      hlast = sweep(0, T1{}, T0{});
+    } else {
+      sweep(0, T1{}, T1{});
+      for (int st = 1; st + 1 < nstripe; st++) sweep(st, T0{}, T1{});
+      hlast = sweep(nstripe - 1, T0{}, T0{});
+    }
+    hend = __builtin_amdgcn_readlane(hlast, (ql - 1) & 63);
+  } else {
+  const int nstripe = (ql + 63) >> 6;
+    for (int st = 0; st < nstripe; st++) {
+      const int i = st * 64 + lane;
+      const int rows = min(64, ql - st * 64);  // live lanes of the stripe
+      const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
+      const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+      const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
+      int Hl = -(sc.go[1] + (i + 1) * sc.ge[1]);  // H(i, -1)
+      int E = sc.boundary_open ? Hl - qrq : kNegInf;
+      int Hd = 0;                                 // H(i-1, j-1) for the next cell
+      int hout = 0, fout = 0;                     // this lane's last cell: H(i, j), F(i+1, j)
+      uint32_t tc = 0, dword = 0;
+      const int nsteps = tl + rows - 1;
+      for (int tt = 0; tt < nsteps; tt++) {
+        const int j = tt - lane;
+        // row above at column tt for lane 0: the top boundary (stripe 0) or the previous stripe's bottom row
+        int hb, fb;
+        if (st == 0) {
+          hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
+          const int qrt = (tt == tl - 1) ? QRtr : QRti;
+          fb = sc.boundary_open ? hb - qrt : kNegInf;
+        } else {
+          hb = tt < tl ? S.botH[tt] : 0;
+          fb = tt < tl ? S.botF[tt] : 0;
+        }
+        const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
+        tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
+        const int Hup = sx16(recv), Fin = (int)recv >> 16;
+        const bool live = j >= 0 && j < tl && i < ql;
+        const int hd = (j == 0) ? (i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1])) : Hd;
+        const bool lc = (j == tl - 1);
+        const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
+        const bool tamb = (tc & (tc - 1u)) != 0u || tc == 0u;
+        const int sub = (tamb || qamb) ? 0 : (qcode == tc ? sc.match : sc.mismatch);
+        int h = hd + sub;
+        uint32_t d = 0;
+        if (Fin > h) { h = Fin; d |= 1u; }
+        if (E > h) { h = E; d |= 2u; }
+        const int fo = h - QRt, fe = Fin - Rt;
+        int Fn = fo;
+        if (fe > fo) { Fn = fe; d |= 4u; }
+        const int eo = h - qrq, ee = E - rq;
+        int En = eo;
+        if (ee > eo) { En = ee; d |= 8u; }
+        if (live) {
+          Hl = h;
+          E = En;
+          hout = h;
+          fout = Fn;
+          if (i == ql - 1 && j == tl - 1) *S.hendp = h;
+          if (lane == 63 && st + 1 < nstripe) {
+            S.botH[j] = h;
+            S.botF[j] = Fn;
+          }
+        }
+        Hd = Hup;
+        (void)Hl;
+        dword |= d << ((tt & 7) * 4);
+        if ((tt & 7) == 7 || tt == nsteps - 1) {
+          S.dir[(st * TW + (tt >> 3)) * 64 + lane] = dword;
+          dword = 0;
         }
       }
-      Hd = Hup;
-      (void)Hl;
-      dword |= d << ((tt & 7) * 4);
-      if ((tt & 7) == 7 || tt == nsteps - 1) {
-        S.dir[(st * TW + (tt >> 3)) * 64 + lane] = dword;
-        dword = 0;
-      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    hend = *S.hendp;
   }
-  if (lane != 0) return;
-  // backtrack16 from (ql-1, tl-1): diagonal unless the cell took up (D) / left (I); a run continues while
-  // the cell's extension bit says the gap was extended
   uint8_t* o = ops + (int64_t)k * kOpsStride;
-  int n = 0, i = ql - 1, j = tl - 1, aligned = 0, matches = 0;
-  uint32_t op = 0;
-  while (i >= 0 && j >= 0) {
-    aligned++;
-    const int l = i & 63, tt = j + l;
-    const uint32_t d = (S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
-    if (op == 'I' && (d & 8u)) {
-      j--;
-    } else if (op == 'D' && (d & 4u)) {
-      i--;
-    } else if (d & 2u) {
-      j--;
-      op = 'I';
-    } else if (d & 1u) {
-      i--;
-      op = 'D';
-    } else {
-      const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
-      const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
-      if (qc & tc) matches++;
-      i--;
-      j--;
-      op = 'M';
+  const unsigned long long c2 = pw ? __builtin_readcyclecounter() : 0ull;
+  if constexpr (kGrouped) {
+    // backtrack16 from (ql-1, tl-1) as wave-uniform scalar code: the cell's direction word by one LDS read and
+    // readfirstlane, the decisions and counters in SGPRs, the ops shifted into a dword stored every 4 ops
+    // (alignment order ends at o[kOpsStride - 1]; a final partial dword's low bytes, zero, fall below the ops and
+    // are never read).  align_trim's runs are tracked on the way: the first run generated is the alignment's last,
+    // the last one generated its first.
+    static_assert(kOpsStride % 4 == 0, "dword op stores");
+    int n = 0, i = ql - 1, j = tl - 1, matches = 0;
+    uint32_t op = 0, w4 = 0, first_op = 0, run_op = 0;
+    int first_run = 0, run_len = 0;
+    auto emit = [&](uint32_t c) {
+      w4 = (w4 << 8) | c;  // the op generated first (the alignment's later one) at the higher address
+      n++;
+      if ((n & 3) == 0 && lane == 0) *reinterpret_cast<uint32_t*>(o + kOpsStride - n) = w4;
+      if (n == 1) first_op = c;
+      if (c == first_op && first_run == n - 1) first_run = n;
+      run_len = c == run_op ? run_len + 1 : 1;
+      run_op = c;
+    };
+    while (i >= 0 && j >= 0) {
+      const int l = i & 63, tt = j + l;
+      const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l]);
+      const uint32_t d = (word >> ((tt & 7) * 4)) & 15u;
+      if (op == 'I' && (d & 8u)) {
+        j--;
+      } else if (op == 'D' && (d & 4u)) {
+        i--;
+      } else if (d & 2u) {
+        j--;
+        op = 'I';
+      } else if (d & 1u) {
+        i--;
+        op = 'D';
+      } else {
+        const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
+        const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
+        matches += (qc & tc) ? 1 : 0;
+        i--;
+        j--;
+        op = 'M';
+      }
+      emit(op);
     }
-    o[kOpsStride - 1 - n] = (uint8_t)op;
-    n++;
+    for (; i >= 0; i--) emit('D');
+    for (; j >= 0; j--) emit('I');
+    if ((n & 3) != 0 && lane == 0)  // the last n & 3 ops: the newest at o[kOpsStride - n]
+      *reinterpret_cast<uint32_t*>(o + kOpsStride - ((n + 3) & ~3)) = w4 << (8 * (4 - (n & 3)));
+    if (lane != 0) return;
+    if (pw) {
+      const unsigned long long c3 = __builtin_readcyclecounter();
+      atomicAdd(&g_twprof[0], c1 - c0);
+      atomicAdd(&g_twprof[1], c2 - c1);
+      atomicAdd(&g_twprof[2], c3 - c2);
+      atomicAdd(&g_twprof[3], 1ull);
+    }
+    nops[k] = (uint16_t)n;
+    const int tlft = run_op != 'M' ? run_len : 0;
+    const int trgt = (first_op != 'M' && tlft < n) ? first_run : 0;
+    const uint32_t internal = (uint32_t)(n - tlft - trgt);
+    out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)hend & 0xffffu) << 16);
+  } else {
+    if (lane != 0) return;
+    // backtrack16 from (ql-1, tl-1): diagonal unless the cell took up (D) / left (I); a run continues while
+    // the cell's extension bit says the gap was extended
+    int n = 0, i = ql - 1, j = tl - 1, aligned = 0, matches = 0;
+    uint32_t op = 0;
+    while (i >= 0 && j >= 0) {
+      aligned++;
+      const int l = i & 63, tt = j + l;
+      const uint32_t d = (S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
+      if (op == 'I' && (d & 8u)) {
+        j--;
+      } else if (op == 'D' && (d & 4u)) {
+        i--;
+      } else if (d & 2u) {
+        j--;
+        op = 'I';
+      } else if (d & 1u) {
+        i--;
+        op = 'D';
+      } else {
+        const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
+        const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
+        if (qc & tc) matches++;
+        i--;
+        j--;
+        op = 'M';
+      }
+      o[kOpsStride - 1 - n] = (uint8_t)op;
+      n++;
+    }
+    while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
+    while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
+    nops[k] = (uint16_t)n;
+    // align_trim: the first and the last op runs, if gaps, are terminal (alignment order)
+    const uint8_t* a0 = o + kOpsStride - n;
+    int tlft = 0, trgt = 0;
+    if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
+    if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
+    if (tlft >= aligned) trgt = 0;
+    const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
+    out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)hend & 0xffffu) << 16);
   }
-  while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
-  while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
-  nops[k] = (uint16_t)n;
-  // align_trim: the first and the last op runs, if gaps, are terminal (alignment order)
-  const uint8_t* a0 = o + kOpsStride - n;
-  int tlft = 0, trgt = 0;
-  if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
-  if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
-  if (tlft >= aligned) trgt = 0;
-  const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
-  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)*S.hendp & 0xffffu) << 16);
 }
 
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
@@ -2548,9 +2727,24 @@ hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t
   if (npairs <= 0) return hipSuccess;
   if (maxl < 1 || maxl > kMaxLen) return hipErrorInvalidValue;
   const TwLayout lay(maxl);
-  hipLaunchKernelGGL(k_trace_wave, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
-                     (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl);
+  // UMICLUST_TRACE=step: the sweep with per-step tests (the round-3 loop), for A/B
+  static const bool grouped = !(getenv("UMICLUST_TRACE") && strcmp(getenv("UMICLUST_TRACE"), "step") == 0);
+  static const int32_t prof = getenv("UMICLUST_TWPROF") ? 1 : 0;
+  if (grouped)
+    hipLaunchKernelGGL(k_trace_wave<true>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
+                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl, prof);
+  else
+    hipLaunchKernelGGL(k_trace_wave<false>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
+                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl, prof);
   return hipGetLastError();
+}
+hipError_t traceback_profile(unsigned long long out[4], bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_twprof), sizeof(unsigned long long) * 4);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_twprof), z, sizeof z);
+  }
+  return e;
 }
 
 // ------------------------------------------------------------------ K4: consensus

@@ -224,6 +224,7 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
                             const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
                             int32_t maxl);
+hipError_t traceback_profile(unsigned long long out[4], bool reset);  // UMICLUST_TWPROF phase clocks
 // consensus: cluster c members member_seqno[cstart[c] .. cstart[c+1]) (centroid first),
 // member_ops index per member (-1 for centroid), member strand.
 hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t nclusters,

@@ -20,10 +20,17 @@ for st in "$@"; do
     bench) timeout -k 10 600 python3 -u bench.py --steps 5 --warmup 1 > "$out/bench.json" 2> "$out/bench.err"; rc=$? ;;
     calib) timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d "$out/calib" -o run -- tools/pmc_calib \
              > "$out/calib.log" 2>&1; rc=$? ;;
-    busy) timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d "$out/busy" -o run -- python3 $B \
-             > "$out/busy.log" 2>&1; rc=$? ;;
-    busy2) timeout -s KILL 300 rocprofv3 --pmc $SQ2 --output-format csv -d "$out/busy2" -o run -- python3 $B \
-             > "$out/busy2.log" 2>&1; rc=$? ;;
+    busyprobe) # SQ counters with the count-loop-less k_pf_count<2> dispatched beside every counting launch
+          UMICLUST_PFPROBE=1 timeout -s KILL 300 rocprofv3 --pmc $SQ --output-format csv -d "$out/$st" -o run -- python3 $B \
+             > "$out/$st.log" 2>&1; rc=$?
+          if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
+          rm -f "$out/$st/run_counter_collection.csv" ;;
+    busy|busy2) # per-kernel totals only (the full counter CSV exceeds what a call may bring back)
+          [ "$st" = busy ] && CT="$SQ" || CT="$SQ2"
+          timeout -s KILL 300 rocprofv3 --pmc $CT --output-format csv -d "$out/$st" -o run -- python3 $B \
+             > "$out/$st.log" 2>&1; rc=$?
+          if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
+          rm -f "$out/$st/run_counter_collection.csv" ;;
     fetch) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B \
              > "$out/fetch.log" 2>&1; rc=$? ;;
     write) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B \
