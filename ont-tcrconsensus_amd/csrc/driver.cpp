@@ -1685,15 +1685,24 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   for (int32_t s = s0; s < s1; s++) nm += c->target[s] >= 0;
   c->hip(c->h_mpq.ensure((size_t)std::max(nm, 1)), "pin");
   c->hip(c->h_mpt.ensure((size_t)std::max(nm, 1)), "pin");
+  // members with queries of at most 64 nt first: their launch sizes the direction store for one stripe (more
+  // waves per CU); the longer ones follow in a launch of their own
+  int32_t nm1 = 0, maxq1 = 0, maxq2 = 0;
+  // UMICLUST_TWSPLIT=0: one launch for every member (the direction store sized for the longest query)
+  static const int tw_split = getenv("UMICLUST_TWSPLIT") && atoi(getenv("UMICLUST_TWSPLIT")) == 0 ? kMaxLen : 64;
   {
     int32_t x = 0;
-    for (int32_t s = s0; s < s1; s++)
-      if (c->target[s] >= 0) {
-        opsidx[s - s0] = x;
-        c->h_mpq.p[x] = ((uint32_t)s << 1) | c->strand[s];
-        c->h_mpt.p[x] = (uint32_t)c->target[s];
-        x++;
-      }
+    for (int pass = 0; pass < 2; pass++) {
+      for (int32_t s = s0; s < s1; s++)
+        if (c->target[s] >= 0 && (((int)c->hlen[s] <= tw_split) == (pass == 0))) {
+          opsidx[s - s0] = x;
+          c->h_mpq.p[x] = ((uint32_t)s << 1) | c->strand[s];
+          c->h_mpt.p[x] = (uint32_t)c->target[s];
+          (pass ? maxq2 : maxq1) = std::max(pass ? maxq2 : maxq1, (int32_t)c->hlen[s]);
+          x++;
+        }
+      if (pass == 0) nm1 = x;
+    }
   }
   c->hip(c->t_mpq.ensure(nm), "alloc");
   c->hip(c->t_mpt.ensure(nm), "alloc");
@@ -1714,7 +1723,11 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     // every member's chosen hit in one launch (one wave per alignment, any query length)
     // the bin's longest sequence bounds every pair's lengths (one pass over its lengths)
     const int32_t maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
-    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl),
+    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm1, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl,
+                            maxq1),
+           "traceback");
+    c->hip(launch_traceback(ds, c->t_mpq.p + nm1, c->t_mpt.p + nm1, nm - nm1, c->sc, c->t_ops.p + (size_t)nm1 * kOpsStride,
+                            c->t_nops.p + nm1, c->t_mout.p + nm1, c->st, maxl, maxq2),
            "traceback");
   }
   // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's

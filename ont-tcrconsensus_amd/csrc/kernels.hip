@@ -2380,14 +2380,18 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
 // botF[maxl] (F(64 s, j)), hend, tcode[maxl + 64] -- 9.4 KB for 68-nt UMIs instead of 12.4 KB at kMaxLen
 // (16 waves per CU instead of 12).
 constexpr int kTwWaves = 4;
+// maxq: the launch's longest query (its stripes: a launch of queries <= 64 nt needs half the direction store, so
+// more waves fit a CU); maxl: its longest sequence.
 struct TwLayout {
   int words, dir_u32, wave_bytes;
-  __host__ __device__ explicit TwLayout(int maxl) {
+  __host__ __device__ TwLayout(int maxq, int maxl) {
     words = (maxl + 63 + 7) / 8;
-    dir_u32 = ((maxl + 63) / 64) * words * 64;
-    wave_bytes = (dir_u32 * 4 + 2 * maxl * 4 + 4 + maxl + 72 + 15) & ~15;  // tcode: maxl + 64 + 8 (whole 8-step groups)
+    dir_u32 = ((maxq + 63) / 64) * words * 64;
+    // tcode: maxl + 64 + 8 (whole 8-step groups); qraw, traw: maxl each (the backtrack's match test)
+    wave_bytes = (dir_u32 * 4 + 2 * maxl * 4 + 4 + maxl + 72 + 2 * maxl + 15) & ~15;
   }
 };
+static_assert(kMaxLen <= 128, "the backtrack's register prefetch covers two stripes");
 
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
@@ -2400,7 +2404,7 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
                                                               const uint32_t* __restrict__ pt, int32_t npairs,
                                                               Scoring sc, uint8_t* __restrict__ ops,
                                                               uint16_t* __restrict__ nops, uint32_t* __restrict__ out,
-                                                              int32_t maxl, int32_t prof) {
+                                                              int32_t maxq, int32_t maxl, int32_t prof) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tw_smem[];
   // wave-uniform by construction (readfirstlane), so the pair's lengths, the sweep bounds and the backtrack are
   // scalar
@@ -2408,17 +2412,19 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const int k = (int)blockIdx.x * kTwWaves + wave;
   if (k >= npairs) return;  // wave-uniform
   const unsigned long long c0 = prof ? __builtin_readcyclecounter() : 0ull;
-  const TwLayout lay(maxl);
+  const TwLayout lay(maxq, maxl);
   struct {
     uint32_t* dir;
     int32_t *botH, *botF, *hendp;
-    uint8_t* tcode;
+    uint8_t *tcode, *qraw, *traw;
   } S;
   S.dir = (uint32_t*)(tw_smem + (size_t)wave * lay.wave_bytes);
   S.botH = (int32_t*)(S.dir + lay.dir_u32);
   S.botF = S.botH + maxl;
   S.hendp = S.botF + maxl;
   S.tcode = (uint8_t*)(S.hendp + 1);
+  S.qraw = S.tcode + maxl + 72;
+  S.traw = S.qraw + maxl;
   const int TW = lay.words;
   const uint32_t qv = pq[k];
   const int32_t q = (int32_t)(qv >> 1);
@@ -2431,10 +2437,13 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   for (int j = lane; j < tl + 72; j += 64) {
     const uint32_t c = j < tl ? (tcp[j >> 3] >> ((j & 7) * 4)) & 15u : 0u;
     S.tcode[j] = (uint8_t)(kGrouped ? ((c & (c - 1u)) == 0u ? c : 0u) : c);
+    if (kGrouped && j < tl) S.traw[j] = (uint8_t)c;
   }
   // both sequences' code words in VGPRs (lane w holds word w): the backtrack reads them by v_readlane
   // instead of a global / LDS load per diagonal step
   const uint32_t qword = lane < kCodeWords ? qcp[lane] : 0u, tword = lane < kCodeWords ? tcp[lane] : 0u;
+  if constexpr (kGrouped)
+    for (int i = lane; i < ql; i += 64) S.qraw[i] = (uint8_t)((qcp[i >> 3] >> ((i & 7) * 4)) & 15u);
   // identical sequences of one-hot codes (a member equal to its centroid: about (1 - error)^L of them): the all-M
   // path is the only optimum -- any other path trades matches for gaps or mismatches -- so its ops, matches and
   // internal length are known without the DP (codes past the length are 0 in both)
@@ -2617,52 +2626,82 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   uint8_t* o = ops + (int64_t)k * kOpsStride;
   const unsigned long long c2 = pw ? __builtin_readcyclecounter() : 0ull;
   if constexpr (kGrouped) {
-    // backtrack16 from (ql-1, tl-1) as wave-uniform scalar code: the cell's direction word by one LDS read and
-    // readfirstlane, the decisions and counters in SGPRs, the ops shifted into a dword stored every 4 ops
-    // (alignment order ends at o[kOpsStride - 1]; a final partial dword's low bytes, zero, fall below the ops and
-    // are never read).  align_trim's runs are tracked on the way: the first run generated is the alignment's last,
-    // the last one generated its first.
-    static_assert(kOpsStride % 4 == 0, "dword op stores");
-    int n = 0, i = ql - 1, j = tl - 1, matches = 0;
-    uint32_t op = 0, w4 = 0, first_op = 0, run_op = 0;
-    int first_run = 0, run_len = 0;
-    auto emit = [&](uint32_t c) {
-      w4 = (w4 << 8) | c;  // the op generated first (the alignment's later one) at the higher address
-      n++;
-      if ((n & 3) == 0 && lane == 0) *reinterpret_cast<uint32_t*>(o + kOpsStride - n) = w4;
-      if (n == 1) first_op = c;
-      if (c == first_op && first_run == n - 1) first_run = n;
-      run_len = c == run_op ? run_len + 1 : 1;
-      run_op = c;
+    // backtrack16 from (ql-1, tl-1) by runs, the wave deciding up to 64 steps at once: from a cell reached by a
+    // diagonal step (or the start) the path continues diagonally while the cells say neither up nor left -- lane x
+    // reads cell (i - x, j - x), a ballot gives the run; after an I (D) step it continues left (up) while the cells'
+    // extension bits say so -- lane x reads (i, j - x) ((i - x, j)).  A run's ops are stored by its lanes; the
+    // counters, states and align_trim's runs (the first run generated is the alignment's last, the last one its
+    // first) are scalar.  Same decisions as the per-cell loop below, cell for cell.
+    auto nib = [&](int ii, int jj) -> uint32_t {
+      const int l = ii & 63, tt = jj + l;
+      return (S.dir[((ii >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
     };
-    while (i >= 0 && j >= 0) {
-      const int l = i & 63, tt = j + l;
-      const uint32_t word = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l]);
-      const uint32_t d = (word >> ((tt & 7) * 4)) & 15u;
-      if (op == 'I' && (d & 8u)) {
-        j--;
-      } else if (op == 'D' && (d & 4u)) {
-        i--;
-      } else if (d & 2u) {
-        j--;
-        op = 'I';
-      } else if (d & 1u) {
-        i--;
-        op = 'D';
-      } else {
-        const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
-        const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
-        matches += (qc & tc) ? 1 : 0;
-        i--;
-        j--;
-        op = 'M';
+    int n = 0, i = ql - 1, j = tl - 1, matches = 0;
+    uint32_t first_op = 0, run_op = 0;
+    int first_run = 0, run_len = 0;
+    bool first_open = true;
+    auto emit_run = [&](uint32_t c, int r) {  // r >= 1 ops c (wave-uniform)
+      if (lane < r) o[kOpsStride - 1 - (n + lane)] = (uint8_t)c;
+      if (n == 0) first_op = c;
+      if (first_open) {
+        if (c == first_op) first_run += r;
+        else first_open = false;
       }
-      emit(op);
+      run_len = c == run_op ? run_len + r : r;
+      run_op = c;
+      n += r;
+    };
+    enum { kFresh = 0, kInI = 1, kInD = 2 };
+    int state = kFresh;
+    while (i >= 0 && j >= 0) {
+      if (state == kFresh) {
+        const int ii = i - lane, jj = j - lane;
+        const bool valid = ii >= 0 && jj >= 0;
+        const uint32_t d = valid ? nib(ii, jj) : 3u;
+        const unsigned long long stop = __ballot((d & 3u) != 0u);  // invalid cells stop the run too
+        const int r = stop ? __builtin_ctzll(stop) : 64;
+        if (r > 0) {
+          const bool m = lane < r && (S.qraw[valid ? ii : 0] & S.traw[valid ? jj : 0]) != 0;
+          matches += __builtin_popcountll(__ballot(m));
+          emit_run('M', r);
+          i -= r;
+          j -= r;
+        } else {
+          const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+          if (d0 & 2u) {
+            emit_run('I', 1);
+            j--;
+            state = kInI;
+          } else {
+            emit_run('D', 1);
+            i--;
+            state = kInD;
+          }
+        }
+      } else if (state == kInI) {
+        const int jj = j - lane;
+        const uint32_t d = jj >= 0 ? nib(i, jj) : 0u;
+        const unsigned long long stop = __ballot((d & 8u) == 0u);
+        const int r = stop ? __builtin_ctzll(stop) : 64;
+        if (r > 0) {
+          emit_run('I', r);
+          j -= r;
+        }
+        if (r < 64) state = kFresh;
+      } else {
+        const int ii = i - lane;
+        const uint32_t d = ii >= 0 ? nib(ii, j) : 0u;
+        const unsigned long long stop = __ballot((d & 4u) == 0u);
+        const int r = stop ? __builtin_ctzll(stop) : 64;
+        if (r > 0) {
+          emit_run('D', r);
+          i -= r;
+        }
+        if (r < 64) state = kFresh;
+      }
     }
-    for (; i >= 0; i--) emit('D');
-    for (; j >= 0; j--) emit('I');
-    if ((n & 3) != 0 && lane == 0)  // the last n & 3 ops: the newest at o[kOpsStride - n]
-      *reinterpret_cast<uint32_t*>(o + kOpsStride - ((n + 3) & ~3)) = w4 << (8 * (4 - (n & 3)));
+    for (; i >= 0; i -= 64) emit_run('D', min(i + 1, 64));
+    for (; j >= 0; j -= 64) emit_run('I', min(j + 1, 64));
     if (lane != 0) return;
     if (pw) {
       const unsigned long long c3 = __builtin_readcyclecounter();
@@ -2723,19 +2762,20 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
 
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
                             const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
-                            int32_t maxl) {
+                            int32_t maxl, int32_t maxq) {
   if (npairs <= 0) return hipSuccess;
   if (maxl < 1 || maxl > kMaxLen) return hipErrorInvalidValue;
-  const TwLayout lay(maxl);
+  if (maxq <= 0 || maxq > maxl) maxq = maxl;
+  const TwLayout lay(maxq, maxl);
   // UMICLUST_TRACE=step: the sweep with per-step tests (the round-3 loop), for A/B
   static const bool grouped = !(getenv("UMICLUST_TRACE") && strcmp(getenv("UMICLUST_TRACE"), "step") == 0);
   static const int32_t prof = getenv("UMICLUST_TWPROF") ? 1 : 0;
   if (grouped)
     hipLaunchKernelGGL(k_trace_wave<true>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
-                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl, prof);
+                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxq, maxl, prof);
   else
     hipLaunchKernelGGL(k_trace_wave<false>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
-                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxl, prof);
+                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxq, maxl, prof);
   return hipGetLastError();
 }
 hipError_t traceback_profile(unsigned long long out[4], bool reset) {

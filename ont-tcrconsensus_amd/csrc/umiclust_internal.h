@@ -221,9 +221,10 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
 // traceback (one wave per pair, any query length): ops[k*kOpsStride...] ('M','D','I' in alignment order,
 // right-aligned in the slot), nops[k], out[k] as launch_align's
 // maxl: the longest query or target length among the pairs (sizes the kernel's LDS)
+// maxl: the launch's longest sequence; maxq: its longest query (0: maxl) -- every pair's query must fit it
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
                             const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
-                            int32_t maxl);
+                            int32_t maxl, int32_t maxq = 0);
 hipError_t traceback_profile(unsigned long long out[4], bool reset);  // UMICLUST_TWPROF phase clocks
 // consensus: cluster c members member_seqno[cstart[c] .. cstart[c+1]) (centroid first),
 // member_ops index per member (-1 for centroid), member strand.
