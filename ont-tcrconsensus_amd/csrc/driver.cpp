@@ -376,8 +376,12 @@ struct umiclust_ctx {
   // faster (1.62 -> 1.76 ms per count + table on config 2: the counting is bound by the LDS array, ~73 % busy, 60 %
   // of it bank-conflict replays; profiles/r03/pftab_ab.json), so off by default
   bool pf_tab = false;
-  bool rec_direct = false;         // UMICLUST_RECDIRECT=1: k_pack writes outcomes and records straight to pinned host
-                                   // memory (round 4: DMA copies 4.33-4.36 vs 4.21-4.22 M UMIs/s, r04k envab)
+  // k_pack writes the outcomes and records straight into pinned host memory (true) or into device buffers copied by
+  // DMA (false).  Set per clustering call: DMA with one context in the process (config 2: 4.33-4.36 vs 4.21-4.22 M
+  // UMIs/s, the direct PCIe writes held k_pack at 133 us on the pass chain), direct with several (config 3, 8 lanes:
+  // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues); UMICLUST_RECDIRECT=0/1 fixes it.
+  bool rec_direct = false;
+  int rec_direct_env = -1;
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
@@ -1335,6 +1339,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
 // blocks then span bin boundaries and small bins share passes; the prefilter keeps only a query's own bin
 // (PrefilterArgs::qbin) and the results are split per bin.
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
+  c->rec_direct = c->rec_direct_env >= 0 ? c->rec_direct_env != 0 : g_live_ctx.load() > 1;
   const double t0 = now_s();
   if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
     c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
@@ -2233,7 +2238,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct_env = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
