@@ -253,9 +253,10 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=8,
                     help="configs 3/4: bins clustered concurrently per GPU (one device context per lane; 8 measured "
                          "best on config 3 with blocks across length changes: profiles/r03/mixlen_ab.json)")
-    ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "100000")),
+    ap.add_argument("--pack-reads", type=int, default=int(os.environ.get("UMICLUST_PACK_READS", "200000")),
                     help="configs 3/4: cluster each lane's bins in packs of up to this many reads (umiclust_cluster_pack; "
-                         "0: one bin per call; 100k measured best on config 3: profiles/r03/pack_ab.json)")
+                         "0: one bin per call; config 3: 100k and 200k equal on the whole set (7.60 / 7.61 M UMIs/s), "
+                         "200k better on an 8-GPU share (45.6 vs 35.9 M node bound): profiles/r04/pack_ab_c3)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="configs 3/4, one GPU: cluster only the LPT share --shard of a --shard-of-GPU node (the bins that "
                          "rank would get); timing every share this way bounds the node's makespan")
