@@ -262,6 +262,7 @@ def main() -> None:
                          "rank would get); timing every share this way bounds the node's makespan")
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--largest-bin", action="store_true", help="configs 3/4: the largest bin alone")
+    ap.add_argument("--bins", default="", help="configs 3/4: these bins alone (comma-separated indices)")
     ap.add_argument("--shard-sweep", type=int, default=0,
                     help="configs 3/4, one GPU: time every LPT share of an N-GPU node one after another (plus the largest "
                          "bin alone) in one process; the largest share time is the measured N-GPU makespan bound")
@@ -300,7 +301,9 @@ def main() -> None:
     if args.config in (3, 4):
         all_bins = synth.config_bins(args.config, args.scale, workers=min(16, os.cpu_count() or 4))
         costs = [shard.bin_cost(b.umis.n) for b in all_bins]
-        if args.largest_bin:
+        if args.bins:
+            sel = [int(x) for x in args.bins.split(",")]
+        elif args.largest_bin:
             sel = [max(range(len(costs)), key=lambda i: (costs[i], -i))]
         elif args.shard_of > 0:
             if world != 1 or not 0 <= args.shard < args.shard_of:
@@ -349,6 +352,7 @@ def main() -> None:
                     "bin, consensus emitted")
 
     runners = []
+    n_r1 = 0  # configs 3/4: units of round 1 at the head of a step's stats
     if umis is not None:
         params = _lib.params(_lib.PRESET_ROUND1, args.identity, *lens)
         ctx.stage(umis.seq, umis.off)  # the raw records resident in HBM (untimed)
@@ -373,8 +377,9 @@ def main() -> None:
                                             lanes=args.lanes, device=local_rank, pack_reads=args.pack_reads))
 
         def step():
+            nonlocal n_r1
             out = []
-            for r in runners:
+            for ri, r in enumerate(runners):
                 t0 = time.perf_counter()
                 r.prepare()  # A3 on every lane's staged bins -- inside the step
                 t_prep = time.perf_counter() - t0
@@ -382,6 +387,8 @@ def main() -> None:
                 if st:
                     st[0]["t_prepare_s"] = st[0].get("t_prepare_s", 0.0) + t_prep
                 out += st
+                if ri == 0:
+                    n_r1 = len(out)
             return out
 
     def barrier():
@@ -458,6 +465,13 @@ def main() -> None:
             # add up to the step): the largest bin bounds any split of these bins over GPUs
             per_bin = [s["t_total_s"] for s in last]
             out["largest_bin_s"] = max(per_bin) if per_bin else 0.0  # (the largest pack, with packing)
+            if per_bin:
+                w = max(last, key=lambda x: x["t_total_s"])
+                out["slowest_unit"] = {k: w[k] for k in ("t_total_s", "n_kept", "n_clusters", "n_blocks", "n_reruns",
+                                                         "n_alignments", "n_deferred", "t_host_s", "t_sync_s",
+                                                         "t_prefilter_s", "t_align_s") if k in w}
+                out["slowest_unit"]["bins"] = w.get("bins", [])[:8]
+                out["slowest_unit"]["round"] = 1 if any(w is x for x in stats[-1][:n_r1]) else 2
             out["bins_timed"] = len(per_bin)
             out["pack_reads"] = args.pack_reads
             out["lanes"] = args.lanes
@@ -685,9 +699,12 @@ def shard_sweep(args) -> None:
         for r in runners:
             r.close()
         _progress(f"shard-sweep: {len(sel)} bins, {kept} UMIs in {dt:.2f} s")
+        w = max(st, key=lambda x: x["t_total_s"]) if st else {}
         return dict(bins=len(sel), reads=int(bins.n), umis_kept=int(kept), seconds=dt, umis_per_s=kept / dt,
                     cost_share=sum(costs[i] for i in sel) / sum(costs),
-                    largest_pack_s=max((x["t_total_s"] for x in st), default=0.0))
+                    largest_pack_s=max((x["t_total_s"] for x in st), default=0.0),
+                    slowest_unit={k: w[k] for k in ("t_total_s", "n_kept", "n_blocks", "n_reruns", "n_deferred",
+                                                    "t_host_s", "t_sync_s") if k in w} | {"bins": len(w.get("bins", [0]))})
 
     run(plan[0])  # warm-up (untimed): allocations, code objects
     shares = [run(p) for p in plan]

@@ -392,6 +392,10 @@ struct umiclust_ctx {
   int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
+  int blk_max_np = 0;              // the last resolved block's largest peer count (resolve_pass)
+  int st_level = 0, prio_user = 0;  // the main stream's priority now / as umiclust_set_priority left it
+  bool ovf_prio = false;           // UMICLUST_OVF_PRIO=1: a bin's overflow re-runs move its main stream to the greatest
+                                   // priority (config 4: 5.90 vs 6.53 M UMIs/s, off)
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
   int64_t dbg_q[4] = {0, 0, 0, 0};
@@ -1129,6 +1133,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   c->stats.t_sync_s += now_s() - tc0;
   c->dbg_t[1] += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
+  {
+    int m = 0;  // the block's largest in-window peer count (block-size feedback; 255 = an overflow)
+    for (int32_t x = 0; x < nqs; x++) m = std::max<int>(m, hq[x].npeer);
+    c->blk_max_np = m;
+  }
   if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
   // the records are copied into pageable memory first (one streaming read; scattered reads of the DMA'd
   // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
@@ -1338,6 +1347,23 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
 // its own sorted order, the bins one after another: bins never interact, so this is every bin's own vsearch run):
 // blocks then span bin boundaries and small bins share passes; the prefilter keeps only a query's own bin
 // (PrefilterArgs::qbin) and the results are split per bin.
+// The main (counting) stream re-created at the greatest priority (level 1) or as a plain stream (0), after its queued
+// work; no other handle of it is kept (ix_st is st_b or null, events recorded on it have completed).
+hipError_t main_stream_priority(umiclust_ctx* c, int level) {
+  if (c->st_level == level) return hipSuccess;
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  hipStream_t s = nullptr;
+  if (e == hipSuccess) e = hipStreamSynchronize(c->st);  // work queued since the caller's drain (memsets) first
+  if (e == hipSuccess)
+    e = level ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi) : hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  (void)hipStreamDestroy(c->st);
+  c->st = s;
+  c->st_level = level;
+  return hipSuccess;
+}
+
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
   c->rec_direct = c->rec_direct_env >= 0 ? c->rec_direct_env != 0 : g_live_ctx.load() > 1;
   const double t0 = now_s();
@@ -1472,20 +1498,47 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     }
     sync_index(std::min(wnom, rs));
   };
+  static const bool adapt = getenv("UMICLUST_ADAPT") && atoi(getenv("UMICLUST_ADAPT")) != 0;
   // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
   int32_t b_eff = c->pack_on ? B : std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
+  if (adapt) b_eff = std::min(b_eff, 2048);  // the peer-load feedback (below) grows it from the first blocks
   int32_t eff_bin = -1;  // packs: the bin b_eff was last halved in (a deep cluster of one bin does not shrink the next)
+  int32_t b_cap = B;  // the feedback grows blocks up to this: the halved size after an overflow (per bin in packs)
+  // Halving stops at 256 queries (UMICLUST_BLOCK_FLOOR; a floor of kPeerCap / 4 = 32, at which no window can overflow,
+  // ran config 4's giant-molecule bin 200 in 8,578 blocks: 1.44 s alone against 0.6 s at 256, profiles/r04/block_policy)
+  static const int32_t kMinBlock = getenv("UMICLUST_BLOCK_FLOOR") ? std::max(1, atoi(getenv("UMICLUST_BLOCK_FLOOR"))) : 256;
   auto halve = [&](int32_t q) -> bool {  // false: already at the smallest block
     if (c->pack_on && c->hqbin[q] != eff_bin) {
       eff_bin = c->hqbin[q];
       b_eff = B;
     }
-    if (b_eff <= 256) return false;
-    b_eff /= 2;
+    if (b_eff <= kMinBlock) return false;
+    b_eff = std::max(kMinBlock, b_eff / 2);
+    b_cap = b_eff;
     return true;
   };
+  // ... and, opt-in (UMICLUST_ADAPT=1), a peer-load feedback: a window's peers grow with the block size, so the blocks
+  // not yet queued (after block `last`) are re-cut at twice the size when the resolved block's largest peer list was
+  // below a quarter of kPeerCap, and at half the size when it passed three quarters (shrinking before an overflow
+  // forces the synchronous re-run); bins start at 2048-query blocks.  Measured (profiles/r04/block_policy): config 2
+  // unchanged, config 4 6.51 vs 6.31 M UMIs/s, config 5 2.68 vs 3.47 M (smaller blocks cost more there than its few
+  // re-runs) -- so off by default.
   split_blocks(s0, b_eff);
   int32_t nb = (int32_t)blocks.size();
+  auto feedback = [&](int32_t last) {
+    if (!adapt || last + 1 >= nb) return;
+    const int m = c->blk_max_np;
+    int32_t nb_eff = b_eff;
+    const int32_t from = blocks[last].first + blocks[last].second;
+    if (c->pack_on && eff_bin >= 0 && c->hqbin[from] != eff_bin) b_cap = B;
+    if (m < kPeerCap / 4 && b_eff < b_cap) nb_eff = std::min(b_cap, 2 * b_eff);
+    else if (m > 3 * kPeerCap / 4 && m != 255 && b_eff > kMinBlock) nb_eff = std::max(kMinBlock, b_eff / 2);
+    if (nb_eff == b_eff) return;
+    b_eff = nb_eff;
+    blocks.resize((size_t)last + 1);
+    split_blocks(from, b_eff);
+    nb = (int32_t)blocks.size();
+  };
   std::vector<int32_t> new_cents;
   // A block whose peer list overflowed: re-run it alone (window = itself, index complete up to it)
   // in halving pieces, synchronously.
@@ -1602,7 +1655,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
           Q.a_live = false;
           c->hip(hipMemsetAsync(Q.d_anunits.p, 0, 4, c->st), "memset");
         }
-        run_alone(blocks[k].first, blocks[k].second);
+        if (c->ovf_prio) c->hip(main_stream_priority(c, 1), "stream priority");
+      run_alone(blocks[k].first, blocks[k].second);
+      c->blk_max_np = 255;  // the re-run pieces' peer counts say nothing about the queued block size
         if (k + 1 < nb && halve(blocks[k].first)) {
           const int32_t from = blocks[k].first + blocks[k].second;
           blocks.resize((size_t)k + 1);
@@ -1621,6 +1676,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
       if (k + 2 < nb) second_half(k + 2, k + 1, true);
       if (k + 3 < nb) count_half(k + 3, k + 1, 0);
+      if (k + 3 < nb) feedback(k + 3);    // blocks up to k + 3 are queued or built
       c->dbg_t[7] += ta1 - ta0;           // UMICLUST_DEBUG: index appends (host side)
       c->dbg_t[5] += now_s() - ta1;       // and the next passes' enqueue
     }
@@ -1647,7 +1703,12 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
           Q.live = false;
         }
       }
-      run_alone(blocks[k].first, blocks[k].second);
+      // an overflowing bin runs synchronous re-runs from here on: with other lanes sharing the GPU they queue behind
+        // every lane's work unless its main stream goes first (config 4: a 792k-read bin with a giant molecule took
+        // 7.2 s among 8 lanes, 0.6 s alone)
+        if (c->ovf_prio) c->hip(main_stream_priority(c, 1), "stream priority");
+        run_alone(blocks[k].first, blocks[k].second);
+        c->blk_max_np = 255;  // the re-run pieces' peer counts say nothing about the queued block size
       // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
       // same-molecule peers), so the overflow re-runs do not repeat block after block
       if (k + 1 < nb && halve(blocks[k].first)) {
@@ -1666,6 +1727,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
     if (k + D < nb) enqueue(k + D, D - 1);
+    if (k + D < nb) feedback(k + D);  // blocks up to k + D are queued
   }
   }
   c->b_hint = b_eff;
@@ -1676,6 +1738,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   c->ix_st = nullptr;
   c->hip(hipStreamSynchronize(c->st_al), "sync");
   c->hip(hipStreamSynchronize(c->st), "sync");
+  c->hip(main_stream_priority(c, c->prio_user), "stream priority");
   for (size_t i = 0; i < c->nix; i++) {
     float ms = 0;
     c->hip(hipEventElapsedTime(&ms, c->ix_events[i].first, c->ix_events[i].second), "elapsed");
@@ -2260,6 +2323,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PEER_CERT")) c->peer_cert = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_OVF_PRIO")) c->ovf_prio = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
@@ -2276,15 +2340,8 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
 int32_t umiclust_set_priority(umiclust_ctx* c, int32_t level) {
   if (!c || level < 0 || level > 1) return UMICLUST_EINVAL;
   if (hipSetDevice(c->dev) != hipSuccess || hipStreamSynchronize(c->st) != hipSuccess) return UMICLUST_EDEVICE;
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return UMICLUST_EDEVICE;
-  hipStream_t s = nullptr;
-  if ((level ? hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi) : hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) !=
-      hipSuccess)
-    return UMICLUST_EDEVICE;
-  (void)hipStreamDestroy(c->st);  // idle (synchronised above); nothing holds the stream itself
-  c->st = s;
-  return UMICLUST_OK;
+  c->prio_user = level;
+  return main_stream_priority(c, level) == hipSuccess ? UMICLUST_OK : UMICLUST_EDEVICE;
 }
 
 void umiclust_destroy(umiclust_ctx* c) {

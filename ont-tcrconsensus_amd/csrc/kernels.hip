@@ -2344,7 +2344,7 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
       h.flags = (uint8_t)((w.acc ? 1u : 0u) | (np == 255 ? 2u : 0u));
       h.nrel = (uint16_t)nrel;
       h.e = w.e;
-      h.pad = 0;
+      h.npeer = (uint8_t)np;
 #pragma unroll
       for (int j = 0; j < kInlineRel; j++) h.rel[j] = ids[j];
       hq[qs] = h;

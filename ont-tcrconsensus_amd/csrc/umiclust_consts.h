@@ -62,7 +62,7 @@ struct HostQs {
   uint8_t flags;        // bit 0: an accepted hit exists; bit 1: peer list overflow
   uint16_t nrel;        // relevant peers
   uint8_t e;            // walk candidates with an alignment result (record res[0, e))
-  uint8_t pad;
+  uint8_t npeer;        // peers counted in the window (<= kPeerCap; 255: overflow) -- the block-size feedback
   uint16_t rel[kInlineRel];  // the first kInlineRel of them (window ids), so the host reads the
                              // record only when one turns out to be a centroid (or nrel is larger)
 };

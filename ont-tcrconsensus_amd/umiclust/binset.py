@@ -138,7 +138,9 @@ class BinRunner:
         def run(lane):
             for j, m in self.packs(lane):
                 if m == 1:
-                    out[self.plan[lane][j]] = self.ctxs[lane].cluster_bin(j)
+                    st = self.ctxs[lane].cluster_bin(j)
+                    st["bins"] = [self.plan[lane][j]]
+                    out[self.plan[lane][j]] = st
                 else:
                     st = self.ctxs[lane].cluster_pack(j, m)
                     st["bins"] = [self.plan[lane][x] for x in range(j, j + m)]
