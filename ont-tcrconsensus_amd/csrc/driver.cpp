@@ -633,7 +633,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_outidx.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_res.ensure(nqs * (kWalk + kPeerCap)), "alloc");
   c->hip(P.d_hq.ensure(nqs), "alloc");
-  c->hip(P.d_paligned.ensure((size_t)nqs * 2), "alloc");  // two 64-bit masks per query-strand (kPeerCap 128)
+  c->hip(P.d_paligned.ensure((size_t)nqs * (kPeerCap / 64)), "alloc");  // 64-bit aligned-peer masks per query-strand
   c->hip(P.d_ws.ensure(nqs), "alloc");
   c->hip(P.d_reccount.ensure(1), "alloc");
   c->hip(P.h_hq.ensure(nqs), "pin");

@@ -2116,8 +2116,10 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = qs < nqs;  // every lane stays to the slot allocation
   const int np = live ? npeer[qs] : 0;
-  if (live) aligned[(int64_t)qs * 2] = aligned[(int64_t)qs * 2 + 1] = 0ull;
-  unsigned long long rel[2] = {0ull, 0ull};  // peers 0..63, 64..127 (kPeerCap)
+  constexpr int kPH = kPeerCap / 64;  // 64-bit masks per query-strand: peers 0..63, 64..127, ...
+  if (live)
+    for (int hh = 0; hh < kPH; hh++) aligned[(int64_t)qs * kPH + hh] = 0ull;
+  unsigned long long rel[kPH] = {};
   // A peer whose own device walk has already accepted a hit -- within its first w candidates, with w plus its
   // in-window peer count <= kWalk, so no merge can push that hit out of its walk -- is certain to become a member,
   // and members never enter a query's merged walk: its alignment would never be read.  The peer's walk state is
@@ -2155,12 +2157,12 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
           !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])) && !certain_member(ps))
         rel[x >> 6] |= 1ull << (x & 63);
     }
-    aligned[(int64_t)qs * 2] = rel[0];
-    aligned[(int64_t)qs * 2 + 1] = rel[1];
+    for (int hh = 0; hh < kPH; hh++) aligned[(int64_t)qs * kPH + hh] = rel[hh];
   }
   const int32_t q = q0 + (live ? qs : 0) / both;
   const int ql = lens[q];
-  const uint32_t n = (uint32_t)(__builtin_popcountll(rel[0]) + __builtin_popcountll(rel[1]));
+  uint32_t n = 0;
+  for (int hh = 0; hh < kPH; hh++) n += (uint32_t)__builtin_popcountll(rel[hh]);
   const uint32_t si = (uint32_t)(sg.lmax - ql);
   const uint32_t k0 = seg_alloc(n, si, seg_cnt);
   if (!n) return;
@@ -2251,7 +2253,7 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
         const uint32_t cnt = peer_count[(int64_t)qs * kPeerCap + x];
         const uint32_t ps = (uint32_t)w0 + id;
         const bool rel = peer_relevant(w, cnt, lens[ps], ps);
-        const bool al = (aligned[(int64_t)qs * 2 + hh] >> lane) & 1ull;
+        const bool al = (aligned[(int64_t)qs * kH + hh] >> lane) & 1ull;
         pw[i][hh] = id | (cnt << 16) | (rel ? 1u << 24 : 0u) | (al ? 1u << 25 : 0u);
         relb |= rel ? 1u << (i * kH + hh) : 0u;
         alb |= al ? 1u << (i * kH + hh) : 0u;

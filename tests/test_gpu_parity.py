@@ -304,7 +304,7 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
                         split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
                         pattern_rev=synth.UMI_REV_LONG)
     seqs = u.as_list()
-    # blocks of 1024: a two-block window holds ~250 reads of each molecule, past the 128-peer cap
+    # blocks of 1024: a two-block window holds ~250 reads of each molecule, past the 128-peer cap (kPeerCap)
     monkeypatch.setenv("UMICLUST_BLOCK", "1024")
     monkeypatch.setenv("UMICLUST_SPLIT", split)
     with _lib.Context(0) as ctx:
