@@ -312,7 +312,8 @@ struct umiclust_ctx {
                                    // k_align_pk (profiles/r03/band_ab.json)
   bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)
   bool rb_on_b = false;            // UMICLUST_RB_STREAM=b: round B on st_b (behind the index appends) instead of st_copy
-  bool r_on_al = false;            // UMICLUST_RAL=1: second halves' prefilter on the align stream (split passes)
+  bool r_on_al = true;             // UMICLUST_RAL=0: second halves' prefilter (full kernel + merge) on the main stream
+                                   // instead of the align stream (split passes; round 4: 4.67-4.68 vs 4.49-4.53 M UMIs/s)
   bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
                                   // concurrent counting slows the pass chain the host waits for)
   DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
@@ -427,6 +428,8 @@ struct umiclust_ctx {
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   PinBuf<uint32_t> h_mpq, h_mpt;     // the member pairs' pinned staging (traceback launch)
+  hipStream_t st_tw = nullptr;        // early member tracebacks (UMICLUST_TRACE_EARLY), least priority
+  hipEvent_t ev_tw = nullptr;
   PinBuf<int32_t> h_mseq, h_mops, h_cstart;
   PinBuf<uint8_t> h_mstr;
   PinBuf<uint16_t> h_clen;           // consensus lengths / sequences / overflow flag (pinned downloads)
@@ -1540,6 +1543,62 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     nb = (int32_t)blocks.size();
   };
   std::vector<int32_t> new_cents;
+  // Member tracebacks: tw_launch(lo, hi, stream) traces the members among seqnos [lo, hi) (their targets are final),
+  // queries of <= 64 nt in a launch of their own (a one-stripe direction store: more waves per CU), appending to the
+  // pair arrays at tw_n; opsidx maps a member to its traceback slot.  UMICLUST_TRACE_EARLY=f (0 < f < 1) traces the
+  // members of the first f of the blocks on a stream of the least priority while the later blocks are clustered.
+  std::vector<int32_t>& opsidx = c->t_opsidx;
+  opsidx.assign(n, -1);
+  int32_t tw_n = 0, tw_hi = s0;
+  c->hip(c->h_mpq.ensure((size_t)std::max(n, 1)), "pin");
+  c->hip(c->h_mpt.ensure((size_t)std::max(n, 1)), "pin");
+  c->hip(c->t_mpq.ensure(n), "alloc");
+  c->hip(c->t_mpt.ensure(n), "alloc");
+  c->hip(c->t_mout.ensure(n), "alloc");
+  c->hip(c->t_ops.ensure((size_t)std::max(n, 1) * kOpsStride), "alloc");
+  c->hip(c->t_nops.ensure(n), "alloc");
+  const DevSeqs ds = dev_seqs(c);
+  const int32_t tw_maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
+  // UMICLUST_TWSPLIT=0: one launch for every member (the direction store sized for the longest query)
+  static const int tw_split = getenv("UMICLUST_TWSPLIT") && atoi(getenv("UMICLUST_TWSPLIT")) == 0 ? kMaxLen : 64;
+  auto tw_launch = [&](int32_t lo, int32_t hi, hipStream_t stq) {
+    const int32_t x0 = tw_n;
+    int32_t x = x0, nm1 = 0, maxq1 = 0, maxq2 = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      for (int32_t s = lo; s < hi; s++)
+        if (c->target[s] >= 0 && (((int)c->hlen[s] <= tw_split) == (pass == 0))) {
+          opsidx[s - s0] = x;
+          c->h_mpq.p[x] = ((uint32_t)s << 1) | c->strand[s];
+          c->h_mpt.p[x] = (uint32_t)c->target[s];
+          (pass ? maxq2 : maxq1) = std::max(pass ? maxq2 : maxq1, (int32_t)c->hlen[s]);
+          x++;
+        }
+      if (pass == 0) nm1 = x;
+    }
+    tw_n = x;
+    if (x == x0) return;
+    c->hip(hipMemcpyAsync(c->t_mpq.p + x0, c->h_mpq.p + x0, (size_t)(x - x0) * 4, hipMemcpyHostToDevice, stq), "h2d");
+    c->hip(hipMemcpyAsync(c->t_mpt.p + x0, c->h_mpt.p + x0, (size_t)(x - x0) * 4, hipMemcpyHostToDevice, stq), "h2d");
+    c->hip(launch_traceback(ds, c->t_mpq.p + x0, c->t_mpt.p + x0, nm1 - x0, c->sc, c->t_ops.p + (size_t)x0 * kOpsStride,
+                            c->t_nops.p + x0, c->t_mout.p + x0, stq, tw_maxl, maxq1),
+           "traceback");
+    c->hip(launch_traceback(ds, c->t_mpq.p + nm1, c->t_mpt.p + nm1, x - nm1, c->sc, c->t_ops.p + (size_t)nm1 * kOpsStride,
+                            c->t_nops.p + nm1, c->t_mout.p + nm1, stq, tw_maxl, maxq2),
+           "traceback");
+  };
+  const double tw_early = getenv("UMICLUST_TRACE_EARLY") ? atof(getenv("UMICLUST_TRACE_EARLY")) : 0.0;
+  auto tw_maybe_early = [&](int32_t k) {  // block k was just resolved
+    if (!(tw_early > 0.0 && tw_early < 1.0) || tw_hi != s0 || k < (int32_t)(tw_early * nb) || c->o4_T) return;
+    if (!c->st_tw) {
+      int lo = 0, hi = 0;
+      c->hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
+      c->hip(hipStreamCreateWithPriority(&c->st_tw, hipStreamNonBlocking, lo), "stream");
+      c->hip(hipEventCreateWithFlags(&c->ev_tw, hipEventDisableTiming), "event");
+    }
+    tw_hi = blocks[k].first + blocks[k].second;
+    tw_launch(s0, tw_hi, c->st_tw);
+    c->hip(hipEventRecord(c->ev_tw, c->st_tw), "event");
+  };
   // A block whose peer list overflowed: re-run it alone (window = itself, index complete up to it)
   // in halving pieces, synchronously.
   auto run_alone = [&](int32_t q0, int32_t nq) {
@@ -1677,6 +1736,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       if (k + 2 < nb) second_half(k + 2, k + 1, true);
       if (k + 3 < nb) count_half(k + 3, k + 1, 0);
       if (k + 3 < nb) feedback(k + 3);    // blocks up to k + 3 are queued or built
+      tw_maybe_early(k);
       c->dbg_t[7] += ta1 - ta0;           // UMICLUST_DEBUG: index appends (host side)
       c->dbg_t[5] += now_s() - ta1;       // and the next passes' enqueue
     }
@@ -1728,6 +1788,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
     if (k + D < nb) enqueue(k + D, D - 1);
     if (k + D < nb) feedback(k + D);  // blocks up to k + D are queued
+    tw_maybe_early(k);
   }
   }
   c->b_hint = b_eff;
@@ -1746,58 +1807,17 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   }
   // --- member tracebacks first: their pairs (sorted seqno order) need only the targets, so the launch goes out
   // before the host numbers the clusters, which then overlaps the traceback (round 4: the numbering and the
-  // pageable pair uploads were ~16 ms of idle GPU before the traceback of a 2M-read bin)
-  std::vector<int32_t>& opsidx = c->t_opsidx;
-  opsidx.assign(n, -1);
-  int32_t nm = 0;
-  for (int32_t s = s0; s < s1; s++) nm += c->target[s] >= 0;
-  c->hip(c->h_mpq.ensure((size_t)std::max(nm, 1)), "pin");
-  c->hip(c->h_mpt.ensure((size_t)std::max(nm, 1)), "pin");
-  // members with queries of at most 64 nt first: their launch sizes the direction store for one stripe (more
-  // waves per CU); the longer ones follow in a launch of their own
-  int32_t nm1 = 0, maxq1 = 0, maxq2 = 0;
-  // UMICLUST_TWSPLIT=0: one launch for every member (the direction store sized for the longest query)
-  static const int tw_split = getenv("UMICLUST_TWSPLIT") && atoi(getenv("UMICLUST_TWSPLIT")) == 0 ? kMaxLen : 64;
-  {
-    int32_t x = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      for (int32_t s = s0; s < s1; s++)
-        if (c->target[s] >= 0 && (((int)c->hlen[s] <= tw_split) == (pass == 0))) {
-          opsidx[s - s0] = x;
-          c->h_mpq.p[x] = ((uint32_t)s << 1) | c->strand[s];
-          c->h_mpt.p[x] = (uint32_t)c->target[s];
-          (pass ? maxq2 : maxq1) = std::max(pass ? maxq2 : maxq1, (int32_t)c->hlen[s]);
-          x++;
-        }
-      if (pass == 0) nm1 = x;
-    }
-  }
-  c->hip(c->t_mpq.ensure(nm), "alloc");
-  c->hip(c->t_mpt.ensure(nm), "alloc");
-  c->hip(c->t_mout.ensure(nm), "alloc");
-  c->hip(c->t_ops.ensure((size_t)std::max(nm, 1) * kOpsStride), "alloc");
-  c->hip(c->t_nops.ensure(nm), "alloc");
-  if (nm > 0) {
-    c->hip(hipMemcpyAsync(c->t_mpq.p, c->h_mpq.p, (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
-    c->hip(hipMemcpyAsync(c->t_mpt.p, c->h_mpt.p, (size_t)nm * 4, hipMemcpyHostToDevice, c->st), "h2d");
-  }
+  // pageable pair uploads were ~16 ms of idle GPU before the traceback of a 2M-read bin).  The members before
+  // tw_hi went out early (UMICLUST_TRACE_EARLY, while later blocks were counted); these are the rest.
+  tw_launch(tw_hi, s1, c->st);
+  const int32_t nm = tw_n;
+  if (tw_hi > s0) c->hip(hipStreamWaitEvent(c->st, c->ev_tw, 0), "wait");  // the early tracebacks
   if (!c->tev[0]) {
     c->hip(hipEventCreate(&c->tev[0]), "event");
     c->hip(hipEventCreate(&c->tev[1]), "event");
   }
   c->hip(hipEventRecord(c->tev[0], c->st), "event");
-  DevSeqs ds = dev_seqs(c);
-  {
-    // every member's chosen hit in one launch (one wave per alignment, any query length)
-    // the bin's longest sequence bounds every pair's lengths (one pass over its lengths)
-    const int32_t maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
-    c->hip(launch_traceback(ds, c->t_mpq.p, c->t_mpt.p, nm1, c->sc, c->t_ops.p, c->t_nops.p, c->t_mout.p, c->st, maxl,
-                            maxq1),
-           "traceback");
-    c->hip(launch_traceback(ds, c->t_mpq.p + nm1, c->t_mpt.p + nm1, nm - nm1, c->sc, c->t_ops.p + (size_t)nm1 * kOpsStride,
-                            c->t_nops.p + nm1, c->t_mout.p + nm1, c->st, maxl, maxq2),
-           "traceback");
-  }
+  (void)nm;
   // creation numbers: centroids in creation (= sorted seqno) order, members inherit their centroid's
   c->nclusters = (int32_t)c->cent.size();
   for (int32_t k = 0; k < c->nclusters; k++) c->cno[c->cent[k]] = k;
@@ -2263,6 +2283,23 @@ static int al_priority() {
   return (e && atoi(e) == 0) ? lo : hi;
 }
 
+// The alignment stream.  UMICLUST_AL_CUS=k (1..31, experiment): the stream's kernels run on k of every 32 CUs (a CU
+// mask; such a stream has no priority), leaving the rest to the counting chain.
+static hipError_t create_al_stream(umiclust_ctx* c) {
+  if (const char* e = getenv("UMICLUST_AL_CUS")) {
+    const int k = atoi(e);
+    if (k > 0 && k < 32) {
+      std::vector<uint32_t> mask(32, 0u);  // up to 1024 CUs
+      for (int i = 0; i < 32 * 32; i++)
+        if (i % 32 < k) mask[(size_t)(i / 32)] |= 1u << (i % 32);
+      return hipExtStreamCreateWithCUMask(&c->st_al, (uint32_t)mask.size(), mask.data());
+    }
+  }
+  if (getenv("UMICLUST_AL_PRIO") && atoi(getenv("UMICLUST_AL_PRIO")) < 0)
+    return hipStreamCreateWithFlags(&c->st_al, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(&c->st_al, hipStreamNonBlocking, al_priority());
+}
+
 umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device_id < 0 || device_id >= ndev) {
@@ -2278,9 +2315,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_b, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess ||
-      (getenv("UMICLUST_AL_PRIO") && atoi(getenv("UMICLUST_AL_PRIO")) < 0
-           ? hipStreamCreateWithFlags(&c->st_al, hipStreamNonBlocking)
-           : hipStreamCreateWithPriority(&c->st_al, hipStreamNonBlocking, al_priority())) != hipSuccess ||
+      create_al_stream(c) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess || [&] {
         for (Pass& P : c->pass)
@@ -2361,6 +2396,8 @@ void umiclust_destroy(umiclust_ctx* c) {
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st_al) (void)hipStreamDestroy(c->st_al);
+  if (c->st_tw) (void)hipStreamDestroy(c->st_tw);
+  if (c->ev_tw) (void)hipEventDestroy(c->ev_tw);
   if (c->ix_done) (void)hipEventDestroy(c->ix_done);
   for (auto& r : c->a_ev)
     for (hipEvent_t e : r)

@@ -317,6 +317,37 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
     assert st["n_reruns"] > 0  # the overflow re-run and the pipeline restart were exercised
 
 
+@pytest.mark.parametrize("early", ["0.3", "0.75"])
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_early_member_traceback(early, split, monkeypatch):
+    """UMICLUST_TRACE_EARLY: the members of the first blocks are traced on a stream of their own while the later blocks
+    are clustered; membership, strands, centroids, consensus and the alignment count equal the oracle's (deep clusters
+    with overflow re-runs after the early launch, and a config-2-like sample with many blocks)."""
+    monkeypatch.setenv("UMICLUST_TRACE_EARLY", early)
+    monkeypatch.setenv("UMICLUST_SPLIT", split)
+    u = synth.make_umis(8, seed=31, max_reads=2500, orient_mix=0.3, mean_reads=1500.0, error_rate=0.15,
+                        split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
+                        pattern_rev=synth.UMI_REV_LONG)
+    monkeypatch.setenv("UMICLUST_BLOCK", "1024")
+    seqs = u.as_list()
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.75, 80, 110), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(1, 0.75, 80, 110), seqs)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"]
+    monkeypatch.setenv("UMICLUST_BLOCK", "512")
+    v = synth.make_umis(3000, seed=77, max_reads=30000).as_list()
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.9, 58, 68), v)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    o = orc.cluster(orc.params(1, 0.9, 58, 68), v)
+    _cmp_cluster(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["n_blocks"] > 20
+
+
 @pytest.mark.parametrize("split", ["0", "1"])
 def test_two_counter_segments(split, monkeypatch):
     """A bin past one counter segment (> 7 x 65,536 centroids: synth.segment_stress, 470k random 64-mers and
