@@ -829,7 +829,8 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
                                               uint64_t pbase, int part, int thr, int nk, uint32_t km0, uint32_t km1,
                                               int wv, int lane, int tid, uint32_t& T, uint32_t& nlc,
                                               bool skip0 = false, bool skip1 = false, uint32_t* def_ch = nullptr,
-                                              unsigned long long* clk = nullptr) {
+                                              bool prof = false, unsigned long long* clk0 = nullptr,
+                                              unsigned long long* clk1 = nullptr) {
   TileView tvs[kPfTilesPerWave];
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
@@ -867,14 +868,14 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
     sum_ch += nch[j];
     sum_ne += nch[j] ? 1u : 0u;
   }
-  if (clk) clk[0] = __builtin_readcyclecounter();  // phase probe: the list offsets have arrived
+  if (prof) *clk0 = __builtin_readcyclecounter();  // phase probe: the list offsets have arrived
   // window start masks (set below, after block_excl_scan's barriers)
   if (tid < kPfWinBase) tb.wtab[tid] = make_uint4(0u, 0u, 0u, 0u);
   // packed scan: chunks << kListBits | lists (see kListBits)
   uint32_t tot;
   const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
   if (def_ch && dch) atomicAdd(def_ch, dch);  // after the scan's barriers: *def_ch was zeroed before the call
-  if (clk) clk[1] = __builtin_readcyclecounter();
+  if (prof) *clk1 = __builtin_readcyclecounter();
   T = tot >> kListBits;
   nlc = tot & kListMask;
   uint32_t li = ex & kListMask, ci = ex >> kListBits;
@@ -1460,7 +1461,9 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   // phase barriers of sampled workgroups, into a.prof[9 + i] (k_pf_full uses [0, 9))
   const bool prof = a.prof != nullptr && tid == 0 && (blockIdx.x % 61u) == 0u;
   unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[5] = {0, 0, 0, 0, 0};
-  unsigned long long clk[2] = {0, 0}, tsub[2] = {0, 0};  // table sub-phases: offsets arrived, block scan done
+  // table sub-phases: offsets arrived, block scan done (scalars, not an address-taken array: that one lived in
+  // scratch, and its zeroing store from every lane of every workgroup was 537 MB of HBM writes per launch)
+  unsigned long long clk0 = 0, clk1 = 0, tsub[2] = {0, 0};
 #define PFC_MARK(i)                                             \
   if (prof) {                                                   \
     const unsigned long long tn = __builtin_readcyclecounter(); \
@@ -1490,10 +1493,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     if (prof) tsub[0] += __builtin_readcyclecounter() - tprev;
   } else {
     pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
-                  km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof ? clk : nullptr);
+                  km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof, &clk0, &clk1);
     if (prof) {
-      tsub[0] += clk[0] - tprev;
-      tsub[1] += clk[1] - clk[0];
+      tsub[0] += clk0 - tprev;
+      tsub[1] += clk1 - clk0;
     }
   }
   PFC_MARK(1)

@@ -31,10 +31,12 @@ for st in "$@"; do
              > "$out/$st.log" 2>&1; rc=$?
           if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
           rm -f "$out/$st/run_counter_collection.csv" ;;
-    fetch) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- python3 $B \
-             > "$out/fetch.log" 2>&1; rc=$? ;;
-    write) timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- python3 $B \
-             > "$out/write.log" 2>&1; rc=$? ;;
+    fetch|write) # one counter per pass; per-kernel totals only
+          [ "$st" = fetch ] && CT=FETCH_SIZE || CT=WRITE_SIZE
+          timeout -s KILL 300 rocprofv3 --pmc $CT --output-format csv -d "$out/$st" -o run -- python3 $B \
+             > "$out/$st.log" 2>&1; rc=$?
+          if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
+          rm -f "$out/$st/run_counter_collection.csv" ;;
     pfprof) UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof.json" 2> "$out/pfprof.err"; rc=$? ;;
     pfab) for cm in 0 1; do
             UMICLUST_PFCOUNT=$cm timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
@@ -49,6 +51,7 @@ for st in "$@"; do
     solo) # PMC collection serialises the dispatches: the kernel trace of this run holds every kernel's solo duration
           timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv -d "$out/solo" -o run -- \
              python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/solo.log" 2>&1; rc=$?
+          [ $rc = 0 ] && python3 tools/pmc_clock.py "$out/solo/run_counter_collection.csv" "k_pf_count<0>" "$out/pmc_clock_k_pf_count.json"
           rm -f "$out/solo/run_kernel_trace.csv" "$out/solo/run_counter_collection.csv" ;;
     probe) # the counting kernel with and without its count loop, solo (PMC serialises the dispatches)
           UMICLUST_PFPROBE=1 timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv \
