@@ -229,18 +229,15 @@ __device__ __forceinline__ void pk_init_rows(v2s (&H)[TOP], v2s (&E)[TOP], uint3
 
 template <bool B> struct BTag { static constexpr bool value = B; };
 
+// one pair per lane (k_align_pk below loops a wave over its pairs)
 template <int QL>
-__global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __restrict__ pq,
-                                                 const uint32_t* __restrict__ pt, int32_t npairs,
-                                                 const uint32_t* __restrict__ dev_npairs,
-                                                 const uint32_t* __restrict__ outidx, Scoring sc,
-                                                 uint32_t* __restrict__ out) {
+__device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* __restrict__ pq,
+                                              const uint32_t* __restrict__ pt, int k,
+                                              const uint32_t* __restrict__ outidx, const Scoring& sc,
+                                              uint32_t* __restrict__ out, uint16_t* sM) {
   constexpr int TOP = (QL + 1) / 2, BOT = QL - TOP;  // BOT == TOP or TOP - 1
   constexpr int NG = (TOP + 15) / 16;
   constexpr int KL = BOT - 1;                        // register holding row QL-1 (high half)
-  const int k = blockIdx.x * 64 + threadIdx.x;
-  if (k >= npairs) return;
-  if (dev_npairs && k >= (int)*dev_npairs) return;
   const uint32_t qv = pq[k];
   const int32_t q = (int32_t)(qv >> 1);
   const int qstr = (int)(qv & 1u);
@@ -265,7 +262,6 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
   }
   // the per-base row masks move to LDS (lane-private, [base][group][half][lane] u16): two 16-bit reads
   // per group and column instead of 4 NG live VGPRs and the 64-bit shifts
-  __shared__ uint16_t sM[4 * NG * 2 * 64];
   uint16_t* const pM = sM + threadIdx.x;
 #pragma unroll
   for (int b = 0; b < 4; b++)
@@ -406,6 +402,24 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
   const uint32_t acols = (uint32_t)(QL + tl) - (S >> 8);
   const uint32_t internal = acols - (uint32_t)trail;
   out[outidx ? outidx[k] : (uint32_t)k] = m | (internal << 8) | (((uint32_t)Hend & 0xffffu) << 16);
+}
+
+// A wave loops over pairs k0 + lane, k0 += 64 x grid: the launch may hold fewer waves than pairs / 64
+// (launch_align's UMICLUST_AL_WAVES cap), so that alignment waves leave VGPRs for the counting kernel's waves
+// instead of filling every SIMD (166 VGPRs x 3 waves) while a launch is in flight.
+template <int QL>
+__global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __restrict__ pq,
+                                                 const uint32_t* __restrict__ pt, int32_t npairs,
+                                                 const uint32_t* __restrict__ dev_npairs,
+                                                 const uint32_t* __restrict__ outidx, Scoring sc,
+                                                 uint32_t* __restrict__ out) {
+  constexpr int NG = ((QL + 1) / 2 + 15) / 16;
+  __shared__ uint16_t sM[4 * NG * 2 * 64];
+  const int n = dev_npairs ? min(npairs, (int)*dev_npairs) : npairs;
+  for (int k0 = (int)blockIdx.x * 64; k0 < n; k0 += (int)gridDim.x * 64) {  // wave-uniform
+    const int k = k0 + (int)threadIdx.x;
+    if (k < n) align_pk_pair<QL>(s, pq, pt, k, outidx, sc, out, sM);
+  }
 }
 
 // ------------------------------------------------------------------ K3B: banded packed alignment

@@ -1951,6 +1951,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
             "k_pf_count phase clocks per workgroup (%llu sampled): zero %.0f table %.0f count %.0f scan %.0f "
             "peers+out %.0f; chunks per workgroup %.1f; table = offsets %.0f + block scan %.0f + writes\n",
             h[14], h[9] / nc, h[10] / nc, h[11] / nc, h[12] / nc, h[13] / nc, h[15] / nc, h[16] / nc, h[17] / nc);
+    if (h[19])
+      fprintf(stderr, "k_pf_count sampled workgroups: %.0f shader cycles in %.2f us real time = %.2f GHz in the pipeline\n",
+              h[18] / nc, h[19] / nc / 100.0, (double)h[18] / ((double)h[19] / 100e6) / 1e9);
     c->hip(hipMemset(c->pf_prof.p, 0, 24 * sizeof(unsigned long long)), "memset");
   }
   c->stats.t_total_s = now_s() - t0;

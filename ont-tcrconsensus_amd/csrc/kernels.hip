@@ -1461,6 +1461,9 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   // phase barriers of sampled workgroups, into a.prof[9 + i] (k_pf_full uses [0, 9))
   const bool prof = a.prof != nullptr && tid == 0 && (blockIdx.x % 61u) == 0u;
   unsigned long long tprev = prof ? __builtin_readcyclecounter() : 0ull, tacc[5] = {0, 0, 0, 0, 0};
+  // ... and the workgroup's life in shader cycles and in the 100 MHz real-time clock: their ratio is the clock the
+  // kernel ran at inside the pipeline (PMC runs serialise dispatches and see only the solo clock)
+  const unsigned long long rt0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull, cy0 = tprev;
   // table sub-phases: offsets arrived, block scan done (scalars, not an address-taken array: that one lived in
   // scratch, and its zeroing store from every lane of every workgroup was 537 MB of HBM writes per launch)
   unsigned long long clk0 = 0, clk1 = 0, tsub[2] = {0, 0};
@@ -1620,6 +1623,8 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     atomicAdd(&a.prof[15], (unsigned long long)T);
     atomicAdd(&a.prof[16], tsub[0]);
     atomicAdd(&a.prof[17], tsub[1]);
+    atomicAdd(&a.prof[18], __builtin_readcyclecounter() - cy0);
+    atomicAdd(&a.prof[19], __builtin_amdgcn_s_memrealtime() - rt0);
   }
 #undef PFC_MARK
 }
@@ -1959,7 +1964,11 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
   const bool band = !ambig && variant0 == 0 && npairs <= band_max;
   const int64_t lanes = (int64_t)npairs * (band ? band_lanes(qlen) : 1);
   const int v = ambig ? 2 : band ? 3 : variant0;
-  hipLaunchKernelGGL(g_align[kAlignSlots * qlen + v], dim3((unsigned)((lanes + 63) / 64)),
+  int64_t grid = (lanes + 63) / 64;
+  // UMICLUST_AL_WAVES=w: at most w alignment waves per SIMD in flight (k_align_pk loops; experiment)
+  static const int64_t cap = getenv("UMICLUST_AL_WAVES") ? (int64_t)atoi(getenv("UMICLUST_AL_WAVES")) * 1024 : 0;
+  if (cap > 0 && v == 0) grid = std::min(grid, cap);
+  hipLaunchKernelGGL(g_align[kAlignSlots * qlen + v], dim3((unsigned)grid),
                      dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
 }
