@@ -789,7 +789,8 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t n, uint32_t* counter) {
   return b + inc - n;
 }
 
-// exclusive scan over the workgroup (every thread must call it); one DPP scan per wave
+// exclusive scan over the workgroup (every thread must call it); one DPP scan per wave, one barrier: the caller
+// must pass another barrier before wsum is written again (pf_list_table ends with one)
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const int wave = threadIdx.x >> 6;
   const uint32_t inc = wave_scan_dpp(v, OpAdd());
@@ -803,7 +804,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     tot += x;
   }
   total = tot;
-  __syncthreads();
   return base + inc - v;
 }
 
