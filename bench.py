@@ -196,10 +196,48 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
                  ceiling_gcups=ceiling, frac=g_alg / ceiling, frac_computed=g_cmp / ceiling,
                  ceiling_gcups_12ops=ceiling12, frac_12ops=g_alg / ceiling12,
                  speculative_ratio=cells_c / cells if cells else None)
+    # the aligner alone: its kernels' durations in a PMC run (dispatches serialised, so nothing shares the CUs) of the
+    # same workload, per bin, against this run's cells per bin (config 2: one bin per step)
+    solo_p = os.path.join(ROOT, "profiles", "r04", "rocprof_solo_kernel_stats_c2_r04zm.csv")
+    if config == 2 and os.path.exists(solo_p) and stats:
+        t_solo = 0.0
+        for r in csv.DictReader(open(solo_p, newline="")):
+            nm = r["Name"].replace("void ", "").split("(")[0].split("::")[-1]
+            if nm.startswith("k_align_pk") or nm.startswith("k_align_band"):
+                t_solo += float(r["TotalDurationNs"]) * 1e-9
+        bins_solo = 2  # tools/gpu_r04.sh `solo`: bench.py --steps 1 --warmup 1
+        if t_solo > 0:
+            align["gcups_solo"] = (cells / len(stats)) / (t_solo / bins_solo) / 1e9
+            align["frac_solo"] = align["gcups_solo"] / ceiling
+            align["solo_source"] = os.path.relpath(solo_p, ROOT)
     return roof, align
 
 
 def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
+    """Per-CU LDS-array and VALU busy of `kernel` (round 4: from the per-kernel PMC totals of
+    profiles/r04/pmc_busy_c2_final.json, tools/pmc_agg.py; else round 3's CSV below)."""
+    agg_path = os.path.join(ROOT, "profiles", "r04", "pmc_busy_c2_final.json")
+    cal_path = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
+    if os.path.exists(agg_path) and os.path.exists(cal_path):
+        agg = json.load(open(agg_path))
+        k = next((x for x in agg if x.split("<")[0] == kernel and x.endswith("<0>")), None) or \
+            next((x for x in agg if x.split("<")[0] == kernel), None)
+        if k:
+            cal = json.load(open(cal_path))
+            n = agg[k]["dispatches"]
+            per = {c: v / n for c, v in agg[k].items() if isinstance(v, float) and c not in ("mean_us",)}
+            cyc = per["GRBM_GUI_ACTIVE"] / cal["xcds"]
+            return dict(source=os.path.relpath(agg_path, ROOT), calibration=os.path.relpath(cal_path, ROOT),
+                        dispatches=n, kernel_cycles=cyc,
+                        lds_array_busy_per_cu=per["SQ_LDS_IDX_ACTIVE"] * cal["lds_idx_active_cycles_per_unit"] / cal["cus"] / cyc,
+                        valu_busy_per_simd=per["SQ_ACTIVE_INST_VALU"] * cal["active_inst_valu_cycles_per_unit"] / (cal["cus"] * 4) / cyc,
+                        lds_bank_conflict_frac=per.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, per["SQ_LDS_IDX_ACTIVE"]),
+                        lds_array_cycles_per_instr=per["SQ_LDS_IDX_ACTIVE"] / max(1.0, per.get("SQ_INSTS_LDS", 0.0)),
+                        valu_instrs_per_lds_instr=per["SQ_INSTS_VALU"] / max(1.0, per.get("SQ_INSTS_LDS", 0.0)))
+    return _pmc_busy_csv(kernel)
+
+
+def _pmc_busy_csv(kernel: str = "k_pf_count") -> dict | None:
     """Per-CU LDS-array and VALU busy of `kernel`, from the committed rocprofv3 PMC CSV
     (profiles/r03/pmc_busy_<kernel>.csv: SQ_LDS_IDX_ACTIVE, SQ_ACTIVE_INST_VALU, SQ_INSTS_LDS, SQ_INSTS_VALU,
     GRBM_GUI_ACTIVE, ...; one pass, step `busy` of tools/gpu_r03.sh) with the unit factors measured by the calibration
