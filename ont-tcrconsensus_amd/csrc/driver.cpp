@@ -760,11 +760,12 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     if (t->n > 0) P.h_tiles.p[nv++] = view_of(*t);
   if (c->base_tile.n > 0) P.h_tiles.p[nv++] = view_of(c->base_tile);
   if (c->delta_tile[c->delta_cur].n > 0) P.h_tiles.p[nv++] = view_of(c->delta_tile[c->delta_cur]);
-  if (nv > 0)
+  if (nv > kArgTiles)
     c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
   c->hip(hipMemsetAsync(P.d_counters.p, 0, kCountersLen * 4, st), "memset");
   PrefilterArgs a{};
+  for (int32_t i = 0; i < nv && nv <= kArgTiles; i++) a.tv[i] = P.h_tiles.p[i];
   a.seqs = dev_seqs(c);
   a.arena = c->arena.p;
   a.tiles = P.d_tiles.p;
@@ -984,11 +985,12 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
     if (t->n > 0) P.h_tiles_a.p[nv++] = view_of(*t);
   if (c->base_tile.n > 0) P.h_tiles_a.p[nv++] = view_of(c->base_tile);
   if (c->delta_tile[c->delta_cur].n > 0) P.h_tiles_a.p[nv++] = view_of(c->delta_tile[c->delta_cur]);
-  if (nv > 0)
+  if (nv > kArgTiles)
     c->hip(hipMemcpyAsync(P.d_tiles_a.p, P.h_tiles_a.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
   c->hip(hipEventRecord(P.ev_a, st), "event");
   PrefilterArgs a{};
+  for (int32_t i = 0; i < nv && nv <= kArgTiles; i++) a.tv[i] = P.h_tiles_a.p[i];
   a.seqs = dev_seqs(c);
   a.arena = c->arena.p;
   a.tiles = P.d_tiles_a.p;

@@ -682,6 +682,11 @@ __device__ __forceinline__ TileView load_view(const TileView* p) {
   return __builtin_bit_cast(TileView, r);
 }
 
+// centroid tile view i of a pass: from the kernel arguments, or the device array past kArgTiles tiles
+__device__ __forceinline__ TileView cent_view(const PrefilterArgs& a, int i) {
+  return a.ntiles <= kArgTiles ? a.tv[i] : load_view(a.tiles + i);
+}
+
 // packs: the bytes of a counter word from byte nb on (nb <= 0: all four, nb >= 4: none)
 __device__ __forceinline__ uint32_t keep_from(int nb) {
   return nb <= 0 ? 0xffffffffu : nb >= 4 ? 0u : ~((1u << (8 * nb)) - 1u);
@@ -835,7 +840,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
     const int ti = wv + it * kPfWaves;
-    if (ti < nct) tvs[it] = load_view(a.tiles + t0 + ti);
+    if (ti < nct) tvs[it] = cent_view(a, t0 + ti);
     else if (ti < ntl) tvs[it] = a.peer[ti - nct];
     else tvs[it].n = 0;
   }
@@ -1336,7 +1341,7 @@ __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __re
 #pragma unroll
   for (int ti = 0; ti < kPfTiles; ti++) {
     TileView tv;
-    if (ti < nct) tv = load_view(a.tiles + ti);
+    if (ti < nct) tv = cent_view(a, ti);
     else if (ti < ntl) tv = a.peer[ti - nct];
     else tv.n = 0;
     lv[ti] = thr > 0 && ti < ntl && tv.n > 0;

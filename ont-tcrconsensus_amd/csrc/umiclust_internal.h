@@ -80,11 +80,15 @@ __host__ __device__ constexpr uint32_t pf_table_stride(int nlist_cap) {
   return (4u + pf_table_img_words(nlist_cap) + 3u) & ~3u;
 }
 constexpr int kFKmers = 32;  // frequent k-mers of a load eligible for deferral (PrefilterArgs::fkmer)
+// centroid tile views passed in the kernel arguments (a pass reads them by scalar loads either way; in the arguments
+// they need no host-to-device copy, a blit dispatch between every two counting launches)
+constexpr int kArgTiles = 32;
 struct PrefilterArgs {
   DevSeqs seqs;
   const uint16_t* arena;   // postings of every tile
-  const TileView* tiles;   // device array, centroid tiles in segment order
+  const TileView* tiles;   // device array, centroid tiles in segment order (used when ntiles > kArgTiles)
   int32_t ntiles;
+  TileView tv[kArgTiles];  // the same views when ntiles <= kArgTiles
   int32_t nseg;            // counter segments holding centroids (0 if none)
   int32_t seg_tile[kMaxSegs + 1];  // tiles of segment s: [seg_tile[s], seg_tile[s+1])
   uint64_t seg_base[kMaxSegs];     // lowest arena index a pass of segment s reads (peers: last pass)
