@@ -64,7 +64,7 @@ def cpu_baseline_bins(bins, identity: float, lens, budget_s: float = 20.0, prese
     import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
-    cores = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
+    cores = _host_cores()
     order = sorted(bins, key=lambda b: -b.umis.n)
     orc.cluster(orc.params(preset, identity, *lens), order[-1].umis.as_list())  # library load / tables
     lock = threading.Lock()
@@ -107,6 +107,40 @@ def cpu_baseline_prefix(umis, n_sample: int, identity: float, lens, preset: int 
                        f"{r['n_clusters']} clusters) clustered by the C oracle restatement, 1 thread, "
                        f"{dt:.1f} s; CPU cost grows ~N*C, so the full bin is slower per UMI (full-bin oracle "
                        f"time: tests/golden/oracle_config2.json oracle_seconds)",
+                seconds=dt, n_kept=r["stats"]["kept"])
+
+
+def _host_cores() -> int:
+    return min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
+
+
+def cpu_baseline_threads(umis, n_sample: int, identity: float, lens, preset: int = 1) -> dict:
+    """The C oracle in vsearch's multi-threaded mode (policy O4, cluster_core_parallel restated: rounds of
+    `threads` queries searched against the index frozen at the round's start, then re-checked in order) with the
+    round's searches on one OpenMP worker per host core -- how the reference runs vsearch (--threads >= 25,
+    vsearch_umi_cluster.py:33-34, utils.py:56-63) -- on the first n_sample reads of the bin."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    cores = _host_cores()
+    seqs = umis.as_list()[:n_sample]
+    p = orc.params(preset, identity, *lens)
+    p.threads, p.policy_threads = cores, 1
+    old = os.environ.get("ORC_WORKERS")
+    os.environ["ORC_WORKERS"] = str(cores)
+    try:
+        t0 = time.perf_counter()
+        r = orc.cluster(p, seqs)
+        dt = time.perf_counter() - t0
+    finally:
+        if old is None:
+            os.environ.pop("ORC_WORKERS", None)
+        else:
+            os.environ["ORC_WORKERS"] = old
+    return dict(value=r["stats"]["kept"] / dt, unit="UMIs/s", cores=cores, kind="port",
+                sample=f"first {n_sample} reads of the rank-0 bin ({r['stats']['kept']} kept, {r['n_clusters']} "
+                       f"clusters) clustered by the C oracle restatement in vsearch's --threads {cores} mode (policy "
+                       f"O4: rounds of {cores} queries, the round's searches on {cores} OpenMP workers), {dt:.1f} s; "
+                       f"CPU cost grows ~N*C, so the full bin is slower per UMI",
                 seconds=dt, n_kept=r["stats"]["kept"])
 
 
@@ -286,6 +320,8 @@ def main() -> None:
     ap.add_argument("--identity", type=float, default=None,
                     help="default 0.90 (config 2), 0.93 (configs 3, 4 round 1), 0.75 (config 5)")
     ap.add_argument("--cpu-sample", type=int, default=40000)
+    ap.add_argument("--cpu-sample-mt", type=int, default=40000,
+                    help="reads of the multi-threaded (vsearch --threads) CPU baseline's prefix")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the file leg (config 2, N = 1)")
     ap.add_argument("--lanes", type=int, default=8,
@@ -516,7 +552,10 @@ def main() -> None:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             if umis is not None:
-                cpu = cpu_baseline_prefix(umis, args.cpu_sample, args.identity, lens)
+                # the reference's operating mode (vsearch --threads on every core) is the baseline; the
+                # 1-thread sequential definition on a smaller prefix rides along
+                cpu = cpu_baseline_threads(umis, args.cpu_sample_mt, args.identity, lens)
+                cpu["serial_1thread"] = cpu_baseline_prefix(umis, args.cpu_sample, args.identity, lens)
                 full = full_bin_cpu_reference(args.config)
                 if full:
                     cpu["full_bin_oracle"] = full

@@ -10,6 +10,9 @@
  * Deliberately written as plain, scalar, allocation-heavy C: it is the checker, not the
  * product.  Nothing here is shared with ont-tcrconsensus_amd/csrc.
  */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "umiclust_oracle.h"
 
 #include <ctype.h>
@@ -695,20 +698,55 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
     int32_t *extra = (int32_t *)malloc(sizeof(int32_t) * (size_t)T);
     uint32_t *ekm = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(maxl + 8));
     uint64_t *qset = (uint64_t *)calloc(((size_t)1 << (2 * p->wordlength)) / 64 + 1, 8);
+    /* ORC_WORKERS=<n> (built with OpenMP): the round's searches on n worker threads, as vsearch's --threads
+     * workers run them.  Results do not depend on n: every search reads only the index frozen at the round's
+     * start, and the analysis below stays sequential.  Each worker has its own scratch and work counters. */
+    int W = 1;
+#ifdef _OPENMP
+    const char *we = getenv("ORC_WORKERS");
+    if (we && atoi(we) > 1) W = atoi(we) < T ? atoi(we) : T;
+#endif
+    uint32_t **wk_kbuf = (uint32_t **)malloc(sizeof(uint32_t *) * (size_t)W);
+    int32_t **wk_counts = (int32_t **)malloc(sizeof(int32_t *) * (size_t)W);
+    char **wk_rcq = (char **)malloc(sizeof(char *) * (size_t)W);
+    for (int w = 0; w < W; w++) {
+      wk_kbuf[w] = w ? (uint32_t *)malloc(sizeof(uint32_t) * (size_t)(maxl + 8)) : kbuf;
+      wk_counts[w] = w ? (int32_t *)malloc(sizeof(int32_t) * (size_t)(nk + 1)) : counts;
+      wk_rcq[w] = w ? (char *)malloc((size_t)maxl + 2) : rcq;
+    }
     for (int32_t b0 = 0; b0 < nk; b0 += T) {
       const int32_t nb = (nk - b0 < T) ? nk - b0 : T;
+#ifdef _OPENMP
+      #pragma omp parallel for num_threads(W) schedule(dynamic, 1) if (W > 1)
+#endif
       for (int32_t i = 0; i < nb; i++) {
+#ifdef _OPENMP
+        const int w = omp_get_thread_num();
+#else
+        const int w = 0;
+#endif
+        ctx_t cw = c;  /* shares the frozen index; own work counters */
+        cw.alignments = cw.cells = cw.postings = cw.candidates = 0;
         const int32_t s = b0 + i;
-        int64_t a0 = c.alignments;
-        bn[2 * i] = search_strand(&c, p, c.seq[s], c.len[s], 0, kbuf, counts, bh + (size_t)(2 * i) * cap);
-        if (wd) wd[2 * s] = (int16_t)(c.alignments - a0);
-        a0 = c.alignments;
+        bn[2 * i] = search_strand(&cw, p, c.seq[s], c.len[s], 0, wk_kbuf[w], wk_counts[w], bh + (size_t)(2 * i) * cap);
+        if (wd) wd[2 * s] = (int16_t)cw.alignments;
+        const int64_t a0 = cw.alignments;
         bn[2 * i + 1] = 0;
         if (p->strand_both) {
-          revcomp(rcq, c.seq[s], c.len[s]);
-          bn[2 * i + 1] = search_strand(&c, p, rcq, c.len[s], 1, kbuf, counts, bh + (size_t)(2 * i + 1) * cap);
+          revcomp(wk_rcq[w], c.seq[s], c.len[s]);
+          bn[2 * i + 1] = search_strand(&cw, p, wk_rcq[w], c.len[s], 1, wk_kbuf[w], wk_counts[w],
+                                        bh + (size_t)(2 * i + 1) * cap);
         }
-        if (wd) wd[2 * s + 1] = (int16_t)(c.alignments - a0);
+        if (wd) wd[2 * s + 1] = (int16_t)(cw.alignments - a0);
+#ifdef _OPENMP
+        #pragma omp critical(orc_work)
+#endif
+        {
+          c.alignments += cw.alignments;
+          c.cells += cw.cells;
+          c.postings += cw.postings;
+          c.candidates += cw.candidates;
+        }
       }
       int nextra = 0;
       for (int32_t i = 0; i < nb; i++) {
@@ -763,6 +801,14 @@ int64_t orc_cluster(const orc_params *p, int32_t n, const char *const *seqs, con
         if (clusters > before) extra[nextra++] = s;
       }
     }
+    for (int w = 1; w < W; w++) {
+      free(wk_kbuf[w]);
+      free(wk_counts[w]);
+      free(wk_rcq[w]);
+    }
+    free(wk_kbuf);
+    free(wk_counts);
+    free(wk_rcq);
     free(qset);
     free(ekm);
     free(extra);

@@ -1,7 +1,7 @@
 /*
  * umiclust_oracle.h -- CPU ORACLE (test infrastructure only).
  *
- * A single-threaded C restatement of the arithmetic behind the reference's hot path:
+ * A C restatement of the arithmetic behind the reference's hot path:
  *   `vsearch --cluster_fast <fa> --strand both --id X --clusters <dir>/cluster --consout ...
  *    --clusterout_id --clusterout_sort [--gapopen 0E/40I --mismatch -40 --match 10]`
  * as driven by /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:21-54 (round 1) and
@@ -53,6 +53,8 @@ typedef struct orc_params {
                             against the index frozen at the round's start, then, in order, each query
                             re-checked against the round's new centroids (inserted into its hit list by
                             k-mer count and re-walked one alignment at a time) */
+                         /* policy_threads = 1 with the environment's ORC_WORKERS = n: the round's searches run
+                            on n OpenMP worker threads (results unchanged) */
 } orc_params;
 
 /* presets: 1 = round 1 (vsearch_umi_cluster.py:44-50: --gapopen 0E/40I --mismatch -40

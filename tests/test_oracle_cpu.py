@@ -213,3 +213,17 @@ def test_o4_threads25_changes_membership_at_high_error():
     moved = _partition(a) - _partition(b)
     assert len(moved) > 0
     assert sum(len(g) for g in moved) < len(seqs) // 100  # a handful of reads
+
+
+def test_o4_worker_threads_do_not_change_results(monkeypatch):
+    """ORC_WORKERS runs an O4 round's searches on OpenMP workers (bench.py's multi-core CPU baseline); every
+    search reads only the index frozen at the round's start, so clusters, strands, consensus and the work
+    counters are those of one worker."""
+    seqs = synth.make_umis(300, seed=43, max_reads=4000, orient_mix=0.2).as_list()
+    monkeypatch.setenv("ORC_WORKERS", "1")
+    a = orc.cluster(_o4(1, 0.90, 16), seqs)
+    monkeypatch.setenv("ORC_WORKERS", "4")
+    b = orc.cluster(_o4(1, 0.90, 16), seqs)
+    assert (a["cluster"] == b["cluster"]).all() and (a["strand"] == b["strand"]).all()
+    assert (a["centroid"] == b["centroid"]).all() and a["consensus"] == b["consensus"]
+    assert a["stats"] == b["stats"]
