@@ -337,6 +337,8 @@ def main() -> None:
     ap.add_argument("--shard", type=int, default=0)
     ap.add_argument("--largest-bin", action="store_true", help="configs 3/4: the largest bin alone")
     ap.add_argument("--bins", default="", help="configs 3/4: these bins alone (comma-separated indices)")
+    ap.add_argument("--sweep-shares", default="",
+                    help="--shard-sweep: only these share indices (comma-separated; no node value)")
     ap.add_argument("--shard-sweep", type=int, default=0,
                     help="configs 3/4, one GPU: time every LPT share of an N-GPU node one after another (plus the largest "
                          "bin alone) in one process; the largest share time is the measured N-GPU makespan bound")
@@ -781,10 +783,13 @@ def shard_sweep(args) -> None:
                     cost_share=sum(costs[i] for i in sel) / sum(costs),
                     largest_pack_s=max((x["t_total_s"] for x in st), default=0.0),
                     slowest_unit={k: w[k] for k in ("t_total_s", "n_kept", "n_blocks", "n_reruns", "n_deferred",
-                                                    "t_host_s", "t_sync_s") if k in w} | {"bins": len(w.get("bins", [0]))})
+                                                    "t_host_s", "t_sync_s") if k in w} | {"bins": len(w.get("bins", [0]))},
+                    long_units=[{k: x[k] for k in ("t_total_s", "n_kept", "n_blocks", "n_reruns") if k in x}
+                                | {"bins": x.get("bins", [])[:4]} for x in st if x["t_total_s"] > 0.4 * dt])
 
     run(plan[0])  # warm-up (untimed): allocations, code objects
-    shares = [run(p) for p in plan]
+    pick = [int(x) for x in args.sweep_shares.split(",")] if args.sweep_shares else list(range(N))
+    shares = [dict(run(plan[i]), share=i) for i in pick]
     big = run([largest])
     tmax = max(x["seconds"] for x in shares)
     node_umis = sum(x["umis_kept"] for x in shares)
@@ -798,6 +803,8 @@ def shard_sweep(args) -> None:
                       "lanes": args.lanes, "pack_reads": args.pack_reads},
            "shares": shares, "makespan_s": tmax, "sum_s": sum(x["seconds"] for x in shares),
            "largest_bin": dict(big, bin=largest), "measured_on": "one GPU"}
+    if len(pick) < N:  # a subset of the shares: no node figure
+        out.update(value=None, partial_shares=pick)
     print(json.dumps(out), flush=True)
     ctx.close()
     if ctx2 is not None:

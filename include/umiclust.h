@@ -129,9 +129,10 @@ int32_t umiclust_params_from_argv(umiclust_params *p, int32_t argc, const char *
 umiclust_ctx *umiclust_create(int32_t device_id, int32_t *err);
 void umiclust_destroy(umiclust_ctx *ctx);
 /* ABI 7: the context's main (counting) stream at the device's greatest stream priority (level 1) or a plain
- * stream (level 0, the default); its alignment stream is always prioritised.  Lets a caller running several
- * bins at once on one GPU (BinRunner lanes; tcr_consensus.py:231-245 runs one vsearch per bin) put the bin that
- * sets the makespan ahead of the others.  Synchronises the context first.  Results do not depend on it. */
+ * stream (level 0, the default); its alignment stream is prioritised at both levels.  Level -1 (background):
+ * every stream plain, the alignment stream included.  Lets a caller running several bins at once on one GPU
+ * (BinRunner lanes; tcr_consensus.py:231-245 runs one vsearch per bin) put the bins that set the makespan ahead
+ * of the others.  Synchronises the context first.  Results do not depend on it. */
 int32_t umiclust_set_priority(umiclust_ctx *ctx, int32_t level);
 /* human-readable message for the last error on this context */
 const char *umiclust_last_error(const umiclust_ctx *ctx);

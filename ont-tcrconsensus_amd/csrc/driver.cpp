@@ -202,6 +202,12 @@ struct Pass {
 }  // namespace
 
 static std::atomic<int> g_live_ctx{0};  // contexts alive in this process (L3Pin)
+// Exclusive re-runs: a context whose bin overflows a peer list (a giant molecule: synchronous re-runs, small blocks,
+// one host <-> device round trip per block) takes the GPU for the rest of that bin; the other contexts hold at their
+// next block boundary until it is done.  Among 8 lanes such a bin's round trips queued behind every lane's work
+// (config 4: 3.07 s in its lane, 0.22 s alone).  Timing only: every context's results are unchanged.
+struct umiclust_ctx;
+static std::atomic<umiclust_ctx*> g_excl{nullptr};
 
 struct umiclust_ctx {
   int dev = 0;
@@ -383,6 +389,7 @@ struct umiclust_ctx {
   // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues); UMICLUST_RECDIRECT=0/1 fixes it.
   bool rec_direct = false;
   int rec_direct_env = -1;
+  bool excl = true;   // UMICLUST_EXCL=0: an overflowing bin does not take the GPU from the other contexts
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
@@ -394,6 +401,7 @@ struct umiclust_ctx {
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int blk_max_np = 0;              // the last resolved block's largest peer count (resolve_pass)
+  int al_level = 0;                 // the alignment stream: 0 prioritised (al_priority), -1 plain (set_priority -1)
   int st_level = 0, prio_user = 0;  // the main stream's priority now / as umiclust_set_priority left it
   bool ovf_prio = false;           // UMICLUST_OVF_PRIO=1: a bin's overflow re-runs move its main stream to the greatest
                                    // priority (config 4: 5.90 vs 6.53 M UMIs/s, off)
@@ -1369,8 +1377,32 @@ hipError_t main_stream_priority(umiclust_ctx* c, int level) {
   return hipSuccess;
 }
 
+// hold while another context has the GPU to itself (g_excl)
+static void excl_wait(umiclust_ctx* c) {
+  for (;;) {
+    umiclust_ctx* o = g_excl.load(std::memory_order_acquire);
+    if (o == nullptr || o == c) return;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+// released when the bin (or pack) ends, on every exit path
+struct ExclRelease {
+  umiclust_ctx* c;
+  ~ExclRelease() {
+    umiclust_ctx* e = c;
+    g_excl.compare_exchange_strong(e, nullptr, std::memory_order_acq_rel);
+  }
+};
+
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
   c->rec_direct = c->rec_direct_env >= 0 ? c->rec_direct_env != 0 : g_live_ctx.load() > 1;
+  ExclRelease excl_release{c};
+  // an overflowing bin's re-runs and the rest of it run with the GPU to itself (when other contexts are live)
+  auto excl_take = [&]() {
+    if (!c->excl || g_live_ctx.load() < 2) return;
+    umiclust_ctx* e = nullptr;
+    g_excl.compare_exchange_strong(e, c, std::memory_order_acq_rel);
+  };
   const double t0 = now_s();
   if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
     c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
@@ -1702,10 +1734,12 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     prime(0);
     for (int32_t k = 0; k < nb; k++) {
       Pass& P = c->pass[k % 2];
+      excl_wait(c);
       const double tb0 = now_s();
       if (k + 3 < nb) build_peer(k + 3, true);  // queries only: built while the host resolves block k
       c->dbg_t[5] += now_s() - tb0;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+        excl_take();
         // drain everything queued (its windows include block k) and restart the pipeline after block k
         c->hip(hipStreamSynchronize(c->st_al), "sync");
         if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
@@ -1746,6 +1780,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k % D];
+    excl_wait(c);
     if (k + D < nb) {
       // block k+D's peer tile depends on its queries only: build it now, behind the queued prefilters on the
       // main stream, while the host resolves block k (its ring slot was last read by pass k+D-2's prefilter)
@@ -1757,6 +1792,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       t.prebuilt = true;
     }
     if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+      excl_take();
       // drain the queued passes k+1 .. k+D-1 (their windows include block k) and restart the pipeline
       for (int i = 1; i < D; i++) {
         Pass& Q = c->pass[(k + i) % D];
@@ -2342,6 +2378,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct_env = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = getenv("UMICLUST_EXCL")) c->excl = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
   if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
@@ -2378,10 +2415,22 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
 }
 
 int32_t umiclust_set_priority(umiclust_ctx* c, int32_t level) {
-  if (!c || level < 0 || level > 1) return UMICLUST_EINVAL;
+  if (!c || level < -1 || level > 1) return UMICLUST_EINVAL;
   if (hipSetDevice(c->dev) != hipSuccess || hipStreamSynchronize(c->st) != hipSuccess) return UMICLUST_EDEVICE;
-  c->prio_user = level;
-  return main_stream_priority(c, level) == hipSuccess ? UMICLUST_OK : UMICLUST_EDEVICE;
+  // level -1 (background): the alignment stream loses its priority too; 0 / 1 give it back
+  const int al = level < 0 ? -1 : 0;
+  if (al != c->al_level) {
+    hipStream_t s = nullptr;
+    if (hipStreamSynchronize(c->st_al) != hipSuccess ||
+        (al < 0 ? hipStreamCreateWithFlags(&s, hipStreamNonBlocking)
+                : hipStreamCreateWithPriority(&s, hipStreamNonBlocking, al_priority())) != hipSuccess)
+      return UMICLUST_EDEVICE;
+    (void)hipStreamDestroy(c->st_al);
+    c->st_al = s;
+    c->al_level = al;
+  }
+  c->prio_user = level < 0 ? 0 : level;
+  return main_stream_priority(c, c->prio_user) == hipSuccess ? UMICLUST_OK : UMICLUST_EDEVICE;
 }
 
 void umiclust_destroy(umiclust_ctx* c) {

@@ -308,7 +308,8 @@ class Context:
         self._check(lib().umiclust_prepare(self._h, C.byref(p)), "prepare")
 
     def set_priority(self, level: int) -> None:
-        """umiclust_set_priority: 1 = this context's counting stream at the greatest priority, 0 = plain."""
+        """umiclust_set_priority: 1 = this context's counting stream at the greatest priority, 0 = plain (the
+        alignment stream prioritised at both), -1 = every stream plain (background)."""
         self._check(lib().umiclust_set_priority(self._h, int(level)), "set_priority")
 
     def cluster(self) -> dict:

@@ -64,9 +64,10 @@ class BinRunner:
                  maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0, critical_priority=None):
         """pack_reads > 0: a lane clusters its bins in packs (umiclust_cluster_pack) of consecutive bins holding up
         to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack.
-        critical_priority (default: UMICLUST_CRIT_PRIO, off): the lane holding the largest bin -- the bin that sets the
-        makespan when it is far above the rest -- counts on a stream of the greatest priority (umiclust_set_priority)
-        while the other lanes keep plain ones."""
+        critical_priority (default: UMICLUST_CRIT_PRIO, off): 1 / True: the lane holding the largest bin -- the bin that
+        sets the makespan when it is far above the rest -- counts on a stream of the greatest priority
+        (umiclust_set_priority) while the other lanes keep plain ones; 2: every lane holding a bin of at least half
+        the largest one's cost on prioritised streams, the others on plain ones (set_priority -1)."""
         from .shard import bin_cost, lpt_assign
         self.binset = binset
         self.pack_reads = pack_reads
@@ -87,13 +88,24 @@ class BinRunner:
                 self.where[b] = (lane, j)
             self.ctxs[lane].stage(sub.seq, sub.off, sub.bin_start)
         if critical_priority is None:
-            critical_priority = os.environ.get("UMICLUST_CRIT_PRIO", "0") not in ("", "0")
+            critical_priority = int(os.environ.get("UMICLUST_CRIT_PRIO", "0") or 0)
         self.critical_lane = None
+        self.critical_lanes = []
         if critical_priority and len(self.ctxs) > 1 and nb:
             big = max(range(nb), key=lambda b: binset.bins[b].umis.n)
             self.critical_lane = self.where[big][0]
-            for lane, c in enumerate(self.ctxs):
-                c.set_priority(1 if lane == self.critical_lane else 0)
+            if critical_priority == 2:
+                # every lane holding a bin of at least half the largest bin's cost counts and aligns on prioritised
+                # streams, the other lanes on plain ones (background)
+                cmax = bin_cost(binset.bins[big].umis.n)
+                self.critical_lanes = sorted({self.where[b][0] for b in range(nb)
+                                              if bin_cost(binset.bins[b].umis.n) >= 0.5 * cmax})
+                for lane, c in enumerate(self.ctxs):
+                    c.set_priority(1 if lane in self.critical_lanes else -1)
+            else:
+                self.critical_lanes = [self.critical_lane]
+                for lane, c in enumerate(self.ctxs):
+                    c.set_priority(1 if lane == self.critical_lane else 0)
         self.prepare()
 
     def _each_lane(self, fn) -> list:

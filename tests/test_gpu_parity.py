@@ -317,6 +317,31 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
     assert st["n_reruns"] > 0  # the overflow re-run and the pipeline restart were exercised
 
 
+@pytest.mark.parametrize("lanes", [3])
+def test_lanes_with_overflowing_bin(lanes, monkeypatch):
+    """Several lanes, two of whose bins overflow their peer lists (deep clusters): the first overflowing bin takes the
+    GPU for the rest of its run (exclusive re-runs, the other lanes hold at their block boundaries; a second
+    overflowing bin waits for it), and every bin's membership, strands, centroids and consensus equal the oracle's."""
+    from umiclust import binset
+    deep = lambda seed: synth.make_umis(6, seed=seed, max_reads=1800, orient_mix=0.3, mean_reads=1500.0,  # noqa: E731
+                                        error_rate=0.15, split=(0.0, 0.5, 0.5), max_edits=4,
+                                        pattern_fwd=synth.UMI_FWD_LONG, pattern_rev=synth.UMI_REV_LONG)
+    plain = lambda seed: synth.make_umis(150, seed=seed, max_reads=2500, orient_mix=0.2,  # noqa: E731
+                                         pattern_fwd=synth.UMI_FWD_LONG, pattern_rev=synth.UMI_REV_LONG)
+    sets = [deep(51), plain(52), deep(53), plain(54), plain(55)]
+    bs = synth.concat_bins([synth.Bin(0, i, i, 0, u) for i, u in enumerate(sets)])
+    monkeypatch.setenv("UMICLUST_BLOCK", "1024")
+    with _lib.Context(0) as ctx:
+        run = binset.BinRunner(ctx, bs, 1, 0.75, 80, 110, lanes=lanes)
+        st = run.cluster_all()
+        res = run.results()
+        run.close()
+    assert sum(x["n_reruns"] for x in st) > 0
+    for u, r in zip(sets, res):
+        o = orc.cluster(orc.params(1, 0.75, 80, 110), u.as_list())
+        assert binset.digest(r) == binset.digest(o)
+
+
 @pytest.mark.parametrize("early", ["0.3", "0.75"])
 @pytest.mark.parametrize("split", ["0", "1"])
 def test_early_member_traceback(early, split, monkeypatch):

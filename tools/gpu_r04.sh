@@ -77,7 +77,7 @@ for st in "$@"; do
     c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
     sweep3) timeout -k 10 900 python3 -u bench.py --config 3 --shard-sweep 8 > "$out/sweep3.json" 2> "$out/sweep3.err"; rc=$? ;;
     c4e2e) timeout -k 10 900 python3 -u bench.py --config 4 --e2e-files --scale "${SCALE:-1.0}" > "$out/c4e2e.json" 2> "$out/c4e2e.err"; rc=$? ;;
-    sweep4) timeout -k 10 1000 python3 -u bench.py --config 4 --shard-sweep 8 > "$out/sweep4.json" 2> "$out/sweep4.err"; rc=$? ;;
+    sweep4) timeout -k 10 1000 python3 -u bench.py --config 4 --shard-sweep 8 --sweep-shares "${SHARES:-}" > "$out/sweep4.json" 2> "$out/sweep4.err"; rc=$? ;;
     c5) timeout -k 10 300 python3 -u bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
