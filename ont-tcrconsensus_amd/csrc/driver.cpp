@@ -205,7 +205,8 @@ static std::atomic<int> g_live_ctx{0};  // contexts alive in this process (L3Pin
 // Exclusive re-runs: a context whose bin overflows a peer list (a giant molecule: synchronous re-runs, small blocks,
 // one host <-> device round trip per block) takes the GPU for the rest of that bin; the other contexts hold at their
 // next block boundary until it is done.  Among 8 lanes such a bin's round trips queued behind every lane's work
-// (config 4: 3.07 s in its lane, 0.22 s alone).  Timing only: every context's results are unchanged.
+// (config 4: 3.07 s in its lane, 0.22 s alone).  Timing only: every context's results are unchanged.  Opt-in
+// (UMICLUST_EXCL=1): the held lanes lose more than the overflowing bin gains (config-4 share 3: 3.30 vs 3.14 s).
 struct umiclust_ctx;
 static std::atomic<umiclust_ctx*> g_excl{nullptr};
 
@@ -389,7 +390,7 @@ struct umiclust_ctx {
   // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues); UMICLUST_RECDIRECT=0/1 fixes it.
   bool rec_direct = false;
   int rec_direct_env = -1;
-  bool excl = true;   // UMICLUST_EXCL=0: an overflowing bin does not take the GPU from the other contexts
+  bool excl = false;  // UMICLUST_EXCL=1: an overflowing bin takes the GPU from the other contexts (measured slower)
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
   bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save

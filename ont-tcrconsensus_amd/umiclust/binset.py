@@ -64,7 +64,8 @@ class BinRunner:
                  maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0, critical_priority=None):
         """pack_reads > 0: a lane clusters its bins in packs (umiclust_cluster_pack) of consecutive bins holding up
         to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack.
-        critical_priority (default: UMICLUST_CRIT_PRIO, off): 1 / True: the lane holding the largest bin -- the bin that
+        critical_priority (default: UMICLUST_CRIT_PRIO, 1 -- on with several lanes; 0 turns it off): 1 / True: the lane
+        holding the largest bin -- the bin that
         sets the makespan when it is far above the rest -- counts on a stream of the greatest priority
         (umiclust_set_priority) while the other lanes keep plain ones; 2: every lane holding a bin of at least half
         the largest one's cost on prioritised streams, the others on plain ones (set_priority -1)."""
@@ -88,7 +89,7 @@ class BinRunner:
                 self.where[b] = (lane, j)
             self.ctxs[lane].stage(sub.seq, sub.off, sub.bin_start)
         if critical_priority is None:
-            critical_priority = int(os.environ.get("UMICLUST_CRIT_PRIO", "0") or 0)
+            critical_priority = int(os.environ.get("UMICLUST_CRIT_PRIO", "1") or 0)
         self.critical_lane = None
         self.critical_lanes = []
         if critical_priority and len(self.ctxs) > 1 and nb:

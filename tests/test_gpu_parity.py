@@ -319,8 +319,8 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
 
 @pytest.mark.parametrize("lanes", [3])
 def test_lanes_with_overflowing_bin(lanes, monkeypatch):
-    """Several lanes, two of whose bins overflow their peer lists (deep clusters): the first overflowing bin takes the
-    GPU for the rest of its run (exclusive re-runs, the other lanes hold at their block boundaries; a second
+    """Several lanes, two of whose bins overflow their peer lists (deep clusters), with UMICLUST_EXCL=1: the first
+    overflowing bin takes the GPU for the rest of its run (exclusive re-runs, the other lanes hold at their block boundaries; a second
     overflowing bin waits for it), and every bin's membership, strands, centroids and consensus equal the oracle's."""
     from umiclust import binset
     deep = lambda seed: synth.make_umis(6, seed=seed, max_reads=1800, orient_mix=0.3, mean_reads=1500.0,  # noqa: E731
@@ -331,6 +331,7 @@ def test_lanes_with_overflowing_bin(lanes, monkeypatch):
     sets = [deep(51), plain(52), deep(53), plain(54), plain(55)]
     bs = synth.concat_bins([synth.Bin(0, i, i, 0, u) for i, u in enumerate(sets)])
     monkeypatch.setenv("UMICLUST_BLOCK", "1024")
+    monkeypatch.setenv("UMICLUST_EXCL", "1")
     with _lib.Context(0) as ctx:
         run = binset.BinRunner(ctx, bs, 1, 0.75, 80, 110, lanes=lanes)
         st = run.cluster_all()
@@ -727,3 +728,39 @@ def test_stage_prepare_equals_load():
                 _cmp_cluster(ctx.fetch_bin(b), orc.cluster(orc.params(1, 0.93, 58, 68), g))
     with _lib.Context(0) as ctx, pytest.raises(_lib.UmiclustError):
         ctx.prepare(_lib.params(1, 0.93, 58, 68))  # nothing staged
+
+
+def _structure_ok(res, lens):
+    cl = np.asarray(res["cluster"])
+    k = int(res["n_clusters"])
+    kept = cl >= 0
+    sizes = np.bincount(cl[kept], minlength=k)
+    cen = np.asarray(res["centroid"]) == 1
+    cen_len = np.zeros(k, np.int64)
+    cen_len[cl[cen]] = lens[cen]
+    return (bool(np.all(np.diff(sizes) <= 0)) and int(cen.sum()) == k and len(res["consensus"]) == k
+            and bool(np.all(lens[kept] <= cen_len[cl[kept]])))
+
+
+def test_full_size_config3_lanes_and_packs():
+    """BASELINE config 3 at full size (960 bins, ~9.9M reads), as the bench runs it (8 lanes, packs of up to 200k
+    reads) and bin by bin on one lane: every bin's membership, strands, centroids and consensus are the same both ways,
+    the alignment totals match, and every bin is structurally valid (--clusterout_sort order, one centroid per cluster,
+    centroids the longest of their clusters)."""
+    from umiclust import binset
+    bs = synth.concat_bins(synth.config_bins(3, 1.0, workers=16))
+    out = []
+    for lanes, pack in ((8, 200000), (1, 0)):
+        with _lib.Context(0) as ctx:
+            run = binset.BinRunner(ctx, bs, binset.ROUND1["preset"], binset.ROUND1["identity"],
+                                   *synth.CONFIG_LENGTHS[3], lanes=lanes, pack_reads=pack)
+            st = run.cluster_all()
+            res = run.results()
+            run.close()
+        out.append((st, res))
+    (sa, ra), (sb, rb) = out
+    assert sum(x["n_alignments"] for x in sa) == sum(x["n_alignments"] for x in sb)
+    assert sum(x["cells"] for x in sa) == sum(x["cells"] for x in sb)
+    for b, (x, y) in enumerate(zip(ra, rb)):
+        assert binset.digest(x) == binset.digest(y), b
+        assert _structure_ok(x, np.diff(bs.bins[b].umis.off)), b
