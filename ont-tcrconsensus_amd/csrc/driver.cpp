@@ -314,6 +314,7 @@ struct umiclust_ctx {
   bool pin_forced = false;         // UMICLUST_PIN=1: pinned even beside other contexts / ranks
   bool pre_resolve = true;         // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)
+  bool par_inorder = true;         // UMICLUST_PAR_INORDER=0: the in-order resolve phase on the calling thread only
   int32_t band_pairs = 140000;     // UMICLUST_BAND: alignment launches of at most this many pairs run banded
                                    // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
                                    // k_align_pk (profiles/r03/band_ab.json)
@@ -1187,6 +1188,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   env.bin_s = c->bin_s.data();
   env.pre_resolve = c->pre_resolve;
   env.pre_spec = c->pre_spec;
+  // (one context only: several lanes' pools already share the host's cores, config 3 7.59 -> 7.40 M UMIs/s with it)
+  env.par_inorder = c->par_inorder && g_live_ctx.load() <= 1;
   env.debug = c->debug;
   env.target = c->target.data();
   env.strand = c->strand.data();
@@ -1243,6 +1246,13 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   if (dump)
     write_resolve_dump(c, env, q0, nq, w0, state, state_in, hq, recs, *P.h_reccount.p, dpq, dpt, dres, new_cents, rs);
   t_host += th - rs.t_round_b_s;
+  // UMICLUST_BLOCKLOG=1: one line per resolved block (where the host's time goes, block by block)
+  static const bool blocklog = getenv("UMICLUST_BLOCKLOG") != nullptr;
+  if (blocklog)
+    fprintf(stderr, "blk q0 %d nq %d new %zu wait %.3f classify %.3f inorder %.3f roundB %.3f (%lld pairs) merged %lld "
+            "deferred %lld ms-since-wait %.3f\n", q0, nq, new_cents.size(), 1e3 * (tc0 - tsync0), 1e3 * rs.t_classify_s,
+            1e3 * rs.t_inorder_s, 1e3 * rs.t_round_b_s, (long long)rs.pairs_round_b, (long long)rs.n_merged_walks,
+            (long long)rs.n_deferred, 1e3 * (now_s() - tsync0));
   c->stats.t_host_pass1_s += rs.t_classify_s + rs.t_inorder_s;
   c->dbg_t[3] += rs.t_classify_s;
   c->dbg_t[4] += rs.t_inorder_s;
@@ -2378,6 +2388,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PAR_INORDER")) c->par_inorder = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct_env = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_EXCL")) c->excl = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));

@@ -16,8 +16,11 @@
 #include "resolve.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
+#include <memory>
+#include <thread>
 
 namespace uc {
 
@@ -126,6 +129,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
     std::vector<std::pair<unsigned long long, int>> cp, cx;
     std::vector<MCand> L;
     int64_t merged = 0;
+    double t_merged = 0;  // merged-walk time off the sequential path (summed into rst.t_merged_s by phase 2)
   };
   // seq: the in-order phase (debug counters, merged-walk timer); otherwise a classify thread resolving a strand
   // whose peers' states are all final, with its own scratch
@@ -187,8 +191,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
       return 1;
     }
     scr.merged++;
-    double t_unused = 0;
-    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{seq ? &rst.t_merged_s : &t_unused,
+    struct TAcc { double* p; double t0; ~TAcc() { *p += now_s() - t0; } } tacc{seq ? &rst.t_merged_s : &scr.t_merged,
                                                                                now_s()};
     // exact merged walk: T_old (sorted by the prefilter) and the centroid peers (sorted here;
     // usually one or two) are merged linearly; only the first kWalk entries can ever be aligned
@@ -303,7 +306,11 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
   auto strand_outcome = [&](int32_t qs, int32_t q, bool allow_extra, Outcome& o, bool& cert) -> int {
     return strand_outcome_s(qs, q, allow_extra, o, cert, scr0, true);
   };
-  auto resolve = [&](int32_t ql, bool allow_extra, auto&& strand_fn) -> bool {
+  struct Acc {
+    int64_t aln = 0, cells = 0;
+  };
+  // par: a phase-2 worker (its own accumulators; new centroids are collected afterwards, in order)
+  auto resolve = [&](int32_t ql, bool allow_extra, auto&& strand_fn, Acc* par = nullptr) -> bool {
     const int32_t q = q0 + ql;
     Outcome best, os[2];
     int bs = 0;
@@ -323,8 +330,8 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
       return false;
     }
     for (int s = 0; s < both; s++) {
-      rst.n_alignments += os[s].walked;
-      rst.cells += os[s].cells;
+      (par ? par->aln : rst.n_alignments) += os[s].walked;
+      (par ? par->cells : rst.cells) += os[s].cells;
       if (env.walk_dump) {
         env.walk_dump[(size_t)(q - state.s0) * 4 + s] = (int16_t)os[s].walked;
         env.walk_dump[(size_t)(q - state.s0) * 4 + 2 + s] = allow_extra ? 3 : 2;
@@ -340,7 +347,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
       env.strand[q] = (uint8_t)bs;
     } else {
       state[q] = ST_CENT;
-      new_cents.push_back(q);
+      if (!par) new_cents.push_back(q);
     }
     return true;
   };
@@ -436,9 +443,6 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
   // outcome needs no in-order state, and only in-block queries ever read its state, in phase 2, after this
   // phase.  rsx.done: 0 pending (phase 2), 1 member, 2 centroid.
   rsx.done.resize((size_t)nq);
-  struct Acc {
-    int64_t aln = 0, cells = 0;
-  };
   auto classify_query = [&](int32_t ql, Scratch& scr, Acc& acc) {
     bool det = true;
     for (int s = 0; s < both; s++) {
@@ -497,7 +501,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
   const double tp1 = now_s();
   rst.t_classify_s += tp1 - tp0;
   // Phase 2 (sequential, sorted order): confirm the device outcomes against the in-block peers' states
-  auto strand_fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
+  auto strand_fast_s = [&](int32_t qs, int32_t q, Outcome& o, bool& cert, Scratch& scr, bool seq) -> int {
     const HostQs& h = hq[qs];
     cert = false;
     if (rsx.kind[qs] == 0) {
@@ -520,7 +524,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
         o = rsx.pre[qs];
         return 0;
       }
-      return strand_outcome(qs, q, false, o, cert);
+      return strand_outcome_s(qs, q, false, o, cert, scr, seq);
     }
     if (rsx.kind[qs] == 1) {
       const uint16_t* d = rsx.deps.data() + (size_t)qs * kDeps;
@@ -538,14 +542,76 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
         return 0;
       }
     }
-    return strand_outcome(qs, q, false, o, cert);
+    return strand_outcome_s(qs, q, false, o, cert, scr, seq);
   };
-  for (int32_t ql = 0; ql < nq; ql++) {
-    const uint8_t d = rsx.done[ql];
-    if (d == 2) new_cents.push_back(q0 + ql);
-    else if (d == 0 && !resolve(ql, false, strand_fast)) deferred.push_back(ql);
+  auto strand_fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
+    return strand_fast_s(qs, q, o, cert, scr0, true);
+  };
+  std::vector<int32_t> pend;  // queries phase 1 left open, in sorted order
+  for (int32_t ql = 0; ql < nq; ql++)
+    if (rsx.done[ql] == 0) pend.push_back(ql);
+  const int TP = pool.size();
+  if (env.par_inorder && TP > 1 && (int)pend.size() >= env.par_min && !env.o4_T && !env.debug) {
+    // Phase 2 on the pool, with the sequential result: a query reads the states of its in-window peers only (every
+    // peer is an earlier query), so it may run once each of its in-block peers has been processed -- resolved or
+    // deferred -- as it would have been in sorted order.  Workers take the open queries in sorted order, so the
+    // earliest one in progress always has its peers done (no deadlock).
+    const int32_t np = (int32_t)pend.size();
+    std::unique_ptr<std::atomic<uint8_t>[]> proc(new std::atomic<uint8_t>[(size_t)nq]);
+    for (int32_t ql = 0; ql < nq; ql++) proc[ql].store(rsx.done[ql] != 0 ? 1 : 0, std::memory_order_relaxed);
+    std::vector<uint8_t> ok((size_t)np);
+    std::atomic<int32_t> next{0};
+    std::vector<Scratch> scr_p((size_t)TP);
+    std::vector<Acc> acc_p((size_t)TP);
+    pool.run([&](int t) {
+      Scratch& scr = scr_p[(size_t)t];
+      Acc& acc = acc_p[(size_t)t];
+      auto fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
+        return strand_fast_s(qs, q, o, cert, scr, false);
+      };
+      for (;;) {
+        const int32_t i = next.fetch_add(1, std::memory_order_relaxed);
+        if (i >= np) break;
+        const int32_t ql = pend[(size_t)i];
+        for (int s = 0; s < both; s++) {
+          const HostQs& h = hq[ql * both + s];
+          if (h.rec == 0xffffffffu) continue;
+          const Rec R = rec_of(h);
+          for (int y = 0; y < R.np; y++) {
+            const uint32_t id = R.peer[y] & 0xffffu;
+            if (id < inb) continue;
+            for (int spin = 0; !proc[id - inb].load(std::memory_order_acquire); spin++)
+              if (spin > 64) std::this_thread::yield();
+          }
+        }
+        ok[(size_t)i] = resolve(ql, false, fast, &acc) ? 1 : 0;
+        proc[ql].store(1, std::memory_order_release);
+      }
+    });
+    for (const Acc& x : acc_p) {
+      rst.n_alignments += x.aln;
+      rst.cells += x.cells;
+    }
+    for (const Scratch& x : scr_p) {
+      rst.n_merged_walks += x.merged;
+      rst.t_merged_s += x.t_merged;
+    }
+    for (int32_t ql = 0; ql < nq; ql++)
+      if (rsx.done[ql] == 2) new_cents.push_back(q0 + ql);
+    for (int32_t i = 0; i < np; i++) {
+      const int32_t ql = pend[(size_t)i];
+      if (!ok[(size_t)i]) deferred.push_back(ql);
+      else if (state[q0 + ql] == ST_CENT) new_cents.push_back(q0 + ql);
+    }
+    std::sort(new_cents.begin(), new_cents.end());
+  } else {
+    for (int32_t ql = 0; ql < nq; ql++) {
+      const uint8_t d = rsx.done[ql];
+      if (d == 2) new_cents.push_back(q0 + ql);
+      else if (d == 0 && !resolve(ql, false, strand_fast)) deferred.push_back(ql);
+    }
   }
-    rst.t_inorder_s += now_s() - tp1;
+  rst.t_inorder_s += now_s() - tp1;
   rst.n_deferred += (int64_t)deferred.size();
   // --- round B (side stream, so the queued pass keeps the device busy): align every T_old entry and
   // every peer a deferred query could still need, then resolve the deferred queries in order

@@ -30,6 +30,7 @@ struct Outcome {
 enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
 
 // greedy state of the sorted seqnos [s0, s0 + n) of the bin being clustered, indexed by absolute seqno
+constexpr int kParInorderMin = 4096;  // open queries below which the in-order phase stays on the calling thread
 struct StateView {
   uint8_t* p = nullptr;
   int32_t s0 = 0;
@@ -112,6 +113,8 @@ struct ResolveEnv {
   const int32_t* bin_s = nullptr;    // packs: each load bin's first sorted seqno
   bool pre_resolve = true;           // classify threads resolve strands whose peers are all final (kinds 3 / 4)
   bool pre_spec = true;              // ... and speculatively those whose in-block peers all turn out members (kind 5)
+  bool par_inorder = true;           // the in-order phase on the pool, peer by peer (UMICLUST_PAR_INORDER=0: one thread)
+  int par_min = kParInorderMin;      // ... from this many open queries on
   bool debug = false;
   int32_t* target = nullptr;         // absolute seqno -> centroid seqno a member joins (written)
   uint8_t* strand = nullptr;         // absolute seqno -> strand of that hit (written)

@@ -239,7 +239,8 @@ def test_host_argv_under_asan(host_asan):
 # resolve_block's classify phase runs on a worker pool over the window's states and the pass's records while the
 # in-order phase writes the block's states; tools/resolve_tsan_main.cpp replays resolve_block calls recorded from
 # GPU clustering runs (tests/golden/make_resolve_dumps.py: a config-2-like bin, lazy peers with round B, deep
-# clusters, batched O4 rounds) with 1, 3 and 8 threads and checks every output against the recorded one.
+# clusters, batched O4 rounds) with 1, 3 and 8 threads -- and with the in-order phase forced onto 3 and 8 pool threads
+# (its dependency-ordered parallel form) -- and checks every output against the recorded one.
 RESOLVE_DUMPS = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "resolve", "*.bin.gz")))
 
 
@@ -268,4 +269,4 @@ def test_host_resolve_under_tsan(resolve_tsan, path):
     r = subprocess.run([exe, raw], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
-    assert r.stdout.count(": equal") == 3, r.stdout
+    assert r.stdout.count(": equal") == 5, r.stdout

@@ -86,7 +86,9 @@ int replay(const char* path) {
     return 1;
   }
   int bad = 0;
-  for (int T : {1, 3, 8}) {
+  // (threads, in-order phase on the pool from this many open queries): the default threshold, then the pool forced
+  for (const auto& [T, par_min] : std::vector<std::pair<int, int>>{{1, kParInorderMin}, {3, kParInorderMin},
+                                                                    {8, kParInorderMin}, {3, 1}, {8, 1}}) {
     // the bin's states: [s0, w0) final before the window (never read), the window as recorded
     std::vector<uint8_t> st_buf((size_t)(q0 + nq - s0), ST_MEMBER);
     memcpy(st_buf.data() + (w0 - s0), state_in.data(), state_in.size());
@@ -103,6 +105,7 @@ int replay(const char* path) {
     env.maxrejects = hdr[7];
     env.pre_resolve = hdr[8] != 0;
     env.pre_spec = hdr[9] != 0;
+    env.par_min = par_min;
     env.target = target.data();
     env.strand = strand.data();
     size_t served = 0;
@@ -128,8 +131,9 @@ int replay(const char* path) {
     for (int32_t i = 0; i < nq && ok; i++)
       ok = st_buf[(size_t)(q0 + i - s0)] == state_out[i] && target[(size_t)(q0 + i)] == target_out[i] &&
            (state_out[i] != ST_MEMBER || strand[(size_t)(q0 + i)] == strand_out[i]);
-    printf("%s threads %d: block [%d, %d) window %d, %lld round-B pairs, %zu new centroids, %lld alignments: %s\n",
-           path, T, q0, q0 + nq, w0, (long long)nb, cents.size(), (long long)rs.n_alignments, ok ? "equal" : "DIFFERENT");
+    printf("%s threads %d (pool in order from %d): block [%d, %d) window %d, %lld round-B pairs, %zu new centroids, "
+           "%lld alignments: %s\n", path, T, par_min, q0, q0 + nq, w0, (long long)nb, cents.size(),
+           (long long)rs.n_alignments, ok ? "equal" : "DIFFERENT");
     bad += ok ? 0 : 1;
   }
   return bad;
