@@ -315,6 +315,7 @@ struct umiclust_ctx {
   bool pre_resolve = true;         // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
   bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)
   bool par_inorder = true;         // UMICLUST_PAR_INORDER=0: the in-order resolve phase on the calling thread only
+  int par_min = kParInorderMin;    // UMICLUST_PAR_MIN: open queries from which it runs on the pool
   int32_t band_pairs = 140000;     // UMICLUST_BAND: alignment launches of at most this many pairs run banded
                                    // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
                                    // k_align_pk (profiles/r03/band_ab.json)
@@ -1190,6 +1191,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   env.pre_spec = c->pre_spec;
   // (one context only: several lanes' pools already share the host's cores, config 3 7.59 -> 7.40 M UMIs/s with it)
   env.par_inorder = c->par_inorder && g_live_ctx.load() <= 1;
+  env.par_min = c->par_min;
   env.debug = c->debug;
   env.target = c->target.data();
   env.strand = c->strand.data();
@@ -2389,6 +2391,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PAR_INORDER")) c->par_inorder = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));
   if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct_env = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_EXCL")) c->excl = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));

@@ -569,9 +569,12 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
       auto fast = [&](int32_t qs, int32_t q, bool, Outcome& o, bool& cert) -> int {
         return strand_fast_s(qs, q, o, cert, scr, false);
       };
+      // chunks of consecutive open queries (each worker writes runs of neighbouring flags and states); the earliest
+      // unprocessed query is always the one its chunk's worker is on
       for (;;) {
-        const int32_t i = next.fetch_add(1, std::memory_order_relaxed);
-        if (i >= np) break;
+       const int32_t i0 = next.fetch_add(kParChunk, std::memory_order_relaxed);
+       if (i0 >= np) break;
+       for (int32_t i = i0; i < std::min(np, i0 + kParChunk); i++) {
         const int32_t ql = pend[(size_t)i];
         for (int s = 0; s < both; s++) {
           const HostQs& h = hq[ql * both + s];
@@ -586,6 +589,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
         }
         ok[(size_t)i] = resolve(ql, false, fast, &acc) ? 1 : 0;
         proc[ql].store(1, std::memory_order_release);
+       }
       }
     });
     for (const Acc& x : acc_p) {

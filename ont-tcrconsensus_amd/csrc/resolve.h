@@ -30,6 +30,7 @@ struct Outcome {
 enum : uint8_t { ST_UNDET = 0, ST_CENT = 1, ST_MEMBER = 2 };
 
 // greedy state of the sorted seqnos [s0, s0 + n) of the bin being clustered, indexed by absolute seqno
+constexpr int kParChunk = 8;        // open queries a worker takes at a time
 constexpr int kParInorderMin = 4096;  // open queries below which the in-order phase stays on the calling thread
 struct StateView {
   uint8_t* p = nullptr;
