@@ -1929,8 +1929,10 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     if (mode == 1 || mode == 3) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {
-    // the full kernel over the units the lean kernel could not finish (exits at once when there are none)
-    hipLaunchKernelGGL(k_pf_full, dim3(256), dim3(kPfThreads), smem_full, st, a, 1);
+    // the full kernel over the units the lean kernel could not finish (exits at once when there are none); its
+    // workgroups loop over the units (UMICLUST_FULL_WG workgroups, default 256: one per CU)
+    static const int full_wg = getenv("UMICLUST_FULL_WG") ? std::max(64, atoi(getenv("UMICLUST_FULL_WG"))) : 256;
+    hipLaunchKernelGGL(k_pf_full, dim3(full_wg), dim3(kPfThreads), smem_full, st, a, 1);
   } else {
     hipLaunchKernelGGL(k_pf_full, dim3(nqs * kParts), dim3(kPfThreads), smem_full, st, a, 0);
   }
