@@ -474,8 +474,19 @@ namespace {
 // is the process's one live context and the process is its node's only rank (LOCAL_WORLD_SIZE <= 1): several
 // contexts (bin-set lanes) or ranks pinned by where their callers happen to run could all land on one CCD.
 // UMICLUST_PIN=0 turns it off, UMICLUST_PIN=1 forces it on.
+// CPUs the calling thread may run on (its affinity mask: taskset, cgroup cpusets, L3Pin's narrowing)
+int affinity_cpus() {
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) != 0) return 1 << 16;
+  return std::max(1, CPU_COUNT(&set));
+}
+
+// 8 resolve threads (4 beside other contexts), never more than the caller's affinity mask holds: the in-order
+// phase's workers spin on each other's flags, so more threads than CPUs would only take slices from the worker
+// the others wait on
 int pool_threads(const umiclust_ctx* c) {
-  return c->resolve_threads > 0 ? c->resolve_threads : (g_live_ctx.load() > 1 ? 4 : 8);
+  const int want = c->resolve_threads > 0 ? c->resolve_threads : (g_live_ctx.load() > 1 ? 4 : 8);
+  return std::max(1, std::min(want, affinity_cpus()));
 }
 
 struct L3Pin {
@@ -1190,7 +1201,9 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   env.pre_resolve = c->pre_resolve;
   env.pre_spec = c->pre_spec;
   // (one context only: several lanes' pools already share the host's cores, config 3 7.59 -> 7.40 M UMIs/s with it)
-  env.par_inorder = c->par_inorder && g_live_ctx.load() <= 1;
+  // (and only when every pool thread has a CPU of its own under the caller's current mask, L3Pin's included: its
+  // workers spin-wait on each other)
+  env.par_inorder = c->par_inorder && g_live_ctx.load() <= 1 && c->pool->size() <= affinity_cpus();
   env.par_min = c->par_min;
   env.debug = c->debug;
   env.target = c->target.data();
@@ -1245,6 +1258,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   const double th = now_s() - th0;
   if (r == kResolveOverflow) return false;
   if (r == kResolveStuck) c->fail(UMICLUST_EDEVICE, "internal: a deferred query of block %d is still unresolved", q0);
+  if (r == kResolveBadPeer) c->fail(UMICLUST_EDEVICE, "internal: a peer of block %d is not an earlier query", q0);
   if (dump)
     write_resolve_dump(c, env, q0, nq, w0, state, state_in, hq, recs, *P.h_reccount.p, dpq, dpt, dres, new_cents, rs);
   t_host += th - rs.t_round_b_s;
@@ -1519,9 +1533,14 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   // Policy O4 batched rounds (c->o4_T queries each, counted from the first sorted query of q's bin): query q's search
   // sees only the centroids before its round start rstart(q), and the centroids of its round before it are the
   // re-check's extras -- both must be in its pass's peer window, and the index must hold nothing from the round.
-  // So a pass's window starts at min(nominal window start, round start of its first query) (a round tile over
-  // [round start, block start) replaces the nominal previous tiles when the round began earlier), and resolved
-  // centroids wait in `pending` until every later pass's window starts after them.
+  // Every pass that may still run or re-run counts: a queued pass is re-run alone when its block overflows a peer
+  // list (run_alone), against the index as it stands then.  So the index only ever holds the centroids before
+  // W = rstart(first query of the earliest block not yet resolved) -- the oldest window tile's first query -- and a
+  // *round tile* over [W, that query) joins the window in front of the nominal tiles; resolved centroids wait in
+  // `pending` until W has passed them.  (Round 4 synced the index to min(nominal window start, round start of the
+  // pass's own first query): when block k overflowed after pass k+1 had been queued, block k's re-run met centroids
+  // of its own first round in the index -- config 5 under --threads 25 aligned 15-50 more pairs than the oracle and
+  // moved reads between clusters, tests/test_gpu_o4.py::test_o4_config_vs_oracle_golden.)
   const int32_t T4 = c->o4_T;
   auto rstart = [&](int32_t q) { return round_start(c, s0, q); };
   std::vector<int32_t> pending;
@@ -1533,20 +1552,23 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     append_centroids(c, a);
     pending.erase(pending.begin(), pending.begin() + (ptrdiff_t)m);
   };
-  // prevs/nprev of a pass starting at query q with the nominal window start wnom, adjusted for its round
-  auto round_window = [&](int32_t q, int32_t wnom, const Tile** prevs, int& nprev, int32_t region, int slot) {
-    const int32_t rs = rstart(q);
-    if (rs < wnom) {
+  // the window of a pass starting at query q with the nprev tiles prevs (oldest first), adjusted for the rounds:
+  // the round tile (counter region 2; the block tiles of the D = 2 ring use 0 and 1) goes in front
+  auto round_window = [&](int32_t q, const Tile** prevs, int& nprev, int slot) {
+    const int32_t first = nprev ? prevs[0]->base : q;
+    const int32_t W = rstart(first);
+    if (W < first) {
       Tile& rt = c->round_tile[slot & 1];
-      build_tile(c, rt, c->d_iota.p, rs, q - rs, 0, region * kPeerRegion, 1 << 30);
-      rt.base = rs;
-      rt.seg = region;
+      build_tile(c, rt, c->d_iota.p, W, first - W, 0, (kPeerTiles - 1) * kPeerRegion, 1 << 30);
+      rt.base = W;
+      rt.seg = kPeerTiles - 1;
       rt.len = 0;  // several lengths
       rt.prebuilt = false;
+      for (int i = nprev; i > 0; i--) prevs[i] = prevs[i - 1];
       prevs[0] = &rt;
-      nprev = 1;
+      nprev++;
     }
-    sync_index(std::min(wnom, rs));
+    sync_index(W);
   };
   static const bool adapt = getenv("UMICLUST_ADAPT") && atoi(getenv("UMICLUST_ADAPT")) != 0;
   // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
@@ -1655,7 +1677,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       const int32_t m = std::min(piece, q0 + nq - q);
       const Tile* prevs[kPeerTiles];
       int nprev = 0;
-      if (T4) round_window(q, q, prevs, nprev, 1, 0);
+      if (T4) round_window(q, prevs, nprev, 0);
       enqueue_pass(c, P, q, m, prevs, nprev, c->solo_tile, 0);
       c->stats.n_reruns++;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
@@ -1685,8 +1707,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   auto enqueue = [&](int32_t k, int nprev) {
     const Tile* prevs[kPeerTiles];
     for (int i = 0; i < nprev; i++) prevs[i] = &tile_of(k - nprev + i);
-    if (T4) round_window(blocks[k].first, nprev ? blocks[k - nprev].first : blocks[k].first, prevs, nprev,
-                         (k + D - 1) % D, k);
+    if (T4) round_window(blocks[k].first, prevs, nprev, k);
     enqueue_pass(c, c->pass[k % D], blocks[k].first, blocks[k].second, prevs, nprev, tile_of(k), k % D, lazy);
   };
   // split passes shorten the host <-> device cycle of one bin at the price of a wider counting window;

@@ -931,11 +931,14 @@ int32_t umiclust_params_from_argv(umiclust_params* p, int32_t argc, const char* 
     else return UMICLUST_EINVAL;
   }
   if (!have_in) return UMICLUST_EINVAL;
-  // O4: the reference's argv is kept as is; the batched restatement of vsearch's multithreaded clustering is
-  // chosen from the environment (UMICLUST_O4=batched), the sequential definition otherwise
+  // O4: the argv's --threads n > 1 selects vsearch's multithreaded clustering (the batched
+  // restatement of cluster_core_parallel, rounds of n queries) -- what the reference's vsearch computes, since it
+  // always passes --threads n >= 25 (vsearch_umi_cluster.py:33-34,83-84; utils.py:56-63).  --threads 1 (or none) is
+  // the sequential definition.  UMICLUST_O4=sequential forces the sequential definition whatever --threads says.
+  p->policy_threads = p->threads > 1 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_O4")) {
-    if (!strcmp(e, "batched")) p->policy_threads = 1;
-    else if (strcmp(e, "sequential") != 0) return UMICLUST_EINVAL;
+    if (!strcmp(e, "sequential")) p->policy_threads = 0;
+    else if (strcmp(e, "batched") != 0) return UMICLUST_EINVAL;
   }
   return UMICLUST_OK;
 }

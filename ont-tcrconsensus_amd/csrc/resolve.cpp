@@ -551,16 +551,18 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
   for (int32_t ql = 0; ql < nq; ql++)
     if (rsx.done[ql] == 0) pend.push_back(ql);
   const int TP = pool.size();
-  if (env.par_inorder && TP > 1 && (int)pend.size() >= env.par_min && !env.o4_T && !env.debug) {
+  if (env.par_inorder && TP > 1 && (int)pend.size() >= env.par_min && !env.debug) {
     // Phase 2 on the pool, with the sequential result: a query reads the states of its in-window peers only (every
     // peer is an earlier query), so it may run once each of its in-block peers has been processed -- resolved or
     // deferred -- as it would have been in sorted order.  Workers take the open queries in sorted order, so the
-    // earliest one in progress always has its peers done (no deadlock).
+    // earliest one in progress always has its peers done (no deadlock).  Under O4 as well: the re-check's extras
+    // (the round's earlier centroids) are peers of the same record, waited on like the others.
     const int32_t np = (int32_t)pend.size();
     std::unique_ptr<std::atomic<uint8_t>[]> proc(new std::atomic<uint8_t>[(size_t)nq]);
     for (int32_t ql = 0; ql < nq; ql++) proc[ql].store(rsx.done[ql] != 0 ? 1 : 0, std::memory_order_relaxed);
     std::vector<uint8_t> ok((size_t)np);
     std::atomic<int32_t> next{0};
+    std::atomic<bool> bad_peer{false};
     std::vector<Scratch> scr_p((size_t)TP);
     std::vector<Acc> acc_p((size_t)TP);
     pool.run([&](int t) {
@@ -583,6 +585,10 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
           for (int y = 0; y < R.np; y++) {
             const uint32_t id = R.peer[y] & 0xffffu;
             if (id < inb) continue;
+            if (id - inb >= (uint32_t)ql) {  // not an earlier query: waiting on it would never end
+              bad_peer.store(true, std::memory_order_relaxed);
+              continue;
+            }
             for (int spin = 0; !proc[id - inb].load(std::memory_order_acquire); spin++)
               if (spin > 64) std::this_thread::yield();
           }
@@ -592,6 +598,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
        }
       }
     });
+    if (bad_peer.load()) return kResolveBadPeer;
     for (const Acc& x : acc_p) {
       rst.n_alignments += x.aln;
       rst.cells += x.cells;

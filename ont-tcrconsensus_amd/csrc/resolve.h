@@ -139,7 +139,7 @@ struct ResolveStats {
 using RoundB = std::function<void(const std::vector<uint32_t>& pq, const std::vector<uint32_t>& pt,
                                   std::vector<uint32_t>& res)>;
 
-enum : int { kResolveOk = 0, kResolveOverflow = 1, kResolveStuck = 2 };
+enum : int { kResolveOk = 0, kResolveOverflow = 1, kResolveStuck = 2, kResolveBadPeer = 3 };
 
 // Policy O4 (batched rounds of o4_T queries): the first query of q's round.  Rounds are counted from the first
 // sorted query of q's own bin -- in a pack of bins (one greedy order over several bins, hqbin / bin_s given) from
@@ -153,7 +153,9 @@ inline int32_t o4_round_start(int32_t o4_T, const int32_t* hqbin, const int32_t*
 // Resolve block [q0, q0 + nq) (peer window [w0, q0 + nq)) in sorted order from the pass's outcomes hq[nq * both]
 // and records (word array, HostQs::rec offsets).  Every query of the window before the block is resolved.
 // new_cents: the block's new centroids, sorted.  Returns kResolveOverflow (a peer list overflowed: the caller
-// re-runs the block in pieces) or kResolveStuck (a deferred query still unresolved after round B: an internal error).
+// re-runs the block in pieces), kResolveStuck (a deferred query still unresolved after round B: an internal error)
+// or kResolveBadPeer (a record names an in-block peer that is not an earlier query -- the kernels' window bound
+// lim = min(npeer, q - base) rules it out; checked because the parallel in-order phase would wait on it forever).
 int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, const HostQs* hq, const uint32_t* recs,
                   const StateView& state, ResolveScratch& scr, WorkPool& pool, std::vector<int32_t>& new_cents,
                   ResolveStats& st, const RoundB& round_b);

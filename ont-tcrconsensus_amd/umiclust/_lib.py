@@ -195,11 +195,16 @@ def lib() -> C.CDLL:
     return L
 
 
-def params(preset: int = PRESET_ROUND1, identity: float = 0.93, minlen: int = 58, maxlen: int = 68) -> Params:
+def params(preset: int = PRESET_ROUND1, identity: float = 0.93, minlen: int = 58, maxlen: int = 68,
+           threads: int = 1) -> Params:
+    """A preset's parameters; threads > 1 selects vsearch's --threads mode (policy O4, rounds of `threads` queries:
+    umiclust_params.policy_threads = 1), threads = 1 the sequential definition."""
     p = Params()
     rc = lib().umiclust_params_init(C.byref(p), preset, identity, minlen, maxlen)
     if rc != 0:
         raise UmiclustError(rc, "params_init")
+    if threads > 1:
+        p.threads, p.policy_threads = int(threads), 1
     return p
 
 

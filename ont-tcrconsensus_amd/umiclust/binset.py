@@ -61,18 +61,21 @@ class BinRunner:
     their own; lanes keep the GPU fed.  Results do not depend on the lane count."""
 
     def __init__(self, ctx, binset: synth.BinSet, preset: int, identity: float, minlen: int = 58,
-                 maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0, critical_priority=None):
+                 maxlen: int = 68, lanes: int = 1, device: int = 0, pack_reads: int = 0, critical_priority=None,
+                 threads: int = 1):
         """pack_reads > 0: a lane clusters its bins in packs (umiclust_cluster_pack) of consecutive bins holding up
         to pack_reads reads (a larger bin is a pack of its own): small bins share the GPU passes of their pack.
         critical_priority (default: UMICLUST_CRIT_PRIO, 1 -- on with several lanes; 0 turns it off): 1 / True: the lane
         holding the largest bin -- the bin that
         sets the makespan when it is far above the rest -- counts on a stream of the greatest priority
         (umiclust_set_priority) while the other lanes keep plain ones; 2: every lane holding a bin of at least half
-        the largest one's cost on prioritised streams, the others on plain ones (set_priority -1)."""
+        the largest one's cost on prioritised streams, the others on plain ones (set_priority -1).
+        threads > 1: vsearch --threads `threads` (policy O4, the mode the reference runs every bin in:
+        vsearch_umi_cluster.py:33-34, utils.py:56-63); 1: the sequential definition."""
         from .shard import bin_cost, lpt_assign
         self.binset = binset
         self.pack_reads = pack_reads
-        self.params = _lib.params(preset, identity, minlen, maxlen)
+        self.params = _lib.params(preset, identity, minlen, maxlen, threads=threads)
         nb = len(binset.bins)
         lanes = max(1, min(lanes, nb)) if nb else 1
         plan = lpt_assign([bin_cost(b.umis.n) for b in binset.bins], lanes)

@@ -69,16 +69,19 @@ def run_bins(bins: Sequence[tuple[str, str]], worker: Callable[[str, str], dict]
     return out
 
 
-def hip_worker(round_: int = 1, identity: float | None = None, min_len: int = 58, max_len: int = 68):
+def hip_worker(round_: int = 1, identity: float | None = None, min_len: int = 58, max_len: int = 68,
+               threads: int = 25):
     """The per-bin worker on this process's GPU: the reference's exact vsearch argv for the round
-    (vsearch_umi_cluster.py:22-53 / :72-96) through umiclust_run_argv; returns the bin's stats."""
+    (vsearch_umi_cluster.py:22-53 / :72-96) through umiclust_run_argv; returns the bin's stats.  threads = the
+    argv's --threads (the reference passes max(cpus // bins, 25), utils.py:56-63; > 1 = vsearch's multithreaded
+    clustering, policy O4)."""
     from . import vsearch_umi_cluster as v
     ident = identity if identity is not None else (0.93 if round_ == 1 else 0.97)
     fn = v.round1_argv if round_ == 1 else v.round2_argv
 
     def worker(fa, out):
         os.makedirs(out, exist_ok=True)
-        st = v.context().run_argv(fn(fa, out, 1, min_len, max_len, ident))
+        st = v.context().run_argv(fn(fa, out, threads, min_len, max_len, ident))
         return dict(n_kept=int(st["n_kept"]), n_clusters=int(st["n_clusters"]), cells=int(st["cells"]),
                     seconds=float(st["t_run_s"]))
     return worker

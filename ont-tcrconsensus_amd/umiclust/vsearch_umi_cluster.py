@@ -8,7 +8,11 @@ vsearch's option semantics and writes the same files: `<out_dir>/cluster<N>`,
 `<out_dir>/umi_clusters_consensus.fasta` and the log.
 
 Differences that cannot change a successful run's outputs:
-  * `threads` is accepted and ignored (the work runs on the GPU);
+  * `threads` does not set a CPU thread count (the work runs on the GPU); as in vsearch it selects the clustering
+    definition: n > 1 is vsearch's multithreaded cluster_fast (rounds of n queries searched against the index
+    frozen at the round's start, then re-checked in order: policy O4), which is what the
+    reference computes since it always passes n >= 25 (utils.py:56-63); n = 1 the sequential definition.
+    UMICLUST_O4=sequential forces the sequential definition;
   * failures raise `UmiclustError` (the reference silently returns the consout path even when
     vsearch fails, since `subprocess.run` has no `check=`).
 

@@ -4,7 +4,11 @@ stress bin (~96-nt UMIs, 15 % indels, clusters of >1k members), so the GPU parit
 without re-running the CPU oracle (~1 min per config-1 case) on the GPU box.
 
 Test infrastructure only.  Run:  python tests/golden/make_oracle_golden.py [config ...] | multibin [name ...] |
-segments
+segments | o4 [name ...]
+
+o4: the same digests under policy O4 (vsearch --threads T, the mode the reference runs every bin
+in: vsearch_umi_cluster.py:33-34,83-84, utils.py:56-63) -> oracle_o4.json.  The oracle's round searches run on
+ORC_WORKERS OpenMP threads (default: every host CPU); results do not depend on the worker count.
 """
 import hashlib
 import json
@@ -131,6 +135,64 @@ def main(configs):
             json.dump(cases, f, indent=1, sort_keys=True)
 
 
+# O4 cases: name -> (config, scale, preset, identity, T) for single bins, (config, scale, None, None, T) for the
+# multi-bin configs (every bin of config 3 / both rounds of config 4 under O4)
+O4_CASES = {
+    "config1_round1_id093_o4T25": (1, 1.0, 1, 0.93, 25),
+    "config1_round2_id097_o4T25": (1, 1.0, 2, 0.97, 25),
+    "config5_round1_id075_o4T25": (5, 0.1, 1, 0.75, 25),
+    "config5_round1_id090_o4T25": (5, 0.02, 1, 0.90, 25),
+    "config3_bins_s001_o4T25": (3, 0.01, None, None, 25),
+    "config4_rounds_s0002_o4T25": (4, 0.002, None, None, 25),
+    # the headline bin (BASELINE config 2, 2M reads, id 0.90) at full size under --threads 25
+    "config2_round1_id090_o4T25": (2, 1.0, 1, 0.90, 25),
+}
+
+
+def _o4(p, T: int):
+    p.threads, p.policy_threads = T, 1
+    return p
+
+
+def main_o4(names):
+    import orc
+    from umiclust import binset, synth
+    os.environ.setdefault("ORC_WORKERS", str(os.cpu_count() or 1))
+    path = os.path.join(HERE, "oracle_o4.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for name in names:
+        cfg, scale, preset, idn, T = O4_CASES[name]
+        lo, hi = synth.CONFIG_LENGTHS[cfg]
+        t0 = time.perf_counter()
+        if preset is None:
+            bs = synth.concat_bins(synth.config_bins(cfg, scale, workers=4))
+            d = dict(config=cfg, scale=scale, n_bins=len(bs.bins), n_reads=int(bs.n), minlen=lo, maxlen=hi, T=T)
+            rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if cfg == 4 else [])
+            for rname, prm in rounds:
+                op = _o4(orc.params(prm["preset"], prm["identity"], lo, hi), T)
+                res = [orc.cluster(op, b.umis.as_list()) for b in bs.bins]
+                dg = [binset.digest(r) for r in res]
+                d[rname] = dict(preset=prm["preset"], identity=prm["identity"], n_reads=int(bs.n),
+                                combined=binset.combine(dg), n_clusters=[x["n_clusters"] for x in dg],
+                                alignments=sum(r["stats"]["alignments"] for r in res),
+                                cells=sum(r["stats"]["cells"] for r in res))
+                if rname == "round1" and len(rounds) > 1:
+                    bs = binset.round2_binset(bs, res)
+        else:
+            seqs = synth.config_umis(cfg, scale).as_list()
+            r = orc.cluster(_o4(orc.params(preset, idn, lo, hi), T), seqs)
+            d = digest(r)
+            d.update(config=cfg, scale=scale, preset=preset, identity=idn, minlen=lo, maxlen=hi, n_reads=len(seqs),
+                     T=T, alignments=r["stats"]["alignments"], cells=r["stats"]["cells"],
+                     max_cluster=_max_cluster(r["cluster"]))
+        d.update(oracle_seconds=round(time.perf_counter() - t0, 2), oracle_workers=int(os.environ["ORC_WORKERS"]),
+                 host_cpu=_cpu_model())
+        out[name] = d
+        print(name, {k: v for k, v in d.items() if k not in ("round1", "round2")}, flush=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main_segments():
     """oracle_segments.json: synth.segment_stress() (a bin past one 7 x 65,536-centroid counter segment)."""
     import orc
@@ -150,7 +212,9 @@ def main_segments():
 
 if __name__ == "__main__":
     args = sys.argv[1:]
-    if args and args[0] == "segments":
+    if args and args[0] == "o4":
+        main_o4(args[1:] or list(O4_CASES))
+    elif args and args[0] == "segments":
         main_segments()
     elif args and args[0] == "multibin":
         main_multibin(args[1:] or sorted(MULTIBIN_CASES))

@@ -51,25 +51,33 @@ def test_params_from_round2_argv():
 def test_presets_equal_argv_decoding(monkeypatch):
     monkeypatch.delenv("UMICLUST_O4", raising=False)
     a, _ = _lib.params_from_argv(ARGV["calls"][0]["argv"])
-    b = _lib.params(_lib.PRESET_ROUND1, 0.93, 58, 68)
-    b.threads = 25  # the captured argv's --threads 25 (informational under the default O4 policy)
+    b = _lib.params(_lib.PRESET_ROUND1, 0.93, 58, 68, threads=25)  # the captured argv's --threads 25: policy O4
     assert bytes(a) == bytes(b)
     a, _ = _lib.params_from_argv(ARGV["calls"][1]["argv"])
-    b = _lib.params(_lib.PRESET_VSEARCH_DEFAULT, 0.97, 58, 68)
-    b.threads = 25
+    b = _lib.params(_lib.PRESET_VSEARCH_DEFAULT, 0.97, 58, 68, threads=25)
     assert bytes(a) == bytes(b)
 
 
-@pytest.mark.parametrize("env,policy", [(None, 0), ("sequential", 0), ("batched", 1)])
-def test_o4_policy_from_environment(monkeypatch, env, policy):
-    """the reference's argv (--threads 25) is kept as is; UMICLUST_O4 chooses between
-    the sequential definition (default) and the batched restatement of vsearch's multithreaded clustering."""
+@pytest.mark.parametrize("env,policy", [(None, 1), ("sequential", 0), ("batched", 1)])
+def test_o4_policy_from_argv_threads(monkeypatch, env, policy):
+    """the reference's argv carries --threads 25, so by default the drop-in computes vsearch's
+    multithreaded clustering (the batched restatement, rounds of 25 queries); UMICLUST_O4=sequential opts out."""
     if env is None:
         monkeypatch.delenv("UMICLUST_O4", raising=False)
     else:
         monkeypatch.setenv("UMICLUST_O4", env)
     p, _ = _lib.params_from_argv(ARGV["calls"][0]["argv"])
     assert (p.threads, p.policy_threads) == (25, policy)
+
+
+@pytest.mark.parametrize("threads,policy", [("1", 0), ("2", 1), ("64", 1)])
+def test_o4_policy_follows_threads(monkeypatch, threads, policy):
+    """--threads 1 is vsearch's sequential clustering (cluster_core_serial); any n > 1 its rounds of n queries."""
+    monkeypatch.delenv("UMICLUST_O4", raising=False)
+    argv = list(ARGV["calls"][0]["argv"])
+    argv[argv.index("--threads") + 1] = threads
+    p, _ = _lib.params_from_argv(argv)
+    assert (p.threads, p.policy_threads) == (int(threads), policy)
 
 
 def test_o4_policy_bad_environment(monkeypatch):

@@ -144,3 +144,80 @@ def test_batched_rounds_packs(packs, T):
                 _cmp(ctx.fetch_bin(b), o)
                 want += o["stats"]["alignments"]
             assert st["n_alignments"] == want
+
+
+def _o4_golden():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_o4.json")
+    return sorted(json.load(open(path)).items()) if os.path.exists(path) else []
+
+
+_O4_SINGLE = [(k, v) for k, v in _o4_golden() if "n_bins" not in v]
+_O4_MULTI = [(k, v) for k, v in _o4_golden() if "n_bins" in v]
+
+
+@pytest.mark.parametrize("name,gold", _O4_SINGLE, ids=[k for k, _ in _O4_SINGLE])
+def test_o4_config_vs_oracle_golden(gpu_ctx, name, gold):
+    """The reference's operating mode at BASELINE sizes: vsearch --threads 25 (vsearch_umi_cluster.py:33-34,
+    utils.py:56-63; policy O4) on config 1 both rounds (100k reads), config 2 (the headline bin: 2M reads, --id 0.90;
+    the oracle's OpenMP workers took ~21 min on 7 cores) and config-5 stress samples, default blocks: alignment
+    count, cells and the digests of membership, strands, centroids and consensus equal the oracle's
+    (tests/golden/make_oracle_golden.py o4)."""
+    from make_oracle_golden import digest
+    u = synth.config_umis(gold["config"], gold["scale"])
+    gpu_ctx.load(_lib.params(gold["preset"], gold["identity"], gold["minlen"], gold["maxlen"], threads=gold["T"]),
+                 buf=u.seq, off=u.off)
+    st = gpu_ctx.cluster()
+    d = digest(gpu_ctx.fetch())
+    assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
+    for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
+        assert d[k] == gold[k], k
+
+
+@pytest.mark.parametrize("name,gold", _O4_MULTI, ids=[k for k, _ in _O4_MULTI])
+@pytest.mark.parametrize("lanes,pack", [(1, 0), (8, 200000), (4, 3000)])
+def test_o4_multibin_vs_oracle_golden(name, gold, lanes, pack):
+    """Configs 3 (960 Zipf bins) and 4 (both rounds) at reduced scale under --threads 25, as bench.py runs them
+    (8 lanes, packs of 200k reads, the largest bin's lane prioritised), bin by bin on one lane, and in small packs on
+    4 lanes: every bin's digest and cluster count, the alignment count and cells equal the oracle's."""
+    from umiclust import binset
+    bs = synth.concat_bins(synth.config_bins(gold["config"], gold["scale"], workers=4))
+    assert len(bs.bins) == gold["n_bins"] and bs.n == gold["n_reads"]
+    rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if "round2" in gold else [])
+    for rname, prm in rounds:
+        g = gold[rname]
+        with _lib.Context(0) as ctx:
+            run = binset.BinRunner(ctx, bs, prm["preset"], prm["identity"], gold["minlen"], gold["maxlen"],
+                                   lanes=lanes, pack_reads=pack, threads=gold["T"])
+            st = run.cluster_all()
+            res = run.results()
+            run.close()
+        dg = [binset.digest(r) for r in res]
+        assert [x["n_clusters"] for x in dg] == g["n_clusters"], rname
+        assert sum(x["n_alignments"] for x in st) == g["alignments"] and sum(x["cells"] for x in st) == g["cells"]
+        assert binset.combine(dg) == g["combined"], rname
+        if rname == "round1":
+            bs = binset.round2_binset(bs, res)
+
+
+@pytest.mark.parametrize("mix", ["0", "1"])
+@pytest.mark.parametrize("T", [7, 25])
+def test_o4_rerun_after_queued_pass(mix, T, monkeypatch):
+    """Regression (round 5): a block that overflows a peer list is re-run alone after the next block's pass was
+    queued; the re-run must search an index holding no centroid of its own first round.  Round 4 synced the index for
+    the queued pass up to the overflowing block's start, so its re-run met centroids of the round straddling that
+    start (config 5 at --id 0.90: 15-50 extra alignments, reads moved between clusters).  The bin re-runs 18-24
+    blocks here, with blocks of one length and across length changes; every query's walk equals the oracle's."""
+    monkeypatch.setenv("UMICLUST_MIXLEN", mix)
+    monkeypatch.setenv("ORC_WORKERS", "8")
+    lo, hi = synth.CONFIG_LENGTHS[5]
+    seqs = synth.config_umis(5, 0.02).as_list()
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.90, lo, hi, threads=T), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    assert st["n_reruns"] > 0  # the mechanism is exercised
+    o = orc.cluster(_params(orc, 1, 0.90, T, (lo, hi)), seqs)
+    _cmp(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]

@@ -419,9 +419,16 @@ def _read_dir(d):
     return {fn: open(os.path.join(d, fn), "rb").read() for fn in sorted(os.listdir(d)) if not fn.endswith(".log")}
 
 
+@pytest.mark.parametrize("policy", ["o4", "sequential"])
 @pytest.mark.parametrize("round_", [1, 2])
-def test_dropin_files_vs_oracle(tmp_path, round_):
+def test_dropin_files_vs_oracle(tmp_path, round_, policy, monkeypatch):
+    """The drop-in with the reference's arguments (threads=25): byte-identical files to the oracle in vsearch's
+    --threads 25 mode (the default, policy O4) and, with UMICLUST_O4=sequential, in the sequential definition."""
     from umiclust.vsearch_umi_cluster import vsearch_cluster, vsearch_cluster_consensus
+    if policy == "sequential":
+        monkeypatch.setenv("UMICLUST_O4", "sequential")
+    else:
+        monkeypatch.delenv("UMICLUST_O4", raising=False)
     u = synth.make_umis(150, seed=31 + round_, max_reads=2500, orient_mix=0.1,
                        error_rate=0.015 if round_ == 1 else 0.002)
     fa = tmp_path / "region_cluster7_detected_umis.fasta"
@@ -443,6 +450,8 @@ def test_dropin_files_vs_oracle(tmp_path, round_):
     ref = tmp_path / "oracle"
     ref.mkdir()
     op = orc.params(1 if round_ == 1 else 2, 0.93 if round_ == 1 else 0.97, 58, 68)
+    if policy == "o4":
+        op.threads, op.policy_threads = 25, 1
     orc.run_fasta(op, str(fa), str(ref) + "/cluster", str(ref / "umi_clusters_consensus.fasta"))
     assert _read_dir(out) == _read_dir(ref)
     # the consumer runs unchanged on the GPU outputs
@@ -529,7 +538,10 @@ def test_run_argv_matches_reference_argv(tmp_path):
     synth.write_umi_fasta(str(fa), u)
     (tmp_path / "o").mkdir()
     st = context().run_argv(round1_argv(str(fa), str(tmp_path / "o"), 25, 58, 68, 0.93))
-    assert st["n_clusters"] == orc.run_fasta(orc.params(1, 0.93, 58, 68), str(fa), None, None)["n_clusters"]
+    op = orc.params(1, 0.93, 58, 68)
+    op.threads, op.policy_threads = 25, 1  # --threads 25: vsearch's multithreaded clustering
+    o = orc.run_fasta(op, str(fa), None, None)
+    assert (st["n_clusters"], st["n_alignments"]) == (o["n_clusters"], o["alignments"])
 
 
 def test_full_scale_properties():
@@ -764,3 +776,22 @@ def test_full_size_config3_lanes_and_packs():
     for b, (x, y) in enumerate(zip(ra, rb)):
         assert binset.digest(x) == binset.digest(y), b
         assert _structure_ok(x, np.diff(bs.bins[b].umis.off)), b
+
+
+@pytest.mark.parametrize("name", ["config1_round1_id093", "config1_round2_id097"])
+def test_parallel_inorder_phase_every_block(name, monkeypatch):
+    """The dependency-ordered in-order resolve phase on the pool (resolve.cpp, on by default from 4096 open queries)
+    forced onto every block (UMICLUST_PAR_MIN=1) of the full config-1 bin: alignment count, cells and digests equal
+    the oracle's (the default-setting case on 8192-query blocks is the config-2 golden above)."""
+    from make_oracle_golden import digest
+    gold = dict(_golden_cases())[name]
+    monkeypatch.setenv("UMICLUST_PAR_MIN", "1")
+    u = synth.config_umis(gold["config"], gold["scale"])
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(gold["preset"], gold["identity"], gold.get("minlen", 58), gold.get("maxlen", 68)),
+                 buf=u.seq, off=u.off)
+        st = ctx.cluster()
+        d = digest(ctx.fetch())
+    assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
+    for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
+        assert d[k] == gold[k], k

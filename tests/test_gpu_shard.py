@@ -57,6 +57,7 @@ def test_config3_bins_through_shard_on_gpu(tmp_path):
     res1 = run_bins([(fa, os.path.join(tmp, "w1", tag)) for fa, tag in bins], w)
     assert len(res1) == len(bins)
     op = orc.params(1, 0.93, 58, 68)
+    op.threads, op.policy_threads = 25, 1  # the worker's argv carries --threads 25 (vsearch's multithreaded mode)
     for fa, tag in bins:
         ref = os.path.join(tmp, "oracle", tag)
         os.makedirs(ref)
