@@ -657,18 +657,15 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
 typedef void (*AlignFn)(DevSeqs, const uint32_t*, const uint32_t*, int32_t, const uint32_t*,
                         const uint32_t*, Scoring, uint32_t*);
 
-// launch table: align[kAlignSlots L + v] (v: 0 packed, 1 one-cell-per-op, 2 IUPAC, 3 banded packed over
+// launch table: align[kAlignSlots L + v] (v: 0 packed, 1 IUPAC (one cell per op), 2 banded packed over
 // band_lanes(L) lanes; a 2-lane band measured 1.5 % slower than one lane per pair on config 2)
-constexpr int kAlignSlots = 4;
+constexpr int kAlignSlots = 3;
 template <int L, int LO>
 struct AlignRange {
   static void fill(AlignFn* a) {
     a[kAlignSlots * L] = k_align_pk<L>;
-    // the one-cell-per-op kernel for one-hot inputs is a cross-check of the packed one (<= kShortLen)
-    if constexpr (L <= kShortLen) a[kAlignSlots * L + 1] = k_align<L, false>;
-    else a[kAlignSlots * L + 1] = k_align_pk<L>;
-    a[kAlignSlots * L + 2] = k_align<L, true>;
-    a[kAlignSlots * L + 3] = k_align_band<L, band_lanes(L)>;
+    a[kAlignSlots * L + 1] = k_align<L, true>;
+    a[kAlignSlots * L + 2] = k_align_band<L, band_lanes(L)>;
     if constexpr (L > LO) AlignRange<L - 1, LO>::fill(a);
   }
 };

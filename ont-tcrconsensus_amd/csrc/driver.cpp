@@ -158,9 +158,6 @@ struct Pass {
   DevBuf<uint32_t> d_pcand, d_units;  // per-(query-strand, part) prefilter candidates, overflowed units
   DevBuf<uint8_t> d_pncand, d_ppeer_count, d_pnpeer;
   DevBuf<uint32_t> d_ppost;  // postings touched per (query-strand, part), summed by k_pf_merge
-  DevBuf<uint32_t> d_pdef;   // postings of deferred lists per (query-strand, part) (frequent-k-mer deferral)
-  DevBuf<uint32_t> d_pdm;    // deferred k-mer bits of each (query-strand, part)'s candidates (k_pf_merge)
-  DevBuf<uint32_t> d_pftab;  // k_pf_table's list tables of the counting launch (UMICLUST_PFTAB=0: none)
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
@@ -202,13 +199,7 @@ struct Pass {
 }  // namespace
 
 static std::atomic<int> g_live_ctx{0};  // contexts alive in this process (L3Pin)
-// Exclusive re-runs: a context whose bin overflows a peer list (a giant molecule: synchronous re-runs, small blocks,
-// one host <-> device round trip per block) takes the GPU for the rest of that bin; the other contexts hold at their
-// next block boundary until it is done.  Among 8 lanes such a bin's round trips queued behind every lane's work
-// (config 4: 3.07 s in its lane, 0.22 s alone).  Timing only: every context's results are unchanged.  Opt-in
-// (UMICLUST_EXCL=1): the held lanes lose more than the overflowing bin gains (config-4 share 3: 3.30 vs 3.14 s).
 struct umiclust_ctx;
-static std::atomic<umiclust_ctx*> g_excl{nullptr};
 
 struct umiclust_ctx {
   int dev = 0;
@@ -251,7 +242,6 @@ struct umiclust_ctx {
   DevBuf<uint8_t> d_lens;
   DevBuf<uint16_t> d_kmers;
   DevBuf<uint8_t> d_nk;
-  DevBuf<uint8_t> d_strong;       // [seqno * 2 + strand] prefilter's near-identical-peer flags (speculation)
   DevBuf<char> d_masked;
   DevBuf<int32_t> d_iota;
   size_t iota_n = 0;               // d_iota holds 0 .. iota_n - 1
@@ -263,24 +253,12 @@ struct umiclust_ctx {
   PinBuf<uint32_t> h_amb;
   PinBuf<uint16_t> h_xm;
   DevBuf<uint16_t> d_xm;
-  // frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask; exact): the load's most frequent
-  // + strand k-mers (>= defer_freq of the sampled sequences, at most kFKmers) and every (sequence, strand)'s mask
-  // of them; UMICLUST_DEFER = the most k-mers a query-strand defers (default 0: off -- on config 2 deferring 2-4
-  // k-mers streams 14-22 % fewer postings but the counting kernel's launch time is unchanged within noise:
-  // 1.575 ms off, 1.589-1.600 ms at 2-4, profiles/r03/defer_ab.json)
   // packs (umiclust_cluster_pack, multi-bin loads): sorted seqno -> load bin, each bin's first seqno and its first
   // centroid ordinal in the pack being clustered (INT32_MAX until indexed), the per-bin k-mer XOR masks
   std::vector<int32_t> hqbin;
   DevBuf<int32_t> d_qbin, d_bin_seq0, d_bin_ord0;
   PinBuf<int32_t> h_bin_ord0;
   bool pack_on = false;            // the current cluster_all call clusters a pack of several bins
-  DevBuf<uint32_t> d_fmask;
-  DevBuf<uint32_t> d_cent_fm;     // ordinal -> fmask of its + strand (PrefilterArgs::fmask_ord)
-  uint16_t fkmer[kFKmers] = {};
-  int32_t nfk = 0;
-  int32_t defer_max = 0;
-  int32_t defer_min_thr = 6;
-  double defer_freq = 0.02;
   // device: tables
   DevBuf<uint8_t> d_acc;
   DevBuf<uint16_t> d_rank;
@@ -301,9 +279,9 @@ struct umiclust_ctx {
   Pass pass[kPeerTiles];          // passes in flight (the pipeline depth: UMICLUST_DEPTH, <= kPeerTiles)
   Tile blk_tile[kPeerTiles + 1], solo_tile;  // per-block peer tiles (ring of depth + 1), overflow re-runs
   Tile round_tile[2];             // O4 batched rounds: a pass's window from its first query's round start
-  // passes in flight: 2 by default; 3 (window of three blocks) hides more host time but its extra peers cost
-  // more than that on configs 2/3/5 (profiles/r02/pipeline_depth_sweep.json)
-  int32_t depth = 2;
+  // passes in flight: 2; 3 (window of three blocks) hides more host time but its extra peers cost more than that
+  // on configs 2/3/5 (profiles/r02/pipeline_depth_sweep.json)
+  static constexpr int32_t depth = 2;
   // split passes (depth 2, UMICLUST_SPLIT=0 turns them off): a block's counting runs against the index
   // before the block two ahead is resolved, that block's hits flagged; only the merge and the alignment
   // wait for its resolution, so the counting leaves the host <-> device critical cycle
@@ -312,22 +290,13 @@ struct umiclust_ctx {
                                    // config 2 on two boxes: 3.41-3.90 M unpinned, 3.84-3.93 M pinned, profiles/r02/pin_ab.json);
                                    // off by default when LOCAL_WORLD_SIZE > 1
   bool pin_forced = false;         // UMICLUST_PIN=1: pinned even beside other contexts / ranks
-  bool pre_resolve = true;         // UMICLUST_PRERESOLVE=0: strands with only earlier-block peers resolve in order
-  bool pre_spec = true;            // UMICLUST_PRESPEC=0: no speculative classify-phase resolution (kind 5)
-  bool par_inorder = true;         // UMICLUST_PAR_INORDER=0: the in-order resolve phase on the calling thread only
   int par_min = kParInorderMin;    // UMICLUST_PAR_MIN: open queries from which it runs on the pool
   int32_t band_pairs = 140000;     // UMICLUST_BAND: alignment launches of at most this many pairs run banded
                                    // (launch bound: a few one-lane waves per SIMD); 70,000 before the faster
                                    // k_align_pk (profiles/r03/band_ab.json)
-  bool ix_side = true;             // UMICLUST_IXSIDE=0: index appends on the main stream (split passes)
-  bool rb_on_b = false;            // UMICLUST_RB_STREAM=b: round B on st_b (behind the index appends) instead of st_copy
-  bool r_on_al = true;             // UMICLUST_RAL=0: second halves' prefilter (full kernel + merge) on the main stream
-                                   // instead of the align stream (split passes; round 4: 4.67-4.68 vs 4.49-4.53 M UMIs/s)
-  bool split_stream = false;      // UMICLUST_SPLIT=2: counting halves on st_pf (measured slower on config 2: the
-                                  // concurrent counting slows the pass chain the host waits for)
   DevBuf<int32_t> d_seq2ord;      // [seqno - bin start] centroid ordinal or -1 (the merge's flagged hits)
   PinBuf<int32_t> h_seq2ord;
-  hipEvent_t a_ev[4][3] = {};     // counting halves, ring by block: begin / end (st_pf), gate (main stream)
+  hipEvent_t a_ev[4][3] = {};     // counting halves, ring by block: begin / end / spare
   // split passes: index appends and peer-tile builds run on st_b beside the counting on the main stream;
   // they start after the latest second half (every earlier reader of the slots they rebuild precedes it)
   // and the main stream's next pass waits for ix_done
@@ -343,7 +312,6 @@ struct umiclust_ctx {
   int32_t pass_B = 0;
   hipStream_t st_b = nullptr, st_copy = nullptr;
   hipStream_t st_al = nullptr;    // walk / alignment rounds / packing of the passes
-  hipStream_t st_pf = nullptr;    // counting halves of split passes (the main stream does not queue behind them)
   int32_t last_a_slot = -1;       // a_ev slot of the latest counting half
   hipEvent_t evb[2] = {nullptr, nullptr};
   DevBuf<uint32_t> d_bpq, d_bpt, d_bres;
@@ -375,39 +343,30 @@ struct umiclust_ctx {
   std::vector<BinOut> bout;
   umiclust_stats stats{};
   int32_t block_size = 8192;
-  // UMICLUST_BLOCK unset: a bin of n queries uses blocks of about n / block_div (>= 2048): a small bin's
+  // UMICLUST_BLOCK unset: a bin of n queries uses blocks of about n / block_div (>= block_min): a small bin's
   // window then holds fewer same-molecule peers (fewer speculative peer alignments and overflows)
   int32_t block_div = 16;
-  int32_t block_min = 2048;       // UMICLUST_BLOCK_MIN: the smallest default block (bins of < 16 x this)
+  static constexpr int32_t block_min = 2048;
   // UMICLUST_MIXLEN=0: blocks end at every query-length change (one alignment launch per round); =1: a block spans
   // up to kSegLens lengths (one launch per length and round): a small bin is then a few passes, not one per length
-  // UMICLUST_PFTAB=1: the list tables of the counting launch are built ahead by k_pf_table (one wave per unit, no
-  // barriers); the counting workgroups then spend 5.2k instead of 15.6k cycles on the table, but the launch is not
-  // faster (1.62 -> 1.76 ms per count + table on config 2: the counting is bound by the LDS array, ~73 % busy, 60 %
-  // of it bank-conflict replays; profiles/r03/pftab_ab.json), so off by default
-  bool pf_tab = false;
   // k_pack writes the outcomes and records straight into pinned host memory (true) or into device buffers copied by
   // DMA (false).  Set per clustering call: DMA with one context in the process (config 2: 4.33-4.36 vs 4.21-4.22 M
   // UMIs/s, the direct PCIe writes held k_pack at 133 us on the pass chain), direct with several (config 3, 8 lanes:
-  // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues); UMICLUST_RECDIRECT=0/1 fixes it.
+  // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues).
   bool rec_direct = false;
-  int rec_direct_env = -1;
-  bool excl = false;  // UMICLUST_EXCL=1: an overflowing bin takes the GPU from the other contexts (measured slower)
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
-  int32_t spec_thr = 30;          // speculative walk below this best k-mer count (UMICLUST_SPEC; 0 = off)
-  bool peer_predict = false;      // off by default: mispredictions cost more than the skipped pairs save
-  bool peer_cert = true;
+  // speculative walk below this best k-mer count (20 and 30 equal, 45 slower: profiles/r03/spec_ab)
+  static constexpr int32_t spec_thr = 30;
+  // relevant peers certain to become members are not aligned speculatively (config 2 4.02 -> 4.14 M, round 4)
+  static constexpr bool peer_cert = true;
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
-  DevBuf<uint32_t> d_probe;          // UMICLUST_PEER_CERT=0: align relevant peers even when certain to become members
-  int32_t strong_eighths = 6;     // UMICLUST_STRONG: near-identical = sharing >= this many eighths of the k-mers
-  int32_t lazy_permille = 5;      // UMICLUST_LAZY: lazy peers below this new-centroid rate (per mille); 0 = off
+  DevBuf<uint32_t> d_probe;
+  // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
+  static constexpr int32_t lazy_permille = 5;
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
-  int blk_max_np = 0;              // the last resolved block's largest peer count (resolve_pass)
   int al_level = 0;                 // the alignment stream: 0 prioritised (al_priority), -1 plain (set_priority -1)
   int st_level = 0, prio_user = 0;  // the main stream's priority now / as umiclust_set_priority left it
-  bool ovf_prio = false;           // UMICLUST_OVF_PRIO=1: a bin's overflow re-runs move its main stream to the greatest
-                                   // priority (config 4: 5.90 vs 6.53 M UMIs/s, off)
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
   bool debug = getenv("UMICLUST_DEBUG") != nullptr;
   int64_t dbg_q[4] = {0, 0, 0, 0};
@@ -439,8 +398,6 @@ struct umiclust_ctx {
   // traceback / consensus buffers, kept across calls (a bin set clusters hundreds of small bins)
   DevBuf<uint32_t> t_mpq, t_mpt, t_mout;
   PinBuf<uint32_t> h_mpq, h_mpt;     // the member pairs' pinned staging (traceback launch)
-  hipStream_t st_tw = nullptr;        // early member tracebacks (UMICLUST_TRACE_EARLY), least priority
-  hipEvent_t ev_tw = nullptr;
   PinBuf<int32_t> h_mseq, h_mops, h_cstart;
   PinBuf<uint8_t> h_mstr;
   PinBuf<uint16_t> h_clen;           // consensus lengths / sequences / overflow flag (pinned downloads)
@@ -645,8 +602,6 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_ppeer_count.ensure(nqs * kParts * kPeerCap), "alloc");
   c->hip(P.d_pnpeer.ensure(nqs * kParts), "alloc");
   c->hip(P.d_ppost.ensure(nqs * kParts), "alloc");
-  c->hip(P.d_pdef.ensure(nqs * kParts), "alloc");
-  c->hip(P.d_pdm.ensure(nqs * kParts), "alloc");
   c->hip(P.d_peer_id.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
@@ -697,27 +652,12 @@ int32_t block_minlen(const umiclust_ctx* c, int32_t q0, int32_t nq) {
   return m;
 }
 
-// the frequent-k-mer deferral of the lean counting kernel (PrefilterArgs::fmask)
-void set_defer(umiclust_ctx* c, PrefilterArgs& a, Pass& P) {
+// the packs' bin bounds of the prefilter (PrefilterArgs::qbin) and the centroid length table
+void set_bins(umiclust_ctx* c, PrefilterArgs& a) {
   a.qbin = c->pack_on ? c->d_qbin.p : nullptr;
   a.bin_seq0 = c->d_bin_seq0.p;
   a.bin_ord0 = c->d_bin_ord0.p;
   a.cent_len = c->d_cent_len.p;
-  a.fmask = c->d_fmask.p;
-  a.fmask_ord = c->d_cent_fm.p;
-  a.pdef = P.d_pdef.p;
-  a.pdm = P.d_pdm.p;
-  a.pftab = nullptr;
-  if (c->pf_tab && a.nlist_cap > 0) {
-    // sized by this launch (the table stride follows nlist_cap); grown only between passes of this buffer set,
-    // whose previous counting launch has completed (its events were waited on before the set is reused)
-    const size_t need = (size_t)a.nq * a.both * kParts * pf_table_stride(a.nlist_cap);
-    if (need > P.d_pftab.n) c->hip(P.d_pftab.ensure(need + need / 4), "alloc list tables");
-    a.pftab = P.d_pftab.p;
-  }
-  a.defer_max = c->nfk > 0 ? c->defer_max : 0;
-  a.defer_min_thr = c->defer_min_thr;
-  for (int i = 0; i < kFKmers; i++) a.fkmer[i] = c->fkmer[i];
 }
 
 // UMICLUST_PFPROBE=1 (measurement only): after every counting launch, the same launch without its count loop
@@ -734,8 +674,6 @@ void launch_pf_probe(umiclust_ctx* c, const PrefilterArgs& a, hipStream_t st) {
   b.ppeer_id = reinterpret_cast<uint16_t*>(p);
   p += U * (kPeerCap / 2);
   b.ppost = p;
-  b.pdef = p + U;
-  b.pdm = p + 2 * U;
   b.units = p + 3 * U;
   b.pncand = reinterpret_cast<uint8_t*>(p + 4 * U);
   b.pnpeer = reinterpret_cast<uint8_t*>(p + 5 * U);
@@ -764,10 +702,10 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   own.seg = region;
   own.len = block_maxlen(c, q0, nq);  // the block's longest query
   const bool second_half = after_count && P.a_live && P.a_q0 == q0;
-  // r_on_al: a second half's prefilter (full kernel + merge) runs on the align stream ahead of its walk, so the
+  // a second half's prefilter (full kernel + merge) runs on the align stream ahead of its walk, so the
   // main stream's next counting half does not queue behind it.  It needs its counting half (a_ev) and the
   // index / tiles (ix_done; index appends on the side stream wait for the latest second half, last_r_ev)
-  if (second_half && c->r_on_al && c->ix_st && !built_now) {
+  if (second_half && c->ix_st && !built_now) {
     st = c->st_al;
     if (c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");
   }
@@ -853,11 +791,9 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   a.peer_id = P.d_peer_id.p;
   a.peer_count = P.d_peer_count.p;
   a.npeer = P.d_npeer.p;
-  a.strong = c->d_strong.p;
-  a.strong_eighths = c->strong_eighths;
   a.postings_touched = P.d_counters.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
-  set_defer(c, a, P);
+  set_bins(c, a);
   if (second_half) c->hip(hipStreamWaitEvent(st, c->a_ev[P.a_slot][1], 0), "wait");
   c->hip(hipEventRecord(P.ev[0], st), "event");
   P.c_timed = false;
@@ -933,7 +869,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
       if (&Q != &P && Q.nq > 0 && Q.q0 + Q.nq == q0) prev = &Q;
   c->hip(launch_peer_pairs(q0, w0, nqs, both, c->d_lens.p, P.d_ws.p, P.d_peer_id.p, P.d_peer_count.p, P.d_npeer.p,
                            P.d_pq.p, P.d_pt.p, P.d_outidx.p, sg1, segc + kSegLens, cells_p, P.d_counters.p + 8,
-                           peer_out0, c->peer_predict ? c->d_strong.p : nullptr, P.d_paligned.p, lazy_peers ? 0 : 1,
+                           peer_out0, P.d_paligned.p, lazy_peers ? 0 : 1,
                            prev ? prev->d_ws.p : nullptr, prev ? prev->d_npeer.p : nullptr, prev ? prev->q0 : 0,
                            prev ? prev->nq : 0, st),
          "peer pairs");
@@ -979,22 +915,9 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   // last merge): the main stream's next append and second half do not queue behind it
   hipStream_t st = c->st;
   if (c->ix_st && c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");  // index / peer tiles
-  if (c->split_stream) {
-    // created on first use, after the others: HIP hands streams hardware queues in creation order, and an
-    // extra stream created earlier would push the alignment stream onto the main stream's queue
-    if (!c->st_pf) {
-      // the least priority: the pass chain the host waits for is dispatched first
-      int lo = 0, hi = 0;
-      c->hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
-      c->hip(hipStreamCreateWithPriority(&c->st_pf, hipStreamNonBlocking, lo), "stream");
-    }
-    c->hip(hipEventRecord(c->a_ev[slot][2], c->st), "event");
-    st = c->st_pf;
-    c->hip(hipStreamWaitEvent(st, c->a_ev[slot][2], 0), "wait");
-  }
-  // this buffer set's last second half (full kernel + merge on the align stream under r_on_al) has read what
+  // this buffer set's last second half (full kernel + merge on the align stream) has read what
   // the counting half overwrites
-  if (c->r_on_al && c->ix_st) c->hip(hipStreamWaitEvent(st, P.ev[1], 0), "wait");
+  if (c->ix_st) c->hip(hipStreamWaitEvent(st, P.ev[1], 0), "wait");
   c->hip(hipEventSynchronize(P.ev_a), "sync");  // the last upload from h_tiles_a is done
   int32_t nv = 0;
   const size_t need = c->tiles.size() + 2;
@@ -1048,7 +971,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   a.pnpeer = P.d_pnpeer.p;
   a.ppost = P.d_ppost.p;
   a.prof = c->pf_prof.p;  // null unless UMICLUST_PFPROF is set
-  set_defer(c, a, P);
+  set_bins(c, a);
   c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
   c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
   c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
@@ -1144,7 +1067,6 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     P.rec_est = (uint32_t)std::max<size_t>(1u << 16, used + used / 2 + 4096);
   }
   c->stats.kmer_postings += P.h_counters.p[0];
-  c->stats.kmer_postings_deferred += P.h_counters.p[11];
   c->stats.pairs_peer += P.h_counters.p[8];
   // every alignment the device computed for this pass (walk rounds + speculative peers)
   {
@@ -1160,17 +1082,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   c->stats.t_sync_s += now_s() - tc0;
   c->dbg_t[1] += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
-  {
-    int m = 0;  // the block's largest in-window peer count (block-size feedback; 255 = an overflow)
-    for (int32_t x = 0; x < nqs; x++) m = std::max<int>(m, hq[x].npeer);
-    c->blk_max_np = m;
-  }
   if (!c->pool) c->pool.reset(new WorkPool(pool_threads(c)));
   // the records are copied into pageable memory first (one streaming read; scattered reads of the DMA'd
-  // pinned buffer are slow): config 2 +2-3 % (UMICLUST_RECCOPY=0 reads them in place)
+  // pinned buffer are slow): config 2 +2-3 %
   const uint32_t* recs = P.h_rec.p;
-  static const bool rec_copy = !(getenv("UMICLUST_RECCOPY") && atoi(getenv("UMICLUST_RECCOPY")) == 0);
-  if (rec_copy) {
+  {
     const double tc1 = now_s();
     // on the resolve threads: one core's streaming read of pinned memory is the limit (0.05 s per config-2 step)
     const size_t nw = *P.h_reccount.p;
@@ -1198,12 +1114,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   env.maxrejects = c->p.maxrejects;
   env.hqbin = c->pack_on ? c->hqbin.data() : nullptr;
   env.bin_s = c->bin_s.data();
-  env.pre_resolve = c->pre_resolve;
-  env.pre_spec = c->pre_spec;
+
   // (one context only: several lanes' pools already share the host's cores, config 3 7.59 -> 7.40 M UMIs/s with it)
   // (and only when every pool thread has a CPU of its own under the caller's current mask, L3Pin's included: its
   // workers spin-wait on each other)
-  env.par_inorder = c->par_inorder && g_live_ctx.load() <= 1 && c->pool->size() <= affinity_cpus();
+  env.par_inorder = g_live_ctx.load() <= 1 && c->pool->size() <= affinity_cpus();
   env.par_min = c->par_min;
   env.debug = c->debug;
   env.target = c->target.data();
@@ -1214,7 +1129,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // latency on the host's critical path per block with deferred queries (UMICLUST_RB_STREAM=b: st_b)
   auto round_b = [&](const std::vector<uint32_t>& bpq, const std::vector<uint32_t>& bpt, std::vector<uint32_t>& bres) {
     const int32_t nb = (int32_t)bpq.size();
-    hipStream_t sb = c->rb_on_b ? c->st_b : c->st_copy;
+    hipStream_t sb = c->st_copy;
     c->hip(c->d_bpq.ensure(nb), "alloc");
     c->hip(c->d_bpt.ensure(nb), "alloc");
     c->hip(c->d_bres.ensure(nb), "alloc");
@@ -1262,9 +1177,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   if (dump)
     write_resolve_dump(c, env, q0, nq, w0, state, state_in, hq, recs, *P.h_reccount.p, dpq, dpt, dres, new_cents, rs);
   t_host += th - rs.t_round_b_s;
-  // UMICLUST_BLOCKLOG=1: one line per resolved block (where the host's time goes, block by block)
-  static const bool blocklog = getenv("UMICLUST_BLOCKLOG") != nullptr;
-  if (blocklog)
+  // UMICLUST_DEBUG: one line per resolved block (where the host's time goes, block by block)
+  if (c->debug)
     fprintf(stderr, "blk q0 %d nq %d new %zu wait %.3f classify %.3f inorder %.3f roundB %.3f (%lld pairs) merged %lld "
             "deferred %lld ms-since-wait %.3f\n", q0, nq, new_cents.size(), 1e3 * (tc0 - tsync0), 1e3 * rs.t_classify_s,
             1e3 * rs.t_inorder_s, 1e3 * rs.t_round_b_s, (long long)rs.pairs_round_b, (long long)rs.n_merged_walks,
@@ -1332,9 +1246,6 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
          "h2d cent");
   c->hip(hipMemcpyAsync(c->d_cent_len.p + ord0, c->h_cent_len.p + ord0, new_cents.size(), hipMemcpyHostToDevice, st),
          "h2d cent len");
-  if (c->nfk > 0 && c->defer_max > 0)
-    c->hip(launch_fmask_ord(c->d_fmask.p, c->d_cent.p + ord0, (int32_t)new_cents.size(), c->d_cent_fm.p + ord0, st),
-           "centroid k-mer masks");
   const int32_t ordend = (int32_t)c->cent.size();
   if (c->nix >= c->ix_events.size()) {
     hipEvent_t e0, e1;
@@ -1357,7 +1268,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     c->base_tile.n = 0;
   }
   if (ordend - c->base_end > kDelta) {  // fold the delta into the base tile
-    // the base is rebuilt in place: the latest counting half (on st_pf) may still read it
+    // the base is rebuilt in place: the latest counting half may still read it
     if (c->last_a_slot >= 0) c->hip(hipStreamWaitEvent(st, c->a_ev[c->last_a_slot][1], 0), "wait");
     c->base_tile.base = c->sealed_end;
     c->base_tile.seg = c->sealed_end / kSegCentroids;
@@ -1404,32 +1315,8 @@ hipError_t main_stream_priority(umiclust_ctx* c, int level) {
   return hipSuccess;
 }
 
-// hold while another context has the GPU to itself (g_excl)
-static void excl_wait(umiclust_ctx* c) {
-  for (;;) {
-    umiclust_ctx* o = g_excl.load(std::memory_order_acquire);
-    if (o == nullptr || o == c) return;
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
-  }
-}
-// released when the bin (or pack) ends, on every exit path
-struct ExclRelease {
-  umiclust_ctx* c;
-  ~ExclRelease() {
-    umiclust_ctx* e = c;
-    g_excl.compare_exchange_strong(e, nullptr, std::memory_order_acq_rel);
-  }
-};
-
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
-  c->rec_direct = c->rec_direct_env >= 0 ? c->rec_direct_env != 0 : g_live_ctx.load() > 1;
-  ExclRelease excl_release{c};
-  // an overflowing bin's re-runs and the rest of it run with the GPU to itself (when other contexts are live)
-  auto excl_take = [&]() {
-    if (!c->excl || g_live_ctx.load() < 2) return;
-    umiclust_ctx* e = nullptr;
-    g_excl.compare_exchange_strong(e, c, std::memory_order_acq_rel);
-  };
+  c->rec_direct = g_live_ctx.load() > 1;
   const double t0 = now_s();
   if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
     c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
@@ -1450,7 +1337,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   c->hip(hipStreamSynchronize(c->st), "sync");  // no queued work may still read the old tiles
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();
-  if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
   c->base_tile.n = c->delta_tile[0].n = c->delta_tile[1].n = 0;
   c->last_a_slot = -1;
   c->sealed_end = c->base_end = 0;
@@ -1466,7 +1352,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   c->stats.n_kept = n;
   c->hip(c->d_cent.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->d_cent_len.ensure((size_t)n + 1), "alloc cent");
-  c->hip(c->d_cent_fm.ensure((size_t)n + 1), "alloc cent");
   c->hip(c->h_cent.ensure((size_t)n + 1), "pin cent");
   c->hip(c->h_cent_len.ensure((size_t)n + 1), "pin cent");
   c->hip(c->d_seq2ord.ensure((size_t)n + 1), "alloc seq2ord");
@@ -1570,15 +1455,13 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     }
     sync_index(W);
   };
-  static const bool adapt = getenv("UMICLUST_ADAPT") && atoi(getenv("UMICLUST_ADAPT")) != 0;
   // a bin starts at the block size the previous one ended with, doubled (deep bins tend to follow deep bins)
   int32_t b_eff = c->pack_on ? B : std::min<int64_t>(B, std::max<int64_t>(256, (int64_t)c->b_hint * 2));
-  if (adapt) b_eff = std::min(b_eff, 2048);  // the peer-load feedback (below) grows it from the first blocks
   int32_t eff_bin = -1;  // packs: the bin b_eff was last halved in (a deep cluster of one bin does not shrink the next)
-  int32_t b_cap = B;  // the feedback grows blocks up to this: the halved size after an overflow (per bin in packs)
-  // Halving stops at 256 queries (UMICLUST_BLOCK_FLOOR; a floor of kPeerCap / 4 = 32, at which no window can overflow,
-  // ran config 4's giant-molecule bin 200 in 8,578 blocks: 1.44 s alone against 0.6 s at 256, profiles/r04/block_policy)
-  static const int32_t kMinBlock = getenv("UMICLUST_BLOCK_FLOOR") ? std::max(1, atoi(getenv("UMICLUST_BLOCK_FLOOR"))) : 256;
+  // Halving stops at 256 queries (a floor of kPeerCap / 4 = 32, at which no window can overflow, ran config 4's
+  // giant-molecule bin 200 in 8,578 blocks: 1.44 s alone against 0.6 s at 256; a peer-load feedback that re-cut the
+  // queued blocks from each block's largest peer list lost on config 5: profiles/r04/block_policy)
+  constexpr int32_t kMinBlock = 256;
   auto halve = [&](int32_t q) -> bool {  // false: already at the smallest block
     if (c->pack_on && c->hqbin[q] != eff_bin) {
       eff_bin = c->hqbin[q];
@@ -1586,39 +1469,18 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     }
     if (b_eff <= kMinBlock) return false;
     b_eff = std::max(kMinBlock, b_eff / 2);
-    b_cap = b_eff;
     return true;
   };
-  // ... and, opt-in (UMICLUST_ADAPT=1), a peer-load feedback: a window's peers grow with the block size, so the blocks
-  // not yet queued (after block `last`) are re-cut at twice the size when the resolved block's largest peer list was
-  // below a quarter of kPeerCap, and at half the size when it passed three quarters (shrinking before an overflow
-  // forces the synchronous re-run); bins start at 2048-query blocks.  Measured (profiles/r04/block_policy): config 2
-  // unchanged, config 4 6.51 vs 6.31 M UMIs/s, config 5 2.68 vs 3.47 M (smaller blocks cost more there than its few
-  // re-runs) -- so off by default.
   split_blocks(s0, b_eff);
   int32_t nb = (int32_t)blocks.size();
-  auto feedback = [&](int32_t last) {
-    if (!adapt || last + 1 >= nb) return;
-    const int m = c->blk_max_np;
-    int32_t nb_eff = b_eff;
-    const int32_t from = blocks[last].first + blocks[last].second;
-    if (c->pack_on && eff_bin >= 0 && c->hqbin[from] != eff_bin) b_cap = B;
-    if (m < kPeerCap / 4 && b_eff < b_cap) nb_eff = std::min(b_cap, 2 * b_eff);
-    else if (m > 3 * kPeerCap / 4 && m != 255 && b_eff > kMinBlock) nb_eff = std::max(kMinBlock, b_eff / 2);
-    if (nb_eff == b_eff) return;
-    b_eff = nb_eff;
-    blocks.resize((size_t)last + 1);
-    split_blocks(from, b_eff);
-    nb = (int32_t)blocks.size();
-  };
   std::vector<int32_t> new_cents;
   // Member tracebacks: tw_launch(lo, hi, stream) traces the members among seqnos [lo, hi) (their targets are final),
   // queries of <= 64 nt in a launch of their own (a one-stripe direction store: more waves per CU), appending to the
-  // pair arrays at tw_n; opsidx maps a member to its traceback slot.  UMICLUST_TRACE_EARLY=f (0 < f < 1) traces the
-  // members of the first f of the blocks on a stream of the least priority while the later blocks are clustered.
+  // pair arrays at tw_n; opsidx maps a member to its traceback slot.  (Tracing the first blocks' members early on a
+  // least-priority stream while later blocks are clustered measured no faster: round 4 cumask_early_ab/.)
   std::vector<int32_t>& opsidx = c->t_opsidx;
   opsidx.assign(n, -1);
-  int32_t tw_n = 0, tw_hi = s0;
+  int32_t tw_n = 0;
   c->hip(c->h_mpq.ensure((size_t)std::max(n, 1)), "pin");
   c->hip(c->h_mpt.ensure((size_t)std::max(n, 1)), "pin");
   c->hip(c->t_mpq.ensure(n), "alloc");
@@ -1628,8 +1490,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   c->hip(c->t_nops.ensure(n), "alloc");
   const DevSeqs ds = dev_seqs(c);
   const int32_t tw_maxl = s1 > s0 ? *std::max_element(c->hlen.begin() + s0, c->hlen.begin() + s1) : kMaxLen;
-  // UMICLUST_TWSPLIT=0: one launch for every member (the direction store sized for the longest query)
-  static const int tw_split = getenv("UMICLUST_TWSPLIT") && atoi(getenv("UMICLUST_TWSPLIT")) == 0 ? kMaxLen : 64;
+  // members of <= 64-nt queries in a launch of their own (one launch for all measured equal: round 4 twsplit_ab/)
+  constexpr int tw_split = 64;
   auto tw_launch = [&](int32_t lo, int32_t hi, hipStream_t stq) {
     const int32_t x0 = tw_n;
     int32_t x = x0, nm1 = 0, maxq1 = 0, maxq2 = 0;
@@ -1654,19 +1516,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->hip(launch_traceback(ds, c->t_mpq.p + nm1, c->t_mpt.p + nm1, x - nm1, c->sc, c->t_ops.p + (size_t)nm1 * kOpsStride,
                             c->t_nops.p + nm1, c->t_mout.p + nm1, stq, tw_maxl, maxq2),
            "traceback");
-  };
-  const double tw_early = getenv("UMICLUST_TRACE_EARLY") ? atof(getenv("UMICLUST_TRACE_EARLY")) : 0.0;
-  auto tw_maybe_early = [&](int32_t k) {  // block k was just resolved
-    if (!(tw_early > 0.0 && tw_early < 1.0) || tw_hi != s0 || k < (int32_t)(tw_early * nb) || c->o4_T) return;
-    if (!c->st_tw) {
-      int lo = 0, hi = 0;
-      c->hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
-      c->hip(hipStreamCreateWithPriority(&c->st_tw, hipStreamNonBlocking, lo), "stream");
-      c->hip(hipEventCreateWithFlags(&c->ev_tw, hipEventDisableTiming), "event");
-    }
-    tw_hi = blocks[k].first + blocks[k].second;
-    tw_launch(s0, tw_hi, c->st_tw);
-    c->hip(hipEventRecord(c->ev_tw, c->st_tw), "event");
   };
   // A block whose peer list overflowed: re-run it alone (window = itself, index complete up to it)
   // in halving pieces, synchronously.
@@ -1714,7 +1563,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   // multi-bin sets run several lanes on one GPU, which is throughput-bound: there the whole passes win
   // (configs 2 / 5: +12 % / +2 %, config 3: -6 %; profiles/r02/split_ab.json)
   const bool split = !T4 && (c->split_env >= 0 ? c->split_env != 0 : !multi_bin);
-  c->ix_st = (split && D == 2 && c->ix_side) ? c->st_b : nullptr;
+  c->ix_st = (split && D == 2) ? c->st_b : nullptr;
   c->last_r_ev = nullptr;
   if (split && D == 2) {
     // Split passes.  Pass j = counting half A(j) (index of blocks <= j-3, window j-2 .. j with block j-2
@@ -1768,15 +1617,12 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     prime(0);
     for (int32_t k = 0; k < nb; k++) {
       Pass& P = c->pass[k % 2];
-      excl_wait(c);
       const double tb0 = now_s();
       if (k + 3 < nb) build_peer(k + 3, true);  // queries only: built while the host resolves block k
       c->dbg_t[5] += now_s() - tb0;
       if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
-        excl_take();
         // drain everything queued (its windows include block k) and restart the pipeline after block k
         c->hip(hipStreamSynchronize(c->st_al), "sync");
-        if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
         c->hip(hipStreamSynchronize(c->st_b), "sync");
         c->hip(hipStreamSynchronize(c->st), "sync");
         for (Pass& Q : c->pass) {
@@ -1784,9 +1630,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
           Q.a_live = false;
           c->hip(hipMemsetAsync(Q.d_anunits.p, 0, 4, c->st), "memset");
         }
-        if (c->ovf_prio) c->hip(main_stream_priority(c, 1), "stream priority");
       run_alone(blocks[k].first, blocks[k].second);
-      c->blk_max_np = 255;  // the re-run pieces' peer counts say nothing about the queued block size
         if (k + 1 < nb && halve(blocks[k].first)) {
           const int32_t from = blocks[k].first + blocks[k].second;
           blocks.resize((size_t)k + 1);
@@ -1805,8 +1649,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       c->stats.n_lazy_passes += (lazy && k + 2 < nb) ? 1 : 0;
       if (k + 2 < nb) second_half(k + 2, k + 1, true);
       if (k + 3 < nb) count_half(k + 3, k + 1, 0);
-      if (k + 3 < nb) feedback(k + 3);    // blocks up to k + 3 are queued or built
-      tw_maybe_early(k);
       c->dbg_t[7] += ta1 - ta0;           // UMICLUST_DEBUG: index appends (host side)
       c->dbg_t[5] += now_s() - ta1;       // and the next passes' enqueue
     }
@@ -1814,7 +1656,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k % D];
-    excl_wait(c);
     if (k + D < nb) {
       // block k+D's peer tile depends on its queries only: build it now, behind the queued prefilters on the
       // main stream, while the host resolves block k (its ring slot was last read by pass k+D-2's prefilter)
@@ -1826,7 +1667,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       t.prebuilt = true;
     }
     if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
-      excl_take();
       // drain the queued passes k+1 .. k+D-1 (their windows include block k) and restart the pipeline
       for (int i = 1; i < D; i++) {
         Pass& Q = c->pass[(k + i) % D];
@@ -1838,10 +1678,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       // an overflowing bin runs synchronous re-runs from here on: with other lanes sharing the GPU they queue behind
         // every lane's work unless its main stream goes first (config 4: a 792k-read bin with a giant molecule took
         // 7.2 s among 8 lanes, 0.6 s alone)
-        if (c->ovf_prio) c->hip(main_stream_priority(c, 1), "stream priority");
         run_alone(blocks[k].first, blocks[k].second);
-        c->blk_max_np = 255;  // the re-run pieces' peer counts say nothing about the queued block size
-      // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
+        // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
       // same-molecule peers), so the overflow re-runs do not repeat block after block
       if (k + 1 < nb && halve(blocks[k].first)) {
         const int32_t from = blocks[k].first + blocks[k].second;
@@ -1859,14 +1697,11 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
     if (k + D < nb) enqueue(k + D, D - 1);
-    if (k + D < nb) feedback(k + D);  // blocks up to k + D are queued
-    tw_maybe_early(k);
   }
   }
   c->b_hint = b_eff;
   // centroids still pending (O4): creation numbers only, no index is needed any more
   c->cent.insert(c->cent.end(), pending.begin(), pending.end());
-  if (c->st_pf) c->hip(hipStreamSynchronize(c->st_pf), "sync");
   c->hip(hipStreamSynchronize(c->st_b), "sync");
   c->ix_st = nullptr;
   c->hip(hipStreamSynchronize(c->st_al), "sync");
@@ -1880,10 +1715,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   // --- member tracebacks first: their pairs (sorted seqno order) need only the targets, so the launch goes out
   // before the host numbers the clusters, which then overlaps the traceback (round 4: the numbering and the
   // pageable pair uploads were ~16 ms of idle GPU before the traceback of a 2M-read bin).  The members before
-  // tw_hi went out early (UMICLUST_TRACE_EARLY, while later blocks were counted); these are the rest.
-  tw_launch(tw_hi, s1, c->st);
+  tw_launch(s0, s1, c->st);
   const int32_t nm = tw_n;
-  if (tw_hi > s0) c->hip(hipStreamWaitEvent(c->st, c->ev_tw, 0), "wait");  // the early tracebacks
   if (!c->tev[0]) {
     c->hip(hipEventCreate(&c->tev[0]), "event");
     c->hip(hipEventCreate(&c->tev[1]), "event");
@@ -1966,13 +1799,6 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->hip(hipMemcpyAsync(c->h_over.p, c->t_over.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
     c->hip(hipStreamSynchronize(c->st), "sync");
     const int32_t over = *c->h_over.p;
-    if (getenv("UMICLUST_TWPROF")) {
-      unsigned long long tw[4];
-      c->hip(traceback_profile(tw, true), "twprof");
-      const double nw = tw[3] ? (double)tw[3] : 1.0;
-      fprintf(stderr, "traceback phase clocks per sampled wave (%llu): setup %.0f sweep %.0f backtrack %.0f\n", tw[3],
-              tw[0] / nw, tw[1] / nw, tw[2] / nw);
-    }
     float ms = 0;
     c->hip(hipEventElapsedTime(&ms, c->tev[0], c->tev[1]), "elapsed");
     t_cons = ms * 1e-3;
@@ -2173,8 +1999,6 @@ void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
   c->hip(c->d_lens.ensure(ns), "alloc");
   c->hip(c->d_kmers.ensure(ns * 2 * kKmerStride), "alloc");
   c->hip(c->d_nk.ensure(ns * 2), "alloc");
-  c->hip(c->d_strong.ensure(ns * 2), "alloc");
-  c->hip(hipMemsetAsync(c->d_strong.p, 0, ns * 2, c->st), "memset");
   c->hip(c->d_masked.ensure(ns * kMaxLen), "alloc");
   if (c->iota_n < ns) {  // 0, 1, 2, ... (peer tiles index sequences by seqno); the same for every load
     c->hip(c->d_iota.ensure(ns), "alloc");
@@ -2213,39 +2037,6 @@ void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
     c->hip(hipMemcpyAsync(c->d_bin_seq0.p, c->bin_s.data(), (size_t)nbins * 4, hipMemcpyHostToDevice, c->st), "h2d");
     c->hip(hipMemcpyAsync(c->d_xm.p, c->h_xm.p, (size_t)nbins * 2, hipMemcpyHostToDevice, c->st), "h2d");
     c->hip(launch_kmer_xor(c->d_kmers.p, c->d_nk.p, c->n, c->d_qbin.p, c->d_xm.p, c->st), "k-mer masks");
-  }
-  c->hip(c->d_fmask.ensure(ns * 2), "alloc");
-  c->nfk = 0;
-  if (c->defer_max > 0 && c->n > 0) {
-    // frequent k-mers (the lean counting kernel's deferral, UMICLUST_DEFER; off by default): + strand counts over
-    // <= 2^18 sampled sequences, after the per-bin XOR (the lut and the masks are in the k-mers' final space)
-    const int32_t stride = std::max<int32_t>(1, c->n >> 18);
-    std::vector<uint32_t> hist(kBins / kParts);
-    DevBuf<uint32_t> d_hist;
-    c->hip(d_hist.ensure(hist.size()), "alloc");
-    c->hip(hipMemsetAsync(d_hist.p, 0, hist.size() * 4, c->st), "memset");
-    c->hip(launch_kmer_hist(c->d_kmers.p, c->d_nk.p, c->n, stride, d_hist.p, c->st), "k-mer counts");
-    c->hip(hipMemcpyAsync(hist.data(), d_hist.p, hist.size() * 4, hipMemcpyDeviceToHost, c->st), "d2h");
-    c->hip(hipStreamSynchronize(c->st), "sync load");
-    const int64_t sampled = ((int64_t)c->n + stride - 1) / stride;
-    const double min_count = std::max(1.0, c->defer_freq * (double)sampled);
-    std::vector<uint32_t> order;
-    for (uint32_t k = 0; k < (uint32_t)hist.size(); k++)
-      if (hist[k] >= min_count) order.push_back(k);
-    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return hist[x] != hist[y] ? hist[x] > hist[y] : x < y; });
-    c->nfk = (int32_t)std::min<size_t>(order.size(), kFKmers);
-    std::vector<uint8_t> lut(hist.size(), 0xff);
-    for (int i = 0; i < kFKmers; i++) {
-      c->fkmer[i] = i < c->nfk ? (uint16_t)order[i] : 0;
-      if (i < c->nfk) lut[order[i]] = (uint8_t)i;
-    }
-    if (c->nfk > 0) {
-      DevBuf<uint8_t> d_lut;
-      c->hip(d_lut.ensure(lut.size()), "alloc");
-      c->hip(hipMemcpyAsync(d_lut.p, lut.data(), lut.size(), hipMemcpyHostToDevice, c->st), "h2d");
-      c->hip(launch_fmask(c->d_kmers.p, c->d_nk.p, c->n, d_lut.p, c->d_fmask.p, c->st), "k-mer masks");
-      c->hip(hipStreamSynchronize(c->st), "sync load");  // d_lut goes out of scope
-    }
   }
   c->hip(hipStreamSynchronize(c->st), "sync load");
   c->ambig = *c->h_amb.p != 0;
@@ -2345,33 +2136,19 @@ extern "C" {
 int32_t umiclust_abi_version(void) { return UMICLUST_ABI_VERSION; }
 
 
-// The alignment stream is created with an explicit priority, the highest by default: a pass's walk/align/pack
-// chain gates the host's resolution of its block and through it the next passes.  A prioritised stream also
-// gets a hardware queue of its own class instead of sharing the normal-priority queues with the other lanes'
-// streams (config 3, 4 lanes on one MI355X: 1.73 -> 3.1 M UMIs/s).  UMICLUST_AL_PRIO: 1 (default) greatest,
-// 0 least, -1 a plain stream.
+// The alignment stream is created with the device's greatest stream priority: a pass's walk/align/pack chain gates
+// the host's resolution of its block and through it the next passes.  A prioritised stream also gets a hardware
+// queue of its own class instead of sharing the normal-priority queues with the other lanes' streams (config 3, 4
+// lanes on one MI355X: 1.73 -> 3.1 M UMIs/s; least priority or a plain stream measured no better, round 4
+// al_prio_ab/; a CU-masked stream slower, cumask_early_ab/).
 static int al_priority() {
   int lo = 0, hi = 0;
   if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
   if (getenv("UMICLUST_DEBUG")) fprintf(stderr, "stream priorities: least %d greatest %d\n", lo, hi);
-  const char* e = getenv("UMICLUST_AL_PRIO");
-  return (e && atoi(e) == 0) ? lo : hi;
+  return hi;
 }
 
-// The alignment stream.  UMICLUST_AL_CUS=k (1..31, experiment): the stream's kernels run on k of every 32 CUs (a CU
-// mask; such a stream has no priority), leaving the rest to the counting chain.
 static hipError_t create_al_stream(umiclust_ctx* c) {
-  if (const char* e = getenv("UMICLUST_AL_CUS")) {
-    const int k = atoi(e);
-    if (k > 0 && k < 32) {
-      std::vector<uint32_t> mask(32, 0u);  // up to 1024 CUs
-      for (int i = 0; i < 32 * 32; i++)
-        if (i % 32 < k) mask[(size_t)(i / 32)] |= 1u << (i % 32);
-      return hipExtStreamCreateWithCUMask(&c->st_al, (uint32_t)mask.size(), mask.data());
-    }
-  }
-  if (getenv("UMICLUST_AL_PRIO") && atoi(getenv("UMICLUST_AL_PRIO")) < 0)
-    return hipStreamCreateWithFlags(&c->st_al, hipStreamNonBlocking);
   return hipStreamCreateWithPriority(&c->st_al, hipStreamNonBlocking, al_priority());
 }
 
@@ -2402,43 +2179,21 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     if (err) *err = UMICLUST_EDEVICE;
     return nullptr;
   }
-  if (const char* e = getenv("UMICLUST_DEPTH")) c->depth = std::max(2, std::min(kPeerTiles, atoi(e)));
-  if (const char* e = getenv("UMICLUST_IXSIDE")) c->ix_side = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_RB_STREAM")) c->rb_on_b = e[0] == 'b';
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
-  if (const char* e = getenv("UMICLUST_RAL")) c->r_on_al = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_DEFER")) c->defer_max = std::min(4, std::max(0, atoi(e)));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
-  if (const char* e = getenv("UMICLUST_PFTAB")) c->pf_tab = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_PRESPEC")) c->pre_spec = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_PAR_INORDER")) c->par_inorder = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));
-  if (const char* e = getenv("UMICLUST_RECDIRECT")) c->rec_direct_env = atoi(e) != 0 ? 1 : 0;
-  if (const char* e = getenv("UMICLUST_EXCL")) c->excl = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_BLOCK_MIN")) c->block_min = std::min(kMaxBlock, std::max(256, atoi(e)));
-  if (const char* e = getenv("UMICLUST_PRERESOLVE")) c->pre_resolve = atoi(e) != 0;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
     c->pin = atoi(e) != 0;
     c->pin_forced = atoi(e) == 1;
   }
   g_live_ctx++;
-  if (const char* e = getenv("UMICLUST_SPLIT")) {
-    c->split_env = atoi(e) != 0 ? 1 : 0;
-    c->split_stream = atoi(e) == 2;
-  }
+  if (const char* e = getenv("UMICLUST_SPLIT")) c->split_env = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_RESOLVE_THREADS")) c->resolve_threads = std::max(1, std::min(16, atoi(e)));
   if (const char* b = getenv("UMICLUST_BLOCK")) {
     c->block_size = std::max(1, std::min(kTile, atoi(b)));
     c->block_div = 0;
   }
-  if (const char* b = getenv("UMICLUST_BLOCK_DIV")) c->block_div = std::max(0, atoi(b));
-  if (const char* e = getenv("UMICLUST_SPEC")) c->spec_thr = std::max(0, atoi(e));
-  if (const char* e = getenv("UMICLUST_PEER_PREDICT")) c->peer_predict = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_PEER_CERT")) c->peer_cert = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_OVF_PRIO")) c->ovf_prio = atoi(e) != 0;
-  if (const char* e = getenv("UMICLUST_STRONG")) c->strong_eighths = std::max(1, std::min(8, atoi(e)));
-  if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, atoi(e));
   if (getenv("UMICLUST_PFPROF")) {
     if (c->pf_prof.ensure(24) != hipSuccess || hipMemset(c->pf_prof.p, 0, 24 * sizeof(unsigned long long)) != hipSuccess) {
       delete c;
@@ -2486,13 +2241,10 @@ void umiclust_destroy(umiclust_ctx* c) {
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st_al) (void)hipStreamDestroy(c->st_al);
-  if (c->st_tw) (void)hipStreamDestroy(c->st_tw);
-  if (c->ev_tw) (void)hipEventDestroy(c->ev_tw);
   if (c->ix_done) (void)hipEventDestroy(c->ix_done);
   for (auto& r : c->a_ev)
     for (hipEvent_t e : r)
       if (e) (void)hipEventDestroy(e);
-  if (c->st_pf) (void)hipStreamDestroy(c->st_pf);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }

@@ -2,7 +2,7 @@
 //
 // The reference delegates this arithmetic to vsearch (`--cluster_fast`, invoked at
 // /root/reference/ont_tcr_consensus/vsearch_umi_cluster.py:21-54 and :71-97).  Kernels:
-//   K1 k_prep        DUST soft-mask (vsearch mask.cc) + unique 8-mers both strands (unique.cc)
+//   K1 k_prep_wave   DUST soft-mask (vsearch mask.cc) + unique 8-mers both strands (unique.cc)
 //   KI k_index_*     CSR inverted index tile over centroid k-mers (dbindex.cc analogue)
 //   K2 k_prefilter   shared-unique-k-mer counting against every centroid + top-41 selection
 //                    (searchcore.cc search_topscores / minheap.cc order), LDS u8 counters
@@ -76,167 +76,14 @@ __device__ __forceinline__ uint32_t comp4(uint32_t c4) {
 }
 
 // ------------------------------------------------------------------ K1: prep
-// One thread per (sorted) sequence.  LDS scratch per thread: residues, DUST words/counts and
-// the k-mer sort buffer (runtime-indexed arrays must not live in VGPRs).
-constexpr int kPrepThreads = 64;
-struct PrepScratch {
-  uint8_t ch[kMaxLen];     // original characters
-  uint8_t words[64];
-  uint8_t counts[64];
-  uint16_t km[kMaxKmers + 3];
-};
-
-__device__ int dust_wo(const uint8_t* s2, int len, int* beg, int* end, uint8_t* words,
-                       uint8_t* counts) {
-  // vsearch mask.cc wo(): smallest region is 8 => l1 = len - 3 + 1 - 5
-  int l1 = len - 3 + 1 - 5;
-  if (l1 < 0) {
-    *beg = 0;
-    *end = len - 1;
-    return 0;
-  }
-  int w = 0;
-  for (int j = 0; j < len; j++) {
-    w = ((w << 2) | s2[j]) & 63;
-    words[j] = (uint8_t)w;
-  }
-  int bestv = 0, besti = 0, bestj = 0;
-  for (int i = 0; i < l1; i++) {
-    for (int x = 0; x < 64; x++) counts[x] = 0;
-    int sum = 0;
-    for (int j = 2; j < len - i; j++) {
-      int x = words[i + j];
-      int c = counts[x];
-      if (c) {
-        sum += c;
-        // v = 10*sum/j (integer); v > bestv  <=>  10*sum >= (bestv+1)*j
-        if (10 * sum >= (bestv + 1) * j) {
-          bestv = (10 * sum) / j;
-          besti = i;
-          bestj = j;
-        }
-      }
-      counts[x] = (uint8_t)(c + 1);
-    }
-  }
-  *beg = besti;
-  *end = besti + bestj;
-  return bestv;
-}
-
-__global__ __launch_bounds__(kPrepThreads) void k_prep(const char* __restrict__ ascii,
-                                                       const int64_t* __restrict__ offs,
-                                                       const int32_t* __restrict__ perm, int32_t n,
-                                                       int dust, uint32_t* __restrict__ codes,
-                                                       uint8_t* __restrict__ lens,
-                                                       uint16_t* __restrict__ kmers,
-                                                       uint8_t* __restrict__ nk,
-                                                       char* __restrict__ masked,
-                                                       uint32_t* __restrict__ ambig) {
-  __shared__ PrepScratch scr[kPrepThreads];
-  int s = blockIdx.x * kPrepThreads + threadIdx.x;
-  if (s >= n) return;
-  PrepScratch& P = scr[threadIdx.x];
-  int r = perm ? perm[s] : s;
-  int64_t b = offs[r];
-  int len = (int)(offs[r + 1] - b);
-  for (int x = 0; x < len; x++) P.ch[x] = (uint8_t)ascii[b + x];
-  // lower-case mask bits (bit x set = masked), 3 words
-  uint32_t mk[kMaskWords];
-#pragma unroll
-  for (int w = 0; w < kMaskWords; w++) mk[w] = 0;
-  if (dust) {
-    // dust(): the whole sequence upper-cased, masked intervals lower-cased
-    uint8_t* codes2 = reinterpret_cast<uint8_t*>(P.km);  // >= kMaxLen bytes available (2 * kMaxKmers + 6)
-    for (int x = 0; x < len; x++) codes2[x] = (uint8_t)code2_of4(c_map4[P.ch[x]]);
-    for (int i = 0; i < len; i += 32) {
-      int l = (len > i + 64) ? 64 : len - i;
-      int a = 0, e = 0;
-      int v = dust_wo(codes2 + i, l, &a, &e, P.words, P.counts);
-      if (v > 20) {
-        for (int j = a + i; j <= e + i; j++) {
-#pragma unroll
-          for (int w = 0; w < kMaskWords; w++)
-            if ((j >> 5) == w) mk[w] |= 1u << (j & 31);
-        }
-      }
-    }
-  }
-  auto masked_at = [&](int x) -> uint32_t {
-    uint32_t b = 0;
-#pragma unroll
-    for (int w = 0; w < kMaskWords; w++)
-      if ((x >> 5) == w) b = (mk[w] >> (x & 31)) & 1u;
-    return b;
-  };
-  lens[s] = (uint8_t)len;
-  // masked ASCII (what vsearch prints) and 4-bit codes for both strands
-  uint32_t w0[kCodeWords], w1[kCodeWords];
-#pragma unroll
-  for (int w = 0; w < kCodeWords; w++) { w0[w] = 0; w1[w] = 0; }
-  for (int x = 0; x < len; x++) {
-    uint8_t c = P.ch[x];
-    uint8_t up = (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
-    if (dust) c = masked_at(x) ? (uint8_t)(up | 0x20) : up;
-    if (masked) masked[(int64_t)s * kMaxLen + x] = (char)c;
-    P.ch[x] = c;
-  }
-  uint32_t any_amb = 0;
-  for (int x = 0; x < len; x++) {
-    uint32_t c4 = c_map4[P.ch[x]];
-    any_amb |= (c4 != 1u && c4 != 2u && c4 != 4u && c4 != 8u) ? 1u : 0u;
-    int xr = len - 1 - x;
-#pragma unroll
-    for (int w = 0; w < kCodeWords; w++) {
-      if ((x >> 3) == w) w0[w] |= c4 << ((x & 7) * 4);
-      if ((xr >> 3) == w) w1[w] |= comp4(c4) << ((xr & 7) * 4);
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < kCodeWords; w++) {
-    codes[((int64_t)s * 2 + 0) * kCodeWords + w] = w0[w];
-    codes[((int64_t)s * 2 + 1) * kCodeWords + w] = w1[w];
-  }
-  if (any_amb && ambig) atomicOr(ambig, 1u);
-  // unique 8-mers per strand, masked windows skipped (unique.cc), sorted ascending
-  for (int st = 0; st < 2; st++) {
-    uint32_t km = 0, bad = 0;
-    int cnt = 0;
-    for (int y = 0; y < len; y++) {
-      int x = st ? len - 1 - y : y;
-      uint32_t c4 = c_map4[P.ch[x]];
-      if (st) c4 = comp4(c4);
-      bad = ((bad << 1) | masked_at(x)) & 0xffu;
-      km = ((km << 2) | code2_of4(c4)) & 0xffffu;
-      if (y >= 7 && !bad) {
-        // insertion into sorted unique list
-        int pos = cnt;
-        bool dup = false;
-        while (pos > 0 && P.km[pos - 1] >= km) {
-          if (P.km[pos - 1] == km) { dup = true; break; }
-          pos--;
-        }
-        if (!dup) {
-          for (int z = cnt; z > pos; z--) P.km[z] = P.km[z - 1];
-          P.km[pos] = (uint16_t)km;
-          cnt++;
-        }
-      }
-    }
-    uint16_t* dst = kmers + ((int64_t)s * 2 + st) * kKmerStride;
-    for (int z = 0; z < cnt; z++) dst[z] = P.km[z];
-    nk[(int64_t)s * 2 + st] = (uint8_t)cnt;
-  }
-}
-
-// K1, wave form (the default; UMICLUST_PREP=thread selects k_prep above): one wave per sorted sequence, lane x
+// K1 (k_prep_wave): one wave per sorted sequence, lane x
 // holding residue positions x and x + 64.  DUST (mask.cc dust() / wo()): per 64-nt window (every 32 nt) lane i runs
 // wo()'s inner loop for start i over its own triplet counts (a lane-private LDS row); wo()'s result is the
 // lexicographically first (i, j) with the largest floor(10 sum / j) -- its strict `v > bestv` update never replaces
 // an equal value -- so the window's best is the lanes' (v desc, i asc) maximum with the winner's own first j.
 // Codes: 14 lanes pack 8 nibbles each.  Unique 8-mers (unique.cc): each lane builds the k-mers ending at its two
 // positions (masked windows and short prefixes become distinct sentinels above every code), a bitonic sort of the
-// 128 keys across the wave, then neighbour comparison and a ballot compaction -- ascending, as the thread form.
+// 128 keys across the wave, then neighbour comparison and a ballot compaction -- ascending.
 constexpr int kDustRow = 17;  // dwords per lane-private count row (64 u8 counters + 1: rotates the banks per lane)
 
 __global__ __launch_bounds__(64) void k_prep_wave(const char* __restrict__ ascii, const int64_t* __restrict__ offs,
@@ -420,14 +267,8 @@ hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* pe
   hipError_t e = ensure_maps(st);
   if (e != hipSuccess) return e;
   if (n <= 0) return hipSuccess;
-  // UMICLUST_PREP=thread: the one-thread-per-sequence form (A/B and cross-checks)
-  static const bool per_thread = getenv("UMICLUST_PREP") && getenv("UMICLUST_PREP")[0] == 't';
-  if (per_thread)
-    hipLaunchKernelGGL(k_prep, dim3((n + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0, st,
-                       ascii, offs, perm, n, dust, codes, lens, kmers, nk, masked, ambig);
-  else
-    hipLaunchKernelGGL(k_prep_wave, dim3((unsigned)n), dim3(64), 0, st, ascii, offs, perm, n, dust, codes, lens, kmers,
-                       nk, masked, ambig);
+  hipLaunchKernelGGL(k_prep_wave, dim3((unsigned)n), dim3(64), 0, st, ascii, offs, perm, n, dust, codes, lens, kmers,
+                     nk, masked, ambig);
   return hipGetLastError();
 }
 
@@ -833,7 +674,6 @@ struct PfTable {
 __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, int t0, int nct, int ntl,
                                               uint64_t pbase, int part, int thr, int nk, uint32_t km0, uint32_t km1,
                                               int wv, int lane, int tid, uint32_t& T, uint32_t& nlc,
-                                              bool skip0 = false, bool skip1 = false, uint32_t* def_ch = nullptr,
                                               bool prof = false, unsigned long long* clk0 = nullptr,
                                               unsigned long long* clk1 = nullptr) {
   TileView tvs[kPfTilesPerWave];
@@ -844,7 +684,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
     else if (ti < ntl) tvs[it] = a.peer[ti - nct];
     else tvs[it].n = 0;
   }
-  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0, dch = 0;
+  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
   u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
@@ -859,14 +699,10 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
     const uint32_t tbase = (uint32_t)(tvs[it].post_base - pbase);
     const uint32_t c0 = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
     const uint32_t c1 = (live && lane + 64 < nk) ? (o1[it].y - o1[it].x) >> 3 : 0u;
-    // deferred k-mers (k_pf_count's frequent-k-mer deferral): their lists are not streamed
-    // (centroid tiles only: peer tiles are counted in full, so peers and flagged hits stay exact)
-    const bool cen = wv + it * kPfWaves < nct, s0 = skip0 && cen, s1 = skip1 && cen;
-    nch[2 * it] = s0 ? 0u : c0;
+    nch[2 * it] = c0;
     bse[2 * it] = tbase + o0[it].x;
-    nch[2 * it + 1] = s1 ? 0u : c1;
+    nch[2 * it + 1] = c1;
     bse[2 * it + 1] = tbase + o1[it].x;
-    dch += (s0 ? c0 : 0u) + (s1 ? c1 : 0u);
   }
 #pragma unroll
   for (int j = 0; j < kPfSlots; j++) {
@@ -879,7 +715,6 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
   // packed scan: chunks << kListBits | lists (see kListBits)
   uint32_t tot;
   const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
-  if (def_ch && dch) atomicAdd(def_ch, dch);  // after the scan's barriers: *def_ch was zeroed before the call
   if (prof) *clk1 = __builtin_readcyclecounter();
   T = tot >> kListBits;
   nlc = tot & kListMask;
@@ -956,64 +791,6 @@ __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, ui
     v1 = ldv(a1);
     if (w + 2 * S1 < nwin) pf_chunk<kBase>(u0, one(b0));
     if (w + 3 * S1 < nwin) pf_chunk<kBase>(u1, one(b1));
-  }
-}
-
-// The same count with the window addresses computed ahead, kPfPre windows at a time: window() reads the list
-// table in LDS, and an LDS read waits for every LDS operation the wave issued before it -- in the loop above
-// that is the counting atomics of the previous windows, so each pair of windows drained the wave's atomics
-// before its next loads could even be addressed.  Here a round's addresses come first (the table reads of a
-// whole round in flight together, behind no atomics at the start of the stream), then the round's chunks
-// stream through kPfAhead loads in flight while the atomics are issued without any LDS read between them.
-constexpr int kPfPre = 16, kPfAhead = 4;
-template <uint32_t kBase>
-__device__ __forceinline__ void pf_count_stream_pre(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
-                                                    const uint32_t* lstart, const uint32_t* lbias,
-                                                    const uint4* wtab, int lane, int wv) {
-  const uint32_t nwin = (T + 63u) >> 6;
-  const unsigned long long below = (2ull << lane) - 1ull;
-  const uint32_t below_lo = lane < 32 ? (2u << lane) - 1u : 0xffffffffu;
-  const uint32_t below_hi = lane < 32 ? 0u : (2u << (lane - 32)) - 1u;
-  auto window = [&](uint32_t w) -> uint32_t {
-    if (w >= nwin) return 0xffffffffu;
-    const uint32_t g0 = w << 6, g = g0 + (uint32_t)lane;
-    if (w < (uint32_t)kPfWinBase) {
-      const uint4 t = wtab[w];  // one uniform b128 read (was three)
-      const uint32_t L0 = t.x + (uint32_t)__builtin_popcount(t.y & below_lo) + (uint32_t)__builtin_popcount(t.z & below_hi);
-      return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
-    }
-    int lo = 0, hi = (int)nlc - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (lstart[mid] <= g0) lo = mid;
-      else hi = mid - 1;
-    }
-    const uint32_t m = (uint32_t)lo;
-    const uint32_t bit = lstart[m + 1 + lane] - g0;
-    uint32_t lo32 = bit < 32u ? 1u << bit : 0u, hi32 = bit - 32u < 32u ? 1u << (bit - 32u) : 0u;
-    wave_or2_dpp(lo32, hi32);
-    const unsigned long long sm = ((unsigned long long)lane63(hi32) << 32) | lane63(lo32);
-    const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
-    return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
-  };
-  constexpr uint32_t S1 = kPfWaves;
-  for (uint32_t w0 = (uint32_t)wv; w0 < nwin; w0 += kPfPre * S1) {  // wave-uniform
-    const uint32_t nb = min((uint32_t)kPfPre, (nwin - w0 + S1 - 1) / S1);  // windows of this round
-    uint32_t ad[kPfPre];
-#pragma unroll
-    for (int i = 0; i < kPfPre; i++) ad[i] = (uint32_t)i < nb ? window(w0 + i * S1) : 0xffffffffu;
-    uint4 v[kPfAhead];
-#pragma unroll
-    for (int i = 0; i < kPfAhead; i++) v[i] = ld_chunk(arena, ad[i] == 0xffffffffu ? 0u : ad[i]);
-#pragma unroll
-    for (int i = 0; i < kPfPre; i++) {
-      if ((uint32_t)i < nb) {  // wave-uniform; no break, so the loop unrolls and v[] stays in registers
-        const uint4 cur = v[i % kPfAhead];
-        if (i + kPfAhead < kPfPre && (uint32_t)(i + kPfAhead) < nb)
-          v[i % kPfAhead] = ld_chunk(arena, ad[i + kPfAhead] == 0xffffffffu ? 0u : ad[i + kPfAhead]);
-        pf_chunk<kBase>(cur, ad[i] != 0xffffffffu ? 1u : 0u);
-      }
-    }
   }
 }
 
@@ -1295,115 +1072,6 @@ __global__ __launch_bounds__(kPfThreads, 5) void k_pf_full(PrefilterArgs a, int 
   }
 }
 
-// The list table of k_pf_count, built ahead by k_pf_table into global memory: one wave per (query-strand, part)
-// unit, no barriers (a wave-level DPP scan lays the non-empty lists end to end), high occupancy (no counters in
-// LDS), so its latency chain -- tile views, list offsets, scan, writes -- overlaps across many units instead of
-// sitting inside every counting workgroup's lifetime between its barriers.  Unit image (u32 words, 16-B aligned):
-// [0] T (chunks), [1] nlc (lists), [2] deferred chunks, [3] -, then the k_pf_count LDS table image: wtab
-// (uint4 x kPfWinBase), lstart (nlist_cap + 66), lbias (nlist_cap).
-__global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __restrict__ tab, int32_t nunits) {
-  __shared__ uint32_t wl[kPfWinBase], wh[kPfWinBase], wb[kPfWinBase];
-  const int unit = (int)blockIdx.x;
-  if (unit >= nunits) return;
-  const int lane = (int)threadIdx.x;
-  const int part = unit & (kParts - 1);
-  const int qs = unit >> kPartShift;
-  const int strand = qs % a.both;
-  const int32_t q = a.q0 + qs / a.both;
-  const int nk = a.seqs.nk[(int64_t)q * 2 + strand];
-  const uint16_t* qk = a.seqs.kmers + ((int64_t)q * 2 + strand) * kKmerStride;
-  const uint32_t raw0 = qk[lane], raw1 = qk[64 + (lane < kKmerStride - 64 ? lane : 0)];
-  const int thr = nk < a.minwordmatches ? nk : a.minwordmatches;
-  const uint32_t km0 = lane < nk ? raw0 : 0u, km1 = lane + 64 < nk ? raw1 : 0u;
-  // frequent-k-mer deferral (PrefilterArgs::fmask): the lanes holding D's k-mers skip their centroid-tile lists
-  uint32_t dmask = 0u;
-  if (a.defer_max > 0 && thr > 0) {
-    uint32_t m = a.fmask[(int64_t)q * 2 + strand];
-    for (int i = 0; i < a.defer_max && m != 0u && thr - (i + 1) >= a.defer_min_thr; i++) {
-      dmask |= m & (0u - m);
-      m &= m - 1u;
-    }
-  }
-  dmask = (uint32_t)__builtin_amdgcn_readfirstlane((int)dmask);
-  bool skip0 = false, skip1 = false;
-  for (uint32_t m = dmask; m != 0u; m &= m - 1u) {
-    const uint32_t fk = a.fkmer[__builtin_ctz(m)];
-    skip0 |= lane < nk && km0 == fk;
-    skip1 |= lane + 64 < nk && km1 == fk;
-  }
-  const int nct = a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0;
-  const int ntl = nct + kPeerTiles;
-  const uint64_t pbase = a.seg_base[0];
-  // every slot's offsets are loaded unconditionally (an absent tile reads the own peer tile's, list 0 past nk)
-  u32x2 o0[kPfTiles], o1[kPfTiles];
-  uint32_t tb[kPfTiles];
-  bool lv[kPfTiles];
-#pragma unroll
-  for (int ti = 0; ti < kPfTiles; ti++) {
-    TileView tv;
-    if (ti < nct) tv = cent_view(a, ti);
-    else if (ti < ntl) tv = a.peer[ti - nct];
-    else tv.n = 0;
-    lv[ti] = thr > 0 && ti < ntl && tv.n > 0;
-    const uint32_t* op = uniform_ptr((lv[ti] ? tv.off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
-    tb[ti] = lv[ti] ? (uint32_t)(tv.post_base - pbase) : 0u;
-    o0[ti] = ld_off2(op, km0);
-    o1[ti] = ld_off2(op, km1);
-  }
-  uint32_t sum_ch = 0, sum_ne = 0, dch = 0;
-#pragma unroll
-  for (int ti = 0; ti < kPfTiles; ti++) {
-    const bool cen = ti < nct;
-    const uint32_t c0 = (lv[ti] && lane < nk) ? (o0[ti].y - o0[ti].x) >> 3 : 0u;
-    const uint32_t c1 = (lv[ti] && lane + 64 < nk) ? (o1[ti].y - o1[ti].x) >> 3 : 0u;
-    const bool s0 = skip0 && cen, s1 = skip1 && cen;
-    dch += (s0 ? c0 : 0u) + (s1 ? c1 : 0u);
-    o0[ti].y = s0 ? 0u : c0;  // from here on: .x list offset, .y chunks
-    o1[ti].y = s1 ? 0u : c1;
-    sum_ch += o0[ti].y + o1[ti].y;
-    sum_ne += (o0[ti].y ? 1u : 0u) + (o1[ti].y ? 1u : 0u);
-  }
-  if (lane < kPfWinBase / 2) {
-    wl[lane] = wl[lane + 64] = 0u;
-    wh[lane] = wh[lane + 64] = 0u;
-  }
-  // wave scan of (chunks << kListBits | lists): the non-empty lists end to end, lane-major
-  const uint32_t packed = (sum_ch << kListBits) | sum_ne;
-  const uint32_t inc = wave_scan_dpp(packed, OpAdd());
-  const uint32_t tot = lane63(inc), ex = inc - packed;
-  const uint32_t T = tot >> kListBits, nlc = tot & kListMask;
-  uint32_t* img = tab + (size_t)unit * pf_table_stride(a.nlist_cap);
-  uint32_t* lstart = img + 4 + 4 * kPfWinBase;
-  uint32_t* lbias = lstart + a.nlist_cap + 66;
-  uint32_t li = ex & kListMask, ci = ex >> kListBits;
-  auto put = [&](uint32_t nch, uint32_t bse) {
-    if (!nch) return;
-    lstart[li] = ci;
-    lbias[li] = bse - 8u * ci;
-    if ((ci & 63u) != 0u && (ci >> 6) < (uint32_t)kPfWinBase) atomicOr(((ci & 32u) ? wh : wl) + (ci >> 6), 1u << (ci & 31u));
-    for (uint32_t w = (ci + 63u) >> 6; (w << 6) < ci + nch && w < (uint32_t)kPfWinBase; w++) wb[w] = li;
-    li++;
-    ci += nch;
-  };
-#pragma unroll
-  for (int ti = 0; ti < kPfTiles; ti++) {
-    put(o0[ti].y, tb[ti] + o0[ti].x);
-    put(o1[ti].y, tb[ti] + o1[ti].x);
-  }
-  if (lane < 66) lstart[nlc + lane] = T;
-  if (lane == 0) {
-    img[0] = T;
-    img[1] = nlc;
-    img[2] = 0u;
-  }
-  const uint32_t dsum = lane63(wave_scan_dpp(dch, OpAdd()));
-  if (lane == 0) img[2] = dsum;
-  // the window tables (LDS of this wave: its own writes are complete in order) to the image
-  const uint32_t nw = min((T + 63u) >> 6, (uint32_t)kPfWinBase);
-  uint4* gwt = reinterpret_cast<uint4*>(img + 4);
-  for (uint32_t w = (uint32_t)lane; w < nw; w += 64) gwt[w] = make_uint4(wb[w], wl[w], wh[w], 0u);
-}
-
 // The lean counting kernel (one counter segment): list table, count, then every centroid counter >= the
 // threshold becomes a part candidate (count << 24 | ordinal, unsorted, at most kPartCand) and every earlier
 // window query over it a peer (unsorted); lengths, keys and the top-41 are the merge's.  Only what counting
@@ -1411,14 +1079,13 @@ __global__ __launch_bounds__(64) void k_pf_table(PrefilterArgs a, uint32_t* __re
 // the kernel keeps few registers, so up to 8 workgroups share a CU.
 struct PfCountHdr {
   uint32_t wsum[kPfWaves];
-  uint32_t ncand, npc, ndef, pad1;
+  uint32_t ncand, npc, pad0, pad1;
 };
 __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
   return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 16 + (2 * nlist_cap + 66) * 4);
 }
 template <int CM>
-__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off,
-                                                            const uint32_t* __restrict__ gtab) {
+__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
   uint4* wtab = reinterpret_cast<uint4*>(pf_smem + tab_off + sizeof(PfCountHdr));
@@ -1439,24 +1106,6 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   const int64_t pq_ = (int64_t)qs * kParts + part;
   int32_t seq0, ord0;
   pack_bounds(a, q, seq0, ord0);
-  // frequent-k-mer deferral (PrefilterArgs::fmask): D = the lowest set bits of the query-strand's F mask, at most
-  // defer_max of them and thr - |D| >= defer_min_thr; the lanes holding D's k-mers skip their lists
-  uint32_t dmask = 0u;
-  if (a.defer_max > 0 && thr > 0) {
-    uint32_t m = a.fmask[(int64_t)q * 2 + strand];
-    for (int i = 0; i < a.defer_max && m != 0u && thr - (i + 1) >= a.defer_min_thr; i++) {
-      dmask |= m & (0u - m);
-      m &= m - 1u;
-    }
-  }
-  dmask = (uint32_t)__builtin_amdgcn_readfirstlane((int)dmask);
-  const int fd = __builtin_popcount(dmask);
-  bool skip0 = false, skip1 = false;
-  for (uint32_t m = dmask; m != 0u; m &= m - 1u) {
-    const uint32_t fk = a.fkmer[__builtin_ctz(m)];
-    skip0 |= lane < nk && km0 == fk;
-    skip1 |= lane + 64 < nk && km1 == fk;
-  }
   const int nct = a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0;
   const int nsubC = a.ncent > part ? (a.ncent - part + kParts - 1) >> kPartShift : 0;
   const int ncnt = kCentBase + ((nsubC + 15) & ~15);
@@ -1483,52 +1132,29 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   if (tid == 0) {
     H.ncand = 0;
     H.npc = 0;
-    H.ndef = 0;
   }
   uint32_t T, nlc;
   PFC_MARK(0)
-  if (gtab) {
-    // the table k_pf_table built for this unit: its image copied into LDS (16-byte vectors), one barrier
-    const uint32_t* img = gtab + (size_t)blockIdx.x * pf_table_stride(a.nlist_cap);
-    T = (uint32_t)__builtin_amdgcn_readfirstlane((int)img[0]);
-    nlc = (uint32_t)__builtin_amdgcn_readfirstlane((int)img[1]);
-    if (tid == 0) H.ndef = img[2];
-    const uint4* src = reinterpret_cast<const uint4*>(img + 4);
-    uint4* dst = wtab;
-    const int nv4 = (int)((pf_table_img_words(a.nlist_cap) + 3u) >> 2);
-    for (int x = tid; x < nv4; x += kPfThreads) dst[x] = src[x];
-    __syncthreads();
-    if (prof) tsub[0] += __builtin_readcyclecounter() - tprev;
-  } else {
-    pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
-                  km0, km1, wv, lane, tid, T, nlc, skip0, skip1, &H.ndef, prof, &clk0, &clk1);
-    if (prof) {
-      tsub[0] += clk0 - tprev;
-      tsub[1] += clk1 - clk0;
-    }
+  pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
+                km0, km1, wv, lane, tid, T, nlc, prof, &clk0, &clk1);
+  if (prof) {
+    tsub[0] += clk0 - tprev;
+    tsub[1] += clk1 - clk0;
   }
   PFC_MARK(1)
-  if (T > 0 && CM != 2) {  // CM 2: the timing probe without the count loop (UMICLUST_PFPROBE)
-    if (CM == 1) pf_count_stream_pre<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
-    else pf_count_stream<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
-  }
+  if (T > 0 && CM != 2)  // CM 2: the timing probe without the count loop (UMICLUST_PFPROBE)
+    pf_count_stream<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
   __syncthreads();
   PFC_MARK(2)
   if (wv == 0) {
     // postings touched (stats): every chunk posting minus the padding ones (the spare counters)
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(cnt);
     const uint32_t pads = lane63(wave_scan_dpp((uint32_t)cb[kDummy + lane], OpAdd()));
-    if (lane == 0) {
-      a.ppost[pq_] = 8u * T - pads;
-      if (a.pdef) a.pdef[pq_] = 8u * H.ndef;
-    }
+    if (lane == 0) a.ppost[pq_] = 8u * T - pads;
   }
   // centroid counters >= thr (SWAR: bytes <= 112, so byte + 128 - thr sets bit 7 iff >= thr); a sweep
-  // of 64 counter vectors with no candidate costs one OR and a ballot.  With deferred k-mers (fd > 0) the
-  // centroid counters lack at most |D| matches: every counter >= thr - |D| is emitted with its partial count and
-  // k_pf_merge adds the deferred matches (PrefilterArgs::pdm).  Peer tiles are counted in full (exact).
+  // of 64 counter vectors with no candidate costs one OR and a ballot.
   const uint32_t add = (uint32_t)(128 - thr) * 0x01010101u;
-  const uint32_t cadd = (uint32_t)(128 - (thr - fd)) * 0x01010101u;
   if (thr > 0) {
     const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
     const uint4* c4 = cnt4 + kCentBase / 16;
@@ -1538,10 +1164,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
       uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
       const int cb = cmin - x * 16;
       if (cb > 0) v = make_uint4(v.x & keep_from(cb), v.y & keep_from(cb - 4), v.z & keep_from(cb - 8), v.w & keep_from(cb - 12));
-      if (__ballot((((v.x + cadd) | (v.y + cadd) | (v.z + cadd) | (v.w + cadd)) & 0x80808080u) != 0u) == 0ull) continue;
+      if (__ballot((((v.x + add) | (v.y + add) | (v.z + add) | (v.w + add)) & 0x80808080u) != 0u) == 0ull) continue;
       const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-      uint32_t mk[4] = {(v.x + cadd) & 0x80808080u, (v.y + cadd) & 0x80808080u, (v.z + cadd) & 0x80808080u,
-                        (v.w + cadd) & 0x80808080u};
+      uint32_t mk[4] = {(v.x + add) & 0x80808080u, (v.y + add) & 0x80808080u, (v.z + add) & 0x80808080u,
+                        (v.w + add) & 0x80808080u};
       const uint32_t n = (uint32_t)(__builtin_popcount(mk[0]) + __builtin_popcount(mk[1]) +
                                     __builtin_popcount(mk[2]) + __builtin_popcount(mk[3]));
       uint32_t slot = wave_alloc(n, &H.ncand);
@@ -1618,7 +1244,6 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const bool ovf = thr == 0 || nc > (uint32_t)kPartCand;
     a.pncand[pq_] = (uint8_t)(ovf ? 255u : nc);
     a.pnpeer[pq_] = (uint8_t)(np > (uint32_t)kPeerCap ? 255u : np);
-    if (a.pdm) a.pdm[pq_] = ovf ? 0u : dmask;  // the full kernel's candidates (ovf) are exact
     if (ovf) a.units[atomicAdd(a.nunits, 1u)] = (uint32_t)pq_;
   }
   PFC_MARK(4)
@@ -1641,10 +1266,10 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
 // part top-41: top-41 of a union = top-41 of the parts' top-41s).  Peers: sorted within each part by
 // (count desc, length asc, window id asc) and concatenated in part order.
 constexpr int kMergeWaves = 4;
-__global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs, int32_t use_pdm) {
+__global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, int32_t nqs) {
   __shared__ unsigned long long keys[kMergeWaves][kParts * kPartCand];
   __shared__ uint32_t pkeys[kMergeWaves][kPeerCap];
-  __shared__ uint32_t wpost[kMergeWaves], wdef[kMergeWaves];
+  __shared__ uint32_t wpost[kMergeWaves];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qs = (int)blockIdx.x * kMergeWaves + wave;
   const bool live = qs < nqs;
@@ -1653,27 +1278,15 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   // postings touched (stats): the parts' counts, one atomic per workgroup into one of kPostSpread lines
   {
     uint32_t pp = (live && lane < kParts) ? a.ppost[p0 + lane] : 0u;
-    uint32_t pd = (live && lane < kParts && a.pdef) ? a.pdef[p0 + lane] : 0u;
 #pragma unroll
-    for (int d = 1; d < kParts; d <<= 1) {
-      pp += __shfl_xor(pp, d, 64);
-      pd += __shfl_xor(pd, d, 64);
-    }
-    if (lane == 0) {
-      wpost[wave] = pp;
-      wdef[wave] = pd;
-    }
+    for (int d = 1; d < kParts; d <<= 1) pp += __shfl_xor(pp, d, 64);
+    if (lane == 0) wpost[wave] = pp;
     __syncthreads();
     if (threadIdx.x == 0 && a.postings_touched) {
-      uint32_t t = 0, td = 0;
+      uint32_t t = 0;
 #pragma unroll
-      for (int w = 0; w < kMergeWaves; w++) {
-        t += wpost[w];
-        td += wdef[w];
-      }
+      for (int w = 0; w < kMergeWaves; w++) t += wpost[w];
       if (t) atomicAdd(a.postings_touched + 16 + 32 * (blockIdx.x % kPostSpread), t);
-      // deferred postings (k_pf_count's frequent-k-mer deferral): the next word of the same line
-      if (td) atomicAdd(a.postings_touched + 17 + 32 * (blockIdx.x % kPostSpread), td);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nunits = 0;  // the full kernel has read it (stream order)
@@ -1688,18 +1301,9 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
   const int o_l = inc - n_l;
   const int total = __shfl(inc, kParts - 1, 64);
-  // frequent-k-mer deferral (PrefilterArgs::pdm): the part's centroid candidates hold partial counts
-  const uint32_t dm_l = (use_pdm && lane < kParts) ? a.pdm[p0 + lane] : 0u;
-  int thr = 0;
-  if (use_pdm) {
-    const int32_t q = a.q0 + qs / a.both;
-    const int nkq = a.seqs.nk[(int64_t)q * 2 + qs % a.both];
-    thr = nkq < a.minwordmatches ? nkq : a.minwordmatches;
-  }
 #pragma unroll
   for (int l = 0; l < kParts; l++) {
     const int n = __shfl(n_l, l, 64), o = __shfl(o_l, l, 64);
-    const uint32_t dm = (uint32_t)__shfl((int)dm_l, l, 64);
     for (int x = lane; x < n; x += 64) {
       const uint32_t e = a.pcand[(p0 + l) * kPartCand + x];
       unsigned long long key = ~0ull;  // a flagged hit that turned out a member: no candidate
@@ -1712,10 +1316,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
       } else {
         const uint32_t ord = e & 0xffffffu;
         const uint32_t len = a.seqs.lens[a.cent_seqno[ord]];
-        uint32_t cv = e >> 24;
-        if (dm) cv += (uint32_t)__builtin_popcount(a.fmask_ord[ord] & dm);  // the deferred matches
-        if (!dm || cv >= (uint32_t)thr)
-          key = ((unsigned long long)(127u - cv) << 56) | ((unsigned long long)len << 48) | ord;
+        key = ((unsigned long long)(127u - (e >> 24)) << 56) | ((unsigned long long)len << 48) | ord;
       }
       K[o + x] = key;
     }
@@ -1757,20 +1358,9 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   const int ptotal = __shfl(pinc, kParts - 1, 64);
   const int po_l = pinc - np_l;
   const bool povf = over || ptotal > kPeerCap;
-  // strong[seqno * 2 + strand]: the query has an earlier window query sharing >= 5/8 of its k-mers (it is
-  // then all but surely a member, not a centroid: later queries need not align against it speculatively)
-  int pmax = 0;
-  if (!povf && lane < kParts)
-    for (int x = 0; x < np_l; x++) pmax = max(pmax, (int)a.ppeer_count[(p0 + lane) * kPeerCap + x]);
-#pragma unroll
-  for (int d = 1; d < kParts; d <<= 1) pmax = max(pmax, __shfl_xor(pmax, d, 64));
   if (lane == 0) {
     a.ntop[qs] = (uint8_t)min(nvalid, kTopHits);
     a.npeer[qs] = (uint8_t)(povf ? 255 : ptotal);
-    const int32_t q = a.q0 + qs / a.both;
-    const int nkq = a.seqs.nk[(int64_t)q * 2 + qs % a.both];
-    a.strong[(int64_t)q * 2 + qs % a.both] =
-        (uint8_t)(!povf && pmax * 8 >= nkq * a.strong_eighths && pmax > a.minwordmatches);
   }
   if (povf) return;
   uint32_t* P = pkeys[wave];
@@ -1807,31 +1397,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void k_pf_merge(PrefilterArgs a, 
   }
 }
 
-// ------------------------------------------------------------------ frequent k-mers (PrefilterArgs::fmask)
-// + strand k-mer frequencies over every stride-th sequence of a load (one wave per sequence), then per
-// (sequence, strand) the mask of the frequent k-mers (lut[k-mer] = bit or 0xff) it holds (one wave each).
-__global__ __launch_bounds__(256) void k_kmer_hist(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
-                                                   int32_t n, int32_t stride, uint32_t* __restrict__ hist) {
-  const int64_t s = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * stride;
-  const int x = threadIdx.x & 63;
-  if (s >= n) return;
-  const int m = nk[s * 2];
-  const uint16_t* k = kmers + s * 2 * kKmerStride;
-  if (x < m) atomicAdd(&hist[k[x]], 1u);
-  if (x + 64 < m) atomicAdd(&hist[k[x + 64]], 1u);
-}
-__global__ __launch_bounds__(256) void k_fmask(const uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
-                                               int64_t n2, const uint8_t* __restrict__ lut, uint32_t* __restrict__ fmask) {
-  const int64_t ss = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // sequence * 2 + strand (wave-uniform)
-  const int x = threadIdx.x & 63;
-  if (ss >= n2) return;
-  const int m = nk[ss];
-  const uint16_t* k = kmers + ss * kKmerStride;
-  const uint32_t b0 = x < m ? lut[k[x]] : 0xffu, b1 = x + 64 < m ? lut[k[x + 64]] : 0xffu;
-  uint32_t v = (b0 < 32u ? 1u << b0 : 0u) | (b1 < 32u ? 1u << b1 : 0u);
-  v = wave_scan_dpp(v, OpOr());
-  if (x == 63) fmask[ss] = v;
-}
+// ------------------------------------------------------------------ packs: per-bin k-mer scrambling
 __global__ __launch_bounds__(256) void k_kmer_xor(uint16_t* __restrict__ kmers, const uint8_t* __restrict__ nk,
                                                   int64_t n2, const int32_t* __restrict__ bin,
                                                   const uint16_t* __restrict__ xmask) {
@@ -1851,43 +1417,16 @@ hipError_t launch_kmer_xor(uint16_t* kmers, const uint8_t* nk, int32_t n, const 
   hipLaunchKernelGGL(k_kmer_xor, dim3((unsigned)((n2 + 3) / 4)), dim3(256), 0, st, kmers, nk, n2, bin, xmask);
   return hipGetLastError();
 }
-__global__ __launch_bounds__(256) void k_fmask_ord(const uint32_t* __restrict__ fmask, const int32_t* __restrict__ cent,
-                                                   int32_t n, uint32_t* __restrict__ out) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = fmask[(int64_t)cent[i] * 2];
-}
-hipError_t launch_fmask_ord(const uint32_t* fmask, const int32_t* cent, int32_t n, uint32_t* out, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fmask_ord, dim3((n + 255) / 256), dim3(256), 0, st, fmask, cent, n, out);
-  return hipGetLastError();
-}
-hipError_t launch_kmer_hist(const uint16_t* kmers, const uint8_t* nk, int32_t n, int32_t stride, uint32_t* hist,
-                            hipStream_t st) {
-  const int64_t ns = stride > 0 ? ((int64_t)n + stride - 1) / stride : 0;
-  if (ns <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_kmer_hist, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, st, kmers, nk, n, stride, hist);
-  return hipGetLastError();
-}
-hipError_t launch_fmask(const uint16_t* kmers, const uint8_t* nk, int32_t n, const uint8_t* lut, uint32_t* fmask,
-                        hipStream_t st) {
-  const int64_t n2 = (int64_t)n * 2;
-  if (n2 <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fmask, dim3((unsigned)((n2 + 3) / 4)), dim3(256), 0, st, kmers, nk, n2, lut, fmask);
-  return hipGetLastError();
-}
 
 hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   const int nqs = a.nq * a.both;
   if (nqs <= 0) return hipSuccess;
   const int full_most = kPfSharedBytes + kCentBase + kSegCentroids / kParts + 16;
-  // (at least 64 KB: UMICLUST_PFWG pads the counting workgroups' LDS)
-  const int count_most = std::max(65536, kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists) + 16);
+  const int count_most = kCentBase + kSegCentroids / kParts + 16 + (int)pf_count_table_bytes(kPfLists) + 16;
   if (!attr_set_on_device(k_attr_prefilter)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)k_pf_count<0>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_pf_count<1>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
     if (e == hipSuccess)
       e = hipFuncSetAttribute((const void*)k_pf_count<2>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
     if (e != hipSuccess) return e;
@@ -1902,49 +1441,25 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     // lean counting (one counter segment)
     if (a.nseg > 1 || a.nlist_cap < 1 || a.nlist_cap > kPfLists) return hipErrorInvalidValue;
     const uint32_t tab_off = (uint32_t)(kCentBase + sub);
-    // UMICLUST_PFCOUNT: 0 (default) the paired loop, 1 addresses computed a round ahead (pf_count_stream_pre:
-    // measured slower on config 2, 2.13 vs 1.55 ms per launch, profiles/r03/pfcount_ab.json)
-    static const int cm = getenv("UMICLUST_PFCOUNT") ? atoi(getenv("UMICLUST_PFCOUNT")) : 0;
-    // the list tables first (k_pf_table, one wave per unit) when the pass has a table buffer
-    if (a.pftab)
-      hipLaunchKernelGGL(k_pf_table, dim3(nqs * kParts), dim3(64), 0, st, a, a.pftab, nqs * kParts);
     size_t lds = tab_off + pf_count_table_bytes(a.nlist_cap) + 16;  // (+16: the table copy's last vector)
-    // UMICLUST_PFWG=k: pad the workgroup's LDS so that at most k counting workgroups share a CU and the
-    // rest of the CU's LDS (UMICLUST_PFWG_RESERVE bytes, default 16 KB) stays free for alignment waves
-    static const int pfwg = getenv("UMICLUST_PFWG") ? atoi(getenv("UMICLUST_PFWG")) : 0;
-    static const int pfres = getenv("UMICLUST_PFWG_RESERVE") ? atoi(getenv("UMICLUST_PFWG_RESERVE")) : 16384;
-    if (pfwg > 0) {
-      const size_t pad = ((size_t)(160 * 1024 - pfres) / (size_t)pfwg) & ~(size_t)255;
-      if (pad > lds && pad <= 65536) lds = pad;
-    }
     if (mode == 3)  // the timing probe: every phase but the count loop, into scratch outputs (UMICLUST_PFPROBE)
-      hipLaunchKernelGGL(k_pf_count<2>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
-                         (const uint32_t*)a.pftab);
-    else if (cm == 1)
-      hipLaunchKernelGGL(k_pf_count<1>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
-                         (const uint32_t*)a.pftab);
+      hipLaunchKernelGGL(k_pf_count<2>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
     else
-      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off,
-                         (const uint32_t*)a.pftab);
+      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
     if (mode == 1 || mode == 3) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {
     // the full kernel over the units the lean kernel could not finish (exits at once when there are none); its
-    // workgroups loop over the units (UMICLUST_FULL_WG workgroups, default 256: one per CU)
-    static const int full_wg = getenv("UMICLUST_FULL_WG") ? std::max(64, atoi(getenv("UMICLUST_FULL_WG"))) : 256;
-    hipLaunchKernelGGL(k_pf_full, dim3(full_wg), dim3(kPfThreads), smem_full, st, a, 1);
+    // workgroups loop over the units (256: one per CU; 1024 / 2048 measured within noise, round 4 full_wg/)
+    hipLaunchKernelGGL(k_pf_full, dim3(256), dim3(kPfThreads), smem_full, st, a, 1);
   } else {
     hipLaunchKernelGGL(k_pf_full, dim3(nqs * kParts), dim3(kPfThreads), smem_full, st, a, 0);
   }
-  // the lean kernel's candidates (and its per-unit D) exist unless this is a multi-segment whole prefilter
-  const int32_t use_pdm = (a.pdm && a.defer_max > 0 && (mode != 0 || a.nseg <= 1)) ? 1 : 0;
-  hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st,
-                     a, nqs, use_pdm);
+  hipLaunchKernelGGL(k_pf_merge, dim3((nqs + kMergeWaves - 1) / kMergeWaves), dim3(64 * kMergeWaves), 0, st, a, nqs);
   return hipGetLastError();
 }
 
 static AlignFn g_align[kAlignSlots * (kMaxLen + 1)];
-static int g_align_variant0 = 0;
 static std::once_flag g_align_once;
 static void init_align_tables() {
   std::call_once(g_align_once, [] {
@@ -1954,9 +1469,6 @@ static void init_align_tables() {
     fill_align_part3(g_align);
     fill_align_part4(g_align);
     fill_align_part5(g_align);
-    // UMICLUST_ALIGN=scalar selects the one-cell-per-op kernel (cross-checks / benchmarks)
-    const char* v = getenv("UMICLUST_ALIGN");
-    g_align_variant0 = (v && v[0] == 's') ? 1 : 0;
   });
 }
 
@@ -1965,16 +1477,12 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
                         const uint32_t* outidx, const Scoring& sc, uint32_t* out, hipStream_t st,
                         int32_t band_max) {
   init_align_tables();
-  const int variant0 = g_align_variant0;
   if (npairs <= 0) return hipSuccess;
   if (qlen < kMinTplLen || qlen > kMaxLen) return hipErrorInvalidValue;
-  const bool band = !ambig && variant0 == 0 && npairs <= band_max;
+  const bool band = !ambig && npairs <= band_max;
   const int64_t lanes = (int64_t)npairs * (band ? band_lanes(qlen) : 1);
-  const int v = ambig ? 2 : band ? 3 : variant0;
+  const int v = ambig ? 1 : band ? 2 : 0;
   int64_t grid = (lanes + 63) / 64;
-  // UMICLUST_AL_WAVES=w: at most w alignment waves per SIMD in flight (k_align_pk loops; experiment)
-  static const int64_t cap = getenv("UMICLUST_AL_WAVES") ? (int64_t)atoi(getenv("UMICLUST_AL_WAVES")) * 1024 : 0;
-  if (cap > 0 && v == 0) grid = std::min(grid, cap);
   hipLaunchKernelGGL(g_align[kAlignSlots * qlen + v], dim3((unsigned)grid),
                      dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, sc, out);
   return hipGetLastError();
@@ -2126,8 +1634,7 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
                                                     uint32_t* __restrict__ pq, uint32_t* __restrict__ pt,
                                                     uint32_t* __restrict__ outidx, SegTab sg, uint32_t* __restrict__ seg_cnt,
                                                     unsigned long long* __restrict__ cells, uint32_t* __restrict__ nstat,
-                                                    uint32_t out0, const uint8_t* __restrict__ strong,
-                                                    unsigned long long* __restrict__ aligned, int32_t emit,
+                                                    uint32_t out0, unsigned long long* __restrict__ aligned, int32_t emit,
                                                     const WalkState* __restrict__ ws_prev,
                                                     const uint8_t* __restrict__ npeer_prev, int32_t q0_prev,
                                                     int32_t nq_prev) {
@@ -2171,9 +1678,8 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
     const WalkState w = ws[qs];
     for (int x = 0; x < np; x++) {
       const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
-      // relevant, and not predicted to be a member (the host's round B aligns a mispredicted one)
-      if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
-          !(strong && (strong[(int64_t)ps * 2] | strong[(int64_t)ps * 2 + 1])) && !certain_member(ps))
+      // relevant, and not already certain to be a member
+      if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) && !certain_member(ps))
         rel[x >> 6] |= 1ull << (x & 63);
     }
     for (int hh = 0; hh < kPH; hh++) aligned[(int64_t)qs * kPH + hh] = rel[hh];
@@ -2205,11 +1711,11 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, const SegTab& sg,
                              uint32_t* seg_cnt, unsigned long long* cells, uint32_t* nstat, uint32_t out0,
-                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
+                             unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
                              const uint8_t* npeer_prev, int32_t q0_prev, int32_t nq_prev, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
-                     peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, strong, aligned, emit, ws_prev,
+                     peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, aligned, emit, ws_prev,
                      npeer_prev, q0_prev, nq_prev);
   return hipGetLastError();
 }
@@ -2241,15 +1747,10 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
   const int qs0 = ((int)blockIdx.x * kPackWaves + wave) * kPackQ;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // counters[0] = the postings partial sums (k_pf_merge spreads its atomics over kPostSpread lines)
-    // counters[11] = the deferred postings' partial sums (the next word of each line)
     uint32_t v = threadIdx.x < kPostSpread ? counters[16 + 32 * threadIdx.x] : 0u;
-    uint32_t vd = threadIdx.x < kPostSpread ? counters[17 + 32 * threadIdx.x] : 0u;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      v += __shfl_xor(v, d, 64);
-      vd += __shfl_xor(vd, d, 64);
-    }
-    if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : threadIdx.x == 11 ? vd : counters[threadIdx.x];
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d, 64);
+    if (threadIdx.x < 16) hcounters[threadIdx.x] = threadIdx.x == 0 ? v : counters[threadIdx.x];
   }
   constexpr int kH = kPeerCap / 64;  // peers lane, lane + 64, ...
   static_assert(kPackQ * kH <= 32, "relevant / aligned bits per lane");
@@ -2418,21 +1919,17 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
 
-// UMICLUST_TWPROF: sampled waves' shader-clock phase totals (setup, sweep, backtrack) and their count
-__device__ unsigned long long g_twprof[4];
-template <bool kGrouped>
 __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const uint32_t* __restrict__ pq,
                                                               const uint32_t* __restrict__ pt, int32_t npairs,
                                                               Scoring sc, uint8_t* __restrict__ ops,
                                                               uint16_t* __restrict__ nops, uint32_t* __restrict__ out,
-                                                              int32_t maxq, int32_t maxl, int32_t prof) {
+                                                              int32_t maxq, int32_t maxl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tw_smem[];
   // wave-uniform by construction (readfirstlane), so the pair's lengths, the sweep bounds and the backtrack are
   // scalar
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const int k = (int)blockIdx.x * kTwWaves + wave;
   if (k >= npairs) return;  // wave-uniform
-  const unsigned long long c0 = prof ? __builtin_readcyclecounter() : 0ull;
   const TwLayout lay(maxq, maxl);
   struct {
     uint32_t* dir;
@@ -2454,17 +1951,16 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const int tl = s.lens[t], ql = s.lens[q];
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
   const uint32_t* qcp = s.codes + ((int64_t)q * 2 + qstr) * kCodeWords;
-  // kGrouped: the target codes staged one-hot (0 = ambiguous or past the end), so the substitution score is two tests
+  // the target codes staged one-hot (0 = ambiguous or past the end), so the substitution score is two tests
   for (int j = lane; j < tl + 72; j += 64) {
     const uint32_t c = j < tl ? (tcp[j >> 3] >> ((j & 7) * 4)) & 15u : 0u;
-    S.tcode[j] = (uint8_t)(kGrouped ? ((c & (c - 1u)) == 0u ? c : 0u) : c);
-    if (kGrouped && j < tl) S.traw[j] = (uint8_t)c;
+    S.tcode[j] = (uint8_t)((c & (c - 1u)) == 0u ? c : 0u);
+    if (j < tl) S.traw[j] = (uint8_t)c;
   }
   // both sequences' code words in VGPRs (lane w holds word w): the backtrack reads them by v_readlane
   // instead of a global / LDS load per diagonal step
   const uint32_t qword = lane < kCodeWords ? qcp[lane] : 0u, tword = lane < kCodeWords ? tcp[lane] : 0u;
-  if constexpr (kGrouped)
-    for (int i = lane; i < ql; i += 64) S.qraw[i] = (uint8_t)((qcp[i >> 3] >> ((i & 7) * 4)) & 15u);
+  for (int i = lane; i < ql; i += 64) S.qraw[i] = (uint8_t)((qcp[i >> 3] >> ((i & 7) * 4)) & 15u);
   // identical sequences of one-hot codes (a member equal to its centroid: about (1 - error)^L of them): the all-M
   // path is the only optimum -- any other path trades matches for gaps or mismatches -- so its ops, matches and
   // internal length are known without the DP (codes past the length are 0 in both)
@@ -2492,111 +1988,39 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
   const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  const bool pw = prof && (k & 63) == 0;
-  const unsigned long long c1 = pw ? __builtin_readcyclecounter() : 0ull;
   const int nstripe = (ql + 63) >> 6;
   int hend = 0;
-  if constexpr (kGrouped) {
-    // The sweep in groups of 8 steps (one direction word per group, no per-step store test), the diagonal's
-    // column -1 and H(ql - 1, tl - 1) without per-step tests: a lane's H starts as H(i, -1), which the lane below
-    // reads as its diagonal at column 0, and H(ql - 1, tl - 1) is the last H lane (ql - 1) % 64 of the last stripe
-    // kept.  Steps past the stripe's end (to the group's end) touch no live cell.
-    // one sweep per stripe, specialised on the top boundary (stripe 0: computed; later stripes: the previous
-    // stripe's bottom row from LDS) and on whether a stripe follows (lane 63 then stores its row)
-    auto sweep = [&](int st, auto top_c, auto bot_c) {
-      constexpr bool kTop = decltype(top_c)::value, kBot = decltype(bot_c)::value;
-      const int i = st * 64 + lane;
-      const int rows = min(64, ql - st * 64);
-      const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
-      const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-      const uint32_t qm = qamb ? 0u : qcode;
-      const int Mq = qamb ? 0 : sc.match, Xq = qamb ? 0 : sc.mismatch;
-      const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
-      const uint32_t tle = i < ql ? (uint32_t)tl : 0u;  // live columns of this lane
-      int hout = -(sc.go[1] + (i + 1) * sc.ge[1]);      // H(i, -1)
-      int E = sc.boundary_open ? hout - qrq : kNegInf;
-      int Hd = i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1]);  // H(i - 1, -1)
-      int fout = 0;
-      uint32_t tc = 0;
-      const int nsteps = tl + rows - 1;
-      for (int t8 = 0; t8 < nsteps; t8 += 8) {
-        uint32_t dword = 0;
+  // The sweep in groups of 8 steps (one direction word per group, no per-step store test), the diagonal's
+  // column -1 and H(ql - 1, tl - 1) without per-step tests: a lane's H starts as H(i, -1), which the lane below
+  // reads as its diagonal at column 0, and H(ql - 1, tl - 1) is the last H lane (ql - 1) % 64 of the last stripe
+  // kept.  Steps past the stripe's end (to the group's end) touch no live cell.
+  // one sweep per stripe, specialised on the top boundary (stripe 0: computed; later stripes: the previous
+  // stripe's bottom row from LDS) and on whether a stripe follows (lane 63 then stores its row)
+  auto sweep = [&](int st, auto top_c, auto bot_c) {
+    constexpr bool kTop = decltype(top_c)::value, kBot = decltype(bot_c)::value;
+    const int i = st * 64 + lane;
+    const int rows = min(64, ql - st * 64);
+    const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
+    const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
+    const uint32_t qm = qamb ? 0u : qcode;
+    const int Mq = qamb ? 0 : sc.match, Xq = qamb ? 0 : sc.mismatch;
+    const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
+    const uint32_t tle = i < ql ? (uint32_t)tl : 0u;  // live columns of this lane
+    int hout = -(sc.go[1] + (i + 1) * sc.ge[1]);      // H(i, -1)
+    int E = sc.boundary_open ? hout - qrq : kNegInf;
+    int Hd = i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1]);  // H(i - 1, -1)
+    int fout = 0;
+    uint32_t tc = 0;
+    const int nsteps = tl + rows - 1;
+    for (int t8 = 0; t8 < nsteps; t8 += 8) {
+      uint32_t dword = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int tt = t8 + u;
-          int hb, fb;
-          if constexpr (kTop) {
-            hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
-            fb = sc.boundary_open ? hb - ((tt == tl - 1) ? QRtr : QRti) : kNegInf;
-          } else {
-            hb = tt < tl ? S.botH[tt] : 0;
-            fb = tt < tl ? S.botF[tt] : 0;
-          }
-          const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
-          tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
-          const int Hup = sx16(recv), Fin = (int)recv >> 16;
-          const int j = tt - lane;
-          const bool live = (uint32_t)j < tle;
-          const bool lc = j == tl - 1;
-          const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
-          const int sub = (qm & tc) ? Mq : (tc ? Xq : 0);
-          const int diag = Hd + sub;
-          const int m1 = max(diag, Fin);
-          const int h = max(m1, E);
-          const int fo = h - QRt, fe = Fin - Rt;
-          const int eo = h - qrq, ee = E - rq;
-          const uint32_t d = (Fin > diag ? 1u : 0u) | (E > m1 ? 2u : 0u) | (fe > fo ? 4u : 0u) | (ee > eo ? 8u : 0u);
-          E = live ? max(eo, ee) : E;
-          hout = live ? h : hout;
-          fout = live ? max(fo, fe) : fout;
-          if constexpr (kBot) {
-            if (live && lane == 63) {
-              S.botH[j] = hout;
-              S.botF[j] = fout;
-            }
-          }
-          Hd = Hup;
-          dword |= d << (4 * u);
-        }
-        S.dir[(st * TW + (t8 >> 3)) * 64 + lane] = dword;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      return hout;
-    };
-    using T1 = std::integral_constant<bool, true>;
-    using T0 = std::integral_constant<bool, false>;
-    int hlast;
-    if (nstripe == 1) {
-      hlast = sweep(0, T1{}, T0{});
-    } else {
-      sweep(0, T1{}, T1{});
-      for (int st = 1; st + 1 < nstripe; st++) sweep(st, T0{}, T1{});
-      hlast = sweep(nstripe - 1, T0{}, T0{});
-    }
-    hend = __builtin_amdgcn_readlane(hlast, (ql - 1) & 63);
-  } else {
-  const int nstripe = (ql + 63) >> 6;
-    for (int st = 0; st < nstripe; st++) {
-      const int i = st * 64 + lane;
-      const int rows = min(64, ql - st * 64);  // live lanes of the stripe
-      const uint32_t qcode = i < ql ? (qcp[i >> 3] >> ((i & 7) * 4)) & 15u : 0u;
-      const bool qamb = (qcode & (qcode - 1u)) != 0u || qcode == 0u;
-      const int qrq = (i == ql - 1) ? QRqr : QRqi, rq = (i == ql - 1) ? Rqr : Rqi;
-      int Hl = -(sc.go[1] + (i + 1) * sc.ge[1]);  // H(i, -1)
-      int E = sc.boundary_open ? Hl - qrq : kNegInf;
-      int Hd = 0;                                 // H(i-1, j-1) for the next cell
-      int hout = 0, fout = 0;                     // this lane's last cell: H(i, j), F(i+1, j)
-      uint32_t tc = 0, dword = 0;
-      const int nsteps = tl + rows - 1;
-      for (int tt = 0; tt < nsteps; tt++) {
-        const int j = tt - lane;
-        // row above at column tt for lane 0: the top boundary (stripe 0) or the previous stripe's bottom row
+      for (int u = 0; u < 8; u++) {
+        const int tt = t8 + u;
         int hb, fb;
-        if (st == 0) {
+        if constexpr (kTop) {
           hb = -(sc.go[0] + (tt + 1) * sc.ge[0]);
-          const int qrt = (tt == tl - 1) ? QRtr : QRti;
-          fb = sc.boundary_open ? hb - qrt : kNegInf;
+          fb = sc.boundary_open ? hb - ((tt == tl - 1) ? QRtr : QRti) : kNegInf;
         } else {
           hb = tt < tl ? S.botH[tt] : 0;
           fb = tt < tl ? S.botF[tt] : 0;
@@ -2604,181 +2028,129 @@ __global__ __launch_bounds__(64 * kTwWaves) void k_trace_wave(DevSeqs s, const u
         const uint32_t recv = wave_shr1(pack_hf(hout, fout), pack_hf(hb, fb));
         tc = wave_shr1(tc, (uint32_t)S.tcode[tt]);
         const int Hup = sx16(recv), Fin = (int)recv >> 16;
-        const bool live = j >= 0 && j < tl && i < ql;
-        const int hd = (j == 0) ? (i == 0 ? 0 : -(sc.go[1] + i * sc.ge[1])) : Hd;
-        const bool lc = (j == tl - 1);
+        const int j = tt - lane;
+        const bool live = (uint32_t)j < tle;
+        const bool lc = j == tl - 1;
         const int QRt = lc ? QRtr : QRti, Rt = lc ? Rtr : Rti;
-        const bool tamb = (tc & (tc - 1u)) != 0u || tc == 0u;
-        const int sub = (tamb || qamb) ? 0 : (qcode == tc ? sc.match : sc.mismatch);
-        int h = hd + sub;
-        uint32_t d = 0;
-        if (Fin > h) { h = Fin; d |= 1u; }
-        if (E > h) { h = E; d |= 2u; }
+        const int sub = (qm & tc) ? Mq : (tc ? Xq : 0);
+        const int diag = Hd + sub;
+        const int m1 = max(diag, Fin);
+        const int h = max(m1, E);
         const int fo = h - QRt, fe = Fin - Rt;
-        int Fn = fo;
-        if (fe > fo) { Fn = fe; d |= 4u; }
         const int eo = h - qrq, ee = E - rq;
-        int En = eo;
-        if (ee > eo) { En = ee; d |= 8u; }
-        if (live) {
-          Hl = h;
-          E = En;
-          hout = h;
-          fout = Fn;
-          if (i == ql - 1 && j == tl - 1) *S.hendp = h;
-          if (lane == 63 && st + 1 < nstripe) {
-            S.botH[j] = h;
-            S.botF[j] = Fn;
+        const uint32_t d = (Fin > diag ? 1u : 0u) | (E > m1 ? 2u : 0u) | (fe > fo ? 4u : 0u) | (ee > eo ? 8u : 0u);
+        E = live ? max(eo, ee) : E;
+        hout = live ? h : hout;
+        fout = live ? max(fo, fe) : fout;
+        if constexpr (kBot) {
+          if (live && lane == 63) {
+            S.botH[j] = hout;
+            S.botF[j] = fout;
           }
         }
         Hd = Hup;
-        (void)Hl;
-        dword |= d << ((tt & 7) * 4);
-        if ((tt & 7) == 7 || tt == nsteps - 1) {
-          S.dir[(st * TW + (tt >> 3)) * 64 + lane] = dword;
-          dword = 0;
-        }
+        dword |= d << (4 * u);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
+      S.dir[(st * TW + (t8 >> 3)) * 64 + lane] = dword;
     }
-    hend = *S.hendp;
-  }
-  uint8_t* o = ops + (int64_t)k * kOpsStride;
-  const unsigned long long c2 = pw ? __builtin_readcyclecounter() : 0ull;
-  if constexpr (kGrouped) {
-    // backtrack16 from (ql-1, tl-1) by runs, the wave deciding up to 64 steps at once: from a cell reached by a
-    // diagonal step (or the start) the path continues diagonally while the cells say neither up nor left -- lane x
-    // reads cell (i - x, j - x), a ballot gives the run; after an I (D) step it continues left (up) while the cells'
-    // extension bits say so -- lane x reads (i, j - x) ((i - x, j)).  A run's ops are stored by its lanes; the
-    // counters, states and align_trim's runs (the first run generated is the alignment's last, the last one its
-    // first) are scalar.  Same decisions as the per-cell loop below, cell for cell.
-    auto nib = [&](int ii, int jj) -> uint32_t {
-      const int l = ii & 63, tt = jj + l;
-      return (S.dir[((ii >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
-    };
-    int n = 0, i = ql - 1, j = tl - 1, matches = 0;
-    uint32_t first_op = 0, run_op = 0;
-    int first_run = 0, run_len = 0;
-    bool first_open = true;
-    auto emit_run = [&](uint32_t c, int r) {  // r >= 1 ops c (wave-uniform)
-      if (lane < r) o[kOpsStride - 1 - (n + lane)] = (uint8_t)c;
-      if (n == 0) first_op = c;
-      if (first_open) {
-        if (c == first_op) first_run += r;
-        else first_open = false;
-      }
-      run_len = c == run_op ? run_len + r : r;
-      run_op = c;
-      n += r;
-    };
-    enum { kFresh = 0, kInI = 1, kInD = 2 };
-    int state = kFresh;
-    while (i >= 0 && j >= 0) {
-      if (state == kFresh) {
-        const int ii = i - lane, jj = j - lane;
-        const bool valid = ii >= 0 && jj >= 0;
-        const uint32_t d = valid ? nib(ii, jj) : 3u;
-        const unsigned long long stop = __ballot((d & 3u) != 0u);  // invalid cells stop the run too
-        const int r = stop ? __builtin_ctzll(stop) : 64;
-        if (r > 0) {
-          const bool m = lane < r && (S.qraw[valid ? ii : 0] & S.traw[valid ? jj : 0]) != 0;
-          matches += __builtin_popcountll(__ballot(m));
-          emit_run('M', r);
-          i -= r;
-          j -= r;
-        } else {
-          const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
-          if (d0 & 2u) {
-            emit_run('I', 1);
-            j--;
-            state = kInI;
-          } else {
-            emit_run('D', 1);
-            i--;
-            state = kInD;
-          }
-        }
-      } else if (state == kInI) {
-        const int jj = j - lane;
-        const uint32_t d = jj >= 0 ? nib(i, jj) : 0u;
-        const unsigned long long stop = __ballot((d & 8u) == 0u);
-        const int r = stop ? __builtin_ctzll(stop) : 64;
-        if (r > 0) {
-          emit_run('I', r);
-          j -= r;
-        }
-        if (r < 64) state = kFresh;
-      } else {
-        const int ii = i - lane;
-        const uint32_t d = ii >= 0 ? nib(ii, j) : 0u;
-        const unsigned long long stop = __ballot((d & 4u) == 0u);
-        const int r = stop ? __builtin_ctzll(stop) : 64;
-        if (r > 0) {
-          emit_run('D', r);
-          i -= r;
-        }
-        if (r < 64) state = kFresh;
-      }
-    }
-    for (; i >= 0; i -= 64) emit_run('D', min(i + 1, 64));
-    for (; j >= 0; j -= 64) emit_run('I', min(j + 1, 64));
-    if (lane != 0) return;
-    if (pw) {
-      const unsigned long long c3 = __builtin_readcyclecounter();
-      atomicAdd(&g_twprof[0], c1 - c0);
-      atomicAdd(&g_twprof[1], c2 - c1);
-      atomicAdd(&g_twprof[2], c3 - c2);
-      atomicAdd(&g_twprof[3], 1ull);
-    }
-    nops[k] = (uint16_t)n;
-    const int tlft = run_op != 'M' ? run_len : 0;
-    const int trgt = (first_op != 'M' && tlft < n) ? first_run : 0;
-    const uint32_t internal = (uint32_t)(n - tlft - trgt);
-    out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)hend & 0xffffu) << 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    return hout;
+  };
+  using T1 = std::integral_constant<bool, true>;
+  using T0 = std::integral_constant<bool, false>;
+  int hlast;
+  if (nstripe == 1) {
+    hlast = sweep(0, T1{}, T0{});
   } else {
-    if (lane != 0) return;
-    // backtrack16 from (ql-1, tl-1): diagonal unless the cell took up (D) / left (I); a run continues while
-    // the cell's extension bit says the gap was extended
-    int n = 0, i = ql - 1, j = tl - 1, aligned = 0, matches = 0;
-    uint32_t op = 0;
-    while (i >= 0 && j >= 0) {
-      aligned++;
-      const int l = i & 63, tt = j + l;
-      const uint32_t d = (S.dir[((i >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
-      if (op == 'I' && (d & 8u)) {
-        j--;
-      } else if (op == 'D' && (d & 4u)) {
-        i--;
-      } else if (d & 2u) {
-        j--;
-        op = 'I';
-      } else if (d & 1u) {
-        i--;
-        op = 'D';
-      } else {
-        const uint32_t qc = ((uint32_t)__builtin_amdgcn_readlane((int)qword, i >> 3) >> ((i & 7) * 4)) & 15u;
-        const uint32_t tc = ((uint32_t)__builtin_amdgcn_readlane((int)tword, j >> 3) >> ((j & 7) * 4)) & 15u;
-        if (qc & tc) matches++;
-        i--;
-        j--;
-        op = 'M';
-      }
-      o[kOpsStride - 1 - n] = (uint8_t)op;
-      n++;
-    }
-    while (i >= 0) { aligned++; i--; o[kOpsStride - 1 - n] = 'D'; n++; }
-    while (j >= 0) { aligned++; j--; o[kOpsStride - 1 - n] = 'I'; n++; }
-    nops[k] = (uint16_t)n;
-    // align_trim: the first and the last op runs, if gaps, are terminal (alignment order)
-    const uint8_t* a0 = o + kOpsStride - n;
-    int tlft = 0, trgt = 0;
-    if (a0[0] != 'M') { while (tlft < n && a0[tlft] == a0[0]) tlft++; }
-    if (a0[n - 1] != 'M') { while (trgt < n && a0[n - 1 - trgt] == a0[n - 1]) trgt++; }
-    if (tlft >= aligned) trgt = 0;
-    const uint32_t internal = (uint32_t)(aligned - tlft - trgt);
-    out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)hend & 0xffffu) << 16);
+    sweep(0, T1{}, T1{});
+    for (int st = 1; st + 1 < nstripe; st++) sweep(st, T0{}, T1{});
+    hlast = sweep(nstripe - 1, T0{}, T0{});
   }
+  hend = __builtin_amdgcn_readlane(hlast, (ql - 1) & 63);
+  uint8_t* o = ops + (int64_t)k * kOpsStride;
+  // backtrack16 from (ql-1, tl-1) by runs, the wave deciding up to 64 steps at once: from a cell reached by a
+  // diagonal step (or the start) the path continues diagonally while the cells say neither up nor left -- lane x
+  // reads cell (i - x, j - x), a ballot gives the run; after an I (D) step it continues left (up) while the cells'
+  // extension bits say so -- lane x reads (i, j - x) ((i - x, j)).  A run's ops are stored by its lanes; the
+  // counters, states and align_trim's runs (the first run generated is the alignment's last, the last one its
+  // first) are scalar.  Same decisions as the per-cell loop below, cell for cell.
+  auto nib = [&](int ii, int jj) -> uint32_t {
+    const int l = ii & 63, tt = jj + l;
+    return (S.dir[((ii >> 6) * TW + (tt >> 3)) * 64 + l] >> ((tt & 7) * 4)) & 15u;
+  };
+  int n = 0, i = ql - 1, j = tl - 1, matches = 0;
+  uint32_t first_op = 0, run_op = 0;
+  int first_run = 0, run_len = 0;
+  bool first_open = true;
+  auto emit_run = [&](uint32_t c, int r) {  // r >= 1 ops c (wave-uniform)
+    if (lane < r) o[kOpsStride - 1 - (n + lane)] = (uint8_t)c;
+    if (n == 0) first_op = c;
+    if (first_open) {
+      if (c == first_op) first_run += r;
+      else first_open = false;
+    }
+    run_len = c == run_op ? run_len + r : r;
+    run_op = c;
+    n += r;
+  };
+  enum { kFresh = 0, kInI = 1, kInD = 2 };
+  int state = kFresh;
+  while (i >= 0 && j >= 0) {
+    if (state == kFresh) {
+      const int ii = i - lane, jj = j - lane;
+      const bool valid = ii >= 0 && jj >= 0;
+      const uint32_t d = valid ? nib(ii, jj) : 3u;
+      const unsigned long long stop = __ballot((d & 3u) != 0u);  // invalid cells stop the run too
+      const int r = stop ? __builtin_ctzll(stop) : 64;
+      if (r > 0) {
+        const bool m = lane < r && (S.qraw[valid ? ii : 0] & S.traw[valid ? jj : 0]) != 0;
+        matches += __builtin_popcountll(__ballot(m));
+        emit_run('M', r);
+        i -= r;
+        j -= r;
+      } else {
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+        if (d0 & 2u) {
+          emit_run('I', 1);
+          j--;
+          state = kInI;
+        } else {
+          emit_run('D', 1);
+          i--;
+          state = kInD;
+        }
+      }
+    } else if (state == kInI) {
+      const int jj = j - lane;
+      const uint32_t d = jj >= 0 ? nib(i, jj) : 0u;
+      const unsigned long long stop = __ballot((d & 8u) == 0u);
+      const int r = stop ? __builtin_ctzll(stop) : 64;
+      if (r > 0) {
+        emit_run('I', r);
+        j -= r;
+      }
+      if (r < 64) state = kFresh;
+    } else {
+      const int ii = i - lane;
+      const uint32_t d = ii >= 0 ? nib(ii, j) : 0u;
+      const unsigned long long stop = __ballot((d & 4u) == 0u);
+      const int r = stop ? __builtin_ctzll(stop) : 64;
+      if (r > 0) {
+        emit_run('D', r);
+        i -= r;
+      }
+      if (r < 64) state = kFresh;
+    }
+  }
+  for (; i >= 0; i -= 64) emit_run('D', min(i + 1, 64));
+  for (; j >= 0; j -= 64) emit_run('I', min(j + 1, 64));
+  if (lane != 0) return;
+  nops[k] = (uint16_t)n;
+  const int tlft = run_op != 'M' ? run_len : 0;
+  const int trgt = (first_op != 'M' && tlft < n) ? first_run : 0;
+  const uint32_t internal = (uint32_t)(n - tlft - trgt);
+  out[k] = (uint32_t)matches | (internal << 8) | (((uint32_t)hend & 0xffffu) << 16);
 }
 
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
@@ -2788,24 +2160,9 @@ hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t
   if (maxl < 1 || maxl > kMaxLen) return hipErrorInvalidValue;
   if (maxq <= 0 || maxq > maxl) maxq = maxl;
   const TwLayout lay(maxq, maxl);
-  // UMICLUST_TRACE=step: the sweep with per-step tests (the round-3 loop), for A/B
-  static const bool grouped = !(getenv("UMICLUST_TRACE") && strcmp(getenv("UMICLUST_TRACE"), "step") == 0);
-  static const int32_t prof = getenv("UMICLUST_TWPROF") ? 1 : 0;
-  if (grouped)
-    hipLaunchKernelGGL(k_trace_wave<true>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
-                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxq, maxl, prof);
-  else
-    hipLaunchKernelGGL(k_trace_wave<false>, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
-                       (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxq, maxl, prof);
+  hipLaunchKernelGGL(k_trace_wave, dim3((npairs + kTwWaves - 1) / kTwWaves), dim3(64 * kTwWaves),
+                     (size_t)lay.wave_bytes * kTwWaves, st, s, pq, pt, npairs, sc, ops, nops, out, maxq, maxl);
   return hipGetLastError();
-}
-hipError_t traceback_profile(unsigned long long out[4], bool reset) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_twprof), sizeof(unsigned long long) * 4);
-  if (e == hipSuccess && reset) {
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_twprof), z, sizeof z);
-  }
-  return e;
 }
 
 // ------------------------------------------------------------------ K4: consensus

@@ -351,7 +351,7 @@ int resolve_block(const ResolveEnv& env, int32_t q0, int32_t nq, int32_t w0, con
     }
     return true;
   };
-  if (env.debug && getenv("UMICLUST_DEBUG_CLASSES")) {
+  if (env.debug) {
     const uint32_t inb = (uint32_t)(q0 - w0);
     for (int32_t ql = 0; ql < nq; ql++) {
       int cls = 0;

@@ -6,7 +6,6 @@
 namespace uc {
 
 constexpr int kMaxLen = 112;         // longest supported UMI (UMICLUST_MAX_LEN; config 5 needs 110)
-constexpr int kShortLen = 72;        // longest length with the one-cell-per-op cross-check aligner
 constexpr int kMinTplLen = 32;       // shortest query length with a compiled aligner
 constexpr int kCodeWords = kMaxLen / 8;  // 4-bit codes, 8 residues per u32
 constexpr int kMaxKmers = kMaxLen - 8 + 1;  // unique 8-mers per strand <= 105

@@ -36,17 +36,9 @@ hipError_t launch_iota(int32_t* out, int32_t n, hipStream_t st);
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
                        char* masked, uint32_t* ambig, hipStream_t st);
-// frequent k-mers of a load (PrefilterArgs::fmask): + strand k-mer counts of every stride-th sequence into
-// hist[65536] (zero on entry); then fmask[s * 2 + strand] = the bits lut[k-mer] (< 32; 0xff = none) it holds
-hipError_t launch_kmer_hist(const uint16_t* kmers, const uint8_t* nk, int32_t n, int32_t stride, uint32_t* hist,
-                            hipStream_t st);
-hipError_t launch_fmask(const uint16_t* kmers, const uint8_t* nk, int32_t n, const uint8_t* lut, uint32_t* fmask,
-                        hipStream_t st);
 // XOR every k-mer of sequence s (both strands) with xmask[bin[s]] (packs: a bijection per bin)
 hipError_t launch_kmer_xor(uint16_t* kmers, const uint8_t* nk, int32_t n, const int32_t* bin, const uint16_t* xmask,
                            hipStream_t st);
-// out[i] = fmask[cent[i] * 2] (the + strand masks of centroid ordinals, PrefilterArgs::fmask_ord)
-hipError_t launch_fmask_ord(const uint32_t* fmask, const int32_t* cent, int32_t n, uint32_t* out, hipStream_t st);
 // index tile build over sequences c in [0, count) with seqno map[first + c] and ordinal
 // x = xoff + c (centroid tiles: the centroid ordinal; peer tiles: c): count (hist[kBins], all zero
 // on entry), scan (padded offsets off[kBins+1], fill cursors, padding postings written into post,
@@ -71,15 +63,6 @@ constexpr int kSegLens = 32;  // query lengths one greedy block may span
 constexpr int kSegSlot = kUnitsSlot + 32;
 constexpr int kCountersLen = kSegSlot + 3 * kSegLens;
 constexpr int kPfWinBase = 128;   // k_pf_count: windows whose base list and start mask are tabulated (the rest: search)
-// k_pf_table's per-unit image of k_pf_count's LDS list table (kernels.hip): header (4 words), then wtab (uint4 x
-// kPfWinBase: base list, start bits 0-31, 32-63, 0), lstart (nlist_cap + 66), lbias (nlist_cap)
-__host__ __device__ constexpr uint32_t pf_table_img_words(int nlist_cap) {
-  return (uint32_t)(4 * kPfWinBase + 2 * nlist_cap + 66);
-}
-__host__ __device__ constexpr uint32_t pf_table_stride(int nlist_cap) {
-  return (4u + pf_table_img_words(nlist_cap) + 3u) & ~3u;
-}
-constexpr int kFKmers = 32;  // frequent k-mers of a load eligible for deferral (PrefilterArgs::fkmer)
 // centroid tile views passed in the kernel arguments (a pass reads them by scalar loads either way; in the arguments
 // they need no host-to-device copy, a blit dispatch between every two counting launches)
 constexpr int kArgTiles = 32;
@@ -135,35 +118,18 @@ struct PrefilterArgs {
   uint16_t* peer_id;       // [nqs*kPeerCap] window-local (seqno - peer_base)
   uint8_t* peer_count;     // [nqs*kPeerCap]
   uint8_t* npeer;          // [nqs] (255 = overflow)
-  uint8_t* strong;         // [seqno * 2 + strand] the query has a near-identical earlier window query
-  int32_t strong_eighths;  // ... sharing >= strong_eighths / 8 of its k-mers
   uint32_t* postings_touched;  // counters[0]; the merge adds into kPostSpread slots 128 B apart after
                                // counters[16], which k_pack sums into the host copy of counters[0]
   unsigned long long* prof;    // [9] optional phase clocks of sampled workgroups (see k_prefilter), then their count
-  // Frequent-k-mer deferral (k_pf_count + k_pf_merge; exact).  F = fkmer[0..kFKmers), the load's most frequent
-  // + strand k-mers, most frequent first; fmask[seqno * 2 + strand] bit b = that strand's unique k-mers hold
-  // fkmer[b].  A query-strand defers D = the (at most defer_max) lowest bits of its own mask: their posting lists
-  // in the centroid tiles are not streamed, so a centroid counter misses at most |D| and the counters >= thr - |D|
-  // are the only possible candidates; the merge adds popcount(fmask_ord[ordinal] & D) to each and drops the ones
-  // still < thr.  defer_max = 0 turns it off; thr - |D| stays >= defer_min_thr.
   // Packs (umiclust_cluster_pack: several bins in one greedy order, their k-mers XOR-scrambled per bin so other
   // bins' postings are sparse noise): query q of load bin qbin[q] takes centroid candidates only from ordinals >=
   // bin_ord0[bin] (INT32_MAX until the bin's first centroid is indexed) and peers / flagged hits only from
   // seqnos >= bin_seq0[bin]; k_pf_full keys centroids by cent_len (lengths are not monotone in the ordinal across
   // bins).  qbin == nullptr: one bin.
-  uint32_t* pftab;  // [nqs*kParts x pf_table_stride(nlist_cap)] k_pf_table's list tables (null: k_pf_count builds its own)
   const int32_t* qbin;
   const int32_t* bin_seq0;
   const int32_t* bin_ord0;
   const uint8_t* cent_len;
-  const uint32_t* fmask;
-  const uint32_t* fmask_ord;  // [ordinal] fmask of centroid ordinal's + strand (fmask[cent_seqno[o] * 2])
-  uint32_t* pdef;            // [nqs*kParts] postings of the deferred lists (chunks x 8, incl. list padding)
-  uint32_t* pdm;             // [nqs*kParts] D of the unit's candidates for k_pf_merge (0: exact, e.g. the full
-                             // kernel's); centroid candidates then hold partial counts >= thr - |D|
-  int32_t defer_max;
-  int32_t defer_min_thr;
-  uint16_t fkmer[kFKmers];
 };
 // two kernels: the per-part counting/selection (grid nqs*kParts) and the per-query-strand merge
 // mode 0: the whole prefilter (lean counting + the full kernel over its overflowed units, or the full
@@ -215,7 +181,7 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              const WalkState* ws, const uint16_t* peer_id, const uint8_t* peer_count,
                              const uint8_t* npeer, uint32_t* pq, uint32_t* pt, uint32_t* outidx, const SegTab& sg,
                              uint32_t* seg_cnt, unsigned long long* cells, uint32_t* nstat, uint32_t out0,
-                             const uint8_t* strong, unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
+                             unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
                              const uint8_t* npeer_prev, int32_t q0_prev, int32_t nq_prev, hipStream_t st);
 hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkState* ws, const uint8_t* ntop,
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
@@ -229,7 +195,6 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
 hipError_t launch_traceback(const DevSeqs& s, const uint32_t* pq, const uint32_t* pt, int32_t npairs,
                             const Scoring& sc, uint8_t* ops, uint16_t* nops, uint32_t* out, hipStream_t st,
                             int32_t maxl, int32_t maxq = 0);
-hipError_t traceback_profile(unsigned long long out[4], bool reset);  // UMICLUST_TWPROF phase clocks
 // consensus: cluster c members member_seqno[cstart[c] .. cstart[c+1]) (centroid first),
 // member_ops index per member (-1 for centroid), member strand.
 hipError_t launch_consensus(const DevSeqs& s, const int32_t* cstart, int32_t nclusters,

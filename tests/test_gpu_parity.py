@@ -237,35 +237,6 @@ def test_pipeline_modes(split, block, monkeypatch):
     assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-@pytest.mark.parametrize("defer", ["1", "4"])
-def test_kmer_deferral(defer, split, monkeypatch):
-    """The lean counting kernel's frequent-k-mer deferral (PrefilterArgs::fmask): a query-strand skips the posting
-    lists of up to UMICLUST_DEFER of its most frequent k-mers and adds them per surviving target -- membership,
-    strands, centroids, consensus, alignments and cells equal the oracle's; the postings it streams plus the
-    deferred lists cover exactly what the undeferred count streams (deferred lists are counted with their
-    padding, <= 7 postings per list)."""
-    u = synth.make_umis(300, seed=27, max_reads=4000, orient_mix=0.2)
-    seqs = u.as_list()
-    monkeypatch.setenv("UMICLUST_BLOCK", "512")
-    monkeypatch.setenv("UMICLUST_SPLIT", split)
-    o = orc.cluster(orc.params(1, 0.90, 58, 68), seqs)
-    out = {}
-    for d in ("0", defer):
-        monkeypatch.setenv("UMICLUST_DEFER", d)
-        with _lib.Context(0) as ctx:
-            ctx.load(_lib.params(1, 0.90, 58, 68), seqs)
-            st = ctx.cluster()
-            g = ctx.fetch()
-        _cmp_cluster(g, o)
-        assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
-        out[d] = st
-    s0, sd = out["0"], out[defer]
-    assert s0["kmer_postings_deferred"] == 0
-    assert sd["kmer_postings_deferred"] > 0 and sd["kmer_postings"] < s0["kmer_postings"]
-    assert sd["kmer_postings"] + sd["kmer_postings_deferred"] >= s0["kmer_postings"]
-
-
 def _ragged_lengths(seed, n_mol=40, max_reads=3000):
     """Long high-error UMIs cut to random lengths 40..112: bins whose blocks span many query lengths."""
     u = synth.make_umis(n_mol, seed=seed, max_reads=max_reads, orient_mix=0.2, mean_reads=80.0, error_rate=0.05,
@@ -319,9 +290,8 @@ def test_pipeline_modes_deep_clusters(split, monkeypatch):
 
 @pytest.mark.parametrize("lanes", [3])
 def test_lanes_with_overflowing_bin(lanes, monkeypatch):
-    """Several lanes, two of whose bins overflow their peer lists (deep clusters), with UMICLUST_EXCL=1: the first
-    overflowing bin takes the GPU for the rest of its run (exclusive re-runs, the other lanes hold at their block boundaries; a second
-    overflowing bin waits for it), and every bin's membership, strands, centroids and consensus equal the oracle's."""
+    """Several lanes, two of whose bins overflow their peer lists (deep clusters: synchronous re-runs while the other
+    lanes keep clustering), and every bin's membership, strands, centroids and consensus equal the oracle's."""
     from umiclust import binset
     deep = lambda seed: synth.make_umis(6, seed=seed, max_reads=1800, orient_mix=0.3, mean_reads=1500.0,  # noqa: E731
                                         error_rate=0.15, split=(0.0, 0.5, 0.5), max_edits=4,
@@ -331,7 +301,6 @@ def test_lanes_with_overflowing_bin(lanes, monkeypatch):
     sets = [deep(51), plain(52), deep(53), plain(54), plain(55)]
     bs = synth.concat_bins([synth.Bin(0, i, i, 0, u) for i, u in enumerate(sets)])
     monkeypatch.setenv("UMICLUST_BLOCK", "1024")
-    monkeypatch.setenv("UMICLUST_EXCL", "1")
     with _lib.Context(0) as ctx:
         run = binset.BinRunner(ctx, bs, 1, 0.75, 80, 110, lanes=lanes)
         st = run.cluster_all()
@@ -341,37 +310,6 @@ def test_lanes_with_overflowing_bin(lanes, monkeypatch):
     for u, r in zip(sets, res):
         o = orc.cluster(orc.params(1, 0.75, 80, 110), u.as_list())
         assert binset.digest(r) == binset.digest(o)
-
-
-@pytest.mark.parametrize("early", ["0.3", "0.75"])
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_early_member_traceback(early, split, monkeypatch):
-    """UMICLUST_TRACE_EARLY: the members of the first blocks are traced on a stream of their own while the later blocks
-    are clustered; membership, strands, centroids, consensus and the alignment count equal the oracle's (deep clusters
-    with overflow re-runs after the early launch, and a config-2-like sample with many blocks)."""
-    monkeypatch.setenv("UMICLUST_TRACE_EARLY", early)
-    monkeypatch.setenv("UMICLUST_SPLIT", split)
-    u = synth.make_umis(8, seed=31, max_reads=2500, orient_mix=0.3, mean_reads=1500.0, error_rate=0.15,
-                        split=(0.0, 0.5, 0.5), max_edits=4, pattern_fwd=synth.UMI_FWD_LONG,
-                        pattern_rev=synth.UMI_REV_LONG)
-    monkeypatch.setenv("UMICLUST_BLOCK", "1024")
-    seqs = u.as_list()
-    with _lib.Context(0) as ctx:
-        ctx.load(_lib.params(1, 0.75, 80, 110), seqs)
-        st = ctx.cluster()
-        g = ctx.fetch()
-    o = orc.cluster(orc.params(1, 0.75, 80, 110), seqs)
-    _cmp_cluster(g, o)
-    assert st["n_alignments"] == o["stats"]["alignments"]
-    monkeypatch.setenv("UMICLUST_BLOCK", "512")
-    v = synth.make_umis(3000, seed=77, max_reads=30000).as_list()
-    with _lib.Context(0) as ctx:
-        ctx.load(_lib.params(1, 0.9, 58, 68), v)
-        st = ctx.cluster()
-        g = ctx.fetch()
-    o = orc.cluster(orc.params(1, 0.9, 58, 68), v)
-    _cmp_cluster(g, o)
-    assert st["n_alignments"] == o["stats"]["alignments"] and st["n_blocks"] > 20
 
 
 @pytest.mark.parametrize("split", ["0", "1"])
