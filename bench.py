@@ -355,13 +355,16 @@ def main() -> None:
     ap.add_argument("--shard-sweep", type=int, default=0,
                     help="configs 3/4, one GPU: time every LPT share of an N-GPU node one after another (plus the largest "
                          "bin alone) in one process; the largest share time is the measured N-GPU makespan bound")
+    ap.add_argument("--no-confine", action="store_true",
+                    help="--shard-sweep: do not confine the process to 1/N of the host CPUs")
     ap.add_argument("--e2e-files", action="store_true",
                     help="config 4 at the file boundary: per-bin FASTA inputs, round 1 through the fused drop-in "
                          "(clustering + parse outputs), round-2 FASTA from its consensus, round 2 to files, every bin "
                          "on `lanes` concurrent contexts (tcr_consensus.py:231-267, :411-446)")
-    ap.add_argument("--read-len", type=int, default=32,
-                    help="--e2e-files: length of the synthetic full read in each header's seq= field (SURVEY §8d "
-                         "--short-read: 32 keeps 70M records at ~19 GB; production reads are ~1,500 nt)")
+    ap.add_argument("--read-len", type=int, default=800,
+                    help="--e2e-files: length of the synthetic full read in each header's seq= field (production reads "
+                         "are ~1,500 nt, SURVEY §8d; 800 is the longest whose 70M-record inputs and round-1 outputs fit "
+                         "the GPU box's ~270 GiB host-memory cap on /dev/shm; 32 = SURVEY's --short-read)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -700,8 +703,8 @@ def e2e_files(args) -> None:
                     if rnd == 1:
                         st, pr = ctxs[li].run_fasta_parse(p1, in1[i], None, os.path.join(d, "umi_clusters_consensus.fasta"),
                                                           os.path.join(d, "vsearch_cluster.log"), pp1, d)
-                    else:
-                        st, pr = ctxs[li].run_fasta_parse(p2, in2[i], os.path.join(d, "cluster"),
+                    else:  # f2 in round 2 as well: the cluster<N> files only feed parse_umi_clusters (tcr_consensus.py:433-446)
+                        st, pr = ctxs[li].run_fasta_parse(p2, in2[i], None,
                                                           os.path.join(d, "umi_clusters_consensus.fasta"),
                                                           os.path.join(d, "vsearch_cluster_consensus.log"), pp2, d)
                     per[i] = dict(seconds=time.perf_counter() - t, kept=st["n_kept"], clusters=st["n_clusters"],
@@ -723,6 +726,15 @@ def e2e_files(args) -> None:
                         files_written=nf, bytes_written=nb), per
         r1, per1 = run_round(1)
         _progress(f"e2e-files: round 1 {r1['wall_s']:.1f} s, {r1['umis_per_s'] / 1e6:.2f} M UMIs/s")
+        shm_peak = _fs_used(root)
+        # round 1's clusters_fa/ and smolecule_clusters.fa go to medaka, not to round 2: freed (untimed) so that the
+        # round-2 inputs fit beside the rest in RAM-backed storage
+        for d in dirs:
+            shutil.rmtree(os.path.join(d, "round1", "clusters_fa"), ignore_errors=True)
+            try:
+                os.remove(os.path.join(d, "round1", "smolecule_clusters.fa"))
+            except OSError:
+                pass
         # round-2 inputs from round 1's consout (untimed: medaka + extract_umis stand-in)
         t0 = time.perf_counter()
         b2 = []
@@ -748,6 +760,7 @@ def e2e_files(args) -> None:
                                       + f", both rounds, {args.read_len}-nt seq= reads",
                           "parallelism": f"one MI355X, {lanes} concurrent per-bin contexts", "output_dir": base},
                "round1": r1, "round2": r2, "input_bytes": [bytes1, bytes2], "input_write_s": [t_gen1, t_gen2],
+               "storage_used_after_round1_bytes": shm_peak, "read_len": args.read_len,
                "note": "value = UMIs of both rounds / (round-1 wall + round-2 wall), each from its first FASTA read to "
                        "its last file; inputs written untimed; RAM-backed output_dir when /dev/shm has room"}
         print(json.dumps(out), flush=True)
@@ -761,11 +774,15 @@ def shard_sweep(args) -> None:
     another, each timed over one full step (stage untimed; prepare + cluster of every round timed), after an untimed
     warm-up of the first share.  The largest share time is the makespan bound of an N-GPU node (each rank runs its
     share on its own GPU, no collective); the largest bin alone bounds any split of the bins."""
-    import torch
     from umiclust import _lib, binset, shard, synth
     if args.config not in (3, 4):
         raise SystemExit("--shard-sweep: configs 3 and 4")
     N = args.shard_sweep
+    # host confinement, before anything touches the GPU: an N-GPU node gives each rank 1/N of the host's logical CPUs
+    # (one process per GPU), so the share runs on 1/N of this process's affinity mask -- whole physical cores with
+    # their SMT siblings, one NUMA node -- and the resolve pool is capped by that mask (driver.cpp pool_threads)
+    confine = _confine_to_node_share(N) if not args.no_confine else None
+    import torch
     ident = args.identity if args.identity is not None else 0.93
     lens = synth.CONFIG_LENGTHS[args.config]
     all_bins = synth.config_bins(args.config, args.scale, workers=min(16, os.cpu_count() or 4))
@@ -813,26 +830,81 @@ def shard_sweep(args) -> None:
     big = run([largest])
     tmax = max(x["seconds"] for x in shares)
     node_umis = sum(x["umis_kept"] for x in shares)
-    out = {"metric": METRIC, "value": node_umis / tmax, "unit": "UMIs/s", "n_gpus": N, "steps": 1, "warmup": 1,
-           "ms_per_step": 1e3 * tmax, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+    # measured on ONE GPU: `value` is this GPU's rate over the shares it ran; the N-GPU node figure is a model
+    # (every share on its own GPU at the time measured here, host confined as above), reported apart
+    tsum = sum(x["seconds"] for x in shares)
+    out = {"metric": METRIC, "value": node_umis / tsum, "unit": "UMIs/s", "n_gpus": 1, "steps": 1, "warmup": 1,
+           "ms_per_step": 1e3 * tsum, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
            "dtype": "int16/int32", "data": "synthetic",
            "config": {"workload": f"BASELINE config {args.config} at scale {args.scale}: every LPT share of an {N}-GPU "
                                   "node clustered alone on one MI355X, one after another",
-                      "parallelism": f"{N} shares (shard.lpt_assign), each timed alone; value = the node's UMIs / the "
-                                     "largest share's time (the makespan of N GPUs running their shares at once)",
-                      "lanes": args.lanes, "pack_reads": args.pack_reads},
-           "shares": shares, "makespan_s": tmax, "sum_s": sum(x["seconds"] for x in shares),
+                      "parallelism": f"{N} shares (shard.lpt_assign), each timed alone on one GPU",
+                      "policy": policy_name(args.threads), "lanes": args.lanes, "pack_reads": args.pack_reads,
+                      "host_confinement": confine},
+           "node_bound_model": {"n_gpus": N, "value": node_umis / tmax, "unit": "UMIs/s", "makespan_s": tmax,
+                                "note": f"a model, not a measurement: the node's UMIs / the largest share's time, as if "
+                                        f"{N} GPUs ran their shares at once, each rank on 1/{N} of the host "
+                                        "(host_confinement); no N-GPU run was made"},
+           "shares": shares, "makespan_s": tmax, "sum_s": tsum,
            "largest_bin": dict(big, bin=largest), "measured_on": "one GPU"}
     if len(pick) < N:  # a subset of the shares: no node figure
-        out.update(value=None, partial_shares=pick)
+        out.update(partial_shares=pick)
+        out["node_bound_model"]["value"] = None
     print(json.dumps(out), flush=True)
     ctx.close()
     if ctx2 is not None:
         ctx2.close()
 
 
+def _confine_to_node_share(n: int) -> dict:
+    """Restrict this process (and the threads it starts later) to 1/n of its affinity mask: whole physical cores with
+    their SMT siblings, taken from one NUMA node (sysfs topology), so that a one-GPU run sees the host share one rank
+    of an n-GPU node gets.  Returns what was applied."""
+    mask = sorted(os.sched_getaffinity(0))
+    want = max(1, len(mask) // n)
+
+    def sib(c):
+        try:
+            txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+            out = set()
+            for part in txt.split(","):
+                a, _, b = part.partition("-")
+                out.update(range(int(a), int(b or a) + 1))
+            return out
+        except OSError:
+            return {c}
+
+    def node(c):
+        for d in glob.glob(f"/sys/devices/system/cpu/cpu{c}/node*"):
+            return os.path.basename(d)
+        return "node0"
+
+    first = node(mask[0])
+    pick = []
+    for c in mask:
+        if len(pick) >= want:
+            break
+        if c in pick or node(c) != first:
+            continue
+        pick += [x for x in sorted(sib(c)) if x in mask and x not in pick]
+    pick = pick[:want]
+    os.sched_setaffinity(0, pick)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return dict(share=f"1/{n}", cpus=len(pick), cpu_list=pick, of_mask=len(mask), numa=first, cgroup_cpu_quota=quota)
+
+
 def _progress(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _fs_used(path: str) -> int:
+    st = os.statvfs(path)
+    return (st.f_blocks - st.f_bfree) * st.f_frsize
 
 
 def _tree_bytes(d: str) -> tuple[int, int]:

@@ -1,0 +1,62 @@
+#!/bin/bash
+# Round-5 GPU session steps.  Every GPU step has its own time limit; the first failure ends the call.
+# Usage: bash tools/gpu_r05.sh <tag> <steps...>
+#   steps: tests | smoke | bench | seq | trace | solo | busy | busy2 | fetch | write | pfprof | c3 | c4 | c5 | c5trace
+#          | sweep3 | sweep4 (SHARES=) | c4e2e (SCALE=, READLEN=)
+# The default bench line is config 2 under --threads 25 (policy O4, the reference's mode); `seq` is --threads 1.
+set -o pipefail
+tag=${1:-r05}
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
+SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT"
+SQ2="SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"
+rc=0
+for st in "$@"; do
+  echo "== $st $(date +%T)"
+  case $st in
+    tests) timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+             > "$out/tests.log" 2>&1; rc=$?; tail -3 "$out/tests.log" ;;
+    smoke) timeout -k 10 300 python3 -u -c 'import __graft_entry__ as g; g.smoke()' > "$out/smoke.log" 2>&1; rc=$? ;;
+    bench) timeout -k 10 900 python3 -u bench.py --steps 5 --warmup 1 > "$out/bench.json" 2> "$out/bench.err"; rc=$? ;;
+    seq) timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --threads 1 \
+           > "$out/seq.json" 2> "$out/seq.err"; rc=$? ;;
+    trace) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$out/trace" -o run -- \
+             python3 $B > "$out/trace.log" 2>&1; rc=$?
+           [ $rc = 0 ] && python3 tools/kstats.py "$out/trace/run_kernel_stats.csv" 6 > "$out/trace_kstats.txt" 2>&1 && python3 tools/gpu_idle.py "$out/trace" > "$out/trace_idle.txt" 2>&1 ;;
+    solo) # PMC collection serialises the dispatches: the kernel trace of this run holds every kernel's solo duration
+          timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv -d "$out/solo" -o run -- \
+             python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/solo.log" 2>&1; rc=$?
+          [ $rc = 0 ] && python3 tools/pmc_clock.py "$out/solo/run_counter_collection.csv" "k_pf_count<0>" "$out/pmc_clock_k_pf_count.json"
+          rm -f "$out/solo/run_kernel_trace.csv" "$out/solo/run_counter_collection.csv" ;;
+    busy|busy2) # per-kernel totals only (the full counter CSV exceeds what a call may bring back)
+          [ "$st" = busy ] && CT="$SQ" || CT="$SQ2"
+          timeout -s KILL 300 rocprofv3 --pmc $CT --output-format csv -d "$out/$st" -o run -- python3 $B \
+             > "$out/$st.log" 2>&1; rc=$?
+          if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
+          rm -f "$out/$st/run_counter_collection.csv" ;;
+    fetch|write) # one counter per pass; per-kernel totals only
+          [ "$st" = fetch ] && CT=FETCH_SIZE || CT=WRITE_SIZE
+          timeout -s KILL 300 rocprofv3 --pmc $CT --output-format csv -d "$out/$st" -o run -- python3 $B \
+             > "$out/$st.log" 2>&1; rc=$?
+          if [ $rc = 0 ]; then python3 tools/pmc_agg.py "$out/$st/run_counter_collection.csv" "$out/${st}_agg.json"; rc=$?; fi
+          rm -f "$out/$st/run_counter_collection.csv" ;;
+    pfprof) UMICLUST_PFPROF=1 timeout -k 10 300 python3 -u $B > "$out/pfprof.json" 2> "$out/pfprof.err"; rc=$? ;;
+    c3) timeout -k 10 500 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline > "$out/c3.json" 2> "$out/c3.err"; rc=$? ;;
+    c4) timeout -k 10 600 python3 -u bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline > "$out/c4.json" 2> "$out/c4.err"; rc=$? ;;
+    c5) timeout -k 10 400 python3 -u bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline > "$out/c5.json" 2> "$out/c5.err"; rc=$? ;;
+    c5trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c5trace" -o run -- \
+             python3 bench.py --config 5 --steps 2 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c5trace.log" 2>&1; rc=$?
+             rm -f "$out/c5trace/run_kernel_trace.csv" ;;
+    sweep3) timeout -k 10 900 python3 -u bench.py --config 3 --shard-sweep 8 > "$out/sweep3.json" 2> "$out/sweep3.err"; rc=$? ;;
+    sweep4) timeout -k 10 1000 python3 -u bench.py --config 4 --shard-sweep 8 --sweep-shares "${SHARES:-}" > "$out/sweep4.json" 2> "$out/sweep4.err"; rc=$? ;;
+    c4e2e) timeout -k 10 1100 python3 -u bench.py --config 4 --e2e-files --scale "${SCALE:-1.0}" --read-len "${READLEN:-1500}" \
+             > "$out/c4e2e.json" 2> "$out/c4e2e.err"; rc=$? ;;
+    *) echo "unknown step $st"; rc=2 ;;
+  esac
+  echo "== $st rc=$rc $(date +%T)"
+  [ $rc != 0 ] && exit $rc
+done
+exit 0
