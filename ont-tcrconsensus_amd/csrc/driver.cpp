@@ -431,11 +431,12 @@ namespace {
 // is the process's one live context and the process is its node's only rank (LOCAL_WORLD_SIZE <= 1): several
 // contexts (bin-set lanes) or ranks pinned by where their callers happen to run could all land on one CCD.
 // UMICLUST_PIN=0 turns it off, UMICLUST_PIN=1 forces it on.
-// CPUs the calling thread may run on (its affinity mask: taskset, cgroup cpusets, L3Pin's narrowing)
+// CPUs the calling thread may run on (its affinity mask: taskset, cgroup cpusets, L3Pin's narrowing), bounded by
+// the process's cgroup CPU quota
 int affinity_cpus() {
   cpu_set_t set;
-  if (sched_getaffinity(0, sizeof set, &set) != 0) return 1 << 16;
-  return std::max(1, CPU_COUNT(&set));
+  if (sched_getaffinity(0, sizeof set, &set) != 0) return io::host_cpus();
+  return std::max(1, std::min(CPU_COUNT(&set), io::host_cpus()));
 }
 
 // 8 resolve threads (4 beside other contexts), never more than the caller's affinity mask holds: the in-order
@@ -2187,7 +2188,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     c->pin = atoi(e) != 0;
     c->pin_forced = atoi(e) == 1;
   }
-  g_live_ctx++;
+  io::set_live_contexts(++g_live_ctx);
   if (const char* e = getenv("UMICLUST_SPLIT")) c->split_env = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_RESOLVE_THREADS")) c->resolve_threads = std::max(1, std::min(16, atoi(e)));
   if (const char* b = getenv("UMICLUST_BLOCK")) {
@@ -2226,7 +2227,7 @@ int32_t umiclust_set_priority(umiclust_ctx* c, int32_t level) {
 
 void umiclust_destroy(umiclust_ctx* c) {
   if (!c) return;
-  g_live_ctx--;
+  io::set_live_contexts(--g_live_ctx);
   (void)hipSetDevice(c->dev);
   for (Tile* t : c->tiles) delete t;
   c->tiles.clear();

@@ -22,8 +22,12 @@ struct IoError {
   std::string msg;
 };
 
-// host threads for file I/O (the box gives a GPU process ~16 cores; UMICLUST_IO_THREADS overrides)
+// CPUs this process may use: its affinity mask, bounded by the cgroup CPU quota (cpu.max) when one is set
+int host_cpus();
+// writer / parser threads of one call: UMICLUST_IO_THREADS, else the process's CPUs shared among the device contexts
+// alive (set_live_contexts; a bin-set runner's lanes write concurrently), at most 16
 int io_threads();
+void set_live_contexts(int n);
 
 // run f(t) for t in [0, T) on T threads (the caller's thread runs t = 0)
 template <typename F>
