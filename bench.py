@@ -159,11 +159,14 @@ def full_bin_cpu_reference(config: int) -> dict | None:
     return None
 
 
-def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
+def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None = None) -> tuple[dict, dict]:
     """The prefilter's counting kernel k_pf_count against the L2-served gather rate (its postings stay
     L2-resident: parts = XCDs), with the HBM fraction as a side figure; k_align against the integer VALU
     issue ceiling.  The kernel's launch time is its own HIP-event bracket on the stream it runs on
-    (umiclust_stats.t_count_s / n_count_launches); the postings are every posting the prefilter streamed."""
+    (umiclust_stats.t_count_s / n_count_launches); the postings are every posting the prefilter streamed.
+    With several lanes on the GPU (configs 3/4) the brackets of different lanes overlap, so `frac` charges each
+    launch the time it shared; `device` divides by the union of the brackets over the timed steps
+    (umiclust_timeline: the time some launch of the kernel held the device)."""
     t_cnt = sum(s.get("t_count_s", 0.0) for s in stats)
     n_cnt = sum(s.get("n_count_launches", 0) for s in stats)
     t_pf = sum(s["t_prefilter_s"] for s in stats)
@@ -247,6 +250,19 @@ def roofline(stats: list, config: int, traffic_json: str) -> tuple[dict, dict]:
             align["gcups_solo"] = (cells / len(stats)) / (t_solo / bins_solo) / 1e9
             align["frac_solo"] = align["gcups_solo"] / ceiling
             align["solo_source"] = os.path.relpath(solo_p, ROOT)
+    if tl_union:
+        tc, nc = tl_union.get("count", (0.0, 0))
+        if tc > 0 and nc:
+            a_dev = pf_bytes / tc / 1e9
+            roof["device"] = dict(union_s=tc, brackets=nc, overlap=t_cnt / tc, ms_per_launch=1e3 * tc / nc,
+                                  achieved=a_dev, frac=a_dev / L2_GATHER_GBS,
+                                  note="the same bytes over the union of the counting launches' brackets across "
+                                       "lanes (overlap = sum of brackets / union)")
+        ta, na = tl_union.get("align", (0.0, 0))
+        if ta > 0 and na:
+            g_dev = cells / ta / 1e9
+            align["device"] = dict(union_s=ta, brackets=na, overlap=t_al / ta, gcups=g_dev, frac=g_dev / ceiling,
+                                   gcups_computed=cells_c / ta / 1e9, frac_computed=cells_c / ta / 1e9 / ceiling)
     return roof, align
 
 
@@ -492,6 +508,7 @@ def main() -> None:
         step()
     barrier()
     torch.cuda.synchronize()
+    _lib.timeline(0, reset=True, device=local_rank)  # the kernels' device-time unions over the timed steps
     t0 = time.perf_counter()
     stats = []
     for _ in range(args.steps):
@@ -499,6 +516,7 @@ def main() -> None:
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    tl_union = {k: _lib.timeline(i) for i, k in enumerate(("count", "align"))}
     t_max = elapsed
     my_umis = sum(s["n_kept"] for s in stats[-1])
     tot_umis = my_umis
@@ -518,7 +536,7 @@ def main() -> None:
 
     if rank == 0:
         flat = [s for st in stats for s in st]
-        roof, align = roofline(flat, args.config, args.traffic_json)
+        roof, align = roofline(flat, args.config, args.traffic_json, tl_union)
         # per-step averages for the breakdown
         bd = {k: v / args.steps for k, v in breakdown(flat).items()}
         bd["t_prepare_s"] = sum(s.get("t_prepare_s", 0.0) for s in flat) / args.steps

@@ -301,6 +301,15 @@ int32_t umiclust_prep(umiclust_ctx *ctx, const umiclust_params *p, const char *s
                       const int64_t *offsets, int64_t n, char *masked, uint16_t *kmers,
                       int32_t kstride, int32_t *nk);
 
+/* ---- measurement (bench.py; no reference counterpart) ---- */
+/* Process-wide device timeline of the counting launches (kind 0) and the alignment chains
+ * (kind 1) of every context: busy_s = the union of their HIP-event brackets since the last
+ * reset, launches = the number of brackets.  reset != 0 clears it and records a new
+ * reference event on device_id first.  Several contexts (lanes) on one device overlap their
+ * brackets, so the union is the time the kernel held the device, and the sum is not. */
+int32_t umiclust_timeline(int32_t device_id, int32_t kind, int32_t reset, double *busy_s,
+                          int64_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -201,6 +201,26 @@ struct Pass {
 static std::atomic<int> g_live_ctx{0};  // contexts alive in this process (L3Pin)
 struct umiclust_ctx;
 
+// Process-wide timeline of the counting launches (kind 0) and the alignment chains (kind 1), for
+// umiclust_timeline: with several contexts (lanes) on one device their HIP-event brackets overlap, so the sum of
+// the brackets overstates the time the kernel held the device; the union of the intervals, each taken against
+// one reference event, does not.
+struct Timeline {
+  std::mutex m;
+  hipEvent_t ref = nullptr;
+  int dev = -1;
+  std::vector<std::pair<float, float>> iv[2];
+};
+static Timeline g_tl;
+static void tl_add(int kind, hipEvent_t a, hipEvent_t b) {
+  std::lock_guard<std::mutex> lk(g_tl.m);
+  if (!g_tl.ref) return;
+  float t0 = 0.f, t1 = 0.f;
+  if (hipEventElapsedTime(&t0, g_tl.ref, a) != hipSuccess || hipEventElapsedTime(&t1, g_tl.ref, b) != hipSuccess)
+    return;
+  g_tl.iv[kind].emplace_back(t0, t1);
+}
+
 struct umiclust_ctx {
   int dev = 0;
   hipStream_t st = nullptr;
@@ -1050,13 +1070,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     t_pf += ms * 1e-3;
     c->stats.t_count_s += ms * 1e-3;
     c->stats.n_count_launches++;
+    tl_add(0, c->a_ev[P.t_slot][0], c->a_ev[P.t_slot][1]);
   } else if (P.c_timed) {
     c->hip(hipEventElapsedTime(&ms, P.ev_c[0], P.ev_c[1]), "elapsed");
     c->stats.t_count_s += ms * 1e-3;
     c->stats.n_count_launches++;
+    tl_add(0, P.ev_c[0], P.ev_c[1]);
   }
   c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;
+  tl_add(1, P.ev[2], P.ev[3]);
   {
     // records past the DMA'd prefix (a pass that used more than the estimate): fetch the rest now
     const size_t used = *P.h_reccount.p, est = std::min<size_t>(P.rec_est, P.d_rec.n);
@@ -2135,6 +2158,43 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
 extern "C" {
 
 int32_t umiclust_abi_version(void) { return UMICLUST_ABI_VERSION; }
+
+int32_t umiclust_timeline(int32_t device_id, int32_t kind, int32_t reset, double* busy_s, int64_t* launches) {
+  if (kind < 0 || kind > 1) return UMICLUST_EINVAL;
+  std::lock_guard<std::mutex> lk(g_tl.m);
+  if (reset) {
+    if (hipSetDevice(device_id) != hipSuccess) return UMICLUST_EDEVICE;
+    if (g_tl.ref && g_tl.dev != device_id) {
+      (void)hipEventDestroy(g_tl.ref);
+      g_tl.ref = nullptr;
+    }
+    if (!g_tl.ref && hipEventCreate(&g_tl.ref) != hipSuccess) {
+      g_tl.ref = nullptr;
+      return UMICLUST_EDEVICE;
+    }
+    g_tl.dev = device_id;
+    if (hipEventRecord(g_tl.ref, nullptr) != hipSuccess || hipEventSynchronize(g_tl.ref) != hipSuccess)
+      return UMICLUST_EDEVICE;
+    g_tl.iv[0].clear();
+    g_tl.iv[1].clear();
+  }
+  std::vector<std::pair<float, float>> v = g_tl.iv[kind];
+  std::sort(v.begin(), v.end());
+  double tot = 0.0, hi = -1e30, lo = 0.0;
+  for (const auto& x : v) {
+    if (x.first > hi) {
+      if (hi > lo) tot += hi - lo;
+      lo = x.first;
+      hi = x.second;
+    } else if (x.second > hi) {
+      hi = x.second;
+    }
+  }
+  if (!v.empty() && hi > lo) tot += hi - lo;
+  if (busy_s) *busy_s = tot * 1e-3;
+  if (launches) *launches = (int64_t)v.size();
+  return 0;
+}
 
 
 // The alignment stream is created with the device's greatest stream priority: a pass's walk/align/pack chain gates

@@ -110,6 +110,7 @@ EXPORTS = [
     "umiclust_load", "umiclust_stage", "umiclust_prepare", "umiclust_set_priority", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
     "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
+    "umiclust_timeline",
 ]
 OVERLAP_MAX_REGIONS = 4096
 
@@ -191,8 +192,20 @@ def lib() -> C.CDLL:
     L.umiclust_prep.restype = C.c_int32
     L.umiclust_prep.argtypes = [C.c_void_p, P(Params), C.c_void_p, P(C.c_int64), C.c_int64, C.c_void_p,
                                 P(C.c_uint16), C.c_int32, P(C.c_int32)]
+    L.umiclust_timeline.restype = C.c_int32
+    L.umiclust_timeline.argtypes = [C.c_int32, C.c_int32, C.c_int32, P(C.c_double), P(C.c_int64)]
     _lib = L
     return L
+
+
+def timeline(kind: int, reset: bool = False, device: int = 0) -> tuple[float, int]:
+    """umiclust_timeline: (union of the kind's HIP-event brackets in seconds, brackets) since the last reset;
+    kind 0 = counting launches, 1 = alignment chains."""
+    s, n = C.c_double(0.0), C.c_int64(0)
+    rc = lib().umiclust_timeline(device, kind, 1 if reset else 0, C.byref(s), C.byref(n))
+    if rc != 0:
+        raise UmiclustError(rc, "timeline")
+    return s.value, n.value
 
 
 def params(preset: int = PRESET_ROUND1, identity: float = 0.93, minlen: int = 58, maxlen: int = 68,
