@@ -58,6 +58,31 @@ def _align_valu_per_cell() -> float:
 ALIGN_VALU_PER_CELL = _align_valu_per_cell()
 
 
+def align_issue_ceiling() -> dict | None:
+    """The aligner's ceiling at the measured issue cost of its own instruction mix: the column loop of
+    k_align_pk<64> (tools/isa_mix.py -> profiles/r05/align_issue_mix_pk64.json: VOP2, packed VOP3P and other VOP3
+    instructions per step of 64 cells per lane) priced with tools/valu_rate.hip's cycles per wave-instruction per
+    SIMD at 4 waves per SIMD (profiles/r05/valu_rate.jsonl: 8-byte VOP3/VOP3P encodings issue ~1.5x slower than
+    4-byte VOP2 ones), in the probe's own 2.4 GHz-nominal cycle units."""
+    mp = os.path.join(ROOT, "profiles", "r05", "align_issue_mix_pk64.json")
+    rp = os.path.join(ROOT, "profiles", "r05", "valu_rate.jsonl")
+    if not (os.path.exists(mp) and os.path.exists(rp)):
+        return None
+    mix = json.load(open(mp))
+    rates = [json.loads(x) for x in open(rp) if x.strip()]
+    cyc = lambda ops: sum(r["cycles_per_instr_at_2.4GHz"] for r in rates  # noqa: E731
+                          if r["op"] in ops and r["chains"] == 8 and r["waves_per_simd"] == 4) / len(ops)
+    c2 = cyc(["v_add_u32"])
+    c3p = cyc(["v_pk_sub_i16", "v_pk_max_i16", "v_pk_ashrrev_i16", "v_pk_mad_u16"])
+    c3 = cyc(["v_add3_u32", "v_and_or_b32", "v_bitop3_b32"])
+    step = mix["vop2"] * c2 + mix["vop3p"] * c3p + mix["vop3"] * c3
+    cells_per_step = 64 * 64  # 64 lanes x (32 packed rows = 64 cells)
+    gcups = 1024 * 2.4e9 * cells_per_step / step / 1e9
+    return dict(ceiling_gcups=gcups, cycles_per_step=step, cycles_vop2=c2, cycles_vop3p=c3p, cycles_vop3=c3,
+                mix={k: mix[k] for k in ("vop2", "vop3p", "vop3")},
+                source=[os.path.relpath(mp, ROOT), os.path.relpath(rp, ROOT)])
+
+
 def cpu_baseline_bins(bins, identity: float, lens, budget_s: float = 20.0, preset: int = 1) -> dict:
     """The C oracle (oracle/) over whole bins on every host core the process may use (the reference runs one
     vsearch process per bin, utils.py:56-63): one thread per core pulls bins largest first until ~budget_s of
@@ -250,6 +275,12 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
             align["gcups_solo"] = (cells / len(stats)) / (t_solo / bins_solo) / 1e9
             align["frac_solo"] = align["gcups_solo"] / ceiling
             align["solo_source"] = os.path.relpath(solo_p, ROOT)
+    iss = align_issue_ceiling()
+    if iss:
+        iss["frac"] = g_alg / iss["ceiling_gcups"]
+        if "gcups_solo" in align:
+            iss["frac_solo"] = align["gcups_solo"] / iss["ceiling_gcups"]
+        align["issue"] = iss
     if tl_union:
         tc, nc = tl_union.get("count", (0.0, 0))
         if tc > 0 and nc:

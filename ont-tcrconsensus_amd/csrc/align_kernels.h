@@ -289,11 +289,17 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
   // carries of the top half's last row, consumed by the bottom half in the next step
   uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDL = 0;
   int Lext = 0, trail = 0;
-  uint32_t tword = 0, tprev = 1;
+  // the target's code words one ahead (the load of word w + 1 is in flight while word w's 8 columns run; a
+  // load at its use cost every wave a full memory wait per 8 columns).  Word w + 1 may lie past the target's
+  // words: it is then the other strand's first word (same row of the codes array), never used.
+  uint32_t tword = 0, tprev = 1, tnext = tcp[0];
   // one step: top half at column j, bottom half at column j-1; LAST: one of the end cell's two steps
   auto step = [&](int j, auto last_tag) __attribute__((always_inline)) {
     constexpr bool LAST = decltype(last_tag)::value;
-    if ((j & 7) == 0) tword = tcp[j >> 3];
+    if ((j & 7) == 0) {
+      tword = tnext;
+      tnext = tcp[(j >> 3) + 1];
+    }
     const uint32_t tcode = tword & 15u;
     tword >>= 4;
     const uint32_t bl = (uint32_t)__builtin_ctz(tcode | 16u) & 3u, bh = (uint32_t)__builtin_ctz(tprev | 16u) & 3u;

@@ -54,6 +54,11 @@ for st in "$@"; do
     sweep4) timeout -k 10 1000 python3 -u bench.py --config 4 --shard-sweep 8 --sweep-shares "${SHARES:-}" > "$out/sweep4.json" 2> "$out/sweep4.err"; rc=$? ;;
     c4e2e) timeout -k 10 1100 python3 -u bench.py --config 4 --e2e-files --scale "${SCALE:-1.0}" --read-len "${READLEN:-1500}" \
              > "$out/c4e2e.json" 2> "$out/c4e2e.err"; rc=$? ;;
+    valu) timeout -k 10 120 ./tools/valu_rate > "$out/valu_rate.jsonl" 2>&1; rc=$? ;;
+    default) timeout -k 10 700 python3 -u bench.py > "$out/bench_default.json" 2> "$out/bench_default.err"; rc=$? ;;
+    c3lazy) for z in ${LAZYS:-5 1000}; do
+              UMICLUST_LAZY=$z timeout -k 10 300 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline \
+                > "$out/c3_lazy$z.json" 2> "$out/c3_lazy$z.err" || { rc=$?; break; }; rc=0; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
