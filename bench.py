@@ -234,7 +234,7 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
     # (tools/pmc_calib.hip, conflict-free), at the clock measured during the kernel (GRBM_GUI_ACTIVE / 8 / duration of
     # its dispatches in a PMC run: tools/pmc_clock.py)
     cal_p = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
-    clk_p = os.path.join(ROOT, "profiles", "r04", "pmc_clock_k_pf_count.json")
+    clk_p = os.path.join(ROOT, "profiles", "r05", "pmc_clock_k_pf_count.json")
     if os.path.exists(cal_p) and os.path.exists(clk_p) and n_cnt:
         cal, clk = json.load(open(cal_p)), json.load(open(clk_p))
         atom = streamed / 64.0 / n_cnt
@@ -263,14 +263,14 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
                  speculative_ratio=cells_c / cells if cells else None)
     # the aligner alone: its kernels' durations in a PMC run (dispatches serialised, so nothing shares the CUs) of the
     # same workload, per bin, against this run's cells per bin (config 2: one bin per step)
-    solo_p = os.path.join(ROOT, "profiles", "r04", "rocprof_solo_kernel_stats_c2_r04zm.csv")
+    solo_p = os.path.join(ROOT, "profiles", "r05", "rocprof_solo_kernel_stats_c2_r05.csv")
     if config == 2 and os.path.exists(solo_p) and stats:
         t_solo = 0.0
         for r in csv.DictReader(open(solo_p, newline="")):
             nm = r["Name"].replace("void ", "").split("(")[0].split("::")[-1]
             if nm.startswith("k_align_pk") or nm.startswith("k_align_band"):
                 t_solo += float(r["TotalDurationNs"]) * 1e-9
-        bins_solo = 2  # tools/gpu_r04.sh `solo`: bench.py --steps 1 --warmup 1
+        bins_solo = 2  # tools/gpu_r05.sh `solo`: bench.py --steps 1 --warmup 1
         if t_solo > 0:
             align["gcups_solo"] = (cells / len(stats)) / (t_solo / bins_solo) / 1e9
             align["frac_solo"] = align["gcups_solo"] / ceiling
@@ -300,7 +300,7 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
 def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     """Per-CU LDS-array and VALU busy of `kernel` (round 4: from the per-kernel PMC totals of
     profiles/r04/pmc_busy_c2_final.json, tools/pmc_agg.py; else round 3's CSV below)."""
-    agg_path = os.path.join(ROOT, "profiles", "r04", "pmc_busy_c2_final.json")
+    agg_path = os.path.join(ROOT, "profiles", "r05", "pmc_busy_c2_r05.json")
     cal_path = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
     if os.path.exists(agg_path) and os.path.exists(cal_path):
         agg = json.load(open(agg_path))
