@@ -213,6 +213,11 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
                 traffic = tj.get("prefilter_hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    # SURVEY 8d's prefilter bytes: postings x 4 B + C x 2 B of counter traffic per query-strand (C = centroids
+    # indexed).  This build's postings are u16 (2 B) and its counters u8 in LDS, so `achieved` counts 2 B per posting
+    # and no counter bytes; `survey` restates the same launches by SURVEY's formula against HBM's 8 TB/s.
+    counter_cells = sum(s.get("counter_cells", 0) for s in stats)
+    survey_bytes = streamed * 4 + counter_cells * 2
     achieved = pf_bytes / t_cnt / 1e9 if t_cnt > 0 else 0.0
     roof = dict(kernel="k_pf_count", bound="l2", achieved=achieved, peak=L2_GATHER_GBS, unit="GB/s",
                 frac=achieved / L2_GATHER_GBS, traffic=traffic,
@@ -235,6 +240,11 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
     # its dispatches in a PMC run: tools/pmc_clock.py)
     cal_p = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
     clk_p = os.path.join(ROOT, "profiles", "r05", "pmc_clock_k_pf_count.json")
+    if counter_cells and t_cnt > 0:
+        roof["survey"] = dict(bytes_per_launch=survey_bytes / max(1, n_cnt), counter_cells=counter_cells,
+                              achieved=survey_bytes / t_cnt / 1e9, frac_hbm=survey_bytes / t_cnt / 1e9 / HBM_PEAK_GBS,
+                              note="SURVEY 8d: postings x 4 B + C x 2 B per query-strand, C = centroids indexed at the "
+                                   "launch; the build stores u16 postings and u8 counters, so `achieved` uses 2 B")
     if os.path.exists(cal_p) and os.path.exists(clk_p) and n_cnt:
         cal, clk = json.load(open(cal_p)), json.load(open(clk_p))
         atom = streamed / 64.0 / n_cnt

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 7
+#define UMICLUST_ABI_VERSION 8
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -68,8 +68,9 @@ typedef struct umiclust_params {
                              restated (cluster_core_parallel): rounds of `threads` queries, each searched
                              against the index frozen at the round's start, then re-checked in order against
                              the round's new centroids (inserted into its hit list by k-mer count and
-                             re-walked one alignment at a time).  umiclust_params_from_argv sets 1 when the
-                             environment has UMICLUST_O4=batched (the reference's argv stays unchanged). */
+                             re-walked one alignment at a time).  umiclust_params_from_argv sets 1 whenever
+                             the argv's --threads is > 1 (the reference's --threads 25: since round 5, ABI 7),
+                             unless the environment has UMICLUST_O4=sequential. */
 } umiclust_params;
 
 /* presets */
@@ -107,7 +108,10 @@ typedef struct umiclust_stats {
   double t_count_s;       /* kernel time, the prefilter's counting kernel alone (k_pf_count, HIP events) */
   int64_t n_count_launches; /* its launches (one per pass over one counter segment) */
   int64_t kmer_postings_deferred; /* postings of the lists the counting kernel deferred (frequent k-mers whose
-                                     matches it adds per surviving target instead; x 8 chunks, incl. padding) */
+                                     matches it adds per surviving target instead; x 8 chunks, incl. padding;
+                                     0 since round 5: the deferral was removed) */
+  int64_t counter_cells;  /* ABI 8: sum over the counting launches of query-strands x centroids indexed (the C of
+                             SURVEY 8d's prefilter bytes, postings x 4 B + C x 2 B counter traffic) */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

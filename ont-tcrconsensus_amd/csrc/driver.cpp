@@ -827,6 +827,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
     c->hip(hipEventRecord(P.ev_c[0], st), "event");
     c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
     c->hip(hipEventRecord(P.ev_c[1], st), "event");
+    c->stats.counter_cells += (int64_t)nq * c->both * a.ncent;
     if (c->pf_probe) launch_pf_probe(c, a, st);
     c->hip(launch_prefilter(a, st, 2), "prefilter");
     P.c_timed = true;
@@ -996,6 +997,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   c->hip(hipEventRecord(c->a_ev[slot][0], st), "event");
   c->hip(launch_prefilter(a, st, 1), "prefilter (count)");
   c->hip(hipEventRecord(c->a_ev[slot][1], st), "event");
+  c->stats.counter_cells += (int64_t)nq * c->both * a.ncent;
   if (c->pf_probe) launch_pf_probe(c, a, st);
   c->last_a_slot = slot;
   P.a_live = true;

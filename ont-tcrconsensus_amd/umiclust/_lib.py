@@ -84,6 +84,7 @@ class Stats(C.Structure):
         ("t_count_s", C.c_double),
         ("n_count_launches", C.c_int64),
         ("kmer_postings_deferred", C.c_int64),
+        ("counter_cells", C.c_int64),
     ]
 
     def as_dict(self) -> dict:
