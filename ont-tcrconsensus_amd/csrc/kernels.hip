@@ -671,28 +671,37 @@ struct PfTable {
   uint4* wtab;  // per window {base list, start bits 0-31, start bits 32-63, 0}
   uint32_t* wsum;
 };
-__device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, int t0, int nct, int ntl,
-                                              uint64_t pbase, int part, int thr, int nk, uint32_t km0, uint32_t km1,
-                                              int wv, int lane, int tid, uint32_t& T, uint32_t& nlc,
-                                              bool prof = false, unsigned long long* clk0 = nullptr,
-                                              unsigned long long* clk1 = nullptr) {
+// the list offsets of a wave's tiles, issued as loads (pf_list_table waits for them): k_pf_count issues them before
+// zeroing its counters, so the zeroing's LDS stores overlap their memory latency
+struct PfOffsets {
   TileView tvs[kPfTilesPerWave];
+  u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
+};
+__device__ __forceinline__ void pf_list_offsets(const PrefilterArgs& a, int t0, int nct, int ntl, int part, int thr,
+                                                uint32_t km0, uint32_t km1, int wv, PfOffsets& r) {
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
     const int ti = wv + it * kPfWaves;
-    if (ti < nct) tvs[it] = cent_view(a, t0 + ti);
-    else if (ti < ntl) tvs[it] = a.peer[ti - nct];
-    else tvs[it].n = 0;
+    if (ti < nct) r.tvs[it] = cent_view(a, t0 + ti);
+    else if (ti < ntl) r.tvs[it] = a.peer[ti - nct];
+    else r.tvs[it].n = 0;
   }
-  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
-  u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
-    const bool live = thr > 0 && tvs[it].n > 0;
-    const uint32_t* op = uniform_ptr((live ? tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
-    o0[it] = ld_off2(op, km0);
-    o1[it] = ld_off2(op, km1);
+    const bool live = thr > 0 && r.tvs[it].n > 0;
+    const uint32_t* op = uniform_ptr((live ? r.tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
+    r.o0[it] = ld_off2(op, km0);
+    r.o1[it] = ld_off2(op, km1);
   }
+}
+__device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, const PfOffsets& r,
+                                              uint64_t pbase, int thr, int nk, int lane, int tid, uint32_t& T,
+                                              uint32_t& nlc, bool prof = false, unsigned long long* clk0 = nullptr,
+                                              unsigned long long* clk1 = nullptr) {
+  const TileView* tvs = r.tvs;
+  const u32x2* o0 = r.o0;
+  const u32x2* o1 = r.o1;
+  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
 #pragma unroll
   for (int it = 0; it < kPfTilesPerWave; it++) {
     const bool live = thr > 0 && tvs[it].n > 0;
@@ -854,8 +863,9 @@ __device__ __forceinline__ void pf_full_unit(const PrefilterArgs& a, uint32_t un
       S.overflow = 0;
     }
     uint32_t T, nlc;
-    pf_list_table(a, PfTable{S.lstart, S.lbias, S.wtab, S.wsum}, t0, nct, ntl, pbase, part, thr, nk,
-                  km0, km1, wv, lane, tid, T, nlc);
+    PfOffsets offs;
+    pf_list_offsets(a, t0, nct, ntl, part, thr, km0, km1, wv, offs);
+    pf_list_table(a, PfTable{S.lstart, S.lbias, S.wtab, S.wsum}, offs, pbase, thr, nk, lane, tid, T, nlc);
     PF_MARK(0)
     if (T > 0) pf_count_stream<kPfSharedBytes>(arena, T, nlc, S.lstart, S.lbias, S.wtab, lane, wv);
     __syncthreads();
@@ -1128,6 +1138,8 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     tprev = tn;                                                 \
   }
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
+  PfOffsets offs;
+  pf_list_offsets(a, 0, nct, nct + kPeerTiles, part, thr, km0, km1, wv, offs);  // in flight during the zeroing
   for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) {
     H.ncand = 0;
@@ -1135,8 +1147,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
   }
   uint32_t T, nlc;
   PFC_MARK(0)
-  pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, 0, nct, nct + kPeerTiles, pbase, part, thr, nk,
-                km0, km1, wv, lane, tid, T, nlc, prof, &clk0, &clk1);
+  pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, offs, pbase, thr, nk, lane, tid, T, nlc, prof, &clk0, &clk1);
   if (prof) {
     tsub[0] += clk0 - tprev;
     tsub[1] += clk1 - clk0;
