@@ -733,3 +733,20 @@ def test_parallel_inorder_phase_every_block(name, monkeypatch):
     assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
     for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
         assert d[k] == gold[k], k
+
+
+def test_timeline_union_and_counter_cells():
+    """umiclust_timeline: one context's counting launches are serial on its stream, so the union of their HIP-event
+    brackets equals their sum (umiclust_stats.t_count_s) and the bracket count equals n_count_launches;
+    counter_cells (ABI 8) = sum over the counting launches of query-strands x centroids indexed."""
+    u = synth.config_umis(1, 0.1)
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(_lib.PRESET_ROUND1, 0.93, 58, 68, threads=25), buf=u.seq, off=u.off)
+        _lib.timeline(0, reset=True)
+        st = ctx.cluster()
+        busy, n = _lib.timeline(0)
+        abusy, an = _lib.timeline(1)
+    assert n == st["n_count_launches"] > 0
+    assert abs(busy - st["t_count_s"]) <= 0.02 * st["t_count_s"] + 1e-4
+    assert an > 0 and 0 < abusy <= st["t_align_s"] * 1.02 + 1e-4
+    assert 0 < st["counter_cells"] <= st["n_count_launches"] * 2 * 8192 * st["n_kept"]
