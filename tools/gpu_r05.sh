@@ -59,6 +59,9 @@ for st in "$@"; do
     c3lazy) for z in ${LAZYS:-5 1000}; do
               UMICLUST_LAZY=$z timeout -k 10 300 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline \
                 > "$out/c3_lazy$z.json" 2> "$out/c3_lazy$z.err" || { rc=$?; break; }; rc=0; done ;;
+    predab) for v in ${PREDS:-1 0}; do for c in ${PCFGS:-3 2 5}; do
+              UMICLUST_PEER_PREDICT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/pred${v}_c$c.json" 2> "$out/pred${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
