@@ -314,7 +314,7 @@ def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     cal_path = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
     if os.path.exists(agg_path) and os.path.exists(cal_path):
         agg = json.load(open(agg_path))
-        k = next((x for x in agg if x.split("<")[0] == kernel and x.endswith("<0>")), None) or \
+        k = next((x for x in agg if x.split("<")[0] == kernel and x.endswith(("<0, 4>", "<0>"))), None) or \
             next((x for x in agg if x.split("<")[0] == kernel), None)
         if k:
             cal = json.load(open(cal_path))

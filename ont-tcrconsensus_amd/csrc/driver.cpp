@@ -379,6 +379,7 @@ struct umiclust_ctx {
   static constexpr int32_t spec_thr = 30;
   // relevant peers certain to become members are not aligned speculatively (config 2 4.02 -> 4.14 M, round 4)
   static constexpr bool peer_cert = true;
+  int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
   DevBuf<uint32_t> d_probe;
   // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
@@ -802,6 +803,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   // list table of the lean kernel: every k-mer of the block's length in every tile it reads
   a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, block_maxlen(c, q0, nq) - 7) *
                                               ((a.nseg > 0 ? a.seg_tile[1] - a.seg_tile[0] : 0) + kPeerTiles));
+  a.pf1_lds = c->pf1_lds;
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;
@@ -988,6 +990,7 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   a.units = P.d_units.p;
   a.nunits = P.d_anunits.p;
   a.nlist_cap = std::min(kMaxKmers * 12, std::max(1, block_maxlen(c, q0, nq) - 7) * (nv + kPeerTiles));
+  a.pf1_lds = c->pf1_lds;
   a.ppeer_id = P.d_ppeer_id.p;
   a.ppeer_count = P.d_ppeer_count.p;
   a.pnpeer = P.d_pnpeer.p;
@@ -2245,6 +2248,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));
+  if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
     c->pin = atoi(e) != 0;

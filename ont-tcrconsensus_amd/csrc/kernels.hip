@@ -430,8 +430,13 @@ constexpr int kListBits = kPfLists < 1024 ? 10 : 11;
 constexpr uint32_t kListMask = (1u << kListBits) - 1u;
 static_assert(kPfLists < (1 << kListBits) && (uint64_t)kPfLists * (kTile / kParts / 8 + 1) < (1ull << (32 - kListBits)),
               "list-table scan overflows");
-constexpr int kPfTilesPerWave = (kPfTiles + kPfWaves - 1) / kPfWaves;
-constexpr int kPfSlots = 2 * kPfTilesPerWave;  // list-table slots per thread (two k-mers per lane)
+// the list table and the count loop for a workgroup of W waves (k_pf_full: 4; k_pf_count: 4, or 1 for small indexes)
+template <int W>
+struct PfW {
+  static constexpr int kThreads = 64 * W;
+  static constexpr int kTilesPerWave = (kPfTiles + W - 1) / W;
+  static constexpr int kSlots = 2 * kTilesPerWave;
+};
 
 constexpr int kCge = (kMaxLen + 4) & ~3;  // cnt_ge entries in LDS, a whole number of 16-byte vectors
 struct PfShared {
@@ -637,14 +642,19 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t n, uint32_t* counter) {
 
 // exclusive scan over the workgroup (every thread must call it); one DPP scan per wave, one barrier: the caller
 // must pass another barrier before wsum is written again (pf_list_table ends with one)
+template <int W = kPfWaves>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
   const int wave = threadIdx.x >> 6;
   const uint32_t inc = wave_scan_dpp(v, OpAdd());
+  if (W == 1) {  // one wave: no barrier, no LDS
+    total = lane63(inc);
+    return inc - v;
+  }
   if ((threadIdx.x & 63) == 63) wsum[wave] = inc;
   __syncthreads();
   uint32_t base = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kPfWaves; w++) {
+  for (int w = 0; w < W; w++) {
     const uint32_t x = wsum[w];
     base += (w < wave) ? x : 0u;
     tot += x;
@@ -673,37 +683,42 @@ struct PfTable {
 };
 // the list offsets of a wave's tiles, issued as loads (pf_list_table waits for them): k_pf_count issues them before
 // zeroing its counters, so the zeroing's LDS stores overlap their memory latency
+template <int W = kPfWaves>
 struct PfOffsets {
-  TileView tvs[kPfTilesPerWave];
-  u32x2 o0[kPfTilesPerWave], o1[kPfTilesPerWave];
+  TileView tvs[PfW<W>::kTilesPerWave];
+  u32x2 o0[PfW<W>::kTilesPerWave], o1[PfW<W>::kTilesPerWave];
 };
+template <int W = kPfWaves>
 __device__ __forceinline__ void pf_list_offsets(const PrefilterArgs& a, int t0, int nct, int ntl, int part, int thr,
-                                                uint32_t km0, uint32_t km1, int wv, PfOffsets& r) {
+                                                uint32_t km0, uint32_t km1, int wv, PfOffsets<W>& r) {
+  constexpr int kTPW = PfW<W>::kTilesPerWave;
 #pragma unroll
-  for (int it = 0; it < kPfTilesPerWave; it++) {
-    const int ti = wv + it * kPfWaves;
+  for (int it = 0; it < kTPW; it++) {
+    const int ti = wv + it * W;
     if (ti < nct) r.tvs[it] = cent_view(a, t0 + ti);
     else if (ti < ntl) r.tvs[it] = a.peer[ti - nct];
     else r.tvs[it].n = 0;
   }
 #pragma unroll
-  for (int it = 0; it < kPfTilesPerWave; it++) {
+  for (int it = 0; it < kTPW; it++) {
     const bool live = thr > 0 && r.tvs[it].n > 0;
     const uint32_t* op = uniform_ptr((live ? r.tvs[it].off : a.peer[kPeerTiles - 1].off) + ((uint32_t)part << 16));
     r.o0[it] = ld_off2(op, km0);
     r.o1[it] = ld_off2(op, km1);
   }
 }
-__device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, const PfOffsets& r,
+template <int W = kPfWaves>
+__device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTable& tb, const PfOffsets<W>& r,
                                               uint64_t pbase, int thr, int nk, int lane, int tid, uint32_t& T,
                                               uint32_t& nlc, bool prof = false, unsigned long long* clk0 = nullptr,
                                               unsigned long long* clk1 = nullptr) {
+  constexpr int kTPW = PfW<W>::kTilesPerWave, kSl = PfW<W>::kSlots;
   const TileView* tvs = r.tvs;
   const u32x2* o0 = r.o0;
   const u32x2* o1 = r.o1;
-  uint32_t nch[kPfSlots], bse[kPfSlots], sum_ch = 0, sum_ne = 0;
+  uint32_t nch[kSl], bse[kSl], sum_ch = 0, sum_ne = 0;
 #pragma unroll
-  for (int it = 0; it < kPfTilesPerWave; it++) {
+  for (int it = 0; it < kTPW; it++) {
     const bool live = thr > 0 && tvs[it].n > 0;
     const uint32_t tbase = (uint32_t)(tvs[it].post_base - pbase);
     const uint32_t c0 = (live && lane < nk) ? (o0[it].y - o0[it].x) >> 3 : 0u;
@@ -714,22 +729,22 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
     bse[2 * it + 1] = tbase + o1[it].x;
   }
 #pragma unroll
-  for (int j = 0; j < kPfSlots; j++) {
+  for (int j = 0; j < kSl; j++) {
     sum_ch += nch[j];
     sum_ne += nch[j] ? 1u : 0u;
   }
   if (prof) *clk0 = __builtin_readcyclecounter();  // phase probe: the list offsets have arrived
-  // window start masks (set below, after block_excl_scan's barriers)
-  if (tid < kPfWinBase) tb.wtab[tid] = make_uint4(0u, 0u, 0u, 0u);
+  // window start masks (set below, after block_excl_scan's barriers; one wave: its LDS operations stay in order)
+  for (int i = tid; i < kPfWinBase; i += PfW<W>::kThreads) tb.wtab[i] = make_uint4(0u, 0u, 0u, 0u);
   // packed scan: chunks << kListBits | lists (see kListBits)
   uint32_t tot;
-  const uint32_t ex = block_excl_scan((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
+  const uint32_t ex = block_excl_scan<W>((sum_ch << kListBits) | sum_ne, tb.wsum, tot);
   if (prof) *clk1 = __builtin_readcyclecounter();
   T = tot >> kListBits;
   nlc = tot & kListMask;
   uint32_t li = ex & kListMask, ci = ex >> kListBits;
 #pragma unroll
-  for (int j = 0; j < kPfSlots; j++)
+  for (int j = 0; j < kSl; j++)
     if (nch[j]) {
       tb.lstart[li] = ci;
       tb.lbias[li] = bse[j] - 8u * ci;
@@ -741,7 +756,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
       li++;
       ci += nch[j];
     }
-  if (tid < 66) tb.lstart[nlc + tid] = T;
+  for (int i = tid; i < 66; i += PfW<W>::kThreads) tb.lstart[nlc + i] = T;
   __syncthreads();
 }
 
@@ -753,7 +768,7 @@ __device__ __forceinline__ void pf_list_table(const PrefilterArgs& a, const PfTa
 // ahead of the batch being counted; two register sets are used alternately (a copy between them would wait
 // for the loads in flight).  A lane past the end of the stream reads chunk 0 and adds 0; a window past the
 // end is skipped (wave-uniform branch).
-template <uint32_t kBase>
+template <uint32_t kBase, int W = kPfWaves>
 __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, uint32_t T, uint32_t nlc,
                                                 const uint32_t* lstart, const uint32_t* lbias,
                                                 const uint4* wtab, int lane, int wv) {
@@ -785,7 +800,7 @@ __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, ui
   };
   auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
   auto one = [](uint32_t i) { return i != 0xffffffffu ? 1u : 0u; };
-  constexpr uint32_t S1 = kPfWaves;
+  constexpr uint32_t S1 = W;
   uint32_t w = (uint32_t)wv;  // wave-uniform (SGPR): the window bounds are scalar branches
   uint32_t a0 = window(w), a1 = window(w + S1);
   uint4 v0 = ldv(a0), v1 = ldv(a1);
@@ -1094,8 +1109,12 @@ struct PfCountHdr {
 __host__ __device__ constexpr uint32_t pf_count_table_bytes(int nlist_cap) {
   return (uint32_t)(sizeof(PfCountHdr) + kPfWinBase * 16 + (2 * nlist_cap + 66) * 4);
 }
-template <int CM>
-__global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
+// W waves per workgroup: 4 (8 workgroups per CU), or 1 when the index is small (up to 32 one-wave workgroups per CU;
+// launch_prefilter): then the table, count and scan phases need no workgroup barrier, and 4x more units are in flight
+// to hide the latency chain (k-mers -> list offsets -> table) that dominates a unit with few postings.
+template <int CM, int W>
+__global__ __launch_bounds__(64 * W, 8) void k_pf_count(PrefilterArgs a, uint32_t tab_off) {
+  constexpr int kThr = PfW<W>::kThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char pf_smem[];
   PfCountHdr& H = *reinterpret_cast<PfCountHdr*>(pf_smem + tab_off);
   uint4* wtab = reinterpret_cast<uint4*>(pf_smem + tab_off + sizeof(PfCountHdr));
@@ -1138,23 +1157,23 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     tprev = tn;                                                 \
   }
   uint4* cnt4 = reinterpret_cast<uint4*>(cnt);
-  PfOffsets offs;
-  pf_list_offsets(a, 0, nct, nct + kPeerTiles, part, thr, km0, km1, wv, offs);  // in flight during the zeroing
-  for (int x = tid; x < (ncnt >> 4); x += kPfThreads) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
+  PfOffsets<W> offs;
+  pf_list_offsets<W>(a, 0, nct, nct + kPeerTiles, part, thr, km0, km1, wv, offs);  // in flight during the zeroing
+  for (int x = tid; x < (ncnt >> 4); x += kThr) cnt4[x] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) {
     H.ncand = 0;
     H.npc = 0;
   }
   uint32_t T, nlc;
   PFC_MARK(0)
-  pf_list_table(a, PfTable{lstart, lbias, wtab, H.wsum}, offs, pbase, thr, nk, lane, tid, T, nlc, prof, &clk0, &clk1);
+  pf_list_table<W>(a, PfTable{lstart, lbias, wtab, H.wsum}, offs, pbase, thr, nk, lane, tid, T, nlc, prof, &clk0, &clk1);
   if (prof) {
     tsub[0] += clk0 - tprev;
     tsub[1] += clk1 - clk0;
   }
   PFC_MARK(1)
   if (T > 0 && CM != 2)  // CM 2: the timing probe without the count loop (UMICLUST_PFPROBE)
-    pf_count_stream<0>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
+    pf_count_stream<0, W>(arena, T, nlc, lstart, lbias, wtab, lane, wv);
   __syncthreads();
   PFC_MARK(2)
   if (wv == 0) {
@@ -1170,7 +1189,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const int lim4 = (nsubC + 15) >> 4;  // counters past nsubC are zero (< thr)
     const uint4* c4 = cnt4 + kCentBase / 16;
     const int32_t cmin = pack_cmin(ord0, 0, part, nsubC);  // packs: earlier bins' centroids are never candidates
-    for (int x0 = (cmin >> 4) + wv * 64; x0 < lim4; x0 += kPfThreads) {
+    for (int x0 = (cmin >> 4) + wv * 64; x0 < lim4; x0 += kThr) {
       const int x = x0 + lane;
       uint4 v = x < lim4 ? c4[x] : make_uint4(0u, 0u, 0u, 0u);
       const int cb = cmin - x * 16;
@@ -1206,7 +1225,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const int nwords = (nsubP + 3) >> 2;
     const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
     const int32_t pmin = pack_pmin(seq0, pv.base, part);  // packs: earlier bins' queries are never peers
-    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kPfThreads) {
+    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kThr) {
       const int x = x0 + lane;
       const uint32_t w = x < nwords ? pw[x] & keep_from(pmin - 4 * x) : 0u;
       const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;  // bytes of peers before q
@@ -1232,7 +1251,7 @@ __global__ __launch_bounds__(kPfThreads, 8) void k_pf_count(PrefilterArgs a, uin
     const int nwords = (nsubP + 3) >> 2;
     const uint32_t* pw = cnt + pv.seg * (kPeerRegion / 4);
     const int32_t pmin = pack_pmin(seq0, pv.base, part);
-    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kPfThreads) {
+    for (int x0 = (pmin >> 2) + wv * 64; x0 < nwords; x0 += kThr) {
       const int x = x0 + lane;
       const uint32_t w = x < nwords ? pw[x] & keep_from(pmin - 4 * x) : 0u;
       const int valid = x < nwords ? min(4, nsubP - 4 * x) : 0;
@@ -1437,9 +1456,13 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
   if (!attr_set_on_device(k_attr_prefilter)) {
     hipError_t e = hipFuncSetAttribute((const void*)k_pf_full, hipFuncAttributeMaxDynamicSharedMemorySize, full_most);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_pf_count<0>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+      e = hipFuncSetAttribute((const void*)k_pf_count<0, kPfWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              count_most);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)k_pf_count<2>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+      e = hipFuncSetAttribute((const void*)k_pf_count<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, count_most);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)k_pf_count<2, kPfWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              count_most);
     if (e != hipSuccess) return e;
     mark_attr_set(k_attr_prefilter);
   }
@@ -1454,9 +1477,11 @@ hipError_t launch_prefilter(const PrefilterArgs& a, hipStream_t st, int mode) {
     const uint32_t tab_off = (uint32_t)(kCentBase + sub);
     size_t lds = tab_off + pf_count_table_bytes(a.nlist_cap) + 16;  // (+16: the table copy's last vector)
     if (mode == 3)  // the timing probe: every phase but the count loop, into scratch outputs (UMICLUST_PFPROBE)
-      hipLaunchKernelGGL(k_pf_count<2>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
+      hipLaunchKernelGGL((k_pf_count<2, kPfWaves>), dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
+    else if ((int64_t)lds <= (int64_t)a.pf1_lds)  // small index: one-wave units
+      hipLaunchKernelGGL((k_pf_count<0, 1>), dim3(nqs * kParts), dim3(64), lds, st, a, tab_off);
     else
-      hipLaunchKernelGGL(k_pf_count<0>, dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
+      hipLaunchKernelGGL((k_pf_count<0, kPfWaves>), dim3(nqs * kParts), dim3(kPfThreads), lds, st, a, tab_off);
     if (mode == 1 || mode == 3) return hipGetLastError();
   }
   if (mode == 2 || a.nseg <= 1) {

@@ -90,6 +90,7 @@ struct PrefilterArgs {
   TileView peer[kPeerTiles];  // oldest first, the block's own tile last (absent ones: n = 0)
   int32_t peer_base;
   int32_t nlist_cap;       // list-table capacity of the lean counting kernel (>= k-mers x tiles)
+  int32_t pf1_lds;         // the lean counting kernel runs one-wave units when its LDS is at most this (bytes)
   // per-(query-strand, part) outputs, merged by launch_prefilter's last kernel: candidates (count >= the
   // threshold) as count << 24 | ordinal, unsorted, at most kPartCand (255 in pncand: overflow, re-run by
   // the full kernel, which writes its exact part top-41 in the same form)

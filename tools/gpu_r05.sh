@@ -29,7 +29,7 @@ for st in "$@"; do
     solo) # PMC collection serialises the dispatches: the kernel trace of this run holds every kernel's solo duration
           timeout -s KILL 400 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --stats --output-format csv -d "$out/solo" -o run -- \
              python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/solo.log" 2>&1; rc=$?
-          [ $rc = 0 ] && python3 tools/pmc_clock.py "$out/solo/run_counter_collection.csv" "k_pf_count<0>" "$out/pmc_clock_k_pf_count.json"
+          [ $rc = 0 ] && python3 tools/pmc_clock.py "$out/solo/run_counter_collection.csv" "k_pf_count<0, 4>" "$out/pmc_clock_k_pf_count.json"
           rm -f "$out/solo/run_kernel_trace.csv" "$out/solo/run_counter_collection.csv" ;;
     busy|busy2) # per-kernel totals only (the full counter CSV exceeds what a call may bring back)
           [ "$st" = busy ] && CT="$SQ" || CT="$SQ2"
@@ -62,6 +62,9 @@ for st in "$@"; do
     predab) for v in ${PREDS:-1 0}; do for c in ${PCFGS:-3 2 5}; do
               UMICLUST_PEER_PREDICT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/pred${v}_c$c.json" 2> "$out/pred${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    pf1ab) for v in ${PF1S:-10240 0}; do for c in ${PCFGS:-3 5 2}; do
+              UMICLUST_PF1=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/pf1_${v}_c$c.json" 2> "$out/pf1_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
