@@ -331,6 +331,7 @@ struct umiclust_ctx {
   int32_t index_end = 0;          // centroid ordinals [0, index_end) are indexed
   int32_t pass_B = 0;
   hipStream_t st_b = nullptr, st_copy = nullptr;
+  PinBuf<uint32_t> h_bpq, h_bpt, h_bres;  // round B's pairs and results (pinned: no staged copies on the host's path)
   hipStream_t st_al = nullptr;    // walk / alignment rounds / packing of the passes
   int32_t last_a_slot = -1;       // a_ev slot of the latest counting half
   hipEvent_t evb[2] = {nullptr, nullptr};
@@ -1162,8 +1163,13 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     c->hip(c->d_bpq.ensure(nb), "alloc");
     c->hip(c->d_bpt.ensure(nb), "alloc");
     c->hip(c->d_bres.ensure(nb), "alloc");
-    c->hip(hipMemcpyAsync(c->d_bpq.p, bpq.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
-    c->hip(hipMemcpyAsync(c->d_bpt.p, bpt.data(), (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+    c->hip(c->h_bpq.ensure(nb), "pin");
+    c->hip(c->h_bpt.ensure(nb), "pin");
+    c->hip(c->h_bres.ensure(nb), "pin");
+    memcpy(c->h_bpq.p, bpq.data(), (size_t)nb * 4);
+    memcpy(c->h_bpt.p, bpt.data(), (size_t)nb * 4);
+    c->hip(hipMemcpyAsync(c->d_bpq.p, c->h_bpq.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+    c->hip(hipMemcpyAsync(c->d_bpt.p, c->h_bpt.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
     c->hip(hipEventRecord(c->evb[0], sb), "event");
     // the pairs are in query order: one launch per run of one query length
     for (int32_t x0 = 0; x0 < nb;) {
@@ -1176,8 +1182,9 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       x0 = x1;
     }
     c->hip(hipEventRecord(c->evb[1], sb), "event");
-    c->hip(hipMemcpyAsync(bres.data(), c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
+    c->hip(hipMemcpyAsync(c->h_bres.p, c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
     c->hip(hipStreamSynchronize(sb), "sync");
+    memcpy(bres.data(), c->h_bres.p, (size_t)nb * 4);
     float bms = 0;
     c->hip(hipEventElapsedTime(&bms, c->evb[0], c->evb[1]), "elapsed");
     t_al += bms * 1e-3;

@@ -65,6 +65,13 @@ for st in "$@"; do
     pf1ab) for v in ${PF1S:-10240 0}; do for c in ${PCFGS:-3 5 2}; do
               UMICLUST_PF1=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/pf1_${v}_c$c.json" 2> "$out/pf1_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    c3trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c3trace" -o run -- \
+             python3 bench.py --config 3 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c3trace.log" 2>&1; rc=$?
+             [ $rc = 0 ] && python3 tools/kstats.py "$out/c3trace/run_kernel_stats.csv" 2 > "$out/c3trace_kstats.txt" 2>&1
+             rm -f "$out/c3trace/run_kernel_trace.csv" ;;
+    prab) for v in ${PRV:-00 10 11 01}; do for c in ${PCFGS:-3 5 2}; do
+              UMICLUST_PEER_PREDICT=${v:0:1} UMICLUST_RB_PRIO=${v:1:1} timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 \
+                --no-cpu-baseline --no-e2e > "$out/pr${v}_c$c.json" 2> "$out/pr${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
