@@ -750,3 +750,22 @@ def test_timeline_union_and_counter_cells():
     assert abs(busy - st["t_count_s"]) <= 0.02 * st["t_count_s"] + 1e-4
     assert an > 0 and 0 < abusy <= st["t_align_s"] * 1.02 + 1e-4
     assert 0 < st["counter_cells"] <= st["n_count_launches"] * 2 * 8192 * st["n_kept"]
+
+
+@pytest.mark.parametrize("pf1", ["0", str(1 << 30)])
+def test_counting_wave_layouts(pf1, monkeypatch):
+    """k_pf_count's two workgroup layouts (4 waves with block-wide scans, or one-wave units, UMICLUST_PF1 = the LDS
+    bound below which units run as one wave) forced over the whole config-1 bin: alignment count, cells and digests
+    equal the oracle's golden either way."""
+    from make_oracle_golden import digest
+    gold = dict(_golden_cases())["config1_round1_id093"]
+    monkeypatch.setenv("UMICLUST_PF1", pf1)
+    u = synth.config_umis(gold["config"], gold["scale"])
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(gold["preset"], gold["identity"], gold.get("minlen", 58), gold.get("maxlen", 68)),
+                 buf=u.seq, off=u.off)
+        st = ctx.cluster()
+        d = digest(ctx.fetch())
+    assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
+    for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
+        assert d[k] == gold[k], k
