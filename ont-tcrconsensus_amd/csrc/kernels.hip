@@ -1663,6 +1663,73 @@ __device__ __forceinline__ bool peer_relevant(const WalkState& w, uint32_t count
   return walk_open(w) || cand_key_dev(count, len, seqno) < w.lastkey;
 }
 
+// A peer whose own device walk has already accepted a hit -- within its first w candidates, with w plus its in-window
+// peer count <= kWalk, so no merge can push that hit out of its walk -- is certain to become a member, and members
+// never enter a query's merged walk: its alignment would never be read.  The peer's walk state is this pass's (an
+// in-block peer, after round 0's evaluation) or the previous block's pass's (final).  (A peer judged wrongly would
+// only cost a round-B alignment: the host aligns every needed peer the pass did not.)
+__device__ __forceinline__ bool certain_member(uint32_t ps, int32_t q0, int32_t nqb, int32_t both,
+                                               const WalkState* __restrict__ ws, const uint8_t* __restrict__ npeer,
+                                               const WalkState* __restrict__ ws_prev,
+                                               const uint8_t* __restrict__ npeer_prev, int32_t q0_prev,
+                                               int32_t nq_prev) {
+  const WalkState* W;
+  const uint8_t* NP;
+  int32_t base;
+  if ((int32_t)ps >= q0 && (int32_t)ps < q0 + nqb) {
+    W = ws;
+    NP = npeer;
+    base = q0;
+  } else if (ws_prev && (int32_t)ps >= q0_prev && (int32_t)ps < q0_prev + nq_prev) {
+    W = ws_prev;
+    NP = npeer_prev;
+    base = q0_prev;
+  } else {
+    return false;
+  }
+  for (int s = 0; s < both; s++) {
+    const int64_t i = (int64_t)((int32_t)ps - base) * both + s;
+    const uint32_t n = NP[i];
+    if (W[i].acc && n != 255u && (uint32_t)W[i].w + n <= (uint32_t)kWalk) return true;
+  }
+  return false;
+}
+
+// The relevant, not certainly-member peers of every query-strand as bit masks (aligned[qs * kPH + h], peers 64 h ..
+// 64 h + 63), one wave per query-strand, a lane per peer: the per-peer tests are dependent loads (the peer's id, then
+// its length and walk states), which a thread per query-strand ran in series over up to kPeerCap peers (~170 us per
+// launch on config 3's dense windows).  k_peer_pairs then allocates and emits the pairs from the masks.
+__global__ __launch_bounds__(256) void k_peer_rel(int32_t q0, int32_t w0, int32_t nqs, int32_t both,
+                                                  const uint8_t* __restrict__ lens, const WalkState* __restrict__ ws,
+                                                  const uint16_t* __restrict__ peer_id,
+                                                  const uint8_t* __restrict__ peer_count,
+                                                  const uint8_t* __restrict__ npeer,
+                                                  unsigned long long* __restrict__ aligned, int32_t emit,
+                                                  const WalkState* __restrict__ ws_prev,
+                                                  const uint8_t* __restrict__ npeer_prev, int32_t q0_prev,
+                                                  int32_t nq_prev) {
+  constexpr int kPH = kPeerCap / 64;
+  const int lane = threadIdx.x & 63;
+  const int qs = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);  // wave-uniform
+  if (qs >= nqs) return;
+  const int np = npeer[qs];
+  const bool any = np != 255 && np != 0 && emit;
+  const WalkState w = ws[qs];
+  const int32_t nqb = nqs / both;
+#pragma unroll
+  for (int hh = 0; hh < kPH; hh++) {
+    const int x = lane + 64 * hh;
+    bool r = false;
+    if (any && x < np) {
+      const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
+      r = peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
+          !certain_member(ps, q0, nqb, both, ws, npeer, ws_prev, npeer_prev, q0_prev, nq_prev);
+    }
+    const unsigned long long m = __ballot(r);
+    if (lane == 0) aligned[(int64_t)qs * kPH + hh] = m;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both,
                                                     const uint8_t* __restrict__ lens, const WalkState* __restrict__ ws,
                                                     const uint16_t* __restrict__ peer_id,
@@ -1677,49 +1744,11 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
   // one thread per (query, strand); the slots come from a wave-aggregated allocation per query length (seg_alloc)
   const int qs = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = qs < nqs;  // every lane stays to the slot allocation
-  const int np = live ? npeer[qs] : 0;
   constexpr int kPH = kPeerCap / 64;  // 64-bit masks per query-strand: peers 0..63, 64..127, ...
-  if (live)
-    for (int hh = 0; hh < kPH; hh++) aligned[(int64_t)qs * kPH + hh] = 0ull;
+  // the relevant, not certainly-member peers, from k_peer_rel (zero masks when nothing is emitted)
   unsigned long long rel[kPH] = {};
-  // A peer whose own device walk has already accepted a hit -- within its first w candidates, with w plus its
-  // in-window peer count <= kWalk, so no merge can push that hit out of its walk -- is certain to become a member,
-  // and members never enter a query's merged walk: its alignment would never be read.  The peer's walk state is
-  // this pass's (an in-block peer, after round 0's evaluation) or the previous block's pass's (final).  (A peer
-  // judged wrongly would only cost a round-B alignment: the host aligns every needed peer the pass did not.)
-  const int32_t nqb = nqs / both;
-  auto certain_member = [&](uint32_t ps) -> bool {
-    const WalkState* W;
-    const uint8_t* NP;
-    int32_t base;
-    if ((int32_t)ps >= q0 && (int32_t)ps < q0 + nqb) {
-      W = ws;
-      NP = npeer;
-      base = q0;
-    } else if (ws_prev && (int32_t)ps >= q0_prev && (int32_t)ps < q0_prev + nq_prev) {
-      W = ws_prev;
-      NP = npeer_prev;
-      base = q0_prev;
-    } else {
-      return false;
-    }
-    for (int s = 0; s < both; s++) {
-      const int64_t i = (int64_t)((int32_t)ps - base) * both + s;
-      const uint32_t n = NP[i];
-      if (W[i].acc && n != 255u && (uint32_t)W[i].w + n <= (uint32_t)kWalk) return true;
-    }
-    return false;
-  };
-  if (live && np != 255 && np != 0 && emit) {
-    const WalkState w = ws[qs];
-    for (int x = 0; x < np; x++) {
-      const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
-      // relevant, and not already certain to be a member
-      if (peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) && !certain_member(ps))
-        rel[x >> 6] |= 1ull << (x & 63);
-    }
-    for (int hh = 0; hh < kPH; hh++) aligned[(int64_t)qs * kPH + hh] = rel[hh];
-  }
+  if (live)
+    for (int hh = 0; hh < kPH; hh++) rel[hh] = aligned[(int64_t)qs * kPH + hh];
   const int32_t q = q0 + (live ? qs : 0) / both;
   const int ql = lens[q];
   uint32_t n = 0;
@@ -1731,8 +1760,9 @@ __global__ __launch_bounds__(256) void k_peer_pairs(int32_t q0, int32_t w0, int3
   uint32_t k = sg.base[si] + k0;
   const uint32_t qv = ((uint32_t)q << 1) | (uint32_t)(qs % both);
   uint32_t tl = 0;
-  for (int x = 0; x < np; x++)
-    if ((rel[x >> 6] >> (x & 63)) & 1ull) {
+  for (int hh = 0; hh < kPH; hh++)
+    for (unsigned long long m = rel[hh]; m; m &= m - 1ull) {
+      const int x = 64 * hh + __builtin_ctzll(m);
       const uint32_t t = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       pq[k] = qv;
       pt[k] = t;
@@ -1750,6 +1780,8 @@ hipError_t launch_peer_pairs(int32_t q0, int32_t w0, int32_t nqs, int32_t both, 
                              unsigned long long* aligned, int32_t emit, const WalkState* ws_prev,
                              const uint8_t* npeer_prev, int32_t q0_prev, int32_t nq_prev, hipStream_t st) {
   if (nqs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_peer_rel, dim3((nqs + 3) / 4), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
+                     peer_count, npeer, aligned, emit, ws_prev, npeer_prev, q0_prev, nq_prev);
   hipLaunchKernelGGL(k_peer_pairs, dim3((nqs + 255) / 256), dim3(256), 0, st, q0, w0, nqs, both, lens, ws, peer_id,
                      peer_count, npeer, pq, pt, outidx, sg, seg_cnt, cells, nstat, out0, aligned, emit, ws_prev,
                      npeer_prev, q0_prev, nq_prev);
