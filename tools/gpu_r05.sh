@@ -72,6 +72,14 @@ for st in "$@"; do
     prab) for v in ${PRV:-00 10 11 01}; do for c in ${PCFGS:-3 5 2}; do
               UMICLUST_PEER_PREDICT=${v:0:1} UMICLUST_RB_PRIO=${v:1:1} timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 \
                 --no-cpu-baseline --no-e2e > "$out/pr${v}_c$c.json" 2> "$out/pr${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    bandab) for v in ${BANDS:-140000 0 20000}; do for c in ${PCFGS:-3 5}; do
+              UMICLUST_BAND=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/band${v}_c$c.json" 2> "$out/band${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    tracefull) # the default bench command itself under the kernel tracer (the roofline's rocprof cross-check)
+          timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/tracefull" -o run -- \
+             python3 bench.py > "$out/tracefull.out" 2> "$out/tracefull.err"; rc=$?
+          [ $rc = 0 ] && python3 tools/kstats.py "$out/tracefull/run_kernel_stats.csv" 6 > "$out/tracefull_kstats.txt" 2>&1
+          rm -f "$out/tracefull/run_kernel_trace.csv" ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
