@@ -244,7 +244,8 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
         roof["survey"] = dict(bytes_per_launch=survey_bytes / max(1, n_cnt), counter_cells=counter_cells,
                               achieved=survey_bytes / t_cnt / 1e9, frac_hbm=survey_bytes / t_cnt / 1e9 / HBM_PEAK_GBS,
                               note="SURVEY 8d: postings x 4 B + C x 2 B per query-strand, C = centroids indexed at the "
-                                   "launch; the build stores u16 postings and u8 counters, so `achieved` uses 2 B")
+                                   "launch; the build stores u16 postings and u8 counters, so `achieved` uses 2 B; the "
+                                   "counters live in LDS, so this rate exceeds HBM's 8 TB/s (frac_hbm > 1) by design")
     if os.path.exists(cal_p) and os.path.exists(clk_p) and n_cnt:
         cal, clk = json.load(open(cal_p)), json.load(open(clk_p))
         atom = streamed / 64.0 / n_cnt
