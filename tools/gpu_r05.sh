@@ -80,6 +80,9 @@ for st in "$@"; do
              python3 bench.py > "$out/tracefull.out" 2> "$out/tracefull.err"; rc=$?
           [ $rc = 0 ] && python3 tools/kstats.py "$out/tracefull/run_kernel_stats.csv" 6 > "$out/tracefull_kstats.txt" 2>&1
           rm -f "$out/tracefull/run_kernel_trace.csv" ;;
+    pf2ab) for v in ${PF2S:-0 24576}; do for c in ${PCFGS:-2 3}; do
+              UMICLUST_PF2=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/pf2_${v}_c$c.json" 2> "$out/pf2_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
