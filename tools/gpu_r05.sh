@@ -83,6 +83,9 @@ for st in "$@"; do
     pf2ab) for v in ${PF2S:-0 24576}; do for c in ${PCFGS:-2 3}; do
               UMICLUST_PF2=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/pf2_${v}_c$c.json" 2> "$out/pf2_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    hqab) for v in ${HQS:-0 1 0 1}; do for c in ${PCFGS:-2}; do
+              UMICLUST_HQ_DIRECT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/hq${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
