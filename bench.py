@@ -305,6 +305,9 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
             g_dev = cells / ta / 1e9
             align["device"] = dict(union_s=ta, brackets=na, overlap=t_al / ta, gcups=g_dev, frac=g_dev / ceiling,
                                    gcups_computed=cells_c / ta / 1e9, frac_computed=cells_c / ta / 1e9 / ceiling)
+            if iss:
+                align["device"]["frac_issue"] = g_dev / iss["ceiling_gcups"]
+                align["device"]["frac_computed_issue"] = cells_c / ta / 1e9 / iss["ceiling_gcups"]
     return roof, align
 
 
