@@ -4,6 +4,8 @@
 #   steps: tests | smoke | bench | seq | trace | solo | busy | busy2 | fetch | write | pfprof | c3 | c4 | c5 | c5trace
 #          | sweep3 | sweep4 (SHARES=) | c4e2e (SCALE=, READLEN=)
 # The default bench line is config 2 under --threads 25 (policy O4, the reference's mode); `seq` is --threads 1.
+# Steps c3lazy, predab, prab, pf2ab and hqab drove A/B runs of experiments that lost and were removed:
+# their UMICLUST_* switches no longer exist, so they now run the default twice.
 set -o pipefail
 tag=${1:-r05}
 shift
