@@ -1663,39 +1663,37 @@ __device__ __forceinline__ bool peer_relevant(const WalkState& w, uint32_t count
   return walk_open(w) || cand_key_dev(count, len, seqno) < w.lastkey;
 }
 
-// A peer whose own device walk has already accepted a hit -- within its first w candidates, with w plus its in-window
-// peer count <= kWalk, so no merge can push that hit out of its walk -- is certain to become a member, and members
-// never enter a query's merged walk: its alignment would never be read.  The peer's walk state is this pass's (an
-// in-block peer, after round 0's evaluation) or the previous block's pass's (final).  (A peer judged wrongly would
-// only cost a round-B alignment: the host aligns every needed peer the pass did not.)
-__device__ __forceinline__ bool certain_member(uint32_t ps, int32_t q0, int32_t nqb, int32_t both,
+// A peer whose own device walk has already accepted a hit is (almost surely) going to be a member, and members never
+// enter a query's merged walk: its alignment would never be read.  Certain when w plus the peer's own in-window peer
+// count is <= kWalk (no merge can push that hit out of its walk); taken as a member whenever it accepted since round 5
+// (the rare peer that then turns out a centroid only costs a round-B alignment -- the host aligns every needed peer the
+// pass did not -- so the result never changes; configs 3 / 4: 6 % / 11 % fewer peer pairs, round-B pairs 10.7 k ->
+// 11.8 k per config-4 step, `profiles/r05/cert_relax_ab/`).  The peer's walk state is this pass's (an in-block peer,
+// after round 0's evaluation) or the previous block's pass's (final).
+__device__ __forceinline__ bool member_expected(uint32_t ps, int32_t q0, int32_t nqb, int32_t both,
                                                const WalkState* __restrict__ ws, const uint8_t* __restrict__ npeer,
                                                const WalkState* __restrict__ ws_prev,
                                                const uint8_t* __restrict__ npeer_prev, int32_t q0_prev,
                                                int32_t nq_prev) {
+  (void)npeer;
+  (void)npeer_prev;
   const WalkState* W;
-  const uint8_t* NP;
   int32_t base;
   if ((int32_t)ps >= q0 && (int32_t)ps < q0 + nqb) {
     W = ws;
-    NP = npeer;
     base = q0;
   } else if (ws_prev && (int32_t)ps >= q0_prev && (int32_t)ps < q0_prev + nq_prev) {
     W = ws_prev;
-    NP = npeer_prev;
     base = q0_prev;
   } else {
     return false;
   }
-  for (int s = 0; s < both; s++) {
-    const int64_t i = (int64_t)((int32_t)ps - base) * both + s;
-    const uint32_t n = NP[i];
-    if (W[i].acc && n != 255u && (uint32_t)W[i].w + n <= (uint32_t)kWalk) return true;
-  }
+  for (int s = 0; s < both; s++)
+    if (W[(int64_t)((int32_t)ps - base) * both + s].acc) return true;
   return false;
 }
 
-// The relevant, not certainly-member peers of every query-strand as bit masks (aligned[qs * kPH + h], peers 64 h ..
+// The relevant peers not expected to be members, of every query-strand as bit masks (aligned[qs * kPH + h], peers 64 h ..
 // 64 h + 63), one wave per query-strand, a lane per peer: the per-peer tests are dependent loads (the peer's id, then
 // its length and walk states), which a thread per query-strand ran in series over up to kPeerCap peers (~170 us per
 // launch on config 3's dense windows).  k_peer_pairs then allocates and emits the pairs from the masks.
@@ -1723,7 +1721,7 @@ __global__ __launch_bounds__(256) void k_peer_rel(int32_t q0, int32_t w0, int32_
     if (any && x < np) {
       const uint32_t ps = (uint32_t)(w0 + peer_id[(int64_t)qs * kPeerCap + x]);
       r = peer_relevant(w, peer_count[(int64_t)qs * kPeerCap + x], lens[ps], ps) &&
-          !certain_member(ps, q0, nqb, both, ws, npeer, ws_prev, npeer_prev, q0_prev, nq_prev);
+          !member_expected(ps, q0, nqb, both, ws, npeer, ws_prev, npeer_prev, q0_prev, nq_prev);
     }
     const unsigned long long m = __ballot(r);
     if (lane == 0) aligned[(int64_t)qs * kPH + hh] = m;
