@@ -381,6 +381,8 @@ struct umiclust_ctx {
   // relevant peers certain to become members are not aligned speculatively (config 2 4.02 -> 4.14 M, round 4)
   static constexpr bool peer_cert = true;
   int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
+  int32_t regrow = 8;        // UMICLUST_REGROW: clean shallow blocks before a halved block size doubles (0: never)
+  int32_t last_max_npeer = 0;
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
   DevBuf<uint32_t> d_probe;
   // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
@@ -1058,10 +1060,12 @@ void write_resolve_dump(const umiclust_ctx* c, const ResolveEnv& env, int32_t q0
 // Wait for a pass and resolve its block on the host in sorted order (resolve.cpp resolve_block).  Returns false if a
 // peer list overflowed (the caller re-runs the block in smaller pieces).
 bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<int32_t>& new_cents,
-                  double& t_pf, double& t_al, double& t_host) {
+                  double& t_pf, double& t_al, double& t_host, int32_t* resolved) {
   const int both = c->both;
-  const int32_t q0 = P.q0, nq = P.nq, w0 = P.w0;
-  const int32_t nqs = nq * both;
+  const int32_t q0 = P.q0, w0 = P.w0;
+  int32_t nq = P.nq;
+  int32_t nqs = nq * both;
+  if (resolved) *resolved = 0;
   const double tsync0 = now_s();
   c->hip(hipEventSynchronize(P.ev[4]), "sync");
   c->stats.t_sync_s += now_s() - tsync0;
@@ -1109,6 +1113,11 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   // are read in place, only for the query-strands whose relevant peers include a centroid
   const double tc0 = now_s();
   P.hq_copy.assign(P.h_hq.p, P.h_hq.p + nqs);
+  {
+    uint32_t mx = 0;  // the block's deepest peer list (regrowth: a window far from the cap may double)
+    for (int32_t qs = 0; qs < nqs; qs++) mx = std::max<uint32_t>(mx, P.hq_copy[qs].npeer);
+    c->last_max_npeer = (int32_t)mx;
+  }
   c->stats.t_sync_s += now_s() - tc0;
   c->dbg_t[1] += now_s() - tc0;
   const HostQs* hq = P.hq_copy.data();
@@ -1204,6 +1213,18 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   };
   ResolveStats rs;
   const double th0 = now_s();
+  // partial resolution (resolved != nullptr): the queries before the block's first overflowing one depend on earlier
+  // queries only, so they are resolved now and only the rest is re-run
+  bool partial = false;
+  if (resolved)
+    for (int32_t qs = 0; qs < nqs; qs++)
+      if (hq[qs].flags & 2u) {
+        if (qs / both == 0) return false;
+        nq = qs / both;
+        nqs = nq * both;
+        partial = true;
+        break;
+      }
   const int r = resolve_block(env, q0, nq, w0, hq, recs, state, P.rsx, *c->pool, new_cents, rs,
                               dump ? round_b_rec : RoundB(round_b));
   const double th = now_s() - th0;
@@ -1234,7 +1255,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     c->dbg_p[i] += rs.dbg_p[i];
     c->dbg_q[i] += rs.dbg_q[i];
   }
-  return true;
+  if (resolved) *resolved = nq;
+  return !partial;
 }
 
 // Append a block's new centroids (sorted seqnos) to the LSM index, enqueued on the main stream
@@ -1509,6 +1531,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   };
   split_blocks(s0, b_eff);
   int32_t nb = (int32_t)blocks.size();
+  int32_t clean = 0;  // blocks resolved since the last overflow (regrowth)
   std::vector<int32_t> new_cents;
   // Member tracebacks: tw_launch(lo, hi, stream) traces the members among seqnos [lo, hi) (their targets are final),
   // queries of <= 64 nt in a launch of their own (a one-stripe direction store: more waves per CU), appending to the
@@ -1565,15 +1588,18 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       if (T4) round_window(q, prevs, nprev, 0);
       enqueue_pass(c, P, q, m, prevs, nprev, c->solo_tile, 0);
       c->stats.n_reruns++;
-      if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+      int32_t done = 0;
+      const bool all = resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host, &done);
+      if (done > 0) {  // the whole piece, or its prefix before the first overflowing query
+        if (T4) pending.insert(pending.end(), new_cents.begin(), new_cents.end());
+        else append_centroids(c, new_cents);
+        c->stats.n_blocks++;
+        q += done;
+      }
+      if (!all && done == 0) {
         if (m == 1) c->fail(UMICLUST_EDEVICE, "peer overflow with block of 1");
         piece = std::max(1, m / 2);
-        continue;
       }
-      if (T4) pending.insert(pending.end(), new_cents.begin(), new_cents.end());
-      else append_centroids(c, new_cents);
-      c->stats.n_blocks++;
-      q += m;
     }
   };
   // Software pipeline over blocks, D = c->depth passes in flight: passes k+1 .. k+D-1 are queued before
@@ -1656,7 +1682,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       const double tb0 = now_s();
       if (k + 3 < nb) build_peer(k + 3, true);  // queries only: built while the host resolves block k
       c->dbg_t[5] += now_s() - tb0;
-      if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+      if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host, nullptr)) {
         // drain everything queued (its windows include block k) and restart the pipeline after block k
         c->hip(hipStreamSynchronize(c->st_al), "sync");
         c->hip(hipStreamSynchronize(c->st_b), "sync");
@@ -1702,7 +1728,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       t.seg = (k + D) % D;
       t.prebuilt = true;
     }
-    if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host)) {
+    int32_t done = 0;
+    if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host, &done)) {
       // drain the queued passes k+1 .. k+D-1 (their windows include block k) and restart the pipeline
       for (int i = 1; i < D; i++) {
         Pass& Q = c->pass[(k + i) % D];
@@ -1711,11 +1738,18 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
           Q.live = false;
         }
       }
+      // the block's prefix before its first overflowing query is resolved (its queries' peers are all earlier)
+      if (done > 0) {
+        if (T4) pending.insert(pending.end(), new_cents.begin(), new_cents.end());
+        else append_centroids(c, new_cents);
+        c->stats.n_blocks++;
+      }
       // an overflowing bin runs synchronous re-runs from here on: with other lanes sharing the GPU they queue behind
-        // every lane's work unless its main stream goes first (config 4: a 792k-read bin with a giant molecule took
-        // 7.2 s among 8 lanes, 0.6 s alone)
-        run_alone(blocks[k].first, blocks[k].second);
-        // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
+      // every lane's work unless its main stream goes first (config 4: a 792k-read bin with a giant molecule took
+      // 7.2 s among 8 lanes, 0.6 s alone)
+      run_alone(blocks[k].first + done, blocks[k].second - done);
+      clean = 0;
+      // deep clusters flood the peer window: later blocks are cut smaller (a smaller window holds fewer
       // same-molecule peers), so the overflow re-runs do not repeat block after block
       if (k + 1 < nb && halve(blocks[k].first)) {
         const int32_t from = blocks[k].first + blocks[k].second;
@@ -1732,6 +1766,21 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     c->stats.n_blocks++;
     lazy = c->lazy_permille > 0 && (int64_t)new_cents.size() * 1000 < (int64_t)blocks[k].second * c->lazy_permille;
     c->stats.n_lazy_passes += (lazy && k + D < nb) ? 1 : 0;
+    // Regrowth: after `regrow` consecutive blocks without an overflow whose deepest peer list stayed below a quarter of
+    // the cap, the blocks not yet queued are cut at twice the size.  With overflowing blocks resolved up to their first
+    // overflowing query (resolve_pass), a giant molecule's stretch no longer pins a bin at 256-query blocks: config 4's
+    // bin 200 7.0 -> 1.6 s among 8 lanes, config 4 6.51 -> 7.59 M UMIs/s; config 5's windows stay deep, so its blocks
+    // do not grow (3.33 / 3.36 M; ungated regrowth after 4 clean blocks: 2.47 M) -- profiles/r05/regrow_ab/.
+    if (c->last_max_npeer >= kPeerCap / 4) clean = 0;  // a deep window: no regrowth yet
+    if (c->regrow > 0 && b_eff < B && ++clean >= c->regrow && k + D < nb) {
+      b_eff = std::min<int32_t>(B, b_eff * 2);
+      clean = 0;
+      const int32_t from = blocks[k + D].first;
+      blocks.resize((size_t)k + D);
+      split_blocks(from, b_eff);
+      nb = (int32_t)blocks.size();
+      tile_of(k + D).prebuilt = false;
+    }
     if (k + D < nb) enqueue(k + D, D - 1);
   }
   }
@@ -2256,6 +2305,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
     c->pin = atoi(e) != 0;

@@ -88,6 +88,9 @@ for st in "$@"; do
     hqab) for v in ${HQS:-0 1 0 1}; do for c in ${PCFGS:-2}; do
               UMICLUST_HQ_DIRECT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/hq${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    regrowab) for v in ${REGS:-0 16 4}; do for c in ${PCFGS:-5 4}; do
+              UMICLUST_REGROW=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/rg${v}_c$c.json" 2> "$out/rg${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
