@@ -221,3 +221,31 @@ def test_o4_rerun_after_queued_pass(mix, T, monkeypatch):
     o = orc.cluster(_params(orc, 1, 0.90, T, (lo, hi)), seqs)
     _cmp(g, o)
     assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+
+
+def test_o4_partial_resolution_and_regrowth(monkeypatch):
+    """Round 5: a block whose peer list overflows is resolved up to its first overflowing query and only the rest is
+    re-run; blocks halved by overflows grow again after `UMICLUST_REGROW` clean, shallow blocks.  A deep molecule's
+    long reads sort first (overflowing windows), then shallow short reads (regrowth: fewer blocks than without it);
+    with regrowth off, after 1 and after 8 clean blocks, every query's walk, the clusters and the alignment totals
+    equal the O4 oracle's."""
+    monkeypatch.setenv("UMICLUST_BLOCK", "2048")
+    monkeypatch.setenv("ORC_WORKERS", "8")
+    deep = synth.make_umis(4, seed=61, max_reads=2500, mean_reads=1500.0, error_rate=0.08, split=(0.4, 0.3, 0.3),
+                           pattern_fwd=synth.UMI_FWD_LONG, pattern_rev=synth.UMI_REV_LONG, orient_mix=0.2)
+    plain = synth.make_umis(900, seed=62, max_reads=12000, orient_mix=0.2)
+    seqs = deep.as_list() + plain.as_list()
+    lens = (58, 110)
+    o = orc.cluster(_params(orc, 1, 0.90, 25, lens), seqs)
+    blocks = {}
+    for regrow in ("0", "1", "8"):
+        monkeypatch.setenv("UMICLUST_REGROW", regrow)
+        with _lib.Context(0) as ctx:
+            ctx.load(_lib.params(1, 0.90, *lens, threads=25), seqs)
+            st = ctx.cluster()
+            g = ctx.fetch()
+        assert st["n_reruns"] > 0  # overflows happened
+        _cmp(g, o)
+        assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
+        blocks[regrow] = st["n_blocks"]
+    assert blocks["1"] < blocks["0"], blocks  # the halved blocks grew again
