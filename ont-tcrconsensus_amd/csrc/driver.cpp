@@ -1469,6 +1469,13 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       } else {
         while (q0 + same < s1 && same < bcap && c->hlen[q0 + same] == c->hlen[q0]) same++;
       }
+      // O4: a block cut by the size cap ends at a round start (trimmed by < 1 round), so the next block's window needs
+      // no round tile: only blocks starting at a length change (or a bin start in a pack) still begin mid-round
+      // (same-box A/B: config 3 +2.2 %, config 5 +1.8 %, config 2 unchanged; profiles/r05/round_align_ab/)
+      if (c->o4_T && same == bcap && q0 + same < s1) {
+        const int32_t r = round_start(c, s0, q0 + same);
+        if (r > q0 + same / 2) same = r - q0;
+      }
       blocks.push_back({q0, same});
       q0 += same;
     }
