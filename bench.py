@@ -326,7 +326,7 @@ def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
             per = {c: v / n for c, v in agg[k].items() if isinstance(v, float) and c not in ("mean_us",)}
             cyc = per["GRBM_GUI_ACTIVE"] / cal["xcds"]
             return dict(source=os.path.relpath(agg_path, ROOT), calibration=os.path.relpath(cal_path, ROOT),
-                        dispatches=n, kernel_cycles=cyc,
+                        dispatches=n, kernel_cycles=cyc, lds_insts_per_dispatch=per.get("SQ_INSTS_LDS"),
                         lds_array_busy_per_cu=per["SQ_LDS_IDX_ACTIVE"] * cal["lds_idx_active_cycles_per_unit"] / cal["cus"] / cyc,
                         valu_busy_per_simd=per["SQ_ACTIVE_INST_VALU"] * cal["active_inst_valu_cycles_per_unit"] / (cal["cus"] * 4) / cyc,
                         lds_bank_conflict_frac=per.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, per["SQ_LDS_IDX_ACTIVE"]),
@@ -617,6 +617,16 @@ def main() -> None:
             busy = pmc_busy("k_pf_count")
             if busy:
                 roof["pmc"] = busy
+                lds = roof.get("lds")
+                if lds and busy.get("lds_insts_per_dispatch"):
+                    # SQ_INSTS_LDS of a PMC-serialised launch split into the counting atomics (one ds_add_u32
+                    # wave-instruction per 64 streamed postings) and the rest: list-table reads/writes, counter
+                    # zeroing, the threshold scan and the peer/candidate phases
+                    tot = busy["lds_insts_per_dispatch"]
+                    lds["insts_split"] = dict(lds_insts=tot, atomics=lds["atomic_wave_instrs_per_launch"],
+                                              other=tot - lds["atomic_wave_instrs_per_launch"],
+                                              atomic_share=lds["atomic_wave_instrs_per_launch"] / tot,
+                                              source=busy["source"])
         if args.config in (3, 4):
             # per-bin wall times of the last step, measured while `lanes` bins share the GPU (so they do not
             # add up to the step): the largest bin bounds any split of these bins over GPUs
