@@ -1266,6 +1266,7 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
   hipStream_t st = c->ix_st ? c->ix_st : c->st;
   if (c->ix_st && c->last_r_ev) c->hip(hipStreamWaitEvent(st, c->last_r_ev, 0), "wait");
   const int32_t ord0 = (int32_t)c->cent.size();
+  int32_t s2o_lo = 0, s2o_n = 0, bo_lo = 0, bo_n = 0;
   for (int32_t q : new_cents) {  // capacity reserved: no reallocation
     c->cent.push_back(q);
     c->cent_len.push_back(c->hlen[q]);
@@ -1275,11 +1276,8 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
     // seqno -> ordinal for the merge's flagged hits (the new centroids are in sorted order)
     const int32_t s0 = c->bin_s[c->cur_bin];
     for (size_t i = 0; i < new_cents.size(); i++) c->h_seq2ord.p[new_cents[i] - s0] = ord0 + (int32_t)i;
-    const int32_t lo = new_cents.front() - s0, hi = new_cents.back() - s0;
-    if (hi >= lo)
-      c->hip(hipMemcpyAsync(c->d_seq2ord.p + lo, c->h_seq2ord.p + lo, (size_t)(hi - lo + 1) * 4, hipMemcpyHostToDevice,
-                            st),
-             "h2d seq2ord");
+    s2o_lo = new_cents.front() - s0;
+    s2o_n = std::max(0, new_cents.back() - s0 - s2o_lo + 1);
   }
   if (c->pack_on) {
     // a bin's first query is always a centroid (nothing of its bin precedes it): its ordinal opens the bin's range
@@ -1293,17 +1291,19 @@ void append_centroids(umiclust_ctx* c, const std::vector<int32_t>& new_cents) {
         bhi = std::max(bhi, b);
       }
     }
-    if (bhi >= blo)
-      c->hip(hipMemcpyAsync(c->d_bin_ord0.p + blo, c->h_bin_ord0.p + blo, (size_t)(bhi - blo + 1) * 4,
-                            hipMemcpyHostToDevice, st),
-             "h2d bin ord0");
+    if (bhi >= blo) {
+      bo_lo = blo;
+      bo_n = bhi - blo + 1;
+    }
   }
   memcpy(c->h_cent.p + ord0, c->cent.data() + ord0, new_cents.size() * 4);
   memcpy(c->h_cent_len.p + ord0, c->cent_len.data() + ord0, new_cents.size());
-  c->hip(hipMemcpyAsync(c->d_cent.p + ord0, c->h_cent.p + ord0, new_cents.size() * 4, hipMemcpyHostToDevice, st),
-         "h2d cent");
-  c->hip(hipMemcpyAsync(c->d_cent_len.p + ord0, c->h_cent_len.p + ord0, new_cents.size(), hipMemcpyHostToDevice, st),
-         "h2d cent len");
+  // one dispatch reads the pinned ranges (as the copies it replaces, at its execution time)
+  c->hip(launch_append_stage(c->h_cent.p + ord0, c->h_cent_len.p + ord0, (int32_t)new_cents.size(), c->d_cent.p + ord0,
+                             c->d_cent_len.p + ord0, c->h_seq2ord.p + s2o_lo, c->d_seq2ord.p + s2o_lo, s2o_n,
+                             bo_n ? c->h_bin_ord0.p + bo_lo : nullptr, bo_n ? c->d_bin_ord0.p + bo_lo : nullptr, bo_n,
+                             st),
+         "append stage");
   const int32_t ordend = (int32_t)c->cent.size();
   if (c->nix >= c->ix_events.size()) {
     hipEvent_t e0, e1;

@@ -372,6 +372,34 @@ __global__ __launch_bounds__(256) void k_index_fill(const uint16_t* __restrict__
   if (x + 64 < n) post[atomicAdd(&cursor[pb | k[x + 64]], 1u)] = val;
 }
 
+// An index append's host-side arrays (new centroids' seqnos and lengths, the seq -> ordinal range they fill, the
+// bins they open) go to the device in one dispatch that reads the pinned host buffers over the bus, instead of up to
+// four hipMemcpyAsync blit copies, each a kernel dispatch of its own queued on the append's stream.
+__global__ __launch_bounds__(256) void k_append_stage(const int32_t* __restrict__ hc, const uint8_t* __restrict__ hl,
+                                                      int32_t n, int32_t* __restrict__ dc, uint8_t* __restrict__ dl,
+                                                      const int32_t* __restrict__ hs, int32_t* __restrict__ ds,
+                                                      int32_t ns, const int32_t* __restrict__ hb,
+                                                      int32_t* __restrict__ db, int32_t nb) {
+  const int32_t m = max(n, max(ns, nb));
+  for (int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x); i < m; i += (int32_t)(gridDim.x * 256)) {
+    if (i < n) {
+      dc[i] = hc[i];
+      dl[i] = hl[i];
+    }
+    if (i < ns) ds[i] = hs[i];
+    if (i < nb) db[i] = hb[i];
+  }
+}
+hipError_t launch_append_stage(const int32_t* hc, const uint8_t* hl, int32_t n, int32_t* dc, uint8_t* dl,
+                               const int32_t* hs, int32_t* ds, int32_t ns, const int32_t* hb, int32_t* db, int32_t nb,
+                               hipStream_t st) {
+  const int32_t m = std::max(n, std::max(ns, nb));
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_append_stage, dim3((unsigned)std::min(64, (m + 255) / 256)), dim3(256), 0, st, hc, hl, n, dc,
+                     dl, hs, ds, ns, hb, db, nb);
+  return hipGetLastError();
+}
+
 hipError_t launch_index_count(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
                               int32_t count, int32_t xoff, uint32_t* hist, hipStream_t st) {
   if (count <= 0) return hipSuccess;

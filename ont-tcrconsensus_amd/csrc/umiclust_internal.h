@@ -52,6 +52,11 @@ hipError_t launch_index_scan(uint32_t* hist, uint32_t* partial, uint32_t* off, u
 hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
                              int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod, uint32_t* cursor,
                              uint16_t* post, hipStream_t st);
+// the host-to-device half of an index append in one dispatch: n centroid seqnos / lengths, ns seq -> ordinal entries
+// and nb bin-start ordinals, each read from pinned host memory and written to its device array
+hipError_t launch_append_stage(const int32_t* hc, const uint8_t* hl, int32_t n, int32_t* dc, uint8_t* dl,
+                               const int32_t* hs, int32_t* ds, int32_t ns, const int32_t* hb, int32_t* db, int32_t nb,
+                               hipStream_t st);
 // prefilter: for query-strands qs in [0, nqs): query seqno = q0 + qs/2 (or qs if !both), strand.
 // postings-touched partial sums: slots counters[16 + 32 s], s < kPostSpread (separate L2 lines)
 constexpr int kPostSpread = 32;
