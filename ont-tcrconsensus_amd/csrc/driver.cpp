@@ -640,7 +640,10 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_hq.ensure(nqs), "alloc");
   c->hip(P.d_paligned.ensure((size_t)nqs * (kPeerCap / 64)), "alloc");  // 64-bit aligned-peer masks per query-strand
   c->hip(P.d_ws.ensure(nqs), "alloc");
-  c->hip(P.d_reccount.ensure(1), "alloc");
+  if (!P.d_reccount.p) {  // [0] record words allocated, [1] k_pack's workgroup tickets; k_pack leaves both zero
+    c->hip(P.d_reccount.ensure(2), "alloc");
+    c->hip(hipMemsetAsync(P.d_reccount.p, 0, 8, c->st), "memset");
+  }
   c->hip(P.h_hq.ensure(nqs), "pin");
   c->hip(P.h_rec.ensure(nqs * kRecWords), "pin");
   c->hip(P.d_rec.ensure(nqs * kRecWords), "alloc");
@@ -908,17 +911,15 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipEventRecord(P.ev[3], st), "event");
   // what the host needs goes straight to pinned host memory; the pass that next reuses these
   // buffers is enqueued only after the host has waited for ev[4]
-  c->hip(hipMemsetAsync(P.d_reccount.p, 0, 4, st), "memset");
   // rec_direct: k_pack writes the outcomes and records straight into the pinned host buffers (no DMA copies on the
   // chain the host waits for: a 3 MB record copy was 0.14 ms per config-2 block); otherwise device buffers + copies
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
                      P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_paligned.p, P.d_reccount.p,
                      c->rec_direct ? P.h_hq.p : P.d_hq.p,
-                     c->rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, st),
+                     c->rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, P.h_reccount.p, st),
          "pack");
   if (!c->rec_direct)
     c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
-  c->hip(hipMemcpyAsync(P.h_reccount.p, P.d_reccount.p, 4, hipMemcpyDeviceToHost, st), "d2h record count");
   if (!c->rec_direct) {
     const size_t est = std::min<size_t>(P.rec_est, P.d_rec.n);
     c->hip(hipMemcpyAsync(P.h_rec.p, P.d_rec.p, est * 4, hipMemcpyDeviceToHost, st), "d2h records");

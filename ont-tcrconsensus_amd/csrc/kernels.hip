@@ -1835,7 +1835,8 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
                                               const unsigned long long* __restrict__ aligned,
                                               uint32_t* __restrict__ reccount,
                                               HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
-                                              const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters) {
+                                              const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters,
+                                              uint32_t* __restrict__ hreccount) {
   __shared__ uint32_t wsize[kPackWaves * kPackQ];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qs0 = ((int)blockIdx.x * kPackWaves + wave) * kPackQ;
@@ -1890,6 +1891,15 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
     const uint32_t b0 = tot ? atomicAdd(reccount, tot) : 0u;
     for (int i = 0; i < kPackWaves * kPackQ; i++)
       if (wsize[i] != 0xffffffffu) wsize[i] += b0;
+    // the workgroup taking the last ticket (reccount[1]) sees every allocation: it writes the record total to
+    // pinned host memory and re-zeroes both counters for the buffer set's next pass, so the chain the host waits on
+    // holds no memset and no 4-byte copy (each a blit dispatch)
+    __threadfence();
+    if (atomicAdd(reccount + 1, 1u) == gridDim.x - 1) {
+      *hreccount = atomicAdd(reccount, 0u);
+      atomicExch(reccount, 0u);
+      atomicExch(reccount + 1, 0u);
+    }
   }
   __syncthreads();
   // phase 2: records and outcomes
@@ -1972,12 +1982,17 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
                        const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
-                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, hipStream_t st) {
-  if (nqs <= 0) return hipSuccess;
+                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, uint32_t* hreccount,
+                       hipStream_t st) {
+  if (nqs <= 0) {
+    *hreccount = 0;  // no launch: nothing of this pass is in flight on the buffer set
+    return hipSuccess;
+  }
   constexpr int per = kPackWaves * kPackQ;
   hipLaunchKernelGGL(k_pack, dim3((nqs + per - 1) / per), dim3(64 * kPackWaves), 0, st, nqs, w0, lens,
                      ws, ntop, top_seqno, top_count,
-                     res, npeer, peer_id, peer_count, peer_res, aligned, reccount, hq, rec, counters, hcounters);
+                     res, npeer, peer_id, peer_count, peer_res, aligned, reccount, hq, rec, counters, hcounters,
+                     hreccount);
   return hipGetLastError();
 }
 
