@@ -151,6 +151,7 @@ struct Fail {
 struct Pass {
   int32_t q0 = 0, nq = 0, w0 = 0;  // block [q0, q0+nq), peer window [w0, q0+nq)
   bool live = false;
+  bool rec_direct = false;  // this pass's outcomes and records written by k_pack into pinned host memory
   PinBuf<TileView> h_tiles;
   DevBuf<TileView> d_tiles;
   DevBuf<uint32_t> d_top_seqno;
@@ -375,6 +376,7 @@ struct umiclust_ctx {
   // UMIs/s, the direct PCIe writes held k_pack at 133 us on the pass chain), direct with several (config 3, 8 lanes:
   // 7.56-7.60 vs 6.42-6.47 M: the lanes' copy dispatches contend for the hardware queues).
   bool rec_direct = false;
+  static constexpr int32_t kDirectRecQ = 4096;  // blocks of at most this many queries write their records directly
   int32_t mix_len = -1;  // -1: bins whose default block is below kMaxBlock (the bin has < 16 x kMaxBlock queries)
   // speculative walk below this best k-mer count (20 and 30 equal, 45 slower: profiles/r03/spec_ab)
   static constexpr int32_t spec_thr = 30;
@@ -911,16 +913,19 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   c->hip(hipEventRecord(P.ev[3], st), "event");
   // what the host needs goes straight to pinned host memory; the pass that next reuses these
   // buffers is enqueued only after the host has waited for ev[4]
+  // small blocks (deep clusters: config 5's ~2k-query blocks) write directly too: their copies are dispatch-bound
+  // (`profiles/r05/recdirect_small_ab/`: config 5 3.52 -> 3.64 M UMIs/s, config 2's 8k-query blocks lose with it)
+  P.rec_direct = c->rec_direct || nq <= umiclust_ctx::kDirectRecQ;
   // rec_direct: k_pack writes the outcomes and records straight into the pinned host buffers (no DMA copies on the
   // chain the host waits for: a 3 MB record copy was 0.14 ms per config-2 block); otherwise device buffers + copies
   c->hip(launch_pack(nqs, w0, c->d_lens.p, P.d_ws.p, P.d_ntop.p, P.d_top_seqno.p, P.d_top_count.p, P.d_res.p,
                      P.d_npeer.p, P.d_peer_id.p, P.d_peer_count.p, P.d_res.p + peer_out0, P.d_paligned.p, P.d_reccount.p,
-                     c->rec_direct ? P.h_hq.p : P.d_hq.p,
-                     c->rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, P.h_reccount.p, st),
+                     P.rec_direct ? P.h_hq.p : P.d_hq.p,
+                     P.rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, P.h_reccount.p, st),
          "pack");
-  if (!c->rec_direct)
+  if (!P.rec_direct)
     c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
-  if (!c->rec_direct) {
+  if (!P.rec_direct) {
     const size_t est = std::min<size_t>(P.rec_est, P.d_rec.n);
     c->hip(hipMemcpyAsync(P.h_rec.p, P.d_rec.p, est * 4, hipMemcpyDeviceToHost, st), "d2h records");
   }
@@ -1094,7 +1099,7 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   {
     // records past the DMA'd prefix (a pass that used more than the estimate): fetch the rest now
     const size_t used = *P.h_reccount.p, est = std::min<size_t>(P.rec_est, P.d_rec.n);
-    if (used > est && !c->rec_direct) {
+    if (used > est && !P.rec_direct) {
       c->hip(hipMemcpyAsync(P.h_rec.p + est, P.d_rec.p + est, (used - est) * 4, hipMemcpyDeviceToHost, c->st_copy),
              "d2h records");
       c->hip(hipStreamSynchronize(c->st_copy), "sync");
