@@ -172,15 +172,24 @@ def cpu_baseline_threads(umis, n_sample: int, identity: float, lens, preset: int
                 seconds=dt, n_kept=r["stats"]["kept"])
 
 
-def full_bin_cpu_reference(config: int) -> dict | None:
-    """The oracle's measured wall time over the whole config-2 bin (tests/golden/make_oracle_golden.py)."""
-    path = os.path.join(ROOT, "tests", "golden", f"oracle_config{config}.json")
+def full_bin_cpu_reference(config: int, threads: int, identity: float) -> dict | None:
+    """The oracle's measured wall time over the whole bin of `config` (tests/golden/make_oracle_golden.py), under the
+    policy `threads` selects: O4 (vsearch --threads n, oracle_o4.json: the round's searches on `oracle_workers` OpenMP
+    threads) or the sequential definition (oracle_config<N>.json, 1 thread)."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    path = os.path.join(gold, "oracle_o4.json") if threads > 1 else os.path.join(gold, f"oracle_config{config}.json")
     if not os.path.exists(path):
         return None
-    for name, g in json.load(open(path)).items():
-        if g.get("scale") == 1.0 and "oracle_seconds" in g:
-            return dict(case=name, seconds=g["oracle_seconds"], umis_per_s=g["n_reads"] / g["oracle_seconds"],
-                        threads=g.get("oracle_threads", 1), host_cpu=g.get("host_cpu"))
+    for name, g in sorted(json.load(open(path)).items()):
+        if g.get("config") == config and g.get("scale") == 1.0 and "oracle_seconds" in g and "n_bins" not in g \
+                and abs(g.get("identity", -1) - identity) < 1e-9 and g.get("preset") == 1:
+            workers = g.get("oracle_workers", g.get("oracle_threads", 1))
+            return dict(case=name, source=os.path.relpath(path, ROOT), seconds=g["oracle_seconds"],
+                        umis_per_s=g["n_reads"] / g["oracle_seconds"], n_reads=g["n_reads"],
+                        policy=policy_name(g.get("T", 1) if threads > 1 else 1),
+                        workers=workers, host_cpu=g.get("host_cpu"),
+                        note="the C oracle over the whole bin when it generated the golden (the builder's container, "
+                             f"{workers} worker thread(s)), not this box")
     return None
 
 
@@ -393,9 +402,10 @@ def main() -> None:
                     help="vsearch --threads of every bin: > 1 = policy O4 (rounds of that many queries, the mode the "
                          "reference runs: vsearch_umi_cluster.py:33-34, utils.py:56-63, n >= 25), 1 = the sequential "
                          "definition")
-    ap.add_argument("--cpu-sample", type=int, default=40000)
-    ap.add_argument("--cpu-sample-mt", type=int, default=40000,
-                    help="reads of the multi-threaded (vsearch --threads) CPU baseline's prefix")
+    ap.add_argument("--cpu-sample", type=int, default=40000,
+                    help="reads of the sequential (--threads 1) CPU side figure's prefix")
+    ap.add_argument("--cpu-sample-mt", type=int, default=200000,
+                    help="reads of the CPU baseline's prefix in vsearch's --threads mode (the GPU line's policy)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the file leg (config 2, N = 1)")
     ap.add_argument("--lanes", type=int, default=8,
@@ -426,6 +436,11 @@ def main() -> None:
                     help="--e2e-files: length of the synthetic full read in each header's seq= field (production reads "
                          "are ~1,500 nt, SURVEY §8d; 800 is the longest whose 70M-record inputs and round-1 outputs fit "
                          "the GPU box's ~270 GiB host-memory cap on /dev/shm; 32 = SURVEY's --short-read)")
+    ap.add_argument("--ranks-share-device", action="store_true",
+                    help="testing only: every rank uses device 0 (rehearses the --gpus N path on a one-GPU box)")
+    ap.add_argument("--digest-out", default="",
+                    help="configs 3/4: each rank writes {bin index: digest} of its bins' last-step results to "
+                         "<digest-out>.rank<r>.json (parity checks of the sharded path)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="measured HBM bytes per prefilter launch (rocprofv3 PMC pass), if present")
     args = ap.parse_args()
@@ -469,11 +484,17 @@ def main() -> None:
     import torch
     dist = None
     if world > 1:
+        # the only cross-rank operations are a barrier and two host-scalar reductions (the bins shard with no data-path
+        # collective): gloo over the host, so no RCCL communicator is ever initialised
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (there is no CPU backend)")
+    ndev = torch.cuda.device_count()
+    if args.ranks_share_device:
+        local_rank = 0  # testing only: every rank on device 0 (a 1-GPU box rehearsing the N-rank path)
+    elif local_rank >= ndev:
+        raise SystemExit(f"bench.py: local rank {local_rank} but {ndev} visible device(s) (one rank per GPU)")
     torch.cuda.set_device(local_rank)
 
     if args.identity is None:
@@ -566,8 +587,7 @@ def main() -> None:
     my_umis = sum(s["n_kept"] for s in stats[-1])
     tot_umis = my_umis
     if dist is not None:
-        t = torch.tensor([elapsed, float(my_umis)], dtype=torch.float64,
-                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([elapsed, float(my_umis)], dtype=torch.float64)
         tm = t.clone()
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -579,6 +599,13 @@ def main() -> None:
     value = total_umis / t_max
     gcups = cells * (world if args.config in (2, 5) else 1) * args.steps / t_max / 1e9
 
+    if args.digest_out and runners:
+        # every rank's bins (indices into the node's bin list) and their digests, per round
+        dg = {"rank": rank, "world": world, "bins": [int(i) for i in sel], "rounds": []}
+        for r in runners:
+            dg["rounds"].append({str(int(sel[b])): binset.digest(x) for b, x in enumerate(r.results())})
+        with open(f"{args.digest_out}.rank{rank}.json", "w") as fh:
+            json.dump(dg, fh)
     if rank == 0:
         flat = [s for st in stats for s in st]
         roof, align = roofline(flat, args.config, args.traffic_json, tl_union)
@@ -650,12 +677,18 @@ def main() -> None:
                 if args.threads > 1:  # the same policy as the GPU line
                     cpu = cpu_baseline_threads(umis, args.cpu_sample_mt, args.identity, lens, threads=args.threads)
                     cpu["serial_1thread"] = cpu_baseline_prefix(umis, args.cpu_sample, args.identity, lens)
+                    cpu["serial_1thread"]["policy"] = policy_name(1)
                 else:
                     cpu = cpu_baseline_prefix(umis, args.cpu_sample, args.identity, lens)
                 cpu["policy"] = policy_name(args.threads)
-                full = full_bin_cpu_reference(args.config)
+                # the whole bin under the line's policy (tests/golden: the oracle's own wall time when it made the
+                # golden), the other policy's whole-bin figure as a labelled side field
+                full = full_bin_cpu_reference(args.config, args.threads, args.identity)
                 if full:
                     cpu["full_bin_oracle"] = full
+                other = full_bin_cpu_reference(args.config, 1 if args.threads > 1 else 25, args.identity)
+                if other:
+                    cpu["full_bin_oracle_other_policy"] = other
             else:
                 cpu = cpu_baseline_bins(runners[0].binset.bins, args.identity, lens)
         out["cpu_baseline"] = cpu

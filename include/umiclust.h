@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define UMICLUST_ABI_VERSION 8
+#define UMICLUST_ABI_VERSION 9
 
 /* error codes (negative returns) */
 #define UMICLUST_OK 0
@@ -69,7 +69,7 @@ typedef struct umiclust_params {
                              against the index frozen at the round's start, then re-checked in order against
                              the round's new centroids (inserted into its hit list by k-mer count and
                              re-walked one alignment at a time).  umiclust_params_from_argv sets 1 whenever
-                             the argv's --threads is > 1 (the reference's --threads 25: since round 5, ABI 7),
+                             the argv's --threads is > 1 (the reference's --threads 25: since round 5, ABI 8),
                              unless the environment has UMICLUST_O4=sequential. */
 } umiclust_params;
 
@@ -112,6 +112,8 @@ typedef struct umiclust_stats {
                                      0 since round 5: the deferral was removed) */
   int64_t counter_cells;  /* ABI 8: sum over the counting launches of query-strands x centroids indexed (the C of
                              SURVEY 8d's prefilter bytes, postings x 4 B + C x 2 B counter traffic) */
+  int64_t n_regrows;      /* ABI 9: times a block size halved by a peer-list overflow doubled again (after `regrow`
+                             clean, shallow blocks; UMICLUST_REGROW) */
 } umiclust_stats;
 
 typedef struct umiclust_ctx umiclust_ctx;

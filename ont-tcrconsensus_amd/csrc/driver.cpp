@@ -211,15 +211,54 @@ struct Timeline {
   hipEvent_t ref = nullptr;
   int dev = -1;
   std::vector<std::pair<float, float>> iv[2];
+  // intervals ending below fold_hi[kind] are folded into folded_ms[kind] (their union's measure) once iv[kind] grows
+  // past kTlCap, so that a long run does not grow the vectors without bound; later intervals are clipped at fold_hi
+  double folded_ms[2] = {0.0, 0.0};
+  float fold_hi[2] = {-1e30f, -1e30f};
+  int64_t n[2] = {0, 0};
 };
 static Timeline g_tl;
-static void tl_add(int kind, hipEvent_t a, hipEvent_t b) {
+constexpr size_t kTlCap = 1 << 16, kTlKeep = 4096;  // keep the latest kTlKeep merged intervals unfolded (late arrivals)
+
+// union of sorted intervals: merges v in place, returns the measure
+static double tl_merge(std::vector<std::pair<float, float>>& v) {
+  std::sort(v.begin(), v.end());
+  size_t w = 0;
+  double tot = 0.0;
+  for (size_t i = 0; i < v.size(); i++) {
+    if (w > 0 && v[i].first <= v[w - 1].second) {
+      v[w - 1].second = std::max(v[w - 1].second, v[i].second);
+    } else {
+      v[w++] = v[i];
+    }
+  }
+  v.resize(w);
+  for (const auto& x : v) tot += x.second - x.first;
+  return tot;
+}
+
+static void tl_add(int dev, int kind, hipEvent_t a, hipEvent_t b) {
   std::lock_guard<std::mutex> lk(g_tl.m);
-  if (!g_tl.ref) return;
+  if (!g_tl.ref || dev != g_tl.dev) return;  // events of another device than the reference's: not comparable
   float t0 = 0.f, t1 = 0.f;
-  if (hipEventElapsedTime(&t0, g_tl.ref, a) != hipSuccess || hipEventElapsedTime(&t1, g_tl.ref, b) != hipSuccess)
+  if (hipEventElapsedTime(&t0, g_tl.ref, a) != hipSuccess || hipEventElapsedTime(&t1, g_tl.ref, b) != hipSuccess) {
+    (void)hipGetLastError();  // measurement only: never leave a sticky error for the caller's next launch check
     return;
-  g_tl.iv[kind].emplace_back(t0, t1);
+  }
+  g_tl.n[kind]++;
+  t0 = std::max(t0, g_tl.fold_hi[kind]);
+  if (t1 <= t0) return;
+  auto& v = g_tl.iv[kind];
+  v.emplace_back(t0, t1);
+  if (v.size() > kTlCap) {
+    tl_merge(v);
+    if (v.size() > kTlKeep) {
+      const size_t f = v.size() - kTlKeep;
+      for (size_t i = 0; i < f; i++) g_tl.folded_ms[kind] += v[i].second - v[i].first;
+      g_tl.fold_hi[kind] = v[f - 1].second;
+      v.erase(v.begin(), v.begin() + (ptrdiff_t)f);
+    }
+  }
 }
 
 struct umiclust_ctx {
@@ -1086,16 +1125,16 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     t_pf += ms * 1e-3;
     c->stats.t_count_s += ms * 1e-3;
     c->stats.n_count_launches++;
-    tl_add(0, c->a_ev[P.t_slot][0], c->a_ev[P.t_slot][1]);
+    tl_add(c->dev, 0, c->a_ev[P.t_slot][0], c->a_ev[P.t_slot][1]);
   } else if (P.c_timed) {
     c->hip(hipEventElapsedTime(&ms, P.ev_c[0], P.ev_c[1]), "elapsed");
     c->stats.t_count_s += ms * 1e-3;
     c->stats.n_count_launches++;
-    tl_add(0, P.ev_c[0], P.ev_c[1]);
+    tl_add(c->dev, 0, P.ev_c[0], P.ev_c[1]);
   }
   c->hip(hipEventElapsedTime(&ms, P.ev[2], P.ev[3]), "elapsed");
   t_al += ms * 1e-3;
-  tl_add(1, P.ev[2], P.ev[3]);
+  tl_add(c->dev, 1, P.ev[2], P.ev[3]);
   {
     // records past the DMA'd prefix (a pass that used more than the estimate): fetch the rest now
     const size_t used = *P.h_reccount.p, est = std::min<size_t>(P.rec_est, P.d_rec.n);
@@ -1784,9 +1823,11 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     // overflowing query (resolve_pass), a giant molecule's stretch no longer pins a bin at 256-query blocks: config 4's
     // bin 200 7.0 -> 1.6 s among 8 lanes, config 4 6.51 -> 7.59 M UMIs/s; config 5's windows stay deep, so its blocks
     // do not grow (3.33 / 3.36 M; ungated regrowth after 4 clean blocks: 2.47 M) -- profiles/r05/regrow_ab/.
-    if (c->last_max_npeer >= kPeerCap / 4) clean = 0;  // a deep window: no regrowth yet
-    if (c->regrow > 0 && b_eff < B && ++clean >= c->regrow && k + D < nb) {
+    if (c->last_max_npeer >= kPeerCap / 4) {
+      clean = 0;  // a deep window: no regrowth yet, and it does not count as a clean block
+    } else if (c->regrow > 0 && b_eff < B && ++clean >= c->regrow && k + D < nb) {
       b_eff = std::min<int32_t>(B, b_eff * 2);
+      c->stats.n_regrows++;
       clean = 0;
       const int32_t from = blocks[k + D].first;
       blocks.resize((size_t)k + D);
@@ -2229,6 +2270,31 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
 }  // namespace
 
 // ====================================================================== C ABI
+// Retired or misspelled UMICLUST_* switches fail loudly (once per process, on stderr) instead of being ignored in
+// silence: every switch the library or its Python binding reads is listed here.
+extern char** environ;
+static void warn_unknown_env() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    static const char* const known[] = {
+        "BAND", "BLOCK", "DEBUG", "IO_THREADS", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
+        "PFPROF", "PIN", "REGROW", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        // read by the Python side (umiclust/, bench.py)
+        "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
+    for (char** e = environ; e && *e; e++) {
+      if (strncmp(*e, "UMICLUST_", 9) != 0) continue;
+      const char* name = *e + 9;
+      const char* eq = strchr(name, '=');
+      const size_t len = eq ? (size_t)(eq - name) : strlen(name);
+      bool ok = false;
+      for (const char* k : known) ok = ok || (strlen(k) == len && strncmp(k, name, len) == 0);
+      if (!ok)
+        fprintf(stderr, "umiclust: warning: unknown environment variable UMICLUST_%.*s ignored (retired or misspelled)\n",
+                (int)len, name);
+    }
+  });
+}
+
 extern "C" {
 
 int32_t umiclust_abi_version(void) { return UMICLUST_ABI_VERSION; }
@@ -2237,36 +2303,34 @@ int32_t umiclust_timeline(int32_t device_id, int32_t kind, int32_t reset, double
   if (kind < 0 || kind > 1) return UMICLUST_EINVAL;
   std::lock_guard<std::mutex> lk(g_tl.m);
   if (reset) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);  // the reset must not move the caller's thread to another device
     if (hipSetDevice(device_id) != hipSuccess) return UMICLUST_EDEVICE;
     if (g_tl.ref && g_tl.dev != device_id) {
       (void)hipEventDestroy(g_tl.ref);
       g_tl.ref = nullptr;
     }
+    int32_t rc = 0;
     if (!g_tl.ref && hipEventCreate(&g_tl.ref) != hipSuccess) {
       g_tl.ref = nullptr;
-      return UMICLUST_EDEVICE;
+      rc = UMICLUST_EDEVICE;
     }
+    if (rc == 0 && (hipEventRecord(g_tl.ref, nullptr) != hipSuccess || hipEventSynchronize(g_tl.ref) != hipSuccess))
+      rc = UMICLUST_EDEVICE;
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (rc) return rc;
     g_tl.dev = device_id;
-    if (hipEventRecord(g_tl.ref, nullptr) != hipSuccess || hipEventSynchronize(g_tl.ref) != hipSuccess)
-      return UMICLUST_EDEVICE;
-    g_tl.iv[0].clear();
-    g_tl.iv[1].clear();
+    for (int k = 0; k < 2; k++) {
+      g_tl.iv[k].clear();
+      g_tl.folded_ms[k] = 0.0;
+      g_tl.fold_hi[k] = -1e30f;
+      g_tl.n[k] = 0;
+    }
   }
   std::vector<std::pair<float, float>> v = g_tl.iv[kind];
-  std::sort(v.begin(), v.end());
-  double tot = 0.0, hi = -1e30, lo = 0.0;
-  for (const auto& x : v) {
-    if (x.first > hi) {
-      if (hi > lo) tot += hi - lo;
-      lo = x.first;
-      hi = x.second;
-    } else if (x.second > hi) {
-      hi = x.second;
-    }
-  }
-  if (!v.empty() && hi > lo) tot += hi - lo;
+  const double tot = g_tl.folded_ms[kind] + tl_merge(v);
   if (busy_s) *busy_s = tot * 1e-3;
-  if (launches) *launches = (int64_t)v.size();
+  if (launches) *launches = g_tl.n[kind];
   return 0;
 }
 
@@ -2314,6 +2378,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
     if (err) *err = UMICLUST_EDEVICE;
     return nullptr;
   }
+  warn_unknown_env();
   if (const char* e = getenv("UMICLUST_BAND")) c->band_pairs = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_MIXLEN")) c->mix_len = atoi(e) != 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));

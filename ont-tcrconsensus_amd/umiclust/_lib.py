@@ -85,6 +85,7 @@ class Stats(C.Structure):
         ("n_count_launches", C.c_int64),
         ("kmer_postings_deferred", C.c_int64),
         ("counter_cells", C.c_int64),
+        ("n_regrows", C.c_int64),
     ]
 
     def as_dict(self) -> dict:
@@ -114,6 +115,7 @@ EXPORTS = [
     "umiclust_timeline",
 ]
 OVERLAP_MAX_REGIONS = 4096
+ABI_VERSION = 9  # include/umiclust.h UMICLUST_ABI_VERSION: the struct layouts below
 
 _lib = None
 
@@ -128,6 +130,9 @@ def lib() -> C.CDLL:
     L = C.CDLL(LIB_PATH)
     P = C.POINTER
     L.umiclust_abi_version.restype = C.c_int32
+    if L.umiclust_abi_version() != ABI_VERSION:  # a stale build would read the structs with the wrong layout
+        raise UmiclustError(-22, f"{LIB_PATH} has ABI {L.umiclust_abi_version()}, this binding expects "
+                                 f"{ABI_VERSION}: rebuild (make -C ont-tcrconsensus_amd)")
     L.umiclust_params_init.restype = C.c_int32
     L.umiclust_params_init.argtypes = [P(Params), C.c_int32, C.c_double, C.c_int32, C.c_int32]
     L.umiclust_params_from_argv.restype = C.c_int32

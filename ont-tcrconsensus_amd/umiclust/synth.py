@@ -230,10 +230,11 @@ def _make_bin(args) -> Bin:
                                                                               max_reads=reads))
 
 
-def config_bins(config: int, scale: float = 1.0, barcodes=None, workers: int = 1) -> list:
+def config_bins(config: int, scale: float = 1.0, barcodes=None, workers: int = 1, shard_ids=None) -> list:
     """BASELINE configs 3 (10M reads, seed 1003) and 4 (70M reads, seed 1004, round 1 input): 24 barcodes
     x 40 Zipf(1.1) region bins of 64-nt dual UMIs (R10.4.1-like 1.5 % errors, NegBin(20, 2) reads per
-    molecule).  `scale` multiplies every bin's read count; `barcodes` restricts the barcodes built.
+    molecule).  `scale` multiplies every bin's read count; `barcodes` restricts the barcodes built, `shard_ids`
+    the bins (shard id = barcode * 40 + region; e.g. [200] = config 4's giant-molecule bin alone).
     Every bin has its own seed, so `workers` > 1 (spawned processes) gives identical bins."""
     if config not in CONFIG_TOTAL_READS:
         raise ValueError(config)
@@ -243,6 +244,8 @@ def config_bins(config: int, scale: float = 1.0, barcodes=None, workers: int = 1
     for b in range(N_BARCODES) if barcodes is None else barcodes:
         for k in range(BINS_PER_BARCODE):
             sid = b * BINS_PER_BARCODE + k
+            if shard_ids is not None and sid not in shard_ids:
+                continue
             jobs.append((b, k, sid, seed0 * 1_000_003 + sid, int(sizes[b, k])))
     if workers <= 1:
         return [_make_bin(j) for j in jobs]

@@ -28,3 +28,20 @@ def gpu_ctx():
     ctx = _lib.Context(0)
     yield ctx
     ctx.close()
+
+
+_BINSETS = {}
+
+
+@pytest.fixture(scope="session")
+def config_binset():
+    """Synthetic BASELINE multi-bin inputs (umiclust.synth.config_bins, deterministic per bin), built once per session
+    and shared by the tests that cluster them (config 3 at full size is ~9.9M reads)."""
+    def get(cfg: int, scale: float, shard_ids=None):
+        from umiclust import synth
+        key = (cfg, scale, tuple(shard_ids) if shard_ids is not None else None)
+        if key not in _BINSETS:
+            _BINSETS[key] = synth.concat_bins(synth.config_bins(cfg, scale, workers=min(16, os.cpu_count() or 4),
+                                                                shard_ids=shard_ids))
+        return _BINSETS[key]
+    return get

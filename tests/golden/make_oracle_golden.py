@@ -146,6 +146,17 @@ O4_CASES = {
     "config4_rounds_s0002_o4T25": (4, 0.002, None, None, 25),
     # the headline bin (BASELINE config 2, 2M reads, id 0.90) at full size under --threads 25
     "config2_round1_id090_o4T25": (2, 1.0, 1, 0.90, 25),
+    # round 6: the sizes bench.py runs -- config 3 whole (960 bins, ~9.9M reads), config 4 at
+    # 2 % scale both rounds, config 5's 300k-read bench bin at --id 0.75
+    "config3_bins_s1_o4T25": (3, 1.0, None, None, 25),
+    "config4_rounds_s002_o4T25": (4, 0.02, None, None, 25),
+    "config5_round1_id075_s1_o4T25": (5, 1.0, 1, 0.75, 25),
+}
+# single bins of a multi-bin config at full size, both rounds: name -> (config, scale, shard ids, T).  Bin 200
+# (barcode 6, region 0: 792k reads, a giant molecule) is config 4's slowest unit, where bench.py partially resolves
+# overflowing blocks, re-runs their rest and regrows the block size
+O4_BIN_CASES = {
+    "config4_bin200_rounds_o4T25": (4, 1.0, [200], 25),
 }
 
 
@@ -161,12 +172,19 @@ def main_o4(names):
     path = os.path.join(HERE, "oracle_o4.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
     for name in names:
-        cfg, scale, preset, idn, T = O4_CASES[name]
+        sids = None
+        if name in O4_BIN_CASES:
+            cfg, scale, sids, T = O4_BIN_CASES[name]
+            preset = idn = None
+        else:
+            cfg, scale, preset, idn, T = O4_CASES[name]
         lo, hi = synth.CONFIG_LENGTHS[cfg]
         t0 = time.perf_counter()
         if preset is None:
-            bs = synth.concat_bins(synth.config_bins(cfg, scale, workers=4))
+            bs = synth.concat_bins(synth.config_bins(cfg, scale, workers=4, shard_ids=sids))
             d = dict(config=cfg, scale=scale, n_bins=len(bs.bins), n_reads=int(bs.n), minlen=lo, maxlen=hi, T=T)
+            if sids is not None:
+                d["shard_ids"] = list(sids)
             rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if cfg == 4 else [])
             for rname, prm in rounds:
                 op = _o4(orc.params(prm["preset"], prm["identity"], lo, hi), T)
@@ -213,7 +231,7 @@ def main_segments():
 if __name__ == "__main__":
     args = sys.argv[1:]
     if args and args[0] == "o4":
-        main_o4(args[1:] or list(O4_CASES))
+        main_o4(args[1:] or list(O4_CASES) + list(O4_BIN_CASES))
     elif args and args[0] == "segments":
         main_segments()
     elif args and args[0] == "multibin":

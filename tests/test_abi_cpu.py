@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     for name in declared:
         assert hasattr(lib, name), name
-    assert _lib.lib().umiclust_abi_version() == 8
+    assert _lib.lib().umiclust_abi_version() == 9
 
 
 def test_argv_matches_reference():

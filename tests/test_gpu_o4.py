@@ -175,14 +175,49 @@ def test_o4_config_vs_oracle_golden(gpu_ctx, name, gold):
         assert d[k] == gold[k], k
 
 
-@pytest.mark.parametrize("name,gold", _O4_MULTI, ids=[k for k, _ in _O4_MULTI])
-@pytest.mark.parametrize("lanes,pack", [(1, 0), (8, 200000), (4, 3000)])
-def test_o4_multibin_vs_oracle_golden(name, gold, lanes, pack):
-    """Configs 3 (960 Zipf bins) and 4 (both rounds) at reduced scale under --threads 25, as bench.py runs them
-    (8 lanes, packs of 200k reads, the largest bin's lane prioritised), bin by bin on one lane, and in small packs on
-    4 lanes: every bin's digest and cluster count, the alignment count and cells equal the oracle's."""
+def _structure_ok(res, lens):
+    """--clusterout_sort order, one centroid per cluster, every member no longer than its centroid."""
+    cl = np.asarray(res["cluster"])
+    k = int(res["n_clusters"])
+    kept = cl >= 0
+    sizes = np.bincount(cl[kept], minlength=k)
+    cen = np.asarray(res["centroid"]) == 1
+    cen_len = np.zeros(k, np.int64)
+    cen_len[cl[cen]] = lens[cen]
+    return (bool(np.all(np.diff(sizes) <= 0)) and int(cen.sum()) == k and len(res["consensus"]) == k
+            and bool(np.all(lens[kept] <= cen_len[cl[kept]])))
+
+
+def _multi_cases():
+    """(name, gold, lanes, pack): reduced-scale goldens bin by bin on one lane, as bench.py runs them (8 lanes, packs of
+    200k reads) and in small packs on 4 lanes; the bench-size goldens (round 6: config 3 whole, config 4 at 2 % and
+    its giant-molecule bin 200 at full size) as bench.py runs them, and config 3 also bin by bin."""
+    out = []
+    for name, gold in _O4_MULTI:
+        if gold["scale"] < 0.02:
+            combos = [(1, 0), (8, 200000), (4, 3000)]
+        elif gold["config"] == 3:
+            combos = [(8, 200000), (1, 0)]
+        else:
+            combos = [(8, 200000)]
+        out += [(name, gold, lanes, pack) for lanes, pack in combos]
+    return out
+
+
+_MULTI_CASES = _multi_cases()
+
+
+@pytest.mark.parametrize("name,gold,lanes,pack", _MULTI_CASES,
+                         ids=[f"{n}-l{la}-p{pk}" for n, _, la, pk in _MULTI_CASES])
+def test_o4_multibin_vs_oracle_golden(name, gold, lanes, pack, config_binset):
+    """Configs 3 (960 Zipf bins) and 4 (both rounds) under --threads 25, as bench.py runs them (8 lanes, packs of
+    200k reads, the largest bin's lane prioritised: bench.py's BinRunner call), bin by bin on one lane, and in small
+    packs on 4 lanes: every bin's digest and cluster count, the alignment count and cells equal the oracle's
+    (tests/golden/make_oracle_golden.py o4).  At bench size: config 3 whole (~9.9M reads), config 4 at 2 % scale and
+    config 4's bin 200 alone at full size (792k reads with a giant molecule), whose round 1 overflows peer lists,
+    resolves the overflowing blocks up to the overflow, re-runs the rest and regrows the halved block size."""
     from umiclust import binset
-    bs = synth.concat_bins(synth.config_bins(gold["config"], gold["scale"], workers=4))
+    bs = config_binset(gold["config"], gold["scale"], gold.get("shard_ids"))
     assert len(bs.bins) == gold["n_bins"] and bs.n == gold["n_reads"]
     rounds = [("round1", binset.ROUND1)] + ([("round2", binset.ROUND2)] if "round2" in gold else [])
     for rname, prm in rounds:
@@ -197,6 +232,11 @@ def test_o4_multibin_vs_oracle_golden(name, gold, lanes, pack):
         assert [x["n_clusters"] for x in dg] == g["n_clusters"], rname
         assert sum(x["n_alignments"] for x in st) == g["alignments"] and sum(x["cells"] for x in st) == g["cells"]
         assert binset.combine(dg) == g["combined"], rname
+        for b, r in enumerate(res):  # (the full-size config-3 run of round 5 checked only this, sequential policy)
+            assert _structure_ok(r, np.diff(bs.bins[b].umis.off)), (rname, b)
+        if gold.get("shard_ids") == [200] and rname == "round1":
+            # the production-depth mechanisms are exercised: overflow re-runs after partial resolution, regrowth
+            assert sum(x["n_reruns"] for x in st) > 0 and sum(x["n_regrows"] for x in st) > 0, st
         if rname == "round1":
             bs = binset.round2_binset(bs, res)
 

@@ -680,42 +680,6 @@ def test_stage_prepare_equals_load():
         ctx.prepare(_lib.params(1, 0.93, 58, 68))  # nothing staged
 
 
-def _structure_ok(res, lens):
-    cl = np.asarray(res["cluster"])
-    k = int(res["n_clusters"])
-    kept = cl >= 0
-    sizes = np.bincount(cl[kept], minlength=k)
-    cen = np.asarray(res["centroid"]) == 1
-    cen_len = np.zeros(k, np.int64)
-    cen_len[cl[cen]] = lens[cen]
-    return (bool(np.all(np.diff(sizes) <= 0)) and int(cen.sum()) == k and len(res["consensus"]) == k
-            and bool(np.all(lens[kept] <= cen_len[cl[kept]])))
-
-
-def test_full_size_config3_lanes_and_packs():
-    """BASELINE config 3 at full size (960 bins, ~9.9M reads), as the bench runs it (8 lanes, packs of up to 200k
-    reads) and bin by bin on one lane: every bin's membership, strands, centroids and consensus are the same both ways,
-    the alignment totals match, and every bin is structurally valid (--clusterout_sort order, one centroid per cluster,
-    centroids the longest of their clusters)."""
-    from umiclust import binset
-    bs = synth.concat_bins(synth.config_bins(3, 1.0, workers=16))
-    out = []
-    for lanes, pack in ((8, 200000), (1, 0)):
-        with _lib.Context(0) as ctx:
-            run = binset.BinRunner(ctx, bs, binset.ROUND1["preset"], binset.ROUND1["identity"],
-                                   *synth.CONFIG_LENGTHS[3], lanes=lanes, pack_reads=pack)
-            st = run.cluster_all()
-            res = run.results()
-            run.close()
-        out.append((st, res))
-    (sa, ra), (sb, rb) = out
-    assert sum(x["n_alignments"] for x in sa) == sum(x["n_alignments"] for x in sb)
-    assert sum(x["cells"] for x in sa) == sum(x["cells"] for x in sb)
-    for b, (x, y) in enumerate(zip(ra, rb)):
-        assert binset.digest(x) == binset.digest(y), b
-        assert _structure_ok(x, np.diff(bs.bins[b].umis.off)), b
-
-
 @pytest.mark.parametrize("name", ["config1_round1_id093", "config1_round2_id097"])
 def test_parallel_inorder_phase_every_block(name, monkeypatch):
     """The dependency-ordered in-order resolve phase on the pool (resolve.cpp, on by default from 4096 open queries)

@@ -68,3 +68,33 @@ def test_config3_bins_through_shard_on_gpu(tmp_path):
     assert [[r["n_kept"], r["n_clusters"], r["cells"]] for _, r in sorted(res1, key=lambda x: x[0])] == res2
     for _, tag in bins:
         assert _read_dir(os.path.join(tmp, "w1", tag)) == _read_dir(os.path.join(tmp, "w2", tag)), tag
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_partition_and_digests(tmp_path):
+    """bench.py's own N-rank path: `--gpus 2` relaunches itself through torch.distributed.run,
+    the ranks rendezvous over gloo (no RCCL communicator: the only cross-rank operations are a barrier and two
+    host-scalar reductions), each rank clusters its LPT share of config 3's 960 bins (both ranks on device 0 here).
+    The ranks' shares partition the bins, the JSON line reports n_gpus 2, and the per-bin digests, put back in bin
+    order, equal the O4 oracle golden of the whole set (tests/golden/oracle_o4.json config3_bins_s001_o4T25)."""
+    import subprocess
+    import sys
+    from umiclust import binset
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gold = json.load(open(os.path.join(root, "tests", "golden", "oracle_o4.json")))["config3_bins_s001_o4T25"]
+    dg = str(tmp_path / "dg")
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "3", "--scale",
+                        str(gold["scale"]), "--steps", "1", "--warmup", "0", "--ranks-share-device", "--digest-out", dg,
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=540, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["scaling"] == "strong"
+    ranks = [json.load(open(f"{dg}.rank{r}.json")) for r in range(2)]
+    b0, b1 = set(ranks[0]["bins"]), set(ranks[1]["bins"])
+    assert not (b0 & b1) and b0 | b1 == set(range(gold["n_bins"])) and b0 and b1
+    per_bin = {**ranks[0]["rounds"][0], **ranks[1]["rounds"][0]}
+    dgs = [per_bin[str(b)] for b in range(gold["n_bins"])]
+    assert [d["n_clusters"] for d in dgs] == gold["round1"]["n_clusters"]
+    assert binset.combine(dgs) == gold["round1"]["combined"]

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 GPU session steps.  Every GPU step has its own time limit; the first failure ends the call.
-# Usage: bash tools/gpu_r05.sh <tag> <steps...>
+# GPU session steps (round 6).  Every GPU step has its own time limit; the first failure ends the call.
+# Usage: bash tools/gpu_r06.sh <tag> <steps...>
 #   steps: tests | smoke | bench | seq | trace | solo | busy | busy2 | fetch | write | pfprof | c3 | c4 | c5 | c5trace
-#          | sweep3 | sweep4 (SHARES=) | c4e2e (SCALE=, READLEN=)
+#          | sweep3 | sweep4 (SHARES=) | c4e2e (SCALE=, READLEN=) | resdump | default | tracefull | pf1ab | bandab
+#          | regrowab | valu | c3trace
 # The default bench line is config 2 under --threads 25 (policy O4, the reference's mode); `seq` is --threads 1.
-# Steps c3lazy, predab, prab, pf2ab and hqab drove A/B runs of experiments that lost and were removed:
-# their UMICLUST_* switches no longer exist, so they now run the default twice.
+# (The round-5 script's c3lazy / predab / prab / pf2ab / hqab steps drove switches that no longer exist: removed.)
 set -o pipefail
-tag=${1:-r05}
+tag=${1:-r06}
 shift
 out=gpurun_out/$tag
 mkdir -p "$out"
@@ -58,12 +58,6 @@ for st in "$@"; do
              > "$out/c4e2e.json" 2> "$out/c4e2e.err"; rc=$? ;;
     valu) timeout -k 10 120 ./tools/valu_rate > "$out/valu_rate.jsonl" 2>&1; rc=$? ;;
     default) timeout -k 10 700 python3 -u bench.py > "$out/bench_default.json" 2> "$out/bench_default.err"; rc=$? ;;
-    c3lazy) for z in ${LAZYS:-5 1000}; do
-              UMICLUST_LAZY=$z timeout -k 10 300 python3 -u bench.py --config 3 --steps 2 --warmup 1 --no-cpu-baseline \
-                > "$out/c3_lazy$z.json" 2> "$out/c3_lazy$z.err" || { rc=$?; break; }; rc=0; done ;;
-    predab) for v in ${PREDS:-1 0}; do for c in ${PCFGS:-3 2 5}; do
-              UMICLUST_PEER_PREDICT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
-                > "$out/pred${v}_c$c.json" 2> "$out/pred${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     pf1ab) for v in ${PF1S:-10240 0}; do for c in ${PCFGS:-3 5 2}; do
               UMICLUST_PF1=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/pf1_${v}_c$c.json" 2> "$out/pf1_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
@@ -71,9 +65,6 @@ for st in "$@"; do
              python3 bench.py --config 3 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c3trace.log" 2>&1; rc=$?
              [ $rc = 0 ] && python3 tools/kstats.py "$out/c3trace/run_kernel_stats.csv" 2 > "$out/c3trace_kstats.txt" 2>&1
              rm -f "$out/c3trace/run_kernel_trace.csv" ;;
-    prab) for v in ${PRV:-00 10 11 01}; do for c in ${PCFGS:-3 5 2}; do
-              UMICLUST_PEER_PREDICT=${v:0:1} UMICLUST_RB_PRIO=${v:1:1} timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 \
-                --no-cpu-baseline --no-e2e > "$out/pr${v}_c$c.json" 2> "$out/pr${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     bandab) for v in ${BANDS:-140000 0 20000}; do for c in ${PCFGS:-3 5}; do
               UMICLUST_BAND=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/band${v}_c$c.json" 2> "$out/band${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
@@ -82,15 +73,11 @@ for st in "$@"; do
              python3 bench.py > "$out/tracefull.out" 2> "$out/tracefull.err"; rc=$?
           [ $rc = 0 ] && python3 tools/kstats.py "$out/tracefull/run_kernel_stats.csv" 6 > "$out/tracefull_kstats.txt" 2>&1
           rm -f "$out/tracefull/run_kernel_trace.csv" ;;
-    pf2ab) for v in ${PF2S:-0 24576}; do for c in ${PCFGS:-2 3}; do
-              UMICLUST_PF2=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
-                > "$out/pf2_${v}_c$c.json" 2> "$out/pf2_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
-    hqab) for v in ${HQS:-0 1 0 1}; do for c in ${PCFGS:-2}; do
-              UMICLUST_HQ_DIRECT=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
-                > "$out/hq${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     regrowab) for v in ${REGS:-0 16 4}; do for c in ${PCFGS:-5 4}; do
               UMICLUST_REGROW=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/rg${v}_c$c.json" 2> "$out/rg${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
+          timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac
   echo "== $st rc=$rc $(date +%T)"
