@@ -309,8 +309,10 @@ struct umiclust_ctx {
   bool staged = false;
   std::vector<uint32_t> rec_len;
   PinBuf<int32_t> h_perm;          // the sorted order's pinned mirror (perm upload)
-  DevBuf<uint32_t> d_amb;
+  DevBuf<uint32_t> d_amb;    // [0] an ambiguous code was seen, [1] sequences whose masked output differs from the input
   PinBuf<uint32_t> h_amb;
+  int64_t n_changed = 0;     // h_amb[1] of the last prepare: 0 -> the cluster files print the input bytes
+  DevBuf<uint8_t> d_mchg;    // [sorted seqno] 1: its masked output differs from its input (the writer needs that row)
   PinBuf<uint16_t> h_xm;
   DevBuf<uint16_t> d_xm;
   // packs (umiclust_cluster_pack, multi-bin loads): sorted seqno -> load bin, each bin's first seqno and its first
@@ -422,6 +424,7 @@ struct umiclust_ctx {
   // relevant peers certain to become members are not aligned speculatively (config 2 4.02 -> 4.14 M, round 4)
   static constexpr bool peer_cert = true;
   int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
+  int32_t arrange = 3;       // UMICLUST_ARRANGE: bank-aware posting order in centroid tiles (1) / peer tiles (2)
   int32_t regrow = 8;        // UMICLUST_REGROW: clean shallow blocks before a halved block size doubles (0: never)
   int32_t last_max_npeer = 0;
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
@@ -637,6 +640,9 @@ void build_tile(umiclust_ctx* c, Tile& t, const int32_t* map, int32_t first, int
   c->hip(launch_index_scan(t.hist.p, t.partial.p, t.off.p, t.cursor.p, post, st), "index scan");
   c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, vbase, seg_mod, t.cursor.p, post, st),
          "index fill");
+  // bank-aware posting order (kernels.hip k_list_arrange): centroid tiles (bit 0) and peer / round tiles (bit 1)
+  if (n > 0 && (c->arrange & (vbase >= kCentBase ? 1 : 2)))
+    c->hip(launch_index_arrange(t.off.p, post, st), "index arrange");
   t.n = n;
   t.built_n = n;
 }
@@ -2144,13 +2150,14 @@ void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
     c->hip(launch_iota(c->d_iota.p, (int32_t)ns, c->st), "iota");
     c->iota_n = ns;
   }
-  c->hip(c->d_amb.ensure(1), "alloc");
-  c->hip(c->h_amb.ensure(1), "pin");
-  c->hip(hipMemsetAsync(c->d_amb.p, 0, 4, c->st), "memset");
+  c->hip(c->d_amb.ensure(2), "alloc");
+  c->hip(c->h_amb.ensure(2), "pin");
+  c->hip(hipMemsetAsync(c->d_amb.p, 0, 8, c->st), "memset");
+  c->hip(c->d_mchg.ensure((size_t)std::max(c->n, 1)), "alloc");
   c->hip(launch_prep(c->d_ascii.p, c->d_offs.p, c->d_perm.p, c->n, p->qmask_dust, c->d_codes.p,
-                     c->d_lens.p, c->d_kmers.p, c->d_nk.p, c->d_masked.p, c->d_amb.p, c->st),
+                     c->d_lens.p, c->d_kmers.p, c->d_nk.p, c->d_masked.p, c->d_amb.p, c->st, c->d_mchg.p),
          "prep");
-  c->hip(hipMemcpyAsync(c->h_amb.p, c->d_amb.p, 4, hipMemcpyDeviceToHost, c->st), "d2h");
+  c->hip(hipMemcpyAsync(c->h_amb.p, c->d_amb.p, 8, hipMemcpyDeviceToHost, c->st), "d2h");
   c->hqbin.clear();
   if (nbins > 1 && c->n > 0) {
     // packs: per-bin XOR masks on the k-mers (a bijection within a bin: counts within a bin are unchanged; other
@@ -2178,7 +2185,8 @@ void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
     c->hip(launch_kmer_xor(c->d_kmers.p, c->d_nk.p, c->n, c->d_qbin.p, c->d_xm.p, c->st), "k-mer masks");
   }
   c->hip(hipStreamSynchronize(c->st), "sync load");
-  c->ambig = *c->h_amb.p != 0;
+  c->ambig = c->h_amb.p[0] != 0;
+  c->n_changed = (int64_t)c->h_amb.p[1];
   c->loaded = true;
   c->clustered = false;
 }
@@ -2216,14 +2224,43 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   const io::ClusterView cv{K, c->ostart.data(), c->omemb.data(), c->perm.data()};
   // both writers build and write disjoint cluster ranges on io_threads() threads
   if (consout) io::write_consout(consout, f, cv, c->cons.data(), c->cons_off.data(), p->clusterout_id != 0, width);
+  const double t_cons = now_s() - t1;
+  double t_mask = 0.0;
   if (clusters_prefix) {
-    // masked sequences (vsearch prints the DUST-masked db sequence): only the cluster<N> files need them
-    std::vector<char> masked((size_t)c->n * kMaxLen);
-    if (c->n > 0)
-      c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
-    io::write_cluster_files(clusters_prefix, f, cv, masked.data(), kMaxLen, c->hlen.data(), width);
+    // vsearch prints the DUST-masked (upper-cased) db sequence.  Where no sequence changed (prepare counted them:
+    // nothing masked, input already upper case) that is the input's own bytes, so the 112 B-per-UMI masked
+    // buffer is downloaded only when some sequence changed
+    std::vector<char> masked;
+    std::vector<int32_t> mrow;
+    if (c->n > 0 && c->n_changed > 0) {
+      const double tm = now_s();
+      if (c->n_changed * 16 < c->n) {  // a few changed rows (config 2: one): their flags, then those rows alone
+        std::vector<uint8_t> chg((size_t)c->n);
+        c->hip(hipMemcpy(chg.data(), c->d_mchg.p, chg.size(), hipMemcpyDeviceToHost), "d2h masked flags");
+        mrow.assign((size_t)c->n, -1);
+        int32_t r = 0;
+        for (int32_t s = 0; s < c->n; s++)
+          if (chg[s]) mrow[s] = r++;
+        masked.resize((size_t)r * kMaxLen);
+        for (int32_t s = 0; s < c->n; s++)
+          if (mrow[s] >= 0)
+            c->hip(hipMemcpyAsync(masked.data() + (size_t)mrow[s] * kMaxLen, c->d_masked.p + (size_t)s * kMaxLen,
+                                  kMaxLen, hipMemcpyDeviceToHost, c->st), "d2h masked row");
+        c->hip(hipStreamSynchronize(c->st), "sync");
+      } else {
+        masked.resize((size_t)c->n * kMaxLen);
+        c->hip(hipMemcpy(masked.data(), c->d_masked.p, masked.size(), hipMemcpyDeviceToHost), "d2h masked");
+      }
+      t_mask = now_s() - tm;
+    }
+    io::write_cluster_files(clusters_prefix, f, cv, masked.empty() ? nullptr : masked.data(), kMaxLen,
+                            c->hlen.data(), width, mrow.empty() ? nullptr : mrow.data());
   }
   const double t_write = now_s() - t1;
+  if (c->debug)
+    fprintf(stderr, "umiclust: file path: read %.3f s, cluster %.3f s, consout %.3f s, masked download %.3f s (%lld changed), "
+                    "cluster files %.3f s\n", t_read, t1 - t0 - t_read, t_cons, t_mask, (long long)c->n_changed,
+            t_write - t_cons - t_mask);
   if (log_path) {
     const umiclust_stats& s = c->stats;
     int64_t nt = 0, singles = 0;
@@ -2277,7 +2314,7 @@ static void warn_unknown_env() {
   static std::once_flag once;
   std::call_once(once, [] {
     static const char* const known[] = {
-        "BAND", "BLOCK", "DEBUG", "IO_THREADS", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
+        "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
         "PFPROF", "PIN", "REGROW", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
@@ -2384,6 +2421,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PAR_MIN")) c->par_min = std::max(1, atoi(e));
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
     c->pin = atoi(e) != 0;

@@ -6,10 +6,12 @@
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/statfs.h>
 #include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
@@ -103,7 +105,9 @@ bool read_fasta(const char* path, Fasta& f) {
   }
   f.size = (size_t)sb.st_size;
   if (f.size > 0) {
-    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    // no MAP_POPULATE: the parse threads fault their own slices in, in parallel (one thread populating 3.5 GB of a
+    // config-2 FASTA took 0.14-0.21 s of a 0.34-0.38 s read; without it 0.21 s: tools/read_probe.cpp)
+    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE, fd, 0);
     if (f.map == MAP_FAILED) {
       f.map = nullptr;
       close(fd);
@@ -185,15 +189,45 @@ bool write_file(const std::string& path, const std::string& data) {
   return ok;
 }
 
-// a file made of parts written side by side: each part at its offset (pwrite), on one thread per part
+// The directory of `path` is RAM-backed (tmpfs / ramfs).  There buffered writes into one file serialise on its inode
+// lock (a config-2 fused drop-in streamed its 2.9 GB smolecule_clusters.fa at ~3 GB/s whatever the thread count),
+// while stores into a shared mapping of it run in parallel; on the GPU box's disk-backed overlay the mapping was 5x
+// slower than pwrite (profiles/r03/e2e_probes.json), so only RAM-backed outputs are mapped.
+bool ram_backed(const std::string& path) {
+  std::string dir = path;
+  const size_t sl = dir.find_last_of('/');
+  dir = sl == std::string::npos ? "." : (sl == 0 ? "/" : dir.substr(0, sl));
+  struct statfs sf;
+  if (statfs(dir.c_str(), &sf) != 0) return false;
+  return (unsigned long)sf.f_type == 0x01021994ul /* TMPFS_MAGIC */ || (unsigned long)sf.f_type == 0x858458f6ul /* RAMFS */;
+}
+
+// fd's first n bytes mapped for writing (the file already extended to n); nullptr if that fails
+char* map_for_write(int fd, size_t n) {
+  if (n == 0) return nullptr;
+  void* m = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  return m == MAP_FAILED ? nullptr : (char*)m;
+}
+
+// a file made of parts written side by side: each part at its offset (pwrite, or stores into a shared mapping on a
+// RAM-backed filesystem), on one thread per part
 bool write_parts(const std::string& path, const std::vector<std::string>& parts) {
-  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  const int fd = open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0666);
   if (fd < 0) return false;
   const int T = (int)parts.size();
   std::vector<off_t> at(T + 1, 0);
   for (int t = 0; t < T; t++) at[t + 1] = at[t] + (off_t)parts[t].size();
   bool ok = at[T] == 0 || ftruncate(fd, at[T]) == 0;
   std::vector<char> good(T, 1);
+  char* map = ok && at[T] > 0 && ram_backed(path) ? map_for_write(fd, (size_t)at[T]) : nullptr;
+  if (map) {
+    parallel_for(T, [&](int t) {
+      if (!parts[t].empty()) memcpy(map + at[t], parts[t].data(), parts[t].size());
+    });
+    ok = munmap(map, (size_t)at[T]) == 0 && ok;
+    ok = (close(fd) == 0) && ok;
+    return ok;
+  }
   if (ok)
     parallel_for(T, [&](int t) {
       const char* p = parts[t].data();
@@ -243,7 +277,9 @@ bool read_fastq(const char* path, Fasta& f) {
   }
   f.size = (size_t)sb.st_size;
   if (f.size > 0) {
-    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    // no MAP_POPULATE: the parse threads fault their own slices in, in parallel (one thread populating 3.5 GB of a
+    // config-2 FASTA took 0.14-0.21 s of a 0.34-0.38 s read; without it 0.21 s: tools/read_probe.cpp)
+    f.map = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE, fd, 0);
     if (f.map == MAP_FAILED) {
       f.map = nullptr;
       close(fd);
@@ -376,11 +412,11 @@ std::string pjoin(const std::string& a, const std::string& b) {
 bool split1(Sv s, const char* sep, Sv& out) {
   const size_t m = strlen(sep);
   const char* e = s.p + s.n;
-  const char* a = std::search(s.p, e, sep, sep + m);
-  if (a == e) return false;
+  const char* a = (const char*)memmem(s.p, s.n, sep, m);  // glibc's vectorised search (the reads are ~1.5 kb)
+  if (!a) return false;
   a += m;
-  const char* b = std::search(a, e, sep, sep + m);
-  out = Sv{a, (size_t)(b - a)};
+  const char* b = (const char*)memmem(a, (size_t)(e - a), sep, m);
+  out = Sv{a, (size_t)((b ? b : e) - a)};
   return true;
 }
 
@@ -427,7 +463,7 @@ void write_consout(const char* path, const Fasta& f, const ClusterView& cv, cons
 }
 
 void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& cv, const char* masked, int stride,
-                         const uint8_t* hlen, int width) {
+                         const uint8_t* hlen, int width, const int32_t* mrow) {
   const int32_t K = cv.K;
   const int T = K < 256 ? 1 : io_threads();
   const std::vector<int32_t> cut = cluster_slices(cv.ostart, K, T);
@@ -442,7 +478,9 @@ void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& 
         out.push_back('>');
         out.append(f.data + f.hdr_off[i], (size_t)f.hdr_len[i]);
         out.push_back('\n');
-        put_wrapped(out, masked + (size_t)s * stride, hlen[s], width);
+        const int64_t row = !masked ? -1 : mrow ? mrow[s] : s;
+        if (row >= 0) put_wrapped(out, masked + (size_t)row * stride, hlen[s], width);
+        else put_wrapped(out, f.seq.data() + f.seq_off[i], f.seq_off[i + 1] - f.seq_off[i], width);
       }
       fn = prefix;
       fn += std::to_string(k);
@@ -590,6 +628,9 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     }
     return true;
   };
+  static const bool debug = getenv("UMICLUST_DEBUG") != nullptr;
+  auto clk = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double tp0 = clk();
   const int T = K < 256 ? 1 : io_threads();
   const std::vector<int32_t> cut = cluster_slices(cv.ostart, K, T);
   std::vector<PClus> res((size_t)K);
@@ -605,6 +646,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       analyze(k, res[k], sc, ents);
     }
   });
+  const double tp1 = clk();
   // the reference's loop in order: its first error, its early exit
   int64_t n_written = 0, reads_found = 0, reads_written = 0;
   int32_t kend = K, kerr = -1;
@@ -637,8 +679,13 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   std::vector<int64_t> smol_off((size_t)kwrite + 1, 0);
   for (int32_t k = 0; k < kwrite; k++) smol_off[k + 1] = smol_off[k] + res[k].smol_bytes;
   const std::string smol_path = pjoin(work_dir, "smolecule_clusters.fa");
-  const int smol_fd = open(smol_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+  const int smol_fd = open(smol_path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0666);
   if (smol_fd < 0) throw IoError{UMICLUST_EIO, "cannot write smolecule_clusters.fa"};
+  // RAM-backed work_dir: the records go straight into a shared mapping of the file (no inode lock; see ram_backed)
+  const size_t smol_total = (size_t)smol_off[kwrite];
+  char* smol_map = nullptr;
+  if (smol_total > 0 && ram_backed(smol_path) && ftruncate(smol_fd, (off_t)smol_total) == 0)
+    smol_map = map_for_write(smol_fd, smol_total);
   // cluster files and the text of clusters [0, kwrite), on the threads
   const std::vector<int32_t> wcut = cluster_slices(cv.ostart, kwrite, T);
   std::vector<std::string> log_p(T), stats_p(T);
@@ -655,7 +702,14 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       int fd;
       off_t at;
       uint8_t& bad;
+      char* map;
       void run() {
+        if (map) {
+          memcpy(map + at, s.data(), s.size());
+          at += (off_t)s.size();
+          s.clear();
+          return;
+        }
         size_t o = 0;
         while (o < s.size()) {
           const ssize_t w = pwrite(fd, s.data() + o, s.size() - o, at + (off_t)o);
@@ -670,7 +724,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
         s.clear();
       }
       ~Flush() { run(); }
-    } flush{smol, smol_fd, (off_t)smol_off[wcut[t]], smol_bad[t]};
+    } flush{smol, smol_fd, (off_t)smol_off[wcut[t]], smol_bad[t], smol_map};
     std::string fname;
     for (int32_t k = wcut[t]; k < wcut[t + 1]; k++) {
       stats_beg[k] = stats_out.size();
@@ -713,6 +767,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
                    "\t" + std::to_string(r.w_all) + "\t" + std::to_string(r.written) + "\n";
     }
   });
+  const double tp2 = clk();
   // an unwritable cluster file: the reference stops there (OSError) -- files the other threads wrote past it go,
   // and the stats and smolecule records end before it, as the reference's `with` blocks leave them
   int32_t kbad = -1;
@@ -723,6 +778,7 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     for (int32_t k = kbad + 1; k < kwrite; k++)
       if (wrote[k]) unlink(pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta").c_str());
   bool smol_ok = true;
+  if (smol_map) smol_ok = munmap(smol_map, smol_total) == 0;
   for (int t = 0; t < T; t++) smol_ok = smol_ok && !smol_bad[t];
   if (kbad >= 0) smol_ok = ftruncate(smol_fd, (off_t)smol_off[kkeep]) == 0 && smol_ok;
   smol_ok = close(smol_fd) == 0 && smol_ok;
@@ -750,6 +806,9 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   log += "Reads: " + std::to_string(reads_found) + " found\n";
   log += "Reads: " + std::to_string((int64_t)(reads_written * 100.0 / reads_found)) + "% in written clusters\n";
   if (!write_file(pjoin(work_dir, "parse_cluster.log"), log)) throw IoError{UMICLUST_EIO, "cannot write parse_cluster.log"};
+  if (debug)
+    fprintf(stderr, "umiclust: parse: analysis %.3f s, files + smolecule %.3f s, close + stats + log %.3f s (%d threads)\n",
+            tp1 - tp0, tp2 - tp1, clk() - tp2, T);
 }
 
 // ---------------------------------------------------------------- detected-UMI FASTA (§8f f1)

@@ -74,9 +74,10 @@ std::vector<int32_t> cluster_slices(const int32_t* ostart, int32_t K, int T);
 void write_consout(const char* path, const Fasta& f, const ClusterView& cv, const char* cons, const int64_t* cons_off,
                    bool clusterout_id, int width);
 // --clusters: <prefix><k> per cluster, the members' labels and masked sequences (masked[s * stride], length
-// hlen[s]) in cluster order
+// hlen[s]) in cluster order; masked == nullptr: every sequence prints as its input bytes (no sequence changed);
+// mrow != nullptr: sorted seqno s prints masked row mrow[s], or its input bytes where mrow[s] < 0
 void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& cv, const char* masked, int stride,
-                         const uint8_t* hlen, int width);
+                         const uint8_t* hlen, int width, const int32_t* mrow = nullptr);
 // a small text file (the log)
 void write_text(const char* path, const std::string& text);
 // whole-buffer write / create-write-close (false on an I/O error)

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(64) void k_prep_wave(const char* __restrict__ ascii
                                                   const int32_t* __restrict__ perm, int32_t n, int dust,
                                                   uint32_t* __restrict__ codes, uint8_t* __restrict__ lens,
                                                   uint16_t* __restrict__ kmers, uint8_t* __restrict__ nk,
-                                                  char* __restrict__ masked, uint32_t* __restrict__ ambig) {
+                                                  char* __restrict__ masked, uint32_t* __restrict__ ambig,
+                                                  uint8_t* __restrict__ mchg) {
   __shared__ uint8_t s_c2[2][kMaxLen + 8];   // 2-bit bases of the + strand and of its reverse complement
   __shared__ uint8_t s_c4[kMaxLen + 8];      // 4-bit codes of the output characters
   __shared__ uint8_t s_w[64];                // the DUST window's triplet words
@@ -169,6 +170,11 @@ __global__ __launch_bounds__(64) void k_prep_wave(const char* __restrict__ ascii
   if (masked) {
     if (in0) masked[(int64_t)s * kMaxLen + lane] = (char)f0;
     if (in1) masked[(int64_t)s * kMaxLen + 64 + lane] = (char)f1;
+    // sequences whose output characters differ from their input (DUST-masked or upper-cased): the file writer
+    // prints the input bytes unless some sequence changed (ambig[1] counts them)
+    const unsigned long long chg = __ballot((in0 && f0 != ch0) || (in1 && f1 != ch1));
+    if (chg && lane == 0 && ambig) atomicAdd(ambig + 1, 1u);
+    if (lane == 0 && mchg) mchg[s] = chg ? 1 : 0;
   }
   const uint32_t c40 = c_map4[f0], c41 = c_map4[f1];
   auto amb = [](uint32_t c4) { return c4 != 1u && c4 != 2u && c4 != 4u && c4 != 8u; };
@@ -263,12 +269,12 @@ hipError_t launch_iota(int32_t* out, int32_t n, hipStream_t st) {
 
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
-                       char* masked, uint32_t* ambig, hipStream_t st) {
+                       char* masked, uint32_t* ambig, hipStream_t st, uint8_t* mchg) {
   hipError_t e = ensure_maps(st);
   if (e != hipSuccess) return e;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_prep_wave, dim3((unsigned)n), dim3(64), 0, st, ascii, offs, perm, n, dust, codes, lens, kmers,
-                     nk, masked, ambig);
+                     nk, masked, ambig, mchg);
   return hipGetLastError();
 }
 
@@ -370,6 +376,70 @@ __global__ __launch_bounds__(256) void k_index_fill(const uint16_t* __restrict__
   const uint16_t val = (uint16_t)(vbase + ((xx % (uint32_t)seg_mod) >> kPartShift));
   if (x < n) post[atomicAdd(&cursor[pb | k[x]], 1u)] = val;
   if (x + 64 < n) post[atomicAdd(&cursor[pb | k[x + 64]], 1u)] = val;
+}
+
+// Bank-aware posting order (round 6).  The counting loop (pf_count_stream) gives lane l the l-th 16-byte chunk of a
+// 64-chunk window and issues the chunks' postings slot by slot: the e-th ds_add_u32 of the wave adds posting e of
+// every lane's chunk.  ds_add_u32 is banked like ds_write_b32 (two 32-lane groups, bank = dword mod 32: a posting c
+// hits bank (c >> 2) & 31), and each extra lane on a bank costs an LDS cycle; with postings in arbitrary order the
+// busiest of 32 banks takes ~3.5 lanes.  Order within a list is free (the kernels only count), so after the fill
+// every list is permuted so that chunk i, slot e holds a posting of bank (i + 4 e) mod 32 where the list's bank
+// supply allows: then the lanes of one instruction that read consecutive chunks of one list hit consecutive banks.
+// The permutation is the sorted matching of the postings (by bank) to the positions (by target bank), which
+// minimises the bank displacement.  Simulated on random lists (scratch model, round 6): the busiest bank per
+// 32-lane group falls from 3.5 to 2.1 inside long lists (most postings of a config-2 query) and to 3.3 for lists
+// of ~11 chunks.  One 64-thread workgroup per list segment of up to kArrCap postings (longer lists: arranged per
+// segment, targets by absolute chunk index, so consecutive segments continue the pattern).
+constexpr int kArrCap = 4096;
+__global__ __launch_bounds__(64) void k_list_arrange(const uint32_t* __restrict__ off, uint16_t* __restrict__ post,
+                                                     int32_t nbins) {
+  __shared__ uint16_t sa[kArrCap], ss[kArrCap];
+  __shared__ uint32_t hb[32], ht[32];
+  const int lane = (int)threadIdx.x;
+  for (int32_t bin = (int32_t)blockIdx.x; bin < nbins; bin += (int32_t)gridDim.x) {
+    const uint32_t o0 = off[bin], o1 = off[bin + 1];
+    if (o1 - o0 <= 8u) continue;  // one chunk: its slots meet other lists' lanes only
+    for (uint32_t seg = o0; seg < o1; seg += kArrCap) {
+      const int m = (int)min<uint32_t>(kArrCap, o1 - seg);
+      if (lane < 32) {
+        hb[lane] = 0u;
+        ht[lane] = 0u;
+      }
+      __syncthreads();
+      for (int u = lane; u < m; u += 64) {
+        const uint32_t p = post[seg + u];
+        sa[u] = (uint16_t)p;
+        atomicAdd(&hb[(p >> 2) & 31u], 1u);
+        atomicAdd(&ht[(((seg + u) >> 3) + 4u * (u & 7)) & 31u], 1u);
+      }
+      __syncthreads();
+      if (lane < 32) {  // exclusive scans -> cursors
+        uint32_t b = hb[lane], t = ht[lane], xb = b, xt = t;
+#pragma unroll
+        for (int d = 1; d < 32; d <<= 1) {
+          const uint32_t ub = (uint32_t)__shfl_up((int)xb, d, 64), ut = (uint32_t)__shfl_up((int)xt, d, 64);
+          if (lane >= d) {
+            xb += ub;
+            xt += ut;
+          }
+        }
+        hb[lane] = xb - b;
+        ht[lane] = xt - t;
+      }
+      __syncthreads();
+      for (int u = lane; u < m; u += 64) {
+        const uint32_t p = sa[u];
+        ss[atomicAdd(&hb[(p >> 2) & 31u], 1u)] = (uint16_t)p;
+      }
+      __syncthreads();
+      for (int u = lane; u < m; u += 64) post[seg + u] = ss[atomicAdd(&ht[(((seg + u) >> 3) + 4u * (u & 7)) & 31u], 1u)];
+      __syncthreads();
+    }
+  }
+}
+hipError_t launch_index_arrange(const uint32_t* off, uint16_t* post, hipStream_t st) {
+  hipLaunchKernelGGL(k_list_arrange, dim3(4096), dim3(64), 0, st, off, post, (int32_t)kBins);
+  return hipGetLastError();
 }
 
 // An index append's host-side arrays (new centroids' seqnos and lengths, the seq -> ordinal range they fill, the

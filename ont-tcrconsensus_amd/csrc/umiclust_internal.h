@@ -35,7 +35,8 @@ struct DevSeqs {
 hipError_t launch_iota(int32_t* out, int32_t n, hipStream_t st);
 hipError_t launch_prep(const char* ascii, const int64_t* offs, const int32_t* perm, int32_t n,
                        int dust, uint32_t* codes, uint8_t* lens, uint16_t* kmers, uint8_t* nk,
-                       char* masked, uint32_t* ambig, hipStream_t st);
+                       char* masked, uint32_t* ambig, hipStream_t st,
+                       uint8_t* mchg = nullptr);
 // XOR every k-mer of sequence s (both strands) with xmask[bin[s]] (packs: a bijection per bin)
 hipError_t launch_kmer_xor(uint16_t* kmers, const uint8_t* nk, int32_t n, const int32_t* bin, const uint16_t* xmask,
                            hipStream_t st);
@@ -52,6 +53,8 @@ hipError_t launch_index_scan(uint32_t* hist, uint32_t* partial, uint32_t* off, u
 hipError_t launch_index_fill(const uint16_t* kmers, const uint8_t* nk, const int32_t* map, int32_t first,
                              int32_t count, int32_t xoff, int32_t vbase, int32_t seg_mod, uint32_t* cursor,
                              uint16_t* post, hipStream_t st);
+// bank-aware posting order within every list of a tile (after the fill; kernels.hip k_list_arrange)
+hipError_t launch_index_arrange(const uint32_t* off, uint16_t* post, hipStream_t st);
 // the host-to-device half of an index append in one dispatch: n centroid seqnos / lengths, ns seq -> ordinal entries
 // and nb bin-start ordinals, each read from pinned host memory and written to its device array
 hipError_t launch_append_stage(const int32_t* hc, const uint8_t* hl, int32_t n, int32_t* dc, uint8_t* dl,

@@ -109,8 +109,27 @@ def _relabel(text, pos_of):
 PARSE_FIX = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "parse", "*.json")))
 
 
+@pytest.fixture(params=["disk", "ram"])
+def out_dir(request, tmp_path):
+    """Where the writers write: tmp_path, or a RAM-backed directory (/dev/shm: tmpfs), where host_io maps the one-file
+    outputs (consout, smolecule_clusters.fa) instead of pwrite-ing them (ram_backed())."""
+    if request.param == "disk":
+        yield tmp_path
+        return
+    import shutil
+    import tempfile
+    if not os.path.isdir("/dev/shm") or not os.access("/dev/shm", os.W_OK):
+        pytest.skip("no /dev/shm")
+    d = tempfile.mkdtemp(prefix="uc_asan_", dir="/dev/shm")
+    try:
+        yield __import__("pathlib").Path(d)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 @pytest.mark.parametrize("path", PARSE_FIX, ids=[os.path.basename(p)[:-5] for p in PARSE_FIX])
-def test_host_parse_vs_reference_fixtures_under_asan(host_asan, tmp_path, path):
+def test_host_parse_vs_reference_fixtures_under_asan(host_asan, out_dir, path):
+    tmp_path = out_dir
     case = json.load(open(path))
     inp, exp = case["inputs"], case["outputs"]
     ids = [int(line.split(";")[-1].split("=")[1]) for line in inp["consout"].splitlines() if line.startswith(">")]
@@ -134,9 +153,10 @@ def test_host_parse_vs_reference_fixtures_under_asan(host_asan, tmp_path, path):
     assert out.split()[3] == ("1" if exp["returned"] is None else "0")
 
 
-def test_host_parse_errors_under_asan(host_asan, tmp_path):
+def test_host_parse_errors_under_asan(host_asan, out_dir):
     """The reference's failures: a missing seq= field in the middle of a written cluster (IndexError: the records
     before it written, no stats line for that cluster), a header without 7 fields, clusters_fa already present."""
+    tmp_path = out_dir
     def rec(i, strand, seq=True):
         tail = f";seq=READ{i}" if seq else ";noseq"
         return f">r{i};strand={strand};umi_fwd_dist=0;umi_rev_dist=0;umi_fwd_seq=A;umi_rev_seq=C{tail}\nACGTACGT\n"
@@ -158,7 +178,8 @@ def test_host_parse_errors_under_asan(host_asan, tmp_path):
     assert host_asan("parse", tmp_path / "bad.fa", "1", w2, 1, 60, 0, 0).startswith("error -17 ")
 
 
-def test_host_writers_under_asan(host_asan, tmp_path):
+def test_host_writers_under_asan(host_asan, out_dir):
+    tmp_path = out_dir
     rng = random.Random(5)
     seqs = ["".join(rng.choice("ACGT") for _ in range(rng.randint(1, 170))) for _ in range(700)]
     sizes = []
@@ -178,6 +199,12 @@ def test_host_writers_under_asan(host_asan, tmp_path):
                                                                 for j in range(i, i + m))
         i += m
     assert (tmp_path / "cons.fa").read_text() == "".join(want)
+    # no sequence changed by masking: the writer prints the input's own bytes (no masked download)
+    host_asan("write_input", tmp_path / "in.fa", ",".join(map(str, sizes)), tmp_path / "icluster", tmp_path / "icons.fa")
+    i = 0
+    for k, m in enumerate(sizes):
+        assert (tmp_path / f"icluster{k}").read_text() == "".join(f">s{j};x\n" + wrap(seqs[j]) for j in range(i, i + m))
+        i += m
 
 
 def test_host_detected_umis_writer_under_asan(host_asan, tmp_path):

@@ -76,6 +76,10 @@ for st in "$@"; do
     regrowab) for v in ${REGS:-0 16 4}; do for c in ${PCFGS:-5 4}; do
               UMICLUST_REGROW=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/rg${v}_c$c.json" 2> "$out/rg${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
+    e2eprobe) timeout -k 10 400 python3 -u tools/e2e_probe.py "$out/e2e_probe.json" > "$out/e2e_probe.log" 2>&1; rc=$? ;;
+    arrab) for v in ${ARRS:-0 3 1 0 3}; do for c in ${PCFGS:-2 3 5}; do
+              UMICLUST_ARRANGE=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/arr${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
