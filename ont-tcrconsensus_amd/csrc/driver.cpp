@@ -424,7 +424,8 @@ struct umiclust_ctx {
   // relevant peers certain to become members are not aligned speculatively (config 2 4.02 -> 4.14 M, round 4)
   static constexpr bool peer_cert = true;
   int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
-  int32_t arrange = 3;       // UMICLUST_ARRANGE: bank-aware posting order in centroid tiles (1) / peer tiles (2)
+  int32_t regrow_depth = kPeerCap / 4;  // UMICLUST_REGROW_DEPTH: a block whose deepest peer list reaches this is not clean
+  int32_t arrange = 1;       // UMICLUST_ARRANGE: bank-aware posting order in large tiles (1) / small tiles (2)
   int32_t regrow = 8;        // UMICLUST_REGROW: clean shallow blocks before a halved block size doubles (0: never)
   int32_t last_max_npeer = 0;
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
@@ -640,8 +641,9 @@ void build_tile(umiclust_ctx* c, Tile& t, const int32_t* map, int32_t first, int
   c->hip(launch_index_scan(t.hist.p, t.partial.p, t.off.p, t.cursor.p, post, st), "index scan");
   c->hip(launch_index_fill(c->d_kmers.p, c->d_nk.p, map, first, n, xoff, vbase, seg_mod, t.cursor.p, post, st),
          "index fill");
-  // bank-aware posting order (kernels.hip k_list_arrange): centroid tiles (bit 0) and peer / round tiles (bit 1)
-  if (n > 0 && (c->arrange & (vbase >= kCentBase ? 1 : 2)))
+  // bank-aware posting order (kernels.hip k_list_arrange): large tiles (bit 0: the base tile and sealed tiles, built
+  // once per fold / seal) and small ones (bit 1: delta, peer and round tiles, rebuilt every block)
+  if (n > 0 && (c->arrange & (n >= 2 * kDelta ? 1 : 2)))
     c->hip(launch_index_arrange(t.off.p, post, st), "index arrange");
   t.n = n;
   t.built_n = n;
@@ -1829,7 +1831,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
     // overflowing query (resolve_pass), a giant molecule's stretch no longer pins a bin at 256-query blocks: config 4's
     // bin 200 7.0 -> 1.6 s among 8 lanes, config 4 6.51 -> 7.59 M UMIs/s; config 5's windows stay deep, so its blocks
     // do not grow (3.33 / 3.36 M; ungated regrowth after 4 clean blocks: 2.47 M) -- profiles/r05/regrow_ab/.
-    if (c->last_max_npeer >= kPeerCap / 4) {
+    if (c->last_max_npeer >= c->regrow_depth) {
       clean = 0;  // a deep window: no regrowth yet, and it does not count as a clean block
     } else if (c->regrow > 0 && b_eff < B && ++clean >= c->regrow && k + D < nb) {
       b_eff = std::min<int32_t>(B, b_eff * 2);
@@ -2315,7 +2317,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "REGROW", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
@@ -2422,6 +2424,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
+  if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {
     c->pin = atoi(e) != 0;

@@ -412,10 +412,22 @@ std::string pjoin(const std::string& a, const std::string& b) {
 bool split1(Sv s, const char* sep, Sv& out) {
   const size_t m = strlen(sep);
   const char* e = s.p + s.n;
-  const char* a = (const char*)memmem(s.p, s.n, sep, m);  // glibc's vectorised search (the reads are ~1.5 kb)
+  if (m == 0) return false;
+  // memchr for the separator's first character, then compare (vectorised; a read of ~1.5 kb never holds the 's' of
+  // "seq=", so the second search is one memchr pass over it)
+  auto find = [&](const char* from) -> const char* {
+    while (from + m <= e) {
+      const char* q = (const char*)memchr(from, sep[0], (size_t)(e - from) - (m - 1));
+      if (!q) return nullptr;
+      if (!memcmp(q, sep, m)) return q;
+      from = q + 1;
+    }
+    return nullptr;
+  };
+  const char* a = find(s.p);
   if (!a) return false;
   a += m;
-  const char* b = (const char*)memmem(a, (size_t)(e - a), sep, m);
+  const char* b = find(a);
   out = Sv{a, (size_t)((b ? b : e) - a)};
   return true;
 }
@@ -521,7 +533,11 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   };
   struct Scratch {
     std::vector<Sv> fields;
-    std::vector<std::pair<Sv, int32_t>> kept[2];  // insertion-ordered dict read id -> record (:61-65)
+    struct Kept {
+      Sv id, last;  // cols[0] and cols[6] of the record's header
+      int32_t rec;
+    };
+    std::vector<Kept> kept[2];  // insertion-ordered dict read id -> record (:61-65)
     std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position)
   };
   // an entry written: its read id (`cols[0]`) and read (`cols[6].split("seq=")[1]`), kept from the analysis so the
@@ -531,8 +547,8 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     const char* read;
     uint32_t rid_n, read_n;
   };
-  auto entry = [&](const PClus& r, const Scratch& sc, int64_t y) -> int32_t {
-    return (y < r.w_fwd ? sc.kept[0][y] : sc.kept[1][y - r.w_fwd]).second;
+  auto entry = [&](const PClus& r, const Scratch& sc, int64_t y) -> const Scratch::Kept& {
+    return y < r.w_fwd ? sc.kept[0][y] : sc.kept[1][y - r.w_fwd];
   };
   // one cluster's counts (and the entries it writes, appended to ents); false on the first error
   auto analyze = [&](int32_t k, PClus& r, Scratch& sc, std::vector<Ent>& ents) -> bool {
@@ -576,9 +592,10 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
           }
         if (pos < 0) {
           sc.index.emplace_back(std::move(key), (int32_t)sc.kept[st].size());
-          sc.kept[st].emplace_back(sc.fields[0], i);
+          sc.kept[st].push_back(Scratch::Kept{sc.fields[0], sc.fields[6], i});
         } else {
-          sc.kept[st][pos].second = i;
+          sc.kept[st][pos].last = sc.fields[6];  // a repeated id: the later record (its id is the same)
+          sc.kept[st][pos].rec = i;
         }
       }
       seen[st]++;
@@ -613,16 +630,16 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       r.written = 1;
       const int64_t head = 3 + (int64_t)std::to_string(k).size();  // '>' k '\n' ... '\n'
       for (int64_t y = 0; y < r.w_all; y++) {  // `cols[6].split("seq=")[1]` of every entry written (:106)
-        const int32_t i = entry(r, sc, y);
-        split_fields(Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}, sc.fields);
+        const Scratch::Kept& ke = entry(r, sc, y);
+        const int32_t i = ke.rec;
         Sv read;
-        if (!split1(sc.fields[6], "seq=", read)) {
+        if (!split1(ke.last, "seq=", read)) {
           r.err = UMICLUST_EFORMAT;
           r.noseq_at = y;  // the entries before it are written (and kept in ents)
           r.msg = "IndexError: no seq= field in " + Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}.str();
           return false;
         }
-        ents.push_back(Ent{sc.fields[0].p, read.p, (uint32_t)sc.fields[0].n, (uint32_t)read.n});
+        ents.push_back(Ent{ke.id.p, read.p, (uint32_t)ke.id.n, (uint32_t)read.n});
         r.smol_bytes += head + (int64_t)read.n;
       }
     }

@@ -396,9 +396,16 @@ __global__ __launch_bounds__(64) void k_list_arrange(const uint32_t* __restrict_
   __shared__ uint16_t sa[kArrCap], ss[kArrCap];
   __shared__ uint32_t hb[32], ht[32];
   const int lane = (int)threadIdx.x;
-  for (int32_t bin = (int32_t)blockIdx.x; bin < nbins; bin += (int32_t)gridDim.x) {
+  // a workgroup takes 64 consecutive bins at a time, one per lane, and arranges the lists of more than one chunk
+  for (int32_t b0 = (int32_t)blockIdx.x * 64; b0 < nbins; b0 += (int32_t)gridDim.x * 64) {
+   const int32_t mybin = b0 + lane;
+   const uint32_t mlen = mybin < nbins ? off[mybin + 1] - off[mybin] : 0u;
+   unsigned long long todo = __ballot(mlen > 8u);  // one chunk: its slots meet other lists' lanes only
+   while (todo) {
+    const int bl = __builtin_ctzll(todo);
+    todo &= todo - 1ull;
+    const int32_t bin = b0 + bl;
     const uint32_t o0 = off[bin], o1 = off[bin + 1];
-    if (o1 - o0 <= 8u) continue;  // one chunk: its slots meet other lists' lanes only
     for (uint32_t seg = o0; seg < o1; seg += kArrCap) {
       const int m = (int)min<uint32_t>(kArrCap, o1 - seg);
       if (lane < 32) {
@@ -435,10 +442,11 @@ __global__ __launch_bounds__(64) void k_list_arrange(const uint32_t* __restrict_
       for (int u = lane; u < m; u += 64) post[seg + u] = ss[atomicAdd(&ht[(((seg + u) >> 3) + 4u * (u & 7)) & 31u], 1u)];
       __syncthreads();
     }
+   }
   }
 }
 hipError_t launch_index_arrange(const uint32_t* off, uint16_t* post, hipStream_t st) {
-  hipLaunchKernelGGL(k_list_arrange, dim3(4096), dim3(64), 0, st, off, post, (int32_t)kBins);
+  hipLaunchKernelGGL(k_list_arrange, dim3(kBins / 64 / 8), dim3(64), 0, st, off, post, (int32_t)kBins);
   return hipGetLastError();
 }
 
@@ -896,7 +904,10 @@ __device__ __forceinline__ void pf_count_stream(__amdgpu_buffer_rsrc_t arena, ui
     const uint32_t L0 = m + (uint32_t)__builtin_popcountll(sm & below);
     return g < T ? lbias[L0] + 8u * g : 0xffffffffu;
   };
-  auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? 0u : i); };
+  // a lane past the end of the stream adds 0 to the postings of chunk `lane` (any valid chunk): with every such lane
+  // on chunk 0, as before round 6, a partial last window's idle lanes all hit the same 8 counter dwords, and
+  // same-address atomics serialise (up to 32 lanes of a group on one address)
+  auto ldv = [&](uint32_t i) { return ld_chunk(arena, i == 0xffffffffu ? (uint32_t)lane << 3 : i); };
   auto one = [](uint32_t i) { return i != 0xffffffffu ? 1u : 0u; };
   constexpr uint32_t S1 = W;
   uint32_t w = (uint32_t)wv;  // wave-uniform (SGPR): the window bounds are scalar branches

@@ -80,6 +80,11 @@ for st in "$@"; do
     arrab) for v in ${ARRS:-0 3 1 0 3}; do for c in ${PCFGS:-2 3 5}; do
               UMICLUST_ARRANGE=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/arr${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    rdab) for v in ${RDS:-32 48 64 96 32}; do for c in ${PCFGS:-5 4}; do
+              UMICLUST_REGROW_DEPTH=$v timeout -k 10 500 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/rd${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    c5dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --config 5 --steps 1 --warmup 1 --no-cpu-baseline \
+             > "$out/c5dbg.json" 2> "$out/c5dbg.err"; rc=$? ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
