@@ -38,6 +38,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -431,7 +432,7 @@ struct umiclust_ctx {
   bool pf_probe = getenv("UMICLUST_PFPROBE") != nullptr;  // the counting kernel's phases without the count loop
   DevBuf<uint32_t> d_probe;
   // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
-  static constexpr int32_t lazy_permille = 5;
+  int32_t lazy_permille = 5;  // UMICLUST_LAZY (0: never lazy)
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int al_level = 0;                 // the alignment stream: 0 prioritised (al_priority), -1 plain (set_priority -1)
@@ -2224,9 +2225,25 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   const int32_t K = c->nclusters;
   const int width = p->fasta_width;
   const io::ClusterView cv{K, c->ostart.data(), c->omemb.data(), c->perm.data()};
-  // both writers build and write disjoint cluster ranges on io_threads() threads
-  if (consout) io::write_consout(consout, f, cv, c->cons.data(), c->cons_off.data(), p->clusterout_id != 0, width);
-  const double t_cons = now_s() - t1;
+  // both writers build and write disjoint cluster ranges on io_threads() threads; the consout (one file: bound by its
+  // page allocation or inode lock, 0.12 s of a config-2 bin on the GPU box) is written beside the cluster<N> files
+  double t_cons = 0.0;
+  std::exception_ptr cons_err;
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } cons_th;
+  if (consout)
+    cons_th.t = std::thread([&] {
+      try {
+        io::write_consout(consout, f, cv, c->cons.data(), c->cons_off.data(), p->clusterout_id != 0, width);
+      } catch (...) {
+        cons_err = std::current_exception();
+      }
+      t_cons = now_s() - t1;
+    });
   double t_mask = 0.0;
   if (clusters_prefix) {
     // vsearch prints the DUST-masked (upper-cased) db sequence.  Where no sequence changed (prepare counted them:
@@ -2258,11 +2275,14 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
     io::write_cluster_files(clusters_prefix, f, cv, masked.empty() ? nullptr : masked.data(), kMaxLen,
                             c->hlen.data(), width, mrow.empty() ? nullptr : mrow.data());
   }
+  const double t_files = now_s() - t1;
+  if (cons_th.t.joinable()) cons_th.t.join();
+  if (cons_err) std::rethrow_exception(cons_err);
   const double t_write = now_s() - t1;
   if (c->debug)
-    fprintf(stderr, "umiclust: file path: read %.3f s, cluster %.3f s, consout %.3f s, masked download %.3f s (%lld changed), "
-                    "cluster files %.3f s\n", t_read, t1 - t0 - t_read, t_cons, t_mask, (long long)c->n_changed,
-            t_write - t_cons - t_mask);
+    fprintf(stderr, "umiclust: file path: read %.3f s, cluster %.3f s, masked download %.3f s (%lld changed), "
+                    "cluster files done at %.3f s, consout (beside them) at %.3f s\n", t_read, t1 - t0 - t_read, t_mask,
+            (long long)c->n_changed, t_files, t_cons);
   if (log_path) {
     const umiclust_stats& s = c->stats;
     int64_t nt = 0, singles = 0;
@@ -2316,7 +2336,7 @@ static void warn_unknown_env() {
   static std::once_flag once;
   std::call_once(once, [] {
     static const char* const known[] = {
-        "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
+        "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
         "PFPROF", "PIN", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
@@ -2424,6 +2444,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
+  if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, std::min(1000, atoi(e)));
   if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {

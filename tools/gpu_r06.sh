@@ -85,6 +85,9 @@ for st in "$@"; do
                 > "$out/rd${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     c5dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --config 5 --steps 1 --warmup 1 --no-cpu-baseline \
              > "$out/c5dbg.json" 2> "$out/c5dbg.err"; rc=$? ;;
+    lazyab) for v in ${LAZYS:-5 0 5 0}; do for c in ${PCFGS:-5 2 3 4}; do
+              UMICLUST_LAZY=$v timeout -k 10 500 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/lz${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
