@@ -2215,6 +2215,16 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
     if (L > kMaxLen && L <= p->maxseqlength) c->fail(UMICLUST_ERANGE, "sequence longer than %d", kMaxLen);
   }
   const double t_read = now_s() - t0;
+  // the fused drop-in: the headers' fields parse_clusters needs, computed on a few host threads while the GPU
+  // clusters (the resolve pool keeps the rest of the CPUs)
+  std::vector<io::RecFields> pre;
+  struct PreJoin {
+    std::thread t;
+    ~PreJoin() {
+      if (t.joinable()) t.join();
+    }
+  } pre_th;
+  if (pp) pre_th.t = std::thread([&] { io::precompute_fields(f, pre, std::max(1, std::min(4, io::host_cpus() / 4))); });
   load_impl(c, p, f.seq.data(), f.seq_off.data(), n);
   if (c->bin_s.size() != 2) c->fail(UMICLUST_EINVAL, "file path: one bin per load");
   {
@@ -2317,7 +2327,10 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   if (pp) {
     if (!c->p.clusterout_sort || !c->p.clusterout_id)
       c->fail(UMICLUST_EINVAL, "in-process parse needs --clusterout_sort and --clusterout_id numbering");
-    io::parse_clusters(f, cv, pp, work_dir, pr);
+    const double tj = now_s();
+    if (pre_th.t.joinable()) pre_th.t.join();
+    if (c->debug) fprintf(stderr, "umiclust: fused: waited %.3f s for the header fields\n", now_s() - tj);
+    io::parse_clusters(f, cv, pp, work_dir, pr, pre.empty() ? nullptr : pre.data());
   }
   c->stats.t_read_s = t_read;
   c->stats.t_write_s = t_write + (pp ? now_s() - t1 - t_write : 0.0);

@@ -514,8 +514,37 @@ void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& 
 // in order.  On an error the outputs are what the reference leaves behind when it raises: the files and the
 // stats / smolecule lines of the clusters before the failing one (its `with` blocks flush them), plus the
 // records a missing `seq=` field interrupts in the middle of a cluster (:104-116), and no log.
+void precompute_fields(const Fasta& f, std::vector<RecFields>& out, int threads) {
+  const int64_t n = (int64_t)f.hdr_off.size();
+  out.assign((size_t)n, RecFields{});
+  const int T = std::max(1, std::min<int>(threads, (int)(n / 4096 + 1)));
+  parallel_for(T, [&](int t) {
+    std::vector<Sv> fields;
+    for (int64_t i = n * t / T; i < n * (t + 1) / T; i++) {
+      const char* h = f.data + f.hdr_off[i];
+      split_fields(Sv{h, (size_t)f.hdr_len[i]}, fields);
+      if (fields.size() != 7) continue;
+      Sv strand;
+      if (!split1(fields[1], "strand=", strand)) continue;
+      RecFields& r = out[(size_t)i];
+      if (strand == "+") r.strand = 0;
+      else if (strand == "-") r.strand = 1;
+      else continue;
+      r.id_n = (uint32_t)fields[0].n;
+      r.last_off = (uint32_t)(fields[6].p - h);
+      r.last_n = (uint32_t)fields[6].n;
+      Sv read;
+      if (split1(fields[6], "seq=", read)) {
+        r.read_off = (int32_t)(read.p - h);
+        r.read_n = (uint32_t)read.n;
+      }
+      r.ok = 1;
+    }
+  });
+}
+
 void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_params* pp, const char* work_dir_c,
-                    umiclust_parse_result* pr) {
+                    umiclust_parse_result* pr, const RecFields* pre) {
   const int64_t min_reads = pp->min_reads_per_cluster, max_reads = pp->max_reads_per_cluster;
   const std::string work_dir = work_dir_c ? work_dir_c : "";
   const std::string fa_dir = pjoin(work_dir, "clusters_fa");  // :167
@@ -538,7 +567,6 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       int32_t rec;
     };
     std::vector<Kept> kept[2];  // insertion-ordered dict read id -> record (:61-65)
-    std::vector<std::pair<std::string, int32_t>> index;  // (strand-tagged id, position)
   };
   // an entry written: its read id (`cols[0]`) and read (`cols[6].split("seq=")[1]`), kept from the analysis so the
   // write phase never splits a header again
@@ -554,48 +582,55 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   auto analyze = [&](int32_t k, PClus& r, Scratch& sc, std::vector<Ent>& ents) -> bool {
     sc.kept[0].clear();
     sc.kept[1].clear();
-    sc.index.clear();
     int64_t seen[2] = {0, 0};
     for (int32_t x = cv.ostart[k]; x < cv.ostart[k + 1]; x++) {  // cluster<N> file order (:36)
       const int32_t i = cv.perm[cv.omemb[x]];
       const Sv name{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]};
-      split_fields(name, sc.fields);
-      if (sc.fields.size() != 7) {  // :38-47
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "cluster " + std::to_string(k) + ": header has " + std::to_string(sc.fields.size()) +
-                " cols while it should contain 7: " + name.str();
-        return false;
-      }
-      Sv strand;
-      if (!split1(sc.fields[1], "strand=", strand)) {
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "no strand= field: " + name.str();
-        return false;
+      Sv id, last;
+      int st = 0;
+      if (pre && pre[i].ok) {  // fields computed ahead (precompute_fields)
+        id = Sv{name.p, pre[i].id_n};
+        last = Sv{name.p + pre[i].last_off, pre[i].last_n};
+        st = pre[i].strand;
+      } else {
+        split_fields(name, sc.fields);
+        if (sc.fields.size() != 7) {  // :38-47
+          r.err = UMICLUST_EFORMAT;
+          r.msg = "cluster " + std::to_string(k) + ": header has " + std::to_string(sc.fields.size()) +
+                  " cols while it should contain 7: " + name.str();
+          return false;
+        }
+        Sv strand;
+        if (!split1(sc.fields[1], "strand=", strand)) {
+          r.err = UMICLUST_EFORMAT;
+          r.msg = "no strand= field: " + name.str();
+          return false;
+        }
+        if (strand == "+") st = 0;
+        else if (strand == "-") st = 1;
+        else {
+          r.found++;
+          r.err = UMICLUST_EFORMAT;
+          r.msg = "Strand annotation is " + strand.str() + " but only - or + are allowed!";
+          return false;
+        }
+        id = sc.fields[0];
+        last = sc.fields[6];
       }
       r.found++;
-      int st = 0;
-      if (strand == "+") st = 0;
-      else if (strand == "-") st = 1;
-      else {
-        r.err = UMICLUST_EFORMAT;
-        r.msg = "Strand annotation is " + strand.str() + " but only - or + are allowed!";
-        return false;
-      }
       if (seen[st] < max_reads) {  // kept[strand][id] = rec: a repeated id keeps its first position
-        std::string key = sc.fields[0].str();
-        key.push_back((char)('0' + st));
-        int32_t pos = -1;
-        for (auto& e : sc.index)
-          if (e.first == key) {
-            pos = e.second;
+        std::vector<Scratch::Kept>& kv = sc.kept[st];
+        size_t pos = kv.size();
+        for (size_t y = 0; y < kv.size(); y++)
+          if (kv[y].id.n == id.n && !memcmp(kv[y].id.p, id.p, id.n)) {
+            pos = y;
             break;
           }
-        if (pos < 0) {
-          sc.index.emplace_back(std::move(key), (int32_t)sc.kept[st].size());
-          sc.kept[st].push_back(Scratch::Kept{sc.fields[0], sc.fields[6], i});
+        if (pos == kv.size()) {
+          kv.push_back(Scratch::Kept{id, last, i});
         } else {
-          sc.kept[st][pos].last = sc.fields[6];  // a repeated id: the later record (its id is the same)
-          sc.kept[st][pos].rec = i;
+          kv[pos].last = last;  // a repeated id: the later record (its id is the same)
+          kv[pos].rec = i;
         }
       }
       seen[st]++;
@@ -633,7 +668,14 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
         const Scratch::Kept& ke = entry(r, sc, y);
         const int32_t i = ke.rec;
         Sv read;
-        if (!split1(ke.last, "seq=", read)) {
+        bool has_read;
+        if (pre && pre[i].ok) {
+          has_read = pre[i].read_off >= 0;
+          read = Sv{f.data + f.hdr_off[i] + (has_read ? pre[i].read_off : 0), pre[i].read_n};
+        } else {
+          has_read = split1(ke.last, "seq=", read);
+        }
+        if (!has_read) {
           r.err = UMICLUST_EFORMAT;
           r.noseq_at = y;  // the entries before it are written (and kept in ents)
           r.msg = "IndexError: no seq= field in " + Sv{f.data + f.hdr_off[i], (size_t)f.hdr_len[i]}.str();

@@ -87,8 +87,18 @@ bool write_file(const std::string& path, const std::string& data);
 // parse_umi_clusters / polish_cluster (/root/reference/ont_tcr_consensus/parse_umi_clusters.py:10-242) on the
 // in-memory clusters: <work_dir>/clusters_fa/cluster<k>.fasta, smolecule_clusters.fa, vsearch_cluster_stats.tsv,
 // parse_cluster.log; byte-identical to the reference run on the vsearch files
+// The per-record header fields parse_clusters needs (cols[0], the strand, cols[6] and its seq= read), computed
+// ahead -- the fused drop-in runs it on a few threads while the GPU clusters.  ok = 0: the header does not have 7
+// fields or a valid strand= field (parse_clusters re-derives the reference's error from the header).
+struct RecFields {
+  uint32_t id_n = 0, last_off = 0, last_n = 0, read_n = 0;
+  int32_t read_off = -1;  // -1: cols[6] has no seq=
+  uint8_t ok = 0, strand = 0;
+};
+void precompute_fields(const Fasta& f, std::vector<RecFields>& out, int threads);
 void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_params* pp, const char* work_dir,
-                    umiclust_parse_result* pr);
+                    umiclust_parse_result* pr,
+                    const RecFields* pre = nullptr);
 
 // write_fasta of extract_umis (/root/reference/ont_tcr_consensus/extract_umis.py:154-186) for records [0, ngood):
 // res[i*6 ..] = (dist, start, end) of the 5' and 3' UMI in their windows; returns the reads with both UMIs

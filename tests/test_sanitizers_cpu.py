@@ -127,8 +127,9 @@ def out_dir(request, tmp_path):
         shutil.rmtree(d, ignore_errors=True)
 
 
+@pytest.mark.parametrize("mode", ["parse", "parse_pre"])
 @pytest.mark.parametrize("path", PARSE_FIX, ids=[os.path.basename(p)[:-5] for p in PARSE_FIX])
-def test_host_parse_vs_reference_fixtures_under_asan(host_asan, out_dir, path):
+def test_host_parse_vs_reference_fixtures_under_asan(host_asan, out_dir, path, mode):
     tmp_path = out_dir
     case = json.load(open(path))
     inp, exp = case["inputs"], case["outputs"]
@@ -140,7 +141,7 @@ def test_host_parse_vs_reference_fixtures_under_asan(host_asan, out_dir, path):
     work = tmp_path / inp["region"]
     work.mkdir()
     a = inp["args"]
-    out = host_asan("parse", tmp_path / "in.fa", ",".join(map(str, sizes)), work, a.get("min_reads_per_cluster", 20),
+    out = host_asan(mode, tmp_path / "in.fa", ",".join(map(str, sizes)), work, a.get("min_reads_per_cluster", 20),
                     a.get("max_reads_per_cluster", 60), int(a.get("balance_strands", False)),
                     a.get("max_clusters") or 0)
     got = {}
@@ -153,7 +154,8 @@ def test_host_parse_vs_reference_fixtures_under_asan(host_asan, out_dir, path):
     assert out.split()[3] == ("1" if exp["returned"] is None else "0")
 
 
-def test_host_parse_errors_under_asan(host_asan, out_dir):
+@pytest.mark.parametrize("mode", ["parse", "parse_pre"])
+def test_host_parse_errors_under_asan(host_asan, out_dir, mode):
     """The reference's failures: a missing seq= field in the middle of a written cluster (IndexError: the records
     before it written, no stats line for that cluster), a header without 7 fields, clusters_fa already present."""
     tmp_path = out_dir
@@ -164,7 +166,7 @@ def test_host_parse_errors_under_asan(host_asan, out_dir):
     (tmp_path / "in.fa").write_text("".join(recs))
     w = tmp_path / "w1"
     w.mkdir()
-    out = host_asan("parse", tmp_path / "in.fa", "6,3", w, 1, 60, 0, 0)
+    out = host_asan(mode, tmp_path / "in.fa", "6,3", w, 1, 60, 0, 0)
     assert out.startswith(f"error -74 ")
     assert sorted(os.listdir(w / "clusters_fa")) == ["cluster0.fasta", "cluster1.fasta"]
     # cluster 1 writes its '+' reads first: r6, r8, then r7 (the '-' read without seq=) raises
@@ -174,8 +176,14 @@ def test_host_parse_errors_under_asan(host_asan, out_dir):
     (tmp_path / "bad.fa").write_text(">r0;strand=+;a;b\nACGT\n")
     w2 = tmp_path / "w2"
     w2.mkdir()
-    assert host_asan("parse", tmp_path / "bad.fa", "1", w2, 1, 60, 0, 0).startswith("error -74 ")
-    assert host_asan("parse", tmp_path / "bad.fa", "1", w2, 1, 60, 0, 0).startswith("error -17 ")
+    assert host_asan(mode, tmp_path / "bad.fa", "1", w2, 1, 60, 0, 0).startswith("error -74 ")
+    assert host_asan(mode, tmp_path / "bad.fa", "1", w2, 1, 60, 0, 0).startswith("error -17 ")
+    # a strand other than + / - (the precomputed fields leave it to the reference's own error path)
+    (tmp_path / "badstrand.fa").write_text(rec(0, "+") + rec(1, "x"))
+    w3 = tmp_path / "w3"
+    w3.mkdir()
+    out = host_asan(mode, tmp_path / "badstrand.fa", "2", w3, 1, 60, 0, 0)
+    assert out.startswith("error -74 ") and "Strand annotation is x but only - or + are allowed!" in out
 
 
 def test_host_writers_under_asan(host_asan, out_dir):

@@ -4,11 +4,11 @@
 //
 //   host_asan fasta <in.fa> <out.tsv>          read_fasta: "label\tsequence" per record
 //   host_asan fastq <in.fq> <out.tsv>          read_fastq: the same
-//   host_asan parse <in.fa> <sizes> <work_dir> <min> <max> <balance> <max_clusters>
+//   host_asan parse|parse_pre <in.fa> <sizes> <work_dir> <min> <max> <balance> <max_clusters>
 //        parse_clusters over clusters of consecutive records (sizes: comma-separated cluster sizes); prints
 //        "n_written reads_found reads_written empty_region" or "error <code> <message>"
 //   host_asan write <in.fa> <sizes> <prefix> <consout>   write_consout (consensus = the centroid's sequence)
-//        + write_cluster_files (masked = the sequences)
+//        + write_cluster_files (masked = the sequences, cut at 128); write_input: the same from the input bytes
 //   host_asan umis <in.fa> <res.txt> <out.fa> <a3>  write_detected_umis (res: 6 ints per record)
 //   host_asan bgzf <in.bgzf> <out.raw>         inflate_bgzf
 //   host_asan argv <args...>                   umiclust_params_from_argv: the decoded fields
@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
       }
       return dump(f, argv[3]);
     }
-    if (cmd == "parse" && argc == 9) {
+    if ((cmd == "parse" || cmd == "parse_pre") && argc == 9) {
       Fasta f;
       if (!read_fasta(argv[2], f)) return 3;
       Clusters C;
@@ -82,7 +82,9 @@ int main(int argc, char** argv) {
       umiclust_parse_params pp{atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8])};
       umiclust_parse_result pr{};
       try {
-        parse_clusters(f, C.cv, &pp, argv[4], &pr);
+        std::vector<RecFields> pre;  // parse_pre: the header fields computed ahead, as the fused drop-in does
+        if (cmd == "parse_pre") precompute_fields(f, pre, 3);
+        parse_clusters(f, C.cv, &pp, argv[4], &pr, pre.empty() ? nullptr : pre.data());
         printf("%lld %lld %lld %d\n", (long long)pr.n_written, (long long)pr.reads_found, (long long)pr.reads_written,
                pr.empty_region);
       } catch (const IoError& e) {
@@ -90,7 +92,7 @@ int main(int argc, char** argv) {
       }
       return 0;
     }
-    if (cmd == "write" && argc == 6) {
+    if ((cmd == "write" || cmd == "write_input") && argc == 6) {
       Fasta f;
       if (!read_fasta(argv[2], f)) return 3;
       Clusters C;
@@ -112,7 +114,8 @@ int main(int argc, char** argv) {
         hlen[i] = (uint8_t)L;
       }
       write_consout(argv[5], f, C.cv, cons.data(), cons_off.data(), true, 80);
-      write_cluster_files(argv[4], f, C.cv, masked.data(), stride, hlen.data(), 80);
+      // write_input: no masked copy (no sequence changed): the input bytes, whole
+      write_cluster_files(argv[4], f, C.cv, cmd == "write" ? masked.data() : nullptr, stride, hlen.data(), 80);
       return 0;
     }
     if (cmd == "umis" && argc == 6) {
