@@ -58,6 +58,16 @@ def _align_valu_per_cell() -> float:
 ALIGN_VALU_PER_CELL = _align_valu_per_cell()
 
 
+def _prof(*names: str) -> str:
+    """The newest committed measurement among profiles/<round>/<name> (round 6 first, then round 5)."""
+    for rnd in ("r06", "r05"):
+        for n in names:
+            p = os.path.join(ROOT, "profiles", rnd, n)
+            if os.path.exists(p):
+                return p
+    return os.path.join(ROOT, "profiles", "r05", names[-1])
+
+
 def align_issue_ceiling() -> dict | None:
     """The aligner's ceiling at the measured issue cost of its own instruction mix: the column loop of
     k_align_pk<64> (tools/isa_mix.py -> profiles/r05/align_issue_mix_pk64.json: VOP2, packed VOP3P and other VOP3
@@ -248,7 +258,7 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
     # (tools/pmc_calib.hip, conflict-free), at the clock measured during the kernel (GRBM_GUI_ACTIVE / 8 / duration of
     # its dispatches in a PMC run: tools/pmc_clock.py)
     cal_p = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
-    clk_p = os.path.join(ROOT, "profiles", "r05", "pmc_clock_k_pf_count.json")
+    clk_p = _prof("pmc_clock_k_pf_count.json")
     if counter_cells and t_cnt > 0:
         roof["survey"] = dict(bytes_per_launch=survey_bytes / max(1, n_cnt), counter_cells=counter_cells,
                               achieved=survey_bytes / t_cnt / 1e9, frac_hbm=survey_bytes / t_cnt / 1e9 / HBM_PEAK_GBS,
@@ -283,7 +293,7 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
                  speculative_ratio=cells_c / cells if cells else None)
     # the aligner alone: its kernels' durations in a PMC run (dispatches serialised, so nothing shares the CUs) of the
     # same workload, per bin, against this run's cells per bin (config 2: one bin per step)
-    solo_p = os.path.join(ROOT, "profiles", "r05", "rocprof_solo_kernel_stats_c2_r05.csv")
+    solo_p = _prof("rocprof_solo_kernel_stats_c2_r06.csv", "rocprof_solo_kernel_stats_c2_r05.csv")
     if config == 2 and os.path.exists(solo_p) and stats:
         t_solo = 0.0
         for r in csv.DictReader(open(solo_p, newline="")):
@@ -323,7 +333,7 @@ def roofline(stats: list, config: int, traffic_json: str, tl_union: dict | None 
 def pmc_busy(kernel: str = "k_pf_count") -> dict | None:
     """Per-CU LDS-array and VALU busy of `kernel` (round 4: from the per-kernel PMC totals of
     profiles/r04/pmc_busy_c2_final.json, tools/pmc_agg.py; else round 3's CSV below)."""
-    agg_path = os.path.join(ROOT, "profiles", "r05", "pmc_busy_c2_r05.json")
+    agg_path = _prof("pmc_busy_c2_r06.json", "pmc_busy_c2_r05.json")
     cal_path = os.path.join(ROOT, "profiles", "r03", "pmc_calib.json")
     if os.path.exists(agg_path) and os.path.exists(cal_path):
         agg = json.load(open(agg_path))

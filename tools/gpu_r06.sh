@@ -88,6 +88,8 @@ for st in "$@"; do
     lazyab) for v in ${LAZYS:-5 0 5 0}; do for c in ${PCFGS:-5 2 3 4}; do
               UMICLUST_LAZY=$v timeout -k 10 500 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/lz${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    ldsprobe) timeout -k 10 120 ./tools/lds_atom_probe 2.4 > "$out/lds_atom_probe.jsonl" 2>&1; rc=$? ;;
+    arrcheck) timeout -k 10 120 ./tools/arrange_check > "$out/arrange_check.json" 2>&1; rc=$? ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
