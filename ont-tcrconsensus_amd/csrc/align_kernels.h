@@ -204,7 +204,9 @@ __device__ __forceinline__ uint32_t gt_mask(v2s b, v2s a) {
 //    (that closure kept the row arrays in scratch).
 
 // k_align_pk's boundary column -1: H'(i,-1) = -(GO_TL + (i+1) GE_TL) - X (i+1), E'(i,0) opened
-// from it; summaries u + 1 = i + 1, no matches; keep_mask selects the halves to (re)initialise
+// from it; summaries u + 1 = i + 1, no matches; keep_mask selects the halves to (re)initialise.  X is the row
+// potential's coefficient (k_align_pk: mismatch + Bq, k_align_band: mismatch) and QRqi / QRqr the E openings in
+// the caller's frame.
 template <int QL, int TOP>
 __device__ __forceinline__ void pk_init_rows(v2s (&H)[TOP], v2s (&E)[TOP], uint32_t (&SH)[TOP],
                                              uint32_t (&SE)[TOP], uint32_t keep_mask,
@@ -271,11 +273,16 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
       pM[((b * NG + g) * 2 + 1) * 64] = (uint16_t)(MB[g] >> (16 * b));
     }
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int X = sc.mismatch;
-  const int QRti = sc.go[3] + sc.ge[3] + X, Rti = sc.ge[3] + X;  // vertical gaps: + X (potential)
-  const int QRtr = sc.go[5] + sc.ge[5] + X, Rtr = sc.ge[5] + X;
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  // potentials (round 6): the kernel works on H''(i,j) = H(i,j) - (X + Bq)(i+1) + Bq (j+1), E and F alike.  Every
+  // comparison is between states of one cell, so no decision changes; a diagonal step is H'' + e DELTA (the row term
+  // -(X + Bq) and the column term Bq cancel the mismatch score), an interior horizontal gap extension (E) costs
+  // nothing (Bq = its penalty: one v_pk_sub_i16 less per packed row), a vertical step costs X + Bq more (folded into
+  // the F constants) and an E opening Bq less; the end score takes the potentials back off.
+  const int X = sc.mismatch, Bq = sc.ge[2];
+  const int QRti = sc.go[3] + sc.ge[3] + X + Bq, Rti = sc.ge[3] + X + Bq;  // vertical gaps
+  const int QRtr = sc.go[5] + sc.ge[5] + X + Bq, Rtr = sc.ge[5] + X + Bq;
+  const int QRqi = sc.go[2] + sc.ge[2] - Bq;  // horizontal openings; interior extension 0
+  const int QRqr = sc.go[4] + sc.ge[4] - Bq, Rqr = sc.ge[4] - Bq;  // last row (the query's right end)
   const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
   v2s H[TOP], E[TOP];
   uint32_t SH[TOP], SE[TOP];
@@ -285,7 +292,7 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
     E[kk] = as_v2(0u);
     SH[kk] = SE[kk] = 0;
   }
-  pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffffffffu, sc, X, QRqi, QRqr);
+  pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffffffffu, sc, X + Bq, QRqi, QRqr);
   // carries of the top half's last row, consumed by the bottom half in the next step
   uint32_t cHd = 0, cSHd = 0, cF = 0, cSF = 0, cDL = 0;
   int Lext = 0, trail = 0;
@@ -311,9 +318,9 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
     const bool lc0 = LAST && (j == tl - 1), lc1 = LAST && (j == tl);
     const uint32_t QRt = LAST ? pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti) : pk2(QRti, QRti);
     const uint32_t Rt = LAST ? pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti) : pk2(Rti, Rti);
-    // row -1 (top half, column j: potential 0) | carry (bottom half, column j-1)
-    const int hd0 = (j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
+    // row -1 (top half, column j: potential Bq j for H(-1, j-1), Bq (j + 1) for F(0, j)) | carry (bottom half)
+    const int hd0 = ((j == 0) ? 0 : -(sc.go[0] + j * sc.ge[0])) + Bq * j;
+    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) + Bq * (j + 1) : kNegInf;
     v2s Hd = as_v2(pk2(hd0, (int)cHd));
     uint32_t SHd = pk2(j << 8, (int)cSHd);  // H(-1, j-1): u = j - 1
     v2s F = as_v2(pk2(f0, (int)cF));
@@ -361,8 +368,8 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
       }
       SF = bfi(mfx, SF, sh);
       const uint32_t qrq = pk2(QRqi, (TOP + kk == QL - 1) ? QRqr : QRqi);
-      const uint32_t rq = pk2(Rqi, (TOP + kk == QL - 1) ? Rqr : Rqi);
-      const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
+      // interior rows extend E for free; the last row (high half of register KL) pays its terminal extension
+      const v2s eo = h - as_v2(qrq), ee = (TOP + kk == QL - 1) ? Ec - as_v2(pk2(0, Rqr)) : Ec;
       const uint32_t mex = gt_mask(ee, eo);
       if (kk == KL) {
         // trailing I-run counters along the last row; the value left by the last column is the
@@ -389,7 +396,7 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
   for (; j < tl - 1; j++) {
     step(j, BTag<false>{});
     if (j == 0) {
-      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X, QRqi, QRqr);
+      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X + Bq, QRqi, QRqr);
       Lext = 0;
       trail = 0;
     }
@@ -397,12 +404,12 @@ __device__ __forceinline__ void align_pk_pair(const DevSeqs& s, const uint32_t* 
   for (; j <= tl; j++) {
     step(j, BTag<true>{});
     if (j == 0) {
-      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X, QRqi, QRqr);
+      pk_init_rows<QL, TOP>(H, E, SH, SE, 0xffff0000u, sc, X + Bq, QRqi, QRqr);
       Lext = 0;
       trail = 0;
     }
   }
-  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + X * QL;
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + (X + Bq) * QL - Bq * tl;
   const uint32_t S = (SH[KL] >> 16) & 0xffffu;
   const uint32_t m = S & 0xffu;
   const uint32_t acols = (uint32_t)(QL + tl) - (S >> 8);

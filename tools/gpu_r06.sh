@@ -90,6 +90,8 @@ for st in "$@"; do
                 > "$out/lz${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     ldsprobe) timeout -k 10 120 ./tools/lds_atom_probe 2.4 > "$out/lds_atom_probe.jsonl" 2>&1; rc=$? ;;
     arrcheck) timeout -k 10 120 ./tools/arrange_check > "$out/arrange_check.json" 2>&1; rc=$? ;;
+    alignt) timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "align or golden or o4" \
+             > "$out/alignt.log" 2>&1; rc=$?; tail -3 "$out/alignt.log" ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
