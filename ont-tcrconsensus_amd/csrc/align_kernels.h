@@ -496,13 +496,14 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     }
   }
   const uint32_t* tcp = s.codes + (int64_t)t * 2 * kCodeWords;
-  const int X = sc.mismatch;  // k_align_pk's row potential: H' = H - X (global row + 1)
-  const int QRti = sc.go[3] + sc.ge[3] + X, Rti = sc.ge[3] + X;
-  const int QRtr = sc.go[5] + sc.ge[5] + X, Rtr = sc.ge[5] + X;
-  const int QRqi = sc.go[2] + sc.ge[2], Rqi = sc.ge[2];
-  const int QRqr = sc.go[4] + sc.ge[4], Rqr = sc.ge[4];
+  // k_align_pk's potentials: H'' = H - (X + Bq)(global row + 1) + Bq (column + 1), so an interior E extension is free
+  const int X = sc.mismatch, Bq = sc.ge[2];
+  const int QRti = sc.go[3] + sc.ge[3] + X + Bq, Rti = sc.ge[3] + X + Bq;
+  const int QRtr = sc.go[5] + sc.ge[5] + X + Bq, Rtr = sc.ge[5] + X + Bq;
+  const int QRqi = sc.go[2] + sc.ge[2] - Bq;
+  const int QRqr = sc.go[4] + sc.ge[4] - Bq, Rqr = sc.ge[4] - Bq;
   const v2s DELTA = as_v2(pk2(sc.match - sc.mismatch, sc.match - sc.mismatch));
-  const uint32_t qrqL = pk2(QRqi, last ? QRqr : QRqi), rqL = pk2(Rqi, last ? Rqr : Rqi);
+  const uint32_t qrqL = pk2(QRqi, last ? QRqr : QRqi), rqL = pk2(0, last ? Rqr : 0);
   v2s H[TOP], E[TOP];
   // summaries: k_align_pk's m | (u + 1) << 8 with u biased by kSB (> the virtual rows' depth P - 1, so the
   // virtual rows' start values are not negative either)
@@ -515,12 +516,12 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     // values from being hoisted into 2 TOP live VGPRs.
     int vz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
-    const int hbase = vz - sc.go[1] - (r0 + 1) * (sc.ge[1] + X);
+    const int hbase = vz - sc.go[1] - (r0 + 1) * (sc.ge[1] + X + Bq);
     const uint32_t sbase = (uint32_t)vz + pk2((r0 + 1 + kSB) << 8, (r0 + TOP + 1 + kSB) << 8);
 #pragma unroll
     for (int kk = 0; kk < TOP; kk++) {
-      const int h0 = hbase - kk * (sc.ge[1] + X);
-      const int h1 = hbase - (TOP + kk) * (sc.ge[1] + X);
+      const int h0 = hbase - kk * (sc.ge[1] + X + Bq);
+      const int h1 = hbase - (TOP + kk) * (sc.ge[1] + X + Bq);
       const int q1 = (kk == KL && last) ? QRqr : QRqi;
       const int e0 = sc.boundary_open ? h0 - QRqi : kNegInf;
       const int e1 = sc.boundary_open ? h1 - q1 : kNegInf;
@@ -565,8 +566,8 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     const uint32_t QRt = pk2(lc0 ? QRtr : QRti, lc1 ? QRtr : QRti);
     const uint32_t Rt = pk2(lc0 ? Rtr : Rti, lc1 ? Rtr : Rti);
     // the row above the top half: the boundary row -1 (lane 0) or lane g-1's last row | carry (bottom half)
-    const int hd0 = (j <= 0) ? 0 : -(sc.go[0] + j * sc.ge[0]);
-    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) : kNegInf;
+    const int hd0 = (j <= 0) ? 0 : -(sc.go[0] + j * sc.ge[0]) + Bq * j;
+    const int f0 = sc.boundary_open ? -(sc.go[0] + (j + 1) * sc.ge[0]) - (lc0 ? QRtr : QRti) + Bq * (j + 1) : kNegInf;
     // boundary row -1 for lane 0: H(-1, j-1) (u = j - 1), F(0, j) (u = j, one D move)
     const int jb = (j < 0 ? 0 : j) + kSB;
     v2s Hd = as_v2(bfi(fm, (uint32_t)hd0 & 0xffffu, rHF & 0xffffu) | (cHd << 16));
@@ -611,8 +612,7 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
       DL = bfi(mfx | (mF & ~mE), DL + 0x00010001u, 0x00010001u);
       SF = bfi(mfx, SF, sh);
       const uint32_t qrq = kk == KL ? qrqL : pk2(QRqi, QRqi);
-      const uint32_t rq = kk == KL ? rqL : pk2(Rqi, Rqi);
-      const v2s eo = h - as_v2(qrq), ee = Ec - as_v2(rq);
+      const v2s eo = h - as_v2(qrq), ee = kk == KL ? Ec - as_v2(rqL) : Ec;  // interior E extension: free
       const uint32_t mex = gt_mask(ee, eo);
       if (kk == KL) {
         const bool ex = (mex >> 31) != 0;
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
         if (kk == VK) {
           // lane 0's stand-in row leaves exactly what the boundary row -1 gives the row below it
           const int cv = VR < TOP ? j : j - 1;
-          const int hb = cv < 0 ? 0 : -(sc.go[0] + (cv + 1) * sc.ge[0]);
+          const int hb = cv < 0 ? 0 : -(sc.go[0] + (cv + 1) * sc.ge[0]) + Bq * (cv + 1);
           const int fb = sc.boundary_open ? hb - (cv == tl - 1 ? QRtr : QRti) : kNegInf;
           const int sb = (cv < -1 ? -1 : cv) + 1 + kSB;  // H(-1, cv) and F(0, cv): u = cv
           const uint32_t vm = VM & fm;
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
     }
   }
   if (!last) return;
-  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + X * QL;
+  const int Hend = (int)(short)(as_u(H[KL]) >> 16) + (X + Bq) * QL - Bq * tl;
   const uint32_t S = (SH[KL] >> 16) & 0xffffu;
   const uint32_t m = S & 0xffu;
   const uint32_t acols = (uint32_t)(QL + tl + kSB) - (S >> 8);
