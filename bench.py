@@ -70,11 +70,11 @@ def _prof(*names: str) -> str:
 
 def align_issue_ceiling() -> dict | None:
     """The aligner's ceiling at the measured issue cost of its own instruction mix: the column loop of
-    k_align_pk<64> (tools/isa_mix.py -> profiles/r05/align_issue_mix_pk64.json: VOP2, packed VOP3P and other VOP3
+    k_align_pk<64> (tools/isa_mix.py -> profiles/r06/align_issue_mix_pk64.json: VOP2, packed VOP3P and other VOP3
     instructions per step of 64 cells per lane) priced with tools/valu_rate.hip's cycles per wave-instruction per
     SIMD at 4 waves per SIMD (profiles/r05/valu_rate.jsonl: 8-byte VOP3/VOP3P encodings issue ~1.5x slower than
     4-byte VOP2 ones), in the probe's own 2.4 GHz-nominal cycle units."""
-    mp = os.path.join(ROOT, "profiles", "r05", "align_issue_mix_pk64.json")
+    mp = _prof("align_issue_mix_pk64.json")
     rp = os.path.join(ROOT, "profiles", "r05", "valu_rate.jsonl")
     if not (os.path.exists(mp) and os.path.exists(rp)):
         return None

@@ -426,6 +426,9 @@ struct umiclust_ctx {
   static constexpr bool peer_cert = true;
   int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
   int32_t regrow_depth = kPeerCap / 4;  // UMICLUST_REGROW_DEPTH: a block whose deepest peer list reaches this is not clean
+  int32_t pt_side = 1;       // UMICLUST_PT_SIDE: whole passes build the next peer tiles on st_b beside the counting
+  hipEvent_t pt_ev = nullptr;
+  bool pt_pending = false;   // pt_ev recorded since the main stream last waited for it
   int32_t arrange = 1;       // UMICLUST_ARRANGE: bank-aware posting order in large tiles (1) / small tiles (2)
   int32_t regrow = 8;        // UMICLUST_REGROW: clean shallow blocks before a halved block size doubles (0: never)
   int32_t last_max_npeer = 0;
@@ -769,6 +772,10 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   const int32_t nqs = nq * both;
   hipStream_t st = c->st;
   if (c->ix_st && c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");  // index / peer tiles
+  if (c->pt_pending) {  // whole passes: the peer tiles built ahead on the side stream (cluster_all)
+    c->hip(hipStreamWaitEvent(st, c->pt_ev, 0), "wait");
+    c->pt_pending = false;
+  }
   P.q0 = q0;
   P.nq = nq;
   P.w0 = w0;
@@ -996,6 +1003,10 @@ void enqueue_count(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile*
   // last merge): the main stream's next append and second half do not queue behind it
   hipStream_t st = c->st;
   if (c->ix_st && c->ix_done) c->hip(hipStreamWaitEvent(st, c->ix_done, 0), "wait");  // index / peer tiles
+  if (c->pt_pending) {  // whole passes: the peer tiles built ahead on the side stream (cluster_all)
+    c->hip(hipStreamWaitEvent(st, c->pt_ev, 0), "wait");
+    c->pt_pending = false;
+  }
   // this buffer set's last second half (full kernel + merge on the align stream) has read what
   // the counting half overwrites
   if (c->ix_st) c->hip(hipStreamWaitEvent(st, P.ev[1], 0), "wait");
@@ -1780,11 +1791,23 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k % D];
     if (k + D < nb) {
-      // block k+D's peer tile depends on its queries only: build it now, behind the queued prefilters on the
-      // main stream, while the host resolves block k (its ring slot was last read by pass k+D-2's prefilter)
+      // block k+D's peer tile depends on its queries only: build it now, while the host resolves block k (its ring
+      // slot was last read by pass k's prefilter).  Since round 6 on the side stream (after pass k's prefilter), so
+      // the build runs beside the main stream's counting instead of between two counting launches; the pass that
+      // next enqueues on the main stream waits for it (enqueue_pass, pt_ev).  Before, it sat on the main stream.
       Tile& t = tile_of(k + D);
+      hipStream_t bst = nullptr;
+      if (c->pt_side) {
+        bst = c->st_b;
+        c->hip(hipStreamWaitEvent(bst, P.ev[1], 0), "wait");
+        if (!c->pt_ev) c->hip(hipEventCreateWithFlags(&c->pt_ev, hipEventDisableTiming), "event");
+      }
       build_tile(c, t, c->d_iota.p, blocks[k + D].first, blocks[k + D].second, 0, ((k + D) % D) * kPeerRegion,
-                 1 << 30);
+                 1 << 30, bst);
+      if (bst) {
+        c->hip(hipEventRecord(c->pt_ev, bst), "event");
+        c->pt_pending = true;
+      }
       t.base = blocks[k + D].first;
       t.seg = (k + D) % D;
       t.prebuilt = true;
@@ -2350,7 +2373,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "PT_SIDE", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
@@ -2457,6 +2480,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
+  if (const char* e = getenv("UMICLUST_PT_SIDE")) c->pt_side = atoi(e) != 0;
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, std::min(1000, atoi(e)));
   if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
@@ -2516,6 +2540,7 @@ void umiclust_destroy(umiclust_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   if (c->st_b) (void)hipStreamDestroy(c->st_b);
+  if (c->pt_ev) (void)hipEventDestroy(c->pt_ev);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st_al) (void)hipStreamDestroy(c->st_al);
   if (c->ix_done) (void)hipEventDestroy(c->ix_done);

@@ -92,6 +92,9 @@ for st in "$@"; do
     arrcheck) timeout -k 10 120 ./tools/arrange_check > "$out/arrange_check.json" 2>&1; rc=$? ;;
     alignt) timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "align or golden or o4" \
              > "$out/alignt.log" 2>&1; rc=$?; tail -3 "$out/alignt.log" ;;
+    ptab) for v in ${PTS:-1 0 1 0 1 0}; do for c in ${PCFGS:-2 3 5}; do
+              UMICLUST_PT_SIDE=$v timeout -k 10 500 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/pt${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     resdump) # the recorded resolve passes of the ThreadSanitizer replay (tests/golden/resolve/)
           timeout -k 10 300 python3 -u tests/golden/make_resolve_dumps.py "$out/resolve" > "$out/resdump.log" 2>&1; rc=$? ;;
     *) echo "unknown step $st"; rc=2 ;;
