@@ -427,6 +427,7 @@ struct umiclust_ctx {
   int32_t pf1_lds = 10240;  // UMICLUST_PF1: one-wave counting units up to this LDS per unit (0: never)
   int32_t regrow_depth = kPeerCap / 4;  // UMICLUST_REGROW_DEPTH: a block whose deepest peer list reaches this is not clean
   int32_t pt_side = 1;       // UMICLUST_PT_SIDE: whole passes build the next peer tiles on st_b beside the counting
+                             // (1: single-bin loads; 2: always; 0: on the main stream, as before round 6)
   hipEvent_t pt_ev = nullptr;
   bool pt_pending = false;   // pt_ev recorded since the main stream last waited for it
   int32_t arrange = 1;       // UMICLUST_ARRANGE: bank-aware posting order in large tiles (1) / small tiles (2)
@@ -1797,7 +1798,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       // next enqueues on the main stream waits for it (enqueue_pass, pt_ev).  Before, it sat on the main stream.
       Tile& t = tile_of(k + D);
       hipStream_t bst = nullptr;
-      if (c->pt_side) {
+      if (c->pt_side == 2 || (c->pt_side == 1 && !multi_bin)) {  // config 2 +1.6 %, multi-lane config 3 -2 %
         bst = c->st_b;
         c->hip(hipStreamWaitEvent(bst, P.ev[1], 0), "wait");
         if (!c->pt_ev) c->hip(hipEventCreateWithFlags(&c->pt_ev, hipEventDisableTiming), "event");
@@ -2480,7 +2481,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PF1")) c->pf1_lds = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW")) c->regrow = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
-  if (const char* e = getenv("UMICLUST_PT_SIDE")) c->pt_side = atoi(e) != 0;
+  if (const char* e = getenv("UMICLUST_PT_SIDE")) c->pt_side = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, std::min(1000, atoi(e)));
   if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
