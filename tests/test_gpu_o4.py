@@ -289,3 +289,21 @@ def test_o4_partial_resolution_and_regrowth(monkeypatch):
         assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
         blocks[regrow] = st["n_blocks"]
     assert blocks["1"] < blocks["0"], blocks  # the halved blocks grew again
+
+
+def test_deep_blocks_never_regrow(monkeypatch):
+    """Regrowth gate (advisor round 5): a block whose deepest peer list reaches kPeerCap / 4 is not clean, so even with
+    UMICLUST_REGROW=1 a bin whose every window is deep (four molecules of ~600 reads) re-runs overflowing blocks but
+    never doubles its block size again (umiclust_stats.n_regrows, ABI 9); the clusters equal the O4 oracle's."""
+    monkeypatch.setenv("UMICLUST_BLOCK", "2048")
+    monkeypatch.setenv("UMICLUST_REGROW", "1")
+    monkeypatch.setenv("ORC_WORKERS", "8")
+    seqs = synth.make_umis(4, seed=63, max_reads=2400, mean_reads=1500.0, error_rate=0.02, orient_mix=0.2).as_list()
+    with _lib.Context(0) as ctx:
+        ctx.load(_lib.params(1, 0.90, 58, 68, threads=25), seqs)
+        st = ctx.cluster()
+        g = ctx.fetch()
+    assert st["n_reruns"] > 0 and st["n_regrows"] == 0, st
+    o = orc.cluster(_params(orc, 1, 0.90, 25), seqs)
+    _cmp(g, o)
+    assert st["n_alignments"] == o["stats"]["alignments"] and st["cells"] == o["stats"]["cells"]
