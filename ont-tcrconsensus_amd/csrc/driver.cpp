@@ -163,6 +163,7 @@ struct Pass {
   DevBuf<uint16_t> d_ppeer_id;
   DevBuf<uint16_t> d_peer_id;
   DevBuf<uint8_t> d_peer_count, d_npeer;
+  bool ctr_zeroed = false;      // d_counters re-zeroed by the last k_pack on this buffer set
   DevBuf<uint32_t> d_counters;  // [0] postings, [1..5] npairs per walk round, [8] peer pairs,
                                 // [9] target residues of walk pairs, [10] of peer pairs
   DevBuf<uint32_t> d_pq, d_pt, d_outidx, d_res;
@@ -685,6 +686,7 @@ void ensure_pass_buffers(umiclust_ctx* c, Pass& P, int32_t B) {
   c->hip(P.d_peer_count.ensure(nqs * kPeerCap), "alloc");
   c->hip(P.d_npeer.ensure(nqs), "alloc");
   c->hip(P.d_counters.ensure(kCountersLen), "alloc");
+  P.ctr_zeroed = false;  // (a new bin or a grown buffer set: the next pass memsets them)
   // pair lists: a launch aligns up to kWalk walk pairs plus kPeerCap peer pairs per query-strand; results
   // land in d_res: walk candidate x of qs at [qs * kWalk + x], peer y at [nqs * kWalk + qs * kPeerCap + y]
   c->hip(P.d_pq.ensure(nqs * (kWalk + kPeerCap)), "alloc");
@@ -809,7 +811,9 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
   if (nv > kArgTiles)
     c->hip(hipMemcpyAsync(P.d_tiles.p, P.h_tiles.p, (size_t)nv * sizeof(TileView), hipMemcpyHostToDevice, st),
            "tiles");
-  c->hip(hipMemsetAsync(P.d_counters.p, 0, kCountersLen * 4, st), "memset");
+  // the counters are zero unless this buffer set's last pass launched no k_pack (which re-zeroes them at its end)
+  if (!P.ctr_zeroed) c->hip(hipMemsetAsync(P.d_counters.p, 0, kCountersLen * 4, st), "memset");
+  P.ctr_zeroed = false;
   PrefilterArgs a{};
   for (int32_t i = 0; i < nv && nv <= kArgTiles; i++) a.tv[i] = P.h_tiles.p[i];
   a.seqs = dev_seqs(c);
@@ -979,6 +983,7 @@ void enqueue_pass(umiclust_ctx* c, Pass& P, int32_t q0, int32_t nq, const Tile* 
                      P.rec_direct ? P.h_hq.p : P.d_hq.p,
                      P.rec_direct ? P.h_rec.p : P.d_rec.p, P.d_counters.p, P.h_counters.p, P.h_reccount.p, st),
          "pack");
+  P.ctr_zeroed = nqs > 0;
   if (!P.rec_direct)
     c->hip(hipMemcpyAsync(P.h_hq.p, P.d_hq.p, (size_t)nqs * sizeof(HostQs), hipMemcpyDeviceToHost, st), "d2h outcomes");
   if (!P.rec_direct) {

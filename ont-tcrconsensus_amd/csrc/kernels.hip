@@ -1916,9 +1916,10 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
                                               const unsigned long long* __restrict__ aligned,
                                               uint32_t* __restrict__ reccount,
                                               HostQs* __restrict__ hq, uint32_t* __restrict__ rec,
-                                              const uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters,
+                                              uint32_t* __restrict__ counters, uint32_t* __restrict__ hcounters,
                                               uint32_t* __restrict__ hreccount) {
   __shared__ uint32_t wsize[kPackWaves * kPackQ];
+  __shared__ uint32_t last_wg;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qs0 = ((int)blockIdx.x * kPackWaves + wave) * kPackQ;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
@@ -1976,13 +1977,23 @@ __global__ __launch_bounds__(64 * kPackWaves) void k_pack(int32_t nqs, int32_t w
     // pinned host memory and re-zeroes both counters for the buffer set's next pass, so the chain the host waits on
     // holds no memset and no 4-byte copy (each a blit dispatch)
     __threadfence();
+    last_wg = 0u;
     if (atomicAdd(reccount + 1, 1u) == gridDim.x - 1) {
       *hreccount = atomicAdd(reccount, 0u);
       atomicExch(reccount, 0u);
       atomicExch(reccount + 1, 0u);
+      last_wg = 1u;
     }
   }
   __syncthreads();
+  // the last workgroup also re-zeroes the pass counters (every kernel of the pass that adds to them ran before this
+  // one on the align stream, and workgroup 0 copied them out before taking its ticket): the main stream's next pass
+  // on this buffer set needs no memset, a blit dispatch that waited for a CU slot behind the alignment waves
+  // (4-125 us per pass, round 6)
+  if (last_wg) {
+    __threadfence();
+    for (int i = (int)threadIdx.x; i < kCountersLen; i += 64 * kPackWaves) counters[i] = 0u;
+  }
   // phase 2: records and outcomes
 #pragma unroll
   for (int i = 0; i < kPackQ; i++) {
@@ -2063,7 +2074,7 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
                        const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
-                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, uint32_t* hreccount,
+                       uint32_t* rec, uint32_t* counters, uint32_t* hcounters, uint32_t* hreccount,
                        hipStream_t st) {
   if (nqs <= 0) {
     *hreccount = 0;  // no launch: nothing of this pass is in flight on the buffer set

@@ -196,7 +196,7 @@ hipError_t launch_pack(int32_t nqs, int32_t w0, const uint8_t* lens, const WalkS
                        const uint32_t* top_seqno, const uint8_t* top_count, const uint32_t* res,
                        const uint8_t* npeer, const uint16_t* peer_id, const uint8_t* peer_count,
                        const uint32_t* peer_res, const unsigned long long* aligned, uint32_t* reccount, HostQs* hq,
-                       uint32_t* rec, const uint32_t* counters, uint32_t* hcounters, uint32_t* hreccount, hipStream_t st);
+                       uint32_t* rec, uint32_t* counters, uint32_t* hcounters, uint32_t* hreccount, hipStream_t st);
 // traceback (one wave per pair, any query length): ops[k*kOpsStride...] ('M','D','I' in alignment order,
 // right-aligned in the slot), nops[k], out[k] as launch_align's
 // maxl: the longest query or target length among the pairs (sizes the kernel's LDS)
