@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64) void k_list_arrange(const uint32_t* __restrict_
   }
 }
 hipError_t launch_index_arrange(const uint32_t* off, uint16_t* post, hipStream_t st) {
-  hipLaunchKernelGGL(k_list_arrange, dim3(kBins / 64 / 8), dim3(64), 0, st, off, post, (int32_t)kBins);
+  hipLaunchKernelGGL(k_list_arrange, dim3(kBins / 64), dim3(64), 0, st, off, post, (int32_t)kBins);
   return hipGetLastError();
 }
 
