@@ -83,6 +83,8 @@ for st in "$@"; do
     rdab) for v in ${RDS:-32 48 64 96 32}; do for c in ${PCFGS:-5 4}; do
               UMICLUST_REGROW_DEPTH=$v timeout -k 10 500 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/rd${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    c2dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
+             > "$out/c2dbg.json" 2> "$out/c2dbg.err"; rc=$? ;;
     c5dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --config 5 --steps 1 --warmup 1 --no-cpu-baseline \
              > "$out/c5dbg.json" 2> "$out/c5dbg.err"; rc=$? ;;
     lazyab) for v in ${LAZYS:-5 0 5 0}; do for c in ${PCFGS:-5 2 3 4}; do
