@@ -438,12 +438,15 @@ struct umiclust_ctx {
   DevBuf<uint32_t> d_probe;
   // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
   int32_t lazy_permille = 5;  // UMICLUST_LAZY (0: never lazy)
+  int32_t rb_direct = 4096;   // round B: at most this many pairs read / written in pinned memory (UMICLUST_RB_DIRECT)
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
   int al_level = 0;                 // the alignment stream: 0 prioritised (al_priority), -1 plain (set_priority -1)
   int st_level = 0, prio_user = 0;  // the main stream's priority now / as umiclust_set_priority left it
   int64_t dbg[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: mispredicted peers, saved peers, blocked, -
-  bool debug = getenv("UMICLUST_DEBUG") != nullptr;
+  // UMICLUST_DEBUG: per-block lines and sequential in-order resolution; UMICLUST_DEBUG=2: the per-bin summary only (the
+  // production code path, with its parallel in-order phase)
+  bool debug = getenv("UMICLUST_DEBUG") != nullptr && strcmp(getenv("UMICLUST_DEBUG"), "2") != 0;
   int64_t dbg_q[4] = {0, 0, 0, 0};
   // UMICLUST_WALK_DUMP=<file>: per sorted seqno of the bin, the alignments each strand's walk counted and the
   // path that resolved it (0 device, 1 classify thread, 2 in order, 3 round B) -- a parity-debugging aid
@@ -1236,33 +1239,45 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   env.walk_dump = c->wd.empty() ? nullptr : c->wd.data();
   // round B on the copy stream (a hardware queue of its own, otherwise idle): on st_b it queued behind the split
   // passes' index appends and peer-tile builds, which wait for the next counting half -- about one counting launch of
-  // latency on the host's critical path per block with deferred queries (UMICLUST_RB_STREAM=b: st_b)
+  // latency on the host's critical path per block with deferred queries
   auto round_b = [&](const std::vector<uint32_t>& bpq, const std::vector<uint32_t>& bpt, std::vector<uint32_t>& bres) {
     const int32_t nb = (int32_t)bpq.size();
     hipStream_t sb = c->st_copy;
-    c->hip(c->d_bpq.ensure(nb), "alloc");
-    c->hip(c->d_bpt.ensure(nb), "alloc");
-    c->hip(c->d_bres.ensure(nb), "alloc");
     c->hip(c->h_bpq.ensure(nb), "pin");
     c->hip(c->h_bpt.ensure(nb), "pin");
     c->hip(c->h_bres.ensure(nb), "pin");
     memcpy(c->h_bpq.p, bpq.data(), (size_t)nb * 4);
     memcpy(c->h_bpt.p, bpt.data(), (size_t)nb * 4);
-    c->hip(hipMemcpyAsync(c->d_bpq.p, c->h_bpq.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
-    c->hip(hipMemcpyAsync(c->d_bpt.p, c->h_bpt.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+    // small rounds (the usual: tens of pairs) read their pairs from and write their scores to the pinned buffers
+    // directly: one dispatch per query length and no copies on the host's critical path (two uploads and a download
+    // were ~70 us of dispatch latency per block with deferred queries); large ones go through device buffers
+    const bool direct = nb <= c->rb_direct;
+    const uint32_t *pq = c->h_bpq.p, *pt = c->h_bpt.p;
+    uint32_t* pres = c->h_bres.p;
+    if (!direct) {
+      c->hip(c->d_bpq.ensure(nb), "alloc");
+      c->hip(c->d_bpt.ensure(nb), "alloc");
+      c->hip(c->d_bres.ensure(nb), "alloc");
+      c->hip(hipMemcpyAsync(c->d_bpq.p, c->h_bpq.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+      c->hip(hipMemcpyAsync(c->d_bpt.p, c->h_bpt.p, (size_t)nb * 4, hipMemcpyHostToDevice, sb), "h2d");
+      pq = c->d_bpq.p;
+      pt = c->d_bpt.p;
+      pres = c->d_bres.p;
+    }
     c->hip(hipEventRecord(c->evb[0], sb), "event");
     // the pairs are in query order: one launch per run of one query length
     for (int32_t x0 = 0; x0 < nb;) {
       const int32_t L = c->hlen[bpq[x0] >> 1];
       int32_t x1 = x0 + 1;
       while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
-      c->hip(launch_align(dev_seqs(c), L, c->ambig, c->d_bpq.p + x0, c->d_bpt.p + x0, x1 - x0, nullptr, nullptr, c->sc,
-                          c->d_bres.p + x0, sb, c->band_pairs),
+      c->hip(launch_align(dev_seqs(c), L, c->ambig, pq + x0, pt + x0, x1 - x0, nullptr, nullptr, c->sc, pres + x0, sb,
+                          c->band_pairs),
              "align B");
       x0 = x1;
     }
     c->hip(hipEventRecord(c->evb[1], sb), "event");
-    c->hip(hipMemcpyAsync(c->h_bres.p, c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
+    if (!direct)
+      c->hip(hipMemcpyAsync(c->h_bres.p, c->d_bres.p, (size_t)nb * 4, hipMemcpyDeviceToHost, sb), "d2h");
     c->hip(hipStreamSynchronize(sb), "sync");
     memcpy(bres.data(), c->h_bres.p, (size_t)nb * 4);
     float bms = 0;
@@ -1796,6 +1811,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
   for (int32_t i = 0; i < D && i < nb; i++) enqueue(i, i);
   for (int32_t k = 0; k < nb; k++) {
     Pass& P = c->pass[k % D];
+    const double te0 = now_s();
     if (k + D < nb) {
       // block k+D's peer tile depends on its queries only: build it now, while the host resolves block k (its ring
       // slot was last read by pass k's prefilter).  Since round 6 on the side stream (after pass k's prefilter), so
@@ -1818,6 +1834,7 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       t.seg = (k + D) % D;
       t.prebuilt = true;
     }
+    c->dbg_t[5] += now_s() - te0;
     int32_t done = 0;
     if (!resolve_pass(c, P, state, new_cents, t_pf, t_al, t_host, &done)) {
       // drain the queued passes k+1 .. k+D-1 (their windows include block k) and restart the pipeline
@@ -1873,7 +1890,9 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
       nb = (int32_t)blocks.size();
       tile_of(k + D).prebuilt = false;
     }
+    const double te1 = now_s();
     if (k + D < nb) enqueue(k + D, D - 1);
+    c->dbg_t[5] += now_s() - te1;
   }
   }
   c->b_hint = b_eff;
@@ -2054,7 +2073,8 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
             "(round B and the rest %.3f)\n", bin, c->dbg_t[0], c->dbg_t[1], c->dbg_t[2], c->dbg_t[3], c->dbg_t[4],
             c->dbg_t[6], c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[3] - c->dbg_t[4]);
   if (getenv("UMICLUST_DEBUG"))
-    fprintf(stderr, "bin %d: split-pass host: appends %.3f enqueue %.3f s\n", bin, c->dbg_t[7], c->dbg_t[5]);
+    fprintf(stderr, "bin %d: host: split-pass appends %.3f, enqueue (peer tiles, appends, launches) %.3f s; bin %.3f s\n",
+            bin, c->dbg_t[7], c->dbg_t[5], now_s() - t0);
   for (double& x : c->dbg_t) x = 0;
   c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
   c->dbg_p[0] = c->dbg_p[1] = c->dbg_p[2] = c->dbg_p[3] = 0;
@@ -2242,7 +2262,7 @@ void prepare_impl(umiclust_ctx* c, const umiclust_params* p) {
   }
   const double tp2 = now_s();
   c->hip(hipStreamSynchronize(c->st), "sync load");
-  if (c->debug)
+  if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "umiclust: prepare: host sort %.4f s, after the K1 launch %.4f s, sync %.4f s\n", tp1 - tp0,
             tp2 - tp1, now_s() - tp2);
   c->ambig = c->h_amb.p[0] != 0;
@@ -2407,7 +2427,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "PT_SIDE", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
@@ -2516,6 +2536,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_ARRANGE")) c->arrange = atoi(e) & 3;
   if (const char* e = getenv("UMICLUST_PT_SIDE")) c->pt_side = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, std::min(1000, atoi(e)));
+  if (const char* e = getenv("UMICLUST_RB_DIRECT")) c->rb_direct = std::max(0, atoi(e));
   if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {

@@ -85,6 +85,11 @@ for st in "$@"; do
                 > "$out/rd${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     c2dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
              > "$out/c2dbg.json" 2> "$out/c2dbg.err"; rc=$? ;;
+    rbab) for v in ${RBS:-4096 0 4096 0}; do for c in ${PCFGS:-5}; do
+              UMICLUST_RB_DIRECT=$v timeout -k 10 300 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/rb${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    dbg2) for c in ${PCFGS:-2 5}; do UMICLUST_DEBUG=2 timeout -k 10 300 python3 -u bench.py --config $c --steps 2 --warmup 1 \
+             --no-cpu-baseline --no-e2e > "$out/dbg2_c$c.json" 2> "$out/dbg2_c$c.err" || { rc=$?; break; }; rc=0; done ;;
     c5dbg) UMICLUST_DEBUG=1 timeout -k 10 300 python3 -u bench.py --config 5 --steps 1 --warmup 1 --no-cpu-baseline \
              > "$out/c5dbg.json" 2> "$out/c5dbg.err"; rc=$? ;;
     lazyab) for v in ${LAZYS:-5 0 5 0}; do for c in ${PCFGS:-5 2 3 4}; do
