@@ -468,8 +468,9 @@ struct umiclust_ctx {
     return false;
   }
   std::vector<int16_t> wd;
-  double dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // UMICLUST_DEBUG: resolve_pass phases (s): event wait, outcome copy,
-                                               // record copy, classify, in-order resolve, round B + rest, total
+  double dbg_rb[4] = {};  // UMICLUST_DEBUG: round B device time (s), round trips, launches, pairs
+  double dbg_t[10] = {};  // UMICLUST_DEBUG: resolve_pass phases (s): event wait, outcome copy, record copy, classify,
+                          // in-order resolve, enqueue, total, appends, round B round trips, resolve_block
   int64_t dbg_p[4] = {0, 0, 0, 0};  // UMICLUST_DEBUG: strands on the inline path / with > kInlineRel relevant
                                     // peers / reading their record / peers scanned there  // UMICLUST_DEBUG: queries without records / records with only earlier-block
                                     // relevant peers / with an in-block relevant peer / host ns in pass 1
@@ -1266,7 +1267,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     }
     c->hip(hipEventRecord(c->evb[0], sb), "event");
     // the pairs are in query order: one launch per run of one query length
-    for (int32_t x0 = 0; x0 < nb;) {
+    int nl = 0;
+    for (int32_t x0 = 0; x0 < nb; nl++) {
       const int32_t L = c->hlen[bpq[x0] >> 1];
       int32_t x1 = x0 + 1;
       while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
@@ -1283,6 +1285,10 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
     float bms = 0;
     c->hip(hipEventElapsedTime(&bms, c->evb[0], c->evb[1]), "elapsed");
     t_al += bms * 1e-3;
+    c->dbg_rb[0] += bms * 1e-3;
+    c->dbg_rb[1] += 1;
+    c->dbg_rb[2] += nl;
+    c->dbg_rb[3] += nb;
   };
   // UMICLUST_RESOLVE_DUMP: the pass's inputs, round-B pairs / results and outputs, for the host-only replay
   // (tools/resolve_tsan_main.cpp: the ThreadSanitizer harness of the CPU suite)
@@ -1329,6 +1335,8 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
   c->stats.t_host_pass1_s += rs.t_classify_s + rs.t_inorder_s;
   c->dbg_t[3] += rs.t_classify_s;
   c->dbg_t[4] += rs.t_inorder_s;
+  c->dbg_t[8] += rs.t_round_b_s;
+  c->dbg_t[9] += th;
   c->stats.n_alignments += rs.n_alignments;
   c->stats.cells += rs.cells;
   c->stats.n_merged_walks += rs.n_merged_walks;
@@ -2070,11 +2078,18 @@ void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t n
             (long long)c->dbg_p[0], (long long)c->dbg_p[1], (long long)c->dbg_p[2], (long long)c->dbg_p[3]);
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: resolve wait %.3f hq-copy %.3f rec-copy %.3f classify %.3f in-order %.3f total %.3f s "
-            "(round B and the rest %.3f)\n", bin, c->dbg_t[0], c->dbg_t[1], c->dbg_t[2], c->dbg_t[3], c->dbg_t[4],
-            c->dbg_t[6], c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[3] - c->dbg_t[4]);
+            "(round B and the rest %.3f: round-B round trips %.3f, rest of resolve_block %.3f, outside it %.3f)\n", bin,
+            c->dbg_t[0], c->dbg_t[1], c->dbg_t[2], c->dbg_t[3], c->dbg_t[4], c->dbg_t[6],
+            c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[3] - c->dbg_t[4], c->dbg_t[8],
+            c->dbg_t[9] - c->dbg_t[3] - c->dbg_t[4] - c->dbg_t[8],
+            c->dbg_t[6] - c->dbg_t[0] - c->dbg_t[1] - c->dbg_t[2] - c->dbg_t[9]);
   if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "bin %d: host: split-pass appends %.3f, enqueue (peer tiles, appends, launches) %.3f s; bin %.3f s\n",
             bin, c->dbg_t[7], c->dbg_t[5], now_s() - t0);
+  if (getenv("UMICLUST_DEBUG"))
+    fprintf(stderr, "bin %d: round B: %.0f round trips, %.0f launches, %.0f pairs, %.4f s between its first and last "
+            "launch's events\n", bin, c->dbg_rb[1], c->dbg_rb[2], c->dbg_rb[3], c->dbg_rb[0]);
+  for (double& x : c->dbg_rb) x = 0;
   for (double& x : c->dbg_t) x = 0;
   c->dbg_q[0] = c->dbg_q[1] = c->dbg_q[2] = c->dbg_q[3] = 0;
   c->dbg_p[0] = c->dbg_p[1] = c->dbg_p[2] = c->dbg_p[3] = 0;
@@ -2427,7 +2442,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "RB_PRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
@@ -2496,6 +2511,13 @@ static int al_priority() {
   return hi;
 }
 
+// the copy stream carries round B (the host waits for it): at the greatest priority with UMICLUST_RB_PRIO=1
+static hipError_t create_copy_stream(umiclust_ctx* c) {
+  const char* e = getenv("UMICLUST_RB_PRIO");
+  if (e && atoi(e) > 0) return hipStreamCreateWithPriority(&c->st_copy, hipStreamNonBlocking, al_priority());
+  return hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking);
+}
+
 static hipError_t create_al_stream(umiclust_ctx* c) {
   return hipStreamCreateWithPriority(&c->st_al, hipStreamNonBlocking, al_priority());
 }
@@ -2514,8 +2536,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   c->dev = device_id;
   if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->st_b, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess ||
-      create_al_stream(c) != hipSuccess ||
+      create_copy_stream(c) != hipSuccess || create_al_stream(c) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->evb[0]) != hipSuccess || hipEventCreate(&c->evb[1]) != hipSuccess || [&] {
         for (Pass& P : c->pass)
