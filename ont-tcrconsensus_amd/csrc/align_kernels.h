@@ -110,6 +110,7 @@ __global__ __launch_bounds__(64) void k_align(DevSeqs s, const uint32_t* __restr
                                               const uint32_t* __restrict__ outidx, Scoring sc,
                                               uint32_t* __restrict__ out) {
   constexpr int CW = (QL + 7) / 8;
+  if (sc.wave_prio) __builtin_amdgcn_s_setprio(3);
   const int k = blockIdx.x * 64 + threadIdx.x;
   if (k >= npairs) return;
   if (dev_npairs && k >= (int)*dev_npairs) return;
@@ -428,6 +429,7 @@ __global__ __launch_bounds__(64) void k_align_pk(DevSeqs s, const uint32_t* __re
                                                  uint32_t* __restrict__ out) {
   constexpr int NG = ((QL + 1) / 2 + 15) / 16;
   __shared__ uint16_t sM[4 * NG * 2 * 64];
+  if (sc.wave_prio) __builtin_amdgcn_s_setprio(3);
   const int n = dev_npairs ? min(npairs, (int)*dev_npairs) : npairs;
   for (int k0 = (int)blockIdx.x * 64; k0 < n; k0 += (int)gridDim.x * 64) {  // wave-uniform
     const int k = k0 + (int)threadIdx.x;
@@ -467,6 +469,7 @@ __global__ __launch_bounds__(64) void k_align_band(DevSeqs s, const uint32_t* __
   constexpr int VK = VR < TOP ? VR : VR - TOP;             // its register
   constexpr uint32_t VM = VR < TOP ? 0x0000ffffu : 0xffff0000u;  // and half
   static_assert(16 % G == 0 && P < B && BOT >= 1, "band layout");
+  if (sc.wave_prio) __builtin_amdgcn_s_setprio(3);
   const int gid = (int)(blockIdx.x * 64 + threadIdx.x);
   const int k = gid / G, g = gid % G;
   if (k >= npairs) return;  // group-uniform

@@ -438,6 +438,7 @@ struct umiclust_ctx {
   DevBuf<uint32_t> d_probe;
   // lazy peers below this new-centroid rate (per mille; higher rates lose: profiles/r02/lazy_peer_sweep.json)
   int32_t lazy_permille = 5;  // UMICLUST_LAZY (0: never lazy)
+  int32_t rb_wprio = 0;       // round B's alignment waves at raised issue priority (UMICLUST_RB_WPRIO)
   int32_t rb_direct = 4096;   // round B: at most this many pairs read / written in pinned memory (UMICLUST_RB_DIRECT)
   int32_t o4_T = 0;               // policy O4 (umiclust_params.policy_threads): rounds of o4_T queries; 0 = sequential
   int32_t b_hint = 1 << 30;       // block size the last bin ended with (peer overflows halve it)
@@ -1266,13 +1267,15 @@ bool resolve_pass(umiclust_ctx* c, Pass& P, const StateView& state, std::vector<
       pres = c->d_bres.p;
     }
     c->hip(hipEventRecord(c->evb[0], sb), "event");
+    Scoring scb = c->sc;
+    scb.wave_prio = c->rb_wprio;
     // the pairs are in query order: one launch per run of one query length
     int nl = 0;
     for (int32_t x0 = 0; x0 < nb; nl++) {
       const int32_t L = c->hlen[bpq[x0] >> 1];
       int32_t x1 = x0 + 1;
       while (x1 < nb && c->hlen[bpq[x1] >> 1] == L) x1++;
-      c->hip(launch_align(dev_seqs(c), L, c->ambig, pq + x0, pt + x0, x1 - x0, nullptr, nullptr, c->sc, pres + x0, sb,
+      c->hip(launch_align(dev_seqs(c), L, c->ambig, pq + x0, pt + x0, x1 - x0, nullptr, nullptr, scb, pres + x0, sb,
                           c->band_pairs),
              "align B");
       x0 = x1;
@@ -2442,7 +2445,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "RB_PRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "RB_PRIO", "RB_WPRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
@@ -2558,6 +2561,7 @@ umiclust_ctx* umiclust_create(int32_t device_id, int32_t* err) {
   if (const char* e = getenv("UMICLUST_PT_SIDE")) c->pt_side = std::max(0, std::min(2, atoi(e)));
   if (const char* e = getenv("UMICLUST_LAZY")) c->lazy_permille = std::max(0, std::min(1000, atoi(e)));
   if (const char* e = getenv("UMICLUST_RB_DIRECT")) c->rb_direct = std::max(0, atoi(e));
+  if (const char* e = getenv("UMICLUST_RB_WPRIO")) c->rb_wprio = atoi(e) > 0 ? 1 : 0;
   if (const char* e = getenv("UMICLUST_REGROW_DEPTH")) c->regrow_depth = std::max(1, std::min(kPeerCap + 1, atoi(e)));
   if (const char* e = getenv("LOCAL_WORLD_SIZE")) c->pin = atoi(e) <= 1;
   if (const char* e = getenv("UMICLUST_PIN")) {

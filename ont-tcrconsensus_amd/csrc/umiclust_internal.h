@@ -12,6 +12,8 @@ struct Scoring {
   int32_t match, mismatch;
   int32_t go[6], ge[6];  // QL TL QI TI QR TR
   int32_t boundary_open;
+  int32_t wave_prio;  // alignment kernels: nonzero raises the waves' issue priority (s_setprio: round B, which the host
+                      // waits for while the next pass's kernels share the SIMDs)
 };
 
 // One index tile: CSR over bins (part << 16 | k-mer); postings live in one arena shared by all tiles.
