@@ -2444,7 +2444,7 @@ static void warn_unknown_env() {
   static std::once_flag once;
   std::call_once(once, [] {
     static const char* const known[] = {
-        "ARRANGE", "BAND", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
+        "ARRANGE", "BAND", "BAND_WPRIO", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
         "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "RB_PRIO", "RB_WPRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};

@@ -1628,8 +1628,16 @@ hipError_t launch_align(const DevSeqs& s, int32_t qlen, bool ambig, const uint32
   const int64_t lanes = (int64_t)npairs * (band ? band_lanes(qlen) : 1);
   const int v = ambig ? 1 : band ? 2 : 0;
   int64_t grid = (lanes + 63) / 64;
+  // banded launches are latency-bound (about one wave per SIMD) and sit on the pass chain the host waits for, while
+  // the next pass's counting waves share their SIMDs: UMICLUST_BAND_WPRIO=1 raises their issue priority
+  static const int band_prio = [] {
+    const char* e = getenv("UMICLUST_BAND_WPRIO");
+    return e ? atoi(e) : 0;
+  }();
+  Scoring scl = sc;
+  if (band && band_prio > 0) scl.wave_prio = 1;
   hipLaunchKernelGGL(g_align[kAlignSlots * qlen + v], dim3((unsigned)grid),
-                     dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, sc, out);
+                     dim3(64), 0, st, s, pq, pt, npairs, dev_npairs, outidx, scl, out);
   return hipGetLastError();
 }
 
