@@ -1101,6 +1101,9 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500, threads: int
         st = ctx.run_fasta(p, fa, os.path.join(out, "cluster"), os.path.join(out, "umi_clusters_consensus.fasta"),
                            os.path.join(out, "vsearch_cluster.log"))
         t_run = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ctx.wait_host()  # the input's release, which the call leaves on a thread of the context
+        t_rel = time.perf_counter() - t0
         nf, nb = _tree_bytes(out)
         sizes = _numbered_sizes(out, "cluster")
         cons_bytes = os.path.getsize(os.path.join(out, "umi_clusters_consensus.fasta"))
@@ -1116,6 +1119,9 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500, threads: int
         st2, pr = ctx.run_fasta_parse(p, fa, None, os.path.join(work, "umi_clusters_consensus.fasta"),
                                       os.path.join(work, "vsearch_cluster.log"), pp, work)
         t_fused = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ctx.wait_host()
+        t_rel2 = time.perf_counter() - t0
         nf2, nb2 = _tree_bytes(os.path.join(work, "clusters_fa"))
         sizes2 = _numbered_sizes(os.path.join(work, "clusters_fa"), "cluster", ".fasta")
         smol = os.path.getsize(os.path.join(work, "smolecule_clusters.fa"))
@@ -1125,6 +1131,9 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500, threads: int
         bound_f = replay_probe(d, sizes2, smol, io_t)
         return dict(
             umis_per_s=st["n_kept"] / t_run, seconds=t_run, fasta_bytes=size, n_kept=st["n_kept"],
+            # the call returns once every output is written; its input's release (unmapping the FASTA) runs on after
+            # it, on a thread of the context (umiclust_wait_host): counted here as well
+            input_release_s=t_rel, umis_per_s_incl_release=st["n_kept"] / (t_run + t_rel),
             clusters=st["n_clusters"], t_read_s=st.get("t_read_s"), t_cluster_s=st["t_total_s"],
             t_write_s=st.get("t_write_s"), files_written=nf, bytes_written=nb,
             write_gbps=nb / st["t_write_s"] / 1e9 if st.get("t_write_s") else None,
@@ -1132,6 +1141,7 @@ def e2e_leg(ctx, umis, identity: float, lens, read_len: int = 1500, threads: int
             write_replay_ratio=bound["seconds"] / st["t_write_s"] if st.get("t_write_s") else None,
             fasta_write_s=t_gen,
             fused_parse=dict(umis_per_s=st2["n_kept"] / t_fused, seconds=t_fused, t_read_s=st2.get("t_read_s"),
+                             input_release_s=t_rel2, umis_per_s_incl_release=st2["n_kept"] / (t_fused + t_rel2),
                              t_cluster_s=st2["t_total_s"], t_write_s=st2.get("t_write_s"),
                              clusters_written=pr["n_written"], cluster_files=nf2, cluster_file_bytes=nb2,
                              smolecule_bytes=smol, bytes_written=nb_all,

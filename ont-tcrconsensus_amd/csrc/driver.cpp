@@ -367,6 +367,13 @@ struct umiclust_ctx {
   hipStream_t ix_st = nullptr;     // null: the main stream
   hipEvent_t ix_done = nullptr, last_r_ev = nullptr;
   std::unique_ptr<WorkPool> pool;  // host threads of resolve_pass (UMICLUST_RESOLVE_THREADS)
+  // the file path's input (a multi-GB mapping: ~0.11 s of page-table teardown for config 2's 3.5 GB FASTA) is released
+  // on this thread after the call has written its outputs; joined by the context's next file-path call and by
+  // umiclust_destroy
+  std::thread in_release;
+  void join_release() {
+    if (in_release.joinable()) in_release.join();
+  }
   // host threads of resolve_pass (caller included); 0: 8 while this is the process's only context (config 2: host
   // resolve 0.22 -> 0.14 s per step, profiles/r03/resolve_threads_ab.json), 4 beside other contexts (bin-set lanes)
   int32_t resolve_threads = 0;
@@ -2302,7 +2309,9 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
                        umiclust_stats* stats, const umiclust_parse_params* pp = nullptr,
                        const char* work_dir = nullptr, umiclust_parse_result* pr = nullptr) {
   const double t0 = now_s();
-  Fasta f;
+  c->join_release();
+  std::unique_ptr<Fasta> fin(new Fasta());
+  Fasta& f = *fin;
   if (!in_fasta || !io::read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
   const int64_t n = (int64_t)f.hdr_off.size();
   for (int64_t i = 0; i < n; i++) {
@@ -2384,7 +2393,7 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   if (cons_th.t.joinable()) cons_th.t.join();
   if (cons_err) std::rethrow_exception(cons_err);
   const double t_write = now_s() - t1;
-  if (c->debug)
+  if (getenv("UMICLUST_DEBUG"))
     fprintf(stderr, "umiclust: file path: read %.3f s, cluster %.3f s, masked download %.3f s (%lld changed), "
                     "cluster files done at %.3f s, consout (beside them) at %.3f s\n", t_read, t1 - t0 - t_read, t_mask,
             (long long)c->n_changed, t_files, t_cons);
@@ -2429,6 +2438,15 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   }
   c->stats.t_read_s = t_read;
   c->stats.t_write_s = t_write + (pp ? now_s() - t1 - t_write : 0.0);
+  // the outputs are written: the input goes on a thread of its own (UMICLUST_DEBUG prints how long it takes)
+  {
+    Fasta* in = fin.release();
+    c->in_release = std::thread([in] {
+      const double tr = now_s();
+      delete in;
+      if (getenv("UMICLUST_DEBUG")) fprintf(stderr, "umiclust: file path: input released in %.3f s\n", now_s() - tr);
+    });
+  }
   c->stats.t_run_s = now_s() - t0;
   if (stats) *stats = c->stats;
   return K;
@@ -2605,8 +2623,15 @@ int32_t umiclust_set_priority(umiclust_ctx* c, int32_t level) {
   return main_stream_priority(c, c->prio_user) == hipSuccess ? UMICLUST_OK : UMICLUST_EDEVICE;
 }
 
+int32_t umiclust_wait_host(umiclust_ctx* c) {
+  if (!c) return UMICLUST_EINVAL;
+  c->join_release();
+  return UMICLUST_OK;
+}
+
 void umiclust_destroy(umiclust_ctx* c) {
   if (!c) return;
+  c->join_release();
   io::set_live_contexts(--g_live_ctx);
   (void)hipSetDevice(c->dev);
   for (Tile* t : c->tiles) delete t;

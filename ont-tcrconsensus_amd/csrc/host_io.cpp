@@ -55,8 +55,17 @@ int io_threads() {
   return std::max(1, std::min(16, host_cpus() / g_io_ctx.load()));
 }
 
-Fasta::~Fasta() {
+Fasta::~Fasta() { release(); }
+
+void Fasta::release() {
   if (map) munmap(map, size);
+  map = nullptr;
+  data = nullptr;
+  size = 0;
+  std::vector<int64_t>().swap(hdr_off);
+  std::vector<int32_t>().swap(hdr_len);
+  std::vector<char>().swap(seq);
+  std::vector<int64_t>().swap(seq_off);
 }
 
 struct FastaPart {

@@ -51,6 +51,7 @@ struct Fasta {
   Fasta(const Fasta&) = delete;
   Fasta& operator=(const Fasta&) = delete;
   ~Fasta();
+  void release();  // unmap the file and free the arrays
 };
 // vsearch's FASTA reader: labels truncated at the first whitespace, sequence lines keep letters only, lines
 // before the first '>' ignored; parsed by io_threads() threads over slices of the mapping

@@ -112,7 +112,7 @@ EXPORTS = [
     "umiclust_load", "umiclust_stage", "umiclust_prepare", "umiclust_set_priority", "umiclust_cluster", "umiclust_fetch", "umiclust_load_bins", "umiclust_cluster_bin", "umiclust_cluster_pack",
     "umiclust_fetch_bin", "umiclust_overlap_counts", "umiclust_overlap_regions", "umiclust_extract_umis",
     "umiclust_extract_umis_file", "umiclust_region_split", "umiclust_align_pairs", "umiclust_prep",
-    "umiclust_timeline",
+    "umiclust_timeline", "umiclust_wait_host",
 ]
 OVERLAP_MAX_REGIONS = 4096
 ABI_VERSION = 9  # include/umiclust.h UMICLUST_ABI_VERSION: the struct layouts below
@@ -142,6 +142,8 @@ def lib() -> C.CDLL:
     L.umiclust_create.argtypes = [C.c_int32, P(C.c_int32)]
     L.umiclust_destroy.restype = None
     L.umiclust_destroy.argtypes = [C.c_void_p]
+    L.umiclust_wait_host.restype = C.c_int32
+    L.umiclust_wait_host.argtypes = [C.c_void_p]
     L.umiclust_last_error.restype = C.c_char_p
     L.umiclust_last_error.argtypes = [C.c_void_p]
     L.umiclust_run_fasta.restype = C.c_int64
@@ -283,6 +285,10 @@ class Context:
             msg = lib().umiclust_last_error(self._h)
             raise UmiclustError(int(rc), f"{what}: {msg.decode() if msg else ''}")
         return rc
+
+    def wait_host(self) -> None:
+        """Waits for the host work the last file-path call left running (its input's release)."""
+        self._check(lib().umiclust_wait_host(self._h), "wait_host")
 
     def run_fasta(self, p: Params, in_fasta: str, clusters_prefix: str | None, consout: str | None,
                   log: str | None) -> dict:

@@ -733,3 +733,31 @@ def test_counting_wave_layouts(pf1, monkeypatch):
     assert st["n_alignments"] == gold["alignments"] and st["cells"] == gold["cells"]
     for k in ("n_clusters", "cluster", "strand", "centroid", "consensus"):
         assert d[k] == gold[k], k
+
+
+def test_file_path_releases_input_after_return(tmp_path):
+    """The file-path calls release their input on a thread of the context after writing every output
+    (umiclust_wait_host): back-to-back calls on one context (the second joins the first's release) write the oracle's
+    files, and the input can be replaced between them."""
+    u = synth.make_umis(120, seed=77, max_reads=2000, orient_mix=0.1, error_rate=0.01)
+    fa = tmp_path / "in.fasta"
+    synth.write_umi_fasta(str(fa), u)
+    ref = tmp_path / "oracle"
+    ref.mkdir()
+    op = orc.params(1, 0.93, 58, 68)
+    op.threads, op.policy_threads = 25, 1
+    orc.run_fasta(op, str(fa), str(ref) + "/cluster", str(ref / "umi_clusters_consensus.fasta"))
+    p = _lib.params(_lib.PRESET_ROUND1, 0.93, 58, 68, threads=25)
+    with _lib.Context(0) as ctx:
+        for rep in range(3):
+            out = tmp_path / f"gpu{rep}"
+            out.mkdir()
+            ctx.run_fasta(p, str(fa), str(out) + "/cluster", str(out / "umi_clusters_consensus.fasta"), None)
+            if rep == 1:
+                ctx.wait_host()
+                tmp = tmp_path / "in.tmp"
+                synth.write_umi_fasta(str(tmp), u)
+                os.replace(tmp, fa)  # the old file's mapping is gone; the next call maps the new one
+            assert _read_dir(out) == _read_dir(ref)
+        ctx.wait_host()
+        ctx.wait_host()  # idempotent
