@@ -141,8 +141,9 @@ void umiclust_destroy(umiclust_ctx *ctx);
  * of the others.  Synchronises the context first.  Results do not depend on it. */
 int32_t umiclust_set_priority(umiclust_ctx *ctx, int32_t level);
 /* Waits for the host work a file-path call (umiclust_run_fasta / _run_argv / _run_fasta_parse) leaves running after
- * it returns: the release of its input (unmapping a multi-GB FASTA, ~0.11 s for config 2's 3.5 GB), done on a
- * thread of the context once every output is written.  The context's next file-path call and umiclust_destroy wait
+ * it returns: the release of its input (unmapping a multi-GB FASTA, ~0.11 s for config 2's 3.5 GB) and of the fused
+ * path's smolecule_clusters.fa mapping (RAM-backed outputs; the file's contents are in place before the call returns),
+ * done on a thread of the context once every output is written.  The context's next file-path call and umiclust_destroy wait
  * for it too.  Returns UMICLUST_OK.  (Round 6; an added function, the struct layouts are unchanged.) */
 int32_t umiclust_wait_host(umiclust_ctx *ctx);
 /* human-readable message for the last error on this context */

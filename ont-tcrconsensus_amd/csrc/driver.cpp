@@ -2312,6 +2312,13 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
   c->join_release();
   std::unique_ptr<Fasta> fin(new Fasta());
   Fasta& f = *fin;
+  // output mappings handed over by the writers (released with the input; at once if the call fails)
+  struct Unmaps {
+    std::vector<std::pair<void*, size_t>> v;
+    ~Unmaps() {
+      for (auto& m : v) munmap(m.first, m.second);
+    }
+  } unmaps;
   if (!in_fasta || !io::read_fasta(in_fasta, f)) c->fail(UMICLUST_EIO, "cannot read %s", in_fasta ? in_fasta : "(null)");
   const int64_t n = (int64_t)f.hdr_off.size();
   for (int64_t i = 0; i < n; i++) {
@@ -2434,15 +2441,18 @@ int64_t run_fasta_impl(umiclust_ctx* c, const umiclust_params* p, const char* in
     const double tj = now_s();
     if (pre_th.t.joinable()) pre_th.t.join();
     if (c->debug) fprintf(stderr, "umiclust: fused: waited %.3f s for the header fields\n", now_s() - tj);
-    io::parse_clusters(f, cv, pp, work_dir, pr, pre.empty() ? nullptr : pre.data());
+    io::parse_clusters(f, cv, pp, work_dir, pr, pre.empty() ? nullptr : pre.data(), &unmaps.v);
   }
   c->stats.t_read_s = t_read;
   c->stats.t_write_s = t_write + (pp ? now_s() - t1 - t_write : 0.0);
   // the outputs are written: the input goes on a thread of its own (UMICLUST_DEBUG prints how long it takes)
   {
     Fasta* in = fin.release();
-    c->in_release = std::thread([in] {
+    std::vector<std::pair<void*, size_t>> outs;
+    outs.swap(unmaps.v);
+    c->in_release = std::thread([in, outs] {
       const double tr = now_s();
+      for (auto& m : outs) munmap(m.first, m.second);
       delete in;
       if (getenv("UMICLUST_DEBUG")) fprintf(stderr, "umiclust: file path: input released in %.3f s\n", now_s() - tr);
     });

@@ -553,7 +553,7 @@ void precompute_fields(const Fasta& f, std::vector<RecFields>& out, int threads)
 }
 
 void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_params* pp, const char* work_dir_c,
-                    umiclust_parse_result* pr, const RecFields* pre) {
+                    umiclust_parse_result* pr, const RecFields* pre, std::vector<std::pair<void*, size_t>>* unmap) {
   const int64_t min_reads = pp->min_reads_per_cluster, max_reads = pp->max_reads_per_cluster;
   const std::string work_dir = work_dir_c ? work_dir_c : "";
   const std::string fa_dir = pjoin(work_dir, "clusters_fa");  // :167
@@ -846,7 +846,8 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
     for (int32_t k = kbad + 1; k < kwrite; k++)
       if (wrote[k]) unlink(pjoin(fa_dir, "cluster" + std::to_string(k) + ".fasta").c_str());
   bool smol_ok = true;
-  if (smol_map) smol_ok = munmap(smol_map, smol_total) == 0;
+  if (smol_map && unmap) unmap->push_back({smol_map, smol_total});
+  else if (smol_map) smol_ok = munmap(smol_map, smol_total) == 0;
   for (int t = 0; t < T; t++) smol_ok = smol_ok && !smol_bad[t];
   if (kbad >= 0) smol_ok = ftruncate(smol_fd, (off_t)smol_off[kkeep]) == 0 && smol_ok;
   smol_ok = close(smol_fd) == 0 && smol_ok;

@@ -8,6 +8,7 @@
 
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/umiclust.h"
@@ -97,9 +98,11 @@ struct RecFields {
   uint8_t ok = 0, strand = 0;
 };
 void precompute_fields(const Fasta& f, std::vector<RecFields>& out, int threads);
+// unmap: when given, the smolecule file's shared mapping (RAM-backed outputs) is handed over instead of unmapped, for
+// the caller to release once the call has returned (its contents are in the page cache already)
 void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_params* pp, const char* work_dir,
-                    umiclust_parse_result* pr,
-                    const RecFields* pre = nullptr);
+                    umiclust_parse_result* pr, const RecFields* pre = nullptr,
+                    std::vector<std::pair<void*, size_t>>* unmap = nullptr);
 
 // write_fasta of extract_umis (/root/reference/ont_tcr_consensus/extract_umis.py:154-186) for records [0, ngood):
 // res[i*6 ..] = (dist, start, end) of the 5' and 3' UMI in their windows; returns the reads with both UMIs
