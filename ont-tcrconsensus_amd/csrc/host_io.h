@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <memory>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -39,15 +40,37 @@ void parallel_for(int T, F&& f) {
   for (auto& x : th) x.join();
 }
 
+// std::allocator without value-initialisation on resize (large arrays filled in parallel right after)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using RawVec = std::vector<T, NoInitAlloc<T>>;
+
 // The input FASTA (or FASTQ), memory-mapped; labels point into the mapping, sequences are copied out.
 struct Fasta {
   const char* data = nullptr;     // file contents (mapping)
   size_t size = 0;
   void* map = nullptr;
-  std::vector<int64_t> hdr_off;   // label start (after '>' / '@')
-  std::vector<int32_t> hdr_len;   // label length (truncated at whitespace)
-  std::vector<char> seq;          // concatenated sequences
-  std::vector<int64_t> seq_off;   // n+1
+  RawVec<int64_t> hdr_off;   // label start (after '>' / '@')
+  RawVec<int32_t> hdr_len;   // label length (truncated at whitespace)
+  RawVec<char> seq;          // concatenated sequences
+  RawVec<int64_t> seq_off;   // n+1
   Fasta() = default;
   Fasta(const Fasta&) = delete;
   Fasta& operator=(const Fasta&) = delete;

@@ -63,7 +63,8 @@ for st in "$@"; do
                 > "$out/pf1_${v}_c$c.json" 2> "$out/pf1_${v}_c$c.err" || { rc=$?; break 2; }; rc=0; done; done ;;
     c3trace) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/c3trace" -o run -- \
              python3 bench.py --config 3 --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > "$out/c3trace.log" 2>&1; rc=$?
-             [ $rc = 0 ] && python3 tools/kstats.py "$out/c3trace/run_kernel_stats.csv" 2 > "$out/c3trace_kstats.txt" 2>&1
+             [ $rc = 0 ] && python3 tools/kstats.py "$out/c3trace/run_kernel_stats.csv" 2 > "$out/c3trace_kstats.txt" 2>&1 \
+               && python3 tools/gpu_idle.py "$out/c3trace" > "$out/c3trace_idle.txt" 2>&1
              rm -f "$out/c3trace/run_kernel_trace.csv" ;;
     bandab) for v in ${BANDS:-140000 0 20000}; do for c in ${PCFGS:-3 5}; do
               UMICLUST_BAND=$v timeout -k 10 400 python3 -u bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-e2e \
