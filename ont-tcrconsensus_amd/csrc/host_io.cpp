@@ -3,6 +3,7 @@
 #include "host_io.h"
 
 #include <fcntl.h>
+#include <sys/uio.h>
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -496,6 +497,26 @@ void write_consout(const char* path, const Fasta& f, const ClusterView& cv, cons
   if (!write_parts(path, part)) throw IoError{UMICLUST_EIO, std::string("cannot write ") + path};
 }
 
+// writev of every segment (IOV_MAX at a time, partial writes resumed)
+static bool writev_all(int fd, std::vector<iovec>& iov) {
+  size_t at = 0;
+  while (at < iov.size()) {
+    const int n = (int)std::min<size_t>(iov.size() - at, 1024);
+    const ssize_t w = writev(fd, iov.data() + at, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    size_t left = (size_t)w;
+    while (at < iov.size() && left >= iov[at].iov_len) left -= iov[at++].iov_len;
+    if (left) {
+      iov[at].iov_base = (char*)iov[at].iov_base + left;
+      iov[at].iov_len -= left;
+    }
+  }
+  return true;
+}
+
 void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& cv, const char* masked, int stride,
                          const uint8_t* hlen, int width, const int32_t* mrow) {
   const int32_t K = cv.K;
@@ -503,22 +524,59 @@ void write_cluster_files(const char* prefix, const Fasta& f, const ClusterView& 
   const std::vector<int32_t> cut = cluster_slices(cv.ostart, K, T);
   std::vector<int32_t> bad(T, -1);
   parallel_for(T, [&](int t) {
+    // A member whose input record is byte for byte what it prints (">label\n" + its sequence on one line, unmasked,
+    // within the line width) is written straight from the input mapping; the others are formatted into `out`.
+    // Segments: (pointer, length) with pointer null = an offset into `out` (resolved once it stops growing).
     std::string fn, out;
+    std::vector<std::pair<const char*, size_t>> seg;
+    std::vector<iovec> iov;
     for (int32_t k = cut[t]; k < cut[t + 1]; k++) {
       out.clear();
+      seg.clear();
       for (int32_t x = cv.ostart[k]; x < cv.ostart[k + 1]; x++) {
         const int32_t s = cv.omemb[x];
         const int32_t i = cv.perm[s];
-        out.push_back('>');
-        out.append(f.data + f.hdr_off[i], (size_t)f.hdr_len[i]);
-        out.push_back('\n');
         const int64_t row = !masked ? -1 : mrow ? mrow[s] : s;
+        const int64_t L = f.seq_off[i + 1] - f.seq_off[i];
+        const char* h = f.data + f.hdr_off[i];
+        const size_t hl = (size_t)f.hdr_len[i];
+        if (row < 0 && (width <= 0 || L <= width) && f.hdr_off[i] > 0 && h[-1] == '>' &&
+            (size_t)f.hdr_off[i] + hl + 2 + (size_t)L <= f.size && h[hl] == '\n' && h[hl + 1 + L] == '\n' &&
+            memcmp(h + hl + 1, f.seq.data() + f.seq_off[i], (size_t)L) == 0) {
+          seg.push_back({h - 1, hl + (size_t)L + 3});
+          continue;
+        }
+        const size_t o0 = out.size();
+        out.push_back('>');
+        out.append(h, hl);
+        out.push_back('\n');
         if (row >= 0) put_wrapped(out, masked + (size_t)row * stride, hlen[s], width);
-        else put_wrapped(out, f.seq.data() + f.seq_off[i], f.seq_off[i + 1] - f.seq_off[i], width);
+        else put_wrapped(out, f.seq.data() + f.seq_off[i], L, width);
+        seg.push_back({nullptr, o0});
+      }
+      iov.clear();
+      for (size_t j = 0; j < seg.size(); j++) {
+        if (seg[j].first) {
+          iov.push_back({(void*)seg[j].first, seg[j].second});
+        } else {  // this formatted record runs to the next formatted one's start (or out's end)
+          size_t e = out.size();
+          for (size_t u = j + 1; u < seg.size(); u++)
+            if (!seg[u].first) {
+              e = seg[u].second;
+              break;
+            }
+          iov.push_back({(void*)(out.data() + seg[j].second), e - seg[j].second});
+        }
       }
       fn = prefix;
       fn += std::to_string(k);
-      if (!write_file(fn, out)) {
+      const int fd = open(fn.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+      bool ok = fd >= 0;
+      if (ok) {
+        ok = writev_all(fd, iov);
+        ok = close(fd) == 0 && ok;
+      }
+      if (!ok) {
         bad[t] = k;
         return;
       }
