@@ -832,7 +832,8 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
   std::vector<int32_t> bad(T, -1);
   std::vector<uint8_t> wrote((size_t)kwrite, 0), smol_bad(T, 0);
   parallel_for(T, [&](int t) {
-    std::string lines, smol, &log = log_p[t], &stats_out = stats_p[t];
+    std::string smol, &log = log_p[t], &stats_out = stats_p[t];
+    std::vector<iovec> iov;
     smol.reserve(kSmolChunk + (1u << 16));
     // this thread's records, contiguous in the file from its first cluster's offset (also on an early return:
     // the clusters before a failing one keep their records, as the reference's buffered file does)
@@ -875,21 +876,42 @@ void parse_clusters(const Fasta& f, const ClusterView& cv, const umiclust_parse_
       log += "Cluster: " + out_fasta + " has " + std::to_string(r.n_fwd) + "/" + std::to_string(r.max_fwd) +
              " fwd and " + std::to_string(r.n_rev) + "/" + std::to_string(r.max_rev) + " rev reads\n";
       if (r.written) {
-        lines.clear();
+        // the cluster file's records are gathered from the input mapping (writev: no formatting copy of the reads);
+        // the smolecule records go straight into the file's mapping when there is one
+        static const char kGt = '>', kNl = '\n';
+        iov.clear();
         const Ent* e = ents_t[(size_t)ent_thr[k]].data() + ent_beg[k];
         for (int64_t y = 0; y < nw; y++) {
-          lines.push_back('>');
-          lines.append(e[y].rid, e[y].rid_n);
-          lines.push_back('\n');
-          lines.append(e[y].read, e[y].read_n);
-          lines.push_back('\n');
-          smol.push_back('>');
-          smol += kstr;
-          smol.push_back('\n');
-          smol.append(e[y].read, e[y].read_n);
-          smol.push_back('\n');
+          iov.push_back({(void*)&kGt, 1});
+          iov.push_back({(void*)e[y].rid, e[y].rid_n});
+          iov.push_back({(void*)&kNl, 1});
+          iov.push_back({(void*)e[y].read, e[y].read_n});
+          iov.push_back({(void*)&kNl, 1});
+          if (smol_map) {
+            char* d = smol_map + flush.at;
+            *d++ = '>';
+            memcpy(d, kstr.data(), kstr.size());
+            d += kstr.size();
+            *d++ = '\n';
+            memcpy(d, e[y].read, e[y].read_n);
+            d += e[y].read_n;
+            *d++ = '\n';
+            flush.at = (off_t)(d - smol_map);
+          } else {
+            smol.push_back('>');
+            smol += kstr;
+            smol.push_back('\n');
+            smol.append(e[y].read, e[y].read_n);
+            smol.push_back('\n');
+          }
         }
-        if (!write_file(out_fasta, lines)) {
+        const int fd = open(out_fasta.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+        bool ok = fd >= 0;
+        if (ok) {
+          ok = writev_all(fd, iov);
+          ok = close(fd) == 0 && ok;
+        }
+        if (!ok) {
           if (bad[t] < 0) bad[t] = k;
           return;
         }
