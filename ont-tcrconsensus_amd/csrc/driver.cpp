@@ -1478,7 +1478,11 @@ hipError_t main_stream_priority(umiclust_ctx* c, int level) {
 }
 
 void cluster_all(umiclust_ctx* c, int32_t bin, bool multi_bin = false, int32_t npk = 1) {
-  c->rec_direct = g_live_ctx.load() > 1;
+  static const int rec_env = [] {
+    const char* e = getenv("UMICLUST_REC_DIRECT");
+    return e ? atoi(e) : -1;
+  }();
+  c->rec_direct = rec_env >= 0 ? rec_env > 0 : g_live_ctx.load() > 1;
   const double t0 = now_s();
   if (bin < 0 || npk < 1 || bin + npk >= (int32_t)c->bin_s.size())
     c->fail(UMICLUST_EINVAL, "bins [%d, %d) out of range", bin, bin + npk);
@@ -2473,7 +2477,7 @@ static void warn_unknown_env() {
   std::call_once(once, [] {
     static const char* const known[] = {
         "ARRANGE", "BAND", "BAND_WPRIO", "BLOCK", "DEBUG", "IO_THREADS", "LAZY", "MIXLEN", "O4", "OVERLAP_TEST_COLLIDE", "PAR_MIN", "PF1", "PFPROBE",
-        "PFPROF", "PIN", "PT_SIDE", "RB_DIRECT", "RB_PRIO", "RB_WPRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
+        "PFPROF", "PIN", "PT_SIDE", "REC_DIRECT", "RB_DIRECT", "RB_PRIO", "RB_WPRIO", "REGROW", "REGROW_DEPTH", "RESOLVE_DUMP", "RESOLVE_THREADS", "SPLIT", "WALK_DUMP",
         // read by the Python side (umiclust/, bench.py)
         "DEVICE", "CRIT_PRIO", "PACK_READS", "BENCH_THREADS", "E2E_DIR"};
     for (char** e = environ; e && *e; e++) {
