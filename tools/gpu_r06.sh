@@ -98,6 +98,9 @@ for st in "$@"; do
     recab) for v in ${RECS:-1 0 1 0 1 0}; do for c in ${PCFGS:-2}; do
               UMICLUST_REC_DIRECT=$v timeout -k 10 300 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/rec${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
+    rtab) for v in ${RTS:-8 12 16 8 12 16}; do for c in ${PCFGS:-2 5}; do
+              UMICLUST_RESOLVE_THREADS=$v timeout -k 10 300 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
+                > "$out/rt${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
     rbab) for v in ${RBS:-4096 0 4096 0}; do for c in ${PCFGS:-5}; do
               UMICLUST_RB_DIRECT=$v timeout -k 10 300 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e \
                 > "$out/rb${v}_c${c}_$RANDOM.json" 2> /dev/null || { rc=$?; break 2; }; rc=0; done; done ;;
